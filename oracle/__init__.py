@@ -1,0 +1,77 @@
+"""CPU ORACLE loader — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / CPU baseline.  See
+oracle/bcsim_oracle.c for the parity status (ns-3 semantics: parity unpinned;
+glibc rand(): pinned against libc).
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_REPO = os.path.dirname(_HERE)
+sys.path.insert(0, os.path.join(_REPO, "blockchain-simulator_amd"))
+from bcsim import _abi  # noqa: E402  (struct layouts = the public interface)
+
+_LIB = None
+
+
+def build(force=False):
+    so = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "bcsim_oracle.c")
+    if force or not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+    return so
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = C.CDLL(build())
+        _abi.declare(_LIB, "bcsim_oracle_")
+        _LIB.oracle_glibc_rand_seq.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_int32)]
+        _LIB.oracle_glibc_rand_seq.restype = None
+        _LIB.oracle_seconds_to_ns.argtypes = [C.c_double, C.c_int]
+        _LIB.oracle_seconds_to_ns.restype = C.c_int64
+        _LIB.oracle_tx_ns.argtypes = [C.c_uint32, C.c_uint64, C.c_int]
+        _LIB.oracle_tx_ns.restype = C.c_int64
+        _LIB.oracle_msg_tx.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_int,
+                                       C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        _LIB.oracle_msg_tx.restype = None
+        _LIB.oracle_ctr_rand.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64]
+        _LIB.oracle_ctr_rand.restype = C.c_uint32
+    return _LIB
+
+
+class OracleSim(_abi.Handle):
+    def __init__(self, cfg):
+        super().__init__(lib(), "bcsim_oracle_", cfg)
+
+
+def glibc_rand(seed, n):
+    out = (C.c_int32 * n)()
+    lib().oracle_glibc_rand_seq(seed, n, out)
+    return list(out)
+
+
+def seconds_to_ns(s, mode=_abi.TIME_ROUND):
+    return lib().oracle_seconds_to_ns(s, mode)
+
+
+def msg_tx(payload, mtu=1500, rate=3_000_000, mode=_abi.TIME_ROUND):
+    a, b = C.c_int64(), C.c_int64()
+    nf, wt = C.c_uint32(), C.c_uint32()
+    lib().oracle_msg_tx(payload, mtu, rate, mode, C.byref(a), C.byref(b), C.byref(nf), C.byref(wt))
+    return dict(tx_total=a.value, tx_last=b.value, frames=nf.value, wire=wt.value)
+
+
+def run(cfg, t_until=_abi.INT64_MAX, topology=None):
+    """One-shot oracle run -> (trace tuples, counters dict, status dict)."""
+    with OracleSim(cfg) as o:
+        if topology is not None:
+            o.set_topology(*topology)
+        o.run(t_until)
+        return o.trace(), o.counters(), o.status()

@@ -1,0 +1,1218 @@
+/*
+ * bcsim_oracle.c — serial CPU ORACLE (discrete-event restatement) of the
+ * blockchain-simulator hot path.  TEST INFRASTRUCTURE ONLY: loaded by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline, never by the product.
+ *
+ * PARITY STATUS (header as required by DESIGN.md §3):
+ *   - glibc rand(): PINNED (restated TYPE_3 generator, checked against libc).
+ *   - protocol handlers: restated line by line from the reference sources,
+ *     citations below; quirks kept (echo, Paxos off-by-one broadcast, PBFT
+ *     shared globals, Raft vote counters shared with heartbeat counters).
+ *   - ns-3 L1 semantics (event tie order, p2p link FIFO/serialization,
+ *     IPv4 fragmentation, float->Time rounding): PARITY UNPINNED.  ns-3 is not
+ *     present anywhere in this image and the reference has no tests or golden
+ *     logs; the model below is documented in DESIGN.md §2 and is the contract
+ *     the GPU engine is held to bit-exactly.
+ *
+ * Undefined behaviour in the reference gets one fixed meaning:
+ *   uninitialised payload bytes = 0 (NUL; getPacketContent then truncates);
+ *   PbftNode::tx[] zero-initialised; generateTX's dangling pointer = the
+ *   intended header bytes; Paxos *end() broadcast target = dropped send that
+ *   still consumes one rand() draw and one schedule; compat-encoded negative
+ *   tx[] index -> BCSIM_E_ENCODING, index >= pbft_seq_cap -> BCSIM_E_INDEX.
+ *
+ * Event order (canonical key): (t, t_sched, origin, sub, target) where
+ *   t_sched = time the event was scheduled (START/STOP: -1; RECV: transmit
+ *   start of the packet's last frame), origin = node whose code scheduled it
+ *   (RECV: the sender), sub = origin's running schedule counter (RECV: the
+ *   sub of the SendPacket that produced it).  Equal-time events on one node
+ *   therefore run in ns-3's scheduling order whenever their schedulers ran at
+ *   different times; true ties fall back to node id.
+ */
+#include "oracle.h"
+
+#include <limits.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* glibc TYPE_3 random() restatement (glibc stdlib/random_r.c, srandom_r +
+ * random_r; rand() == random()).  Reference call sites: pbft-node.cc:68,401,
+ * raft-node.cc:65,71, paxos-node.cc:399.  Never seeded in the reference
+ * (default seed 1).                                                        */
+typedef struct {
+  int32_t st[31];
+  int f, r;
+} glibc_rng;
+
+static int32_t glibc_next(glibc_rng* g) {
+  uint32_t val = (uint32_t)g->st[g->f] + (uint32_t)g->st[g->r];
+  g->st[g->f] = (int32_t)val;
+  int32_t out = (int32_t)(val >> 1);
+  if (++g->f >= 31) {
+    g->f = 0;
+    ++g->r;
+  } else if (++g->r >= 31) {
+    g->r = 0;
+  }
+  return out;
+}
+
+static void glibc_seed(glibc_rng* g, uint32_t seed) {
+  int32_t word = (int32_t)(seed == 0 ? 1u : seed);
+  g->st[0] = word;
+  for (int i = 1; i < 31; ++i) {
+    long hi = word / 127773;
+    long lo = word % 127773;
+    long w = 16807 * lo - 2836 * hi;
+    if (w < 0) w += 2147483647;
+    word = (int32_t)w;
+    g->st[i] = word;
+  }
+  g->f = 3;
+  g->r = 0;
+  for (int k = 0; k < 310; ++k) (void)glibc_next(g);
+}
+
+void oracle_glibc_rand_seq(uint32_t seed, uint32_t n, int32_t* out) {
+  glibc_rng g;
+  glibc_seed(&g, seed);
+  for (uint32_t i = 0; i < n; ++i) out[i] = glibc_next(&g);
+}
+
+/* Counter RNG (build extension, order independent): splitmix64 chain. */
+static uint64_t sm64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+uint32_t oracle_ctr_rand(uint64_t seed, uint32_t replica, uint32_t node,
+                         uint64_t k) {
+  uint64_t h = sm64(seed);
+  h = sm64(h ^ (uint64_t)replica);
+  h = sm64(h ^ (uint64_t)node);
+  h = sm64(h ^ k);
+  return (uint32_t)(h >> 33);
+}
+
+/* ------------------------------------------------------------------------ */
+/* ns-3 Seconds(double) -> int64 ns.  int64x64_t(double) keeps 64 fractional
+ * bits (truncating below 2^-64), multiplication by the integer factor 1e9 is
+ * exact, then Time(int64x64_t) takes Round() (half away from zero) or
+ * GetHigh() (floor).  Unpinned: the ns-3 version is not recorded.          */
+int64_t oracle_seconds_to_ns(double s, int mode) {
+  if (s == 0.0) return 0;
+  int neg = s < 0;
+  double v = neg ? -s : s;
+  int e;
+  double m = frexp(v, &e); /* v = m * 2^e, m in [0.5,1) */
+  uint64_t M = (uint64_t)ldexp(m, 53);
+  int E = e - 53; /* v = M * 2^E */
+  unsigned __int128 q; /* floor(v * 2^64) */
+  int sh = E + 64;
+  if (sh >= 0)
+    q = (unsigned __int128)M << sh;
+  else if (sh > -128)
+    q = (unsigned __int128)M >> (-sh);
+  else
+    q = 0;
+  uint64_t hi = (uint64_t)(q >> 64);
+  uint64_t lo = (uint64_t)q;
+  unsigned __int128 f = (unsigned __int128)lo * 1000000000ull;
+  uint64_t ns = hi * 1000000000ull + (uint64_t)(f >> 64);
+  uint64_t rem = (uint64_t)f;
+  if (mode == BCSIM_TIME_ROUND && rem >= (1ull << 63)) ns += 1;
+  return neg ? -(int64_t)ns : (int64_t)ns;
+}
+
+/* DataRate::CalculateBytesTxTime: Seconds(double(bytes) * 8 / bps). */
+int64_t oracle_tx_ns(uint32_t wire_bytes, uint64_t rate_bps, int mode) {
+  double s = (double)wire_bytes * 8 / (double)rate_bps;
+  return oracle_seconds_to_ns(s, mode);
+}
+
+/* UDP(8) + IPv4(20) + PPP(2); IPv4 fragments of (mtu-20)&~7 payload bytes. */
+void oracle_msg_tx(uint32_t payload, uint32_t mtu, uint64_t rate_bps, int mode,
+                   int64_t* tx_total, int64_t* tx_last, uint32_t* n_frames,
+                   uint32_t* wire_total) {
+  uint32_t ipp = payload + 8;
+  uint32_t room = mtu - 20;
+  uint32_t frag = room & ~7u;
+  int64_t tot = 0, last = 0;
+  uint32_t nf = 0, wt = 0;
+  if (ipp <= room) {
+    uint32_t w = ipp + 22;
+    last = oracle_tx_ns(w, rate_bps, mode);
+    tot = last;
+    nf = 1;
+    wt = w;
+  } else {
+    uint32_t left = ipp;
+    while (left > 0) {
+      uint32_t p = left > frag ? frag : left;
+      uint32_t w = p + 22;
+      last = oracle_tx_ns(w, rate_bps, mode);
+      tot += last;
+      wt += w;
+      ++nf;
+      left -= p;
+    }
+  }
+  if (tx_total) *tx_total = tot;
+  if (tx_last) *tx_last = last;
+  if (n_frames) *n_frames = nf;
+  if (wire_total) *wire_total = wt;
+}
+
+/* float seconds from the reference's delay helpers, then Seconds(). */
+static int64_t fsec_ns(float f, int mode) {
+  return oracle_seconds_to_ns((double)f, mode);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Events */
+enum { EV_START = 0, EV_STOP = 1, EV_TIMER = 2, EV_SEND = 3, EV_RECV = 4 };
+/* timer kinds */
+enum {
+  TM_PBFT_BLOCK = 0,
+  TM_RAFT_ELECTION = 1,
+  TM_RAFT_HEARTBEAT = 2,
+  TM_RAFT_PROPOSAL = 3,
+  TM_PAXOS_TICKET = 4
+};
+
+typedef struct {
+  int32_t type;  /* charToInt(msg[0]) */
+  int32_t f[3];  /* raw chars data[1..3] (0 = NUL / uninitialised) */
+  int32_t big;   /* 0 = small control payload, 1 = block / proposal */
+} omsg;
+
+typedef struct {
+  int64_t t, ts;
+  uint32_t origin, sub, target, kind;
+  uint32_t aux;  /* TIMER: kind; SEND: edge (UINT32_MAX = dropped);
+                    RECV: edge the packet travelled */
+  omsg m;
+} oev;
+
+typedef struct {
+  uint32_t sub;
+  uint64_t draws;
+  /* PBFT (pbft-node.h:39-56) */
+  int32_t leader, block_num;
+  uint32_t block_ev;
+  /* Raft (raft-node.h:39-53) */
+  int32_t is_leader, has_voted, m_value, vote_success, vote_failed;
+  int32_t add_change_value, blockNum, round;
+  uint32_t next_election, next_heartbeat;
+  /* Paxos (paxos-node.h:40-52) */
+  int32_t t_max, command, t_store, ticket, isCommit, proposal;
+  /* cancelled timer ids (ns-3 Simulator::Cancel) */
+  uint32_t* cancelled;
+  uint32_t n_cancelled, cap_cancelled;
+} onode;
+
+typedef struct {
+  oev* a;
+  size_t n, cap;
+} oheap;
+
+struct bcsim_oracle {
+  bcsim_config cfg;
+  uint32_t N;
+  /* topology (sender-major CSR) */
+  uint32_t *row, *col, *rev, *eid_of_pos;
+  int64_t* prop;
+  int topo_set;
+  /* per replica state */
+  uint32_t R;
+  uint32_t cur_rep;
+  onode* nodes;          /* N, for the replica being run */
+  int32_t *tx_val, *tx_pv, *tx_cv; /* N * seq_cap */
+  int64_t* busy;         /* per edge */
+  oheap heap;
+  glibc_rng grng;
+  int32_t g_v, g_n, g_nround; /* PBFT file-scope globals pbft-node.cc:24-30 */
+  /* precomputed times */
+  int64_t tx_tot[2], tx_last[2];
+  int64_t pbft_period, raft_hb, pbft_delay[3], raft_delay[3], raft_elec[150],
+      paxos_delay[50];
+  uint32_t small_bytes, big_bytes;
+  /* outputs */
+  bcsim_trace_rec* tr;
+  uint64_t ntr, cap_tr;
+  bcsim_counters cnt;
+  int64_t now;
+  int32_t err;
+  int started;
+  /* per-replica run bookkeeping (replicas run one after another) */
+  int64_t* rep_now;
+  int run_all_done;
+};
+
+/* canonical key compare */
+static int ev_less(const oev* x, const oev* y) {
+  if (x->t != y->t) return x->t < y->t;
+  if (x->ts != y->ts) return x->ts < y->ts;
+  if (x->origin != y->origin) return x->origin < y->origin;
+  if (x->sub != y->sub) return x->sub < y->sub;
+  return x->target < y->target;
+}
+
+static int heap_push(oheap* h, const oev* e) {
+  if (h->n == h->cap) {
+    size_t nc = h->cap ? h->cap * 2 : 1024;
+    oev* na = (oev*)realloc(h->a, nc * sizeof(oev));
+    if (!na) return BCSIM_E_NOMEM;
+    h->a = na;
+    h->cap = nc;
+  }
+  size_t i = h->n++;
+  while (i > 0) {
+    size_t p = (i - 1) / 2;
+    if (!ev_less(e, &h->a[p])) break;
+    h->a[i] = h->a[p];
+    i = p;
+  }
+  h->a[i] = *e;
+  return BCSIM_OK;
+}
+
+static void heap_pop(oheap* h, oev* out) {
+  *out = h->a[0];
+  oev last = h->a[--h->n];
+  size_t i = 0, n = h->n;
+  for (;;) {
+    size_t l = 2 * i + 1, r = l + 1, m = i;
+    const oev* best = &last;
+    if (l < n && ev_less(&h->a[l], best)) {
+      m = l;
+      best = &h->a[l];
+    }
+    if (r < n && ev_less(&h->a[r], best)) m = r;
+    if (m == i) break;
+    h->a[i] = h->a[m];
+    i = m;
+  }
+  if (n) h->a[i] = last;
+}
+
+/* ------------------------------------------------------------------------ */
+/* helpers */
+static int32_t enc(const bcsim_oracle* o, int32_t a) { /* intToChar */
+  int32_t c = a + '0';
+  if (o->cfg.encoding == BCSIM_ENC_COMPAT) c = (int32_t)(int8_t)(uint8_t)c;
+  return c;
+}
+static int32_t dec(int32_t c) { return c - '0'; } /* charToInt */
+static int32_t as_char(const bcsim_oracle* o, int32_t c) { /* char member */
+  if (o->cfg.encoding == BCSIM_ENC_COMPAT) c = (int32_t)(int8_t)(uint8_t)c;
+  return c;
+}
+/* msg[i] after getPacketContent's NUL truncation (pbft-node.cc:305-320) */
+static int32_t mchar(const omsg* m, int i) {
+  if (i == 0) return m->type + '0';
+  for (int k = 0; k < i - 1; ++k)
+    if (m->f[k] == 0) return 0;
+  return m->f[i - 1];
+}
+
+static void set_err(bcsim_oracle* o, int32_t e) {
+  if (!o->err) o->err = e;
+}
+
+static int32_t draw(bcsim_oracle* o, uint32_t node) {
+  onode* nd = &o->nodes[node];
+  if (o->cfg.rng_mode == BCSIM_RNG_GLIBC) return glibc_next(&o->grng);
+  return (int32_t)oracle_ctr_rand(o->cfg.seed, o->cur_rep, node, nd->draws++);
+}
+
+static void emit(bcsim_oracle* o, const oev* e, uint32_t node, uint32_t kind,
+                 int32_t a, int32_t b, int32_t c) {
+  if (o->ntr == o->cap_tr) {
+    uint64_t nc = o->cap_tr ? o->cap_tr * 2 : 4096;
+    bcsim_trace_rec* nt =
+        (bcsim_trace_rec*)realloc(o->tr, nc * sizeof(bcsim_trace_rec));
+    if (!nt) {
+      set_err(o, BCSIM_E_NOMEM);
+      return;
+    }
+    o->tr = nt;
+    o->cap_tr = nc;
+  }
+  bcsim_trace_rec* r = &o->tr[o->ntr++];
+  r->t_ns = e->t;
+  r->key_ts = e->ts;
+  r->key_origin = e->origin;
+  r->key_sub = e->sub;
+  r->replica = o->cur_rep;
+  r->node = node;
+  r->kind = kind;
+  r->a = a;
+  r->b = b;
+  r->c = c;
+}
+
+static uint32_t sched_timer(bcsim_oracle* o, uint32_t node, uint32_t tk,
+                            int64_t delay) {
+  onode* nd = &o->nodes[node];
+  oev e;
+  memset(&e, 0, sizeof e);
+  e.t = o->now + delay;
+  e.ts = o->now;
+  e.origin = node;
+  e.sub = nd->sub++;
+  e.target = node;
+  e.kind = EV_TIMER;
+  e.aux = tk;
+  int rc = heap_push(&o->heap, &e);
+  if (rc) set_err(o, rc);
+  return e.sub;
+}
+
+static void cancel_timer(bcsim_oracle* o, uint32_t node, uint32_t id) {
+  onode* nd = &o->nodes[node];
+  if (id == 0) return;
+  if (nd->n_cancelled == nd->cap_cancelled) {
+    uint32_t nc = nd->cap_cancelled ? nd->cap_cancelled * 2 : 8;
+    uint32_t* na = (uint32_t*)realloc(nd->cancelled, nc * sizeof(uint32_t));
+    if (!na) {
+      set_err(o, BCSIM_E_NOMEM);
+      return;
+    }
+    nd->cancelled = na;
+    nd->cap_cancelled = nc;
+  }
+  nd->cancelled[nd->n_cancelled++] = id;
+}
+
+static int take_cancelled(onode* nd, uint32_t id) {
+  for (uint32_t i = 0; i < nd->n_cancelled; ++i)
+    if (nd->cancelled[i] == id) {
+      nd->cancelled[i] = nd->cancelled[--nd->n_cancelled];
+      return 1;
+    }
+  return 0;
+}
+
+/* Simulator::Schedule(Seconds(delay), SendPacket, sock, p) */
+static void sched_send(bcsim_oracle* o, uint32_t node, uint32_t edge,
+                       int64_t delay, const omsg* m) {
+  onode* nd = &o->nodes[node];
+  oev e;
+  memset(&e, 0, sizeof e);
+  e.t = o->now + delay;
+  e.ts = o->now;
+  e.origin = node;
+  e.sub = nd->sub++;
+  e.target = node;
+  e.kind = EV_SEND;
+  e.aux = edge;
+  e.m = *m;
+  int rc = heap_push(&o->heap, &e);
+  if (rc) set_err(o, rc);
+}
+
+static int64_t app_delay(bcsim_oracle* o, uint32_t node) {
+  if (o->cfg.delay_mode == BCSIM_DELAY_FIXED) return o->cfg.app_delay_ns;
+  int32_t r = draw(o, node);
+  switch (o->cfg.protocol) {
+    case BCSIM_PBFT:
+      return o->pbft_delay[r % 3];
+    case BCSIM_RAFT:
+      return o->raft_delay[r % 3];
+    default:
+      return o->paxos_delay[r % 50];
+  }
+}
+
+/* broadcast Send(uint8_t[]): pbft-node.cc:349-368, raft-node.cc:370-388 */
+static void bcast(bcsim_oracle* o, uint32_t node, const omsg* m) {
+  for (uint32_t p = o->row[node]; p < o->row[node + 1]; ++p) {
+    int64_t d = app_delay(o, node);
+    sched_send(o, node, p, d, m);
+  }
+}
+/* Paxos broadcast paxos-node.cc:450-505: iterator advanced before use, so
+ * peers[1..deg-1] are reached and the last iteration targets *end()
+ * (dropped); every iteration draws a delay and schedules a SendPacket.     */
+static void bcast_paxos(bcsim_oracle* o, uint32_t node, const omsg* m) {
+  uint32_t b = o->row[node], e = o->row[node + 1];
+  for (uint32_t p = b; p < e; ++p) {
+    int64_t d = app_delay(o, node);
+    uint32_t edge = (p + 1 < e) ? p + 1 : UINT32_MAX;
+    sched_send(o, node, edge, d, m);
+  }
+}
+/* unicast Send(data, from): pbft-node.cc:328-346 */
+static void unicast(bcsim_oracle* o, uint32_t node, uint32_t in_edge,
+                    const omsg* m) {
+  int64_t d = app_delay(o, node);
+  sched_send(o, node, o->rev[in_edge], d, m);
+}
+
+static omsg mk(int32_t type, int32_t f0, int32_t f1, int32_t f2, int32_t big) {
+  omsg m;
+  m.type = type;
+  m.f[0] = f0;
+  m.f[1] = f1;
+  m.f[2] = f2;
+  m.big = big;
+  return m;
+}
+
+/* link FIFO: returns arrival, sets *ts_last */
+static int64_t link_xmit(bcsim_oracle* o, uint32_t edge, int big,
+                         int64_t* ts_last) {
+  int64_t start = o->busy[edge] > o->now ? o->busy[edge] : o->now;
+  int64_t end = start + o->tx_tot[big];
+  o->busy[edge] = end;
+  *ts_last = end - o->tx_last[big];
+  return end + o->prop[edge];
+}
+
+/* ------------------------------------------------------------------------ */
+/* PBFT (pbft/pbft-node.cc) */
+enum {
+  P_PRE_PREPARE = 1, P_PREPARE = 2, P_COMMIT = 3, P_PREPARE_RES = 5,
+  P_COMMIT_RES = 6, P_VIEW_CHANGE = 8
+};
+
+static void pbft_start(bcsim_oracle* o, uint32_t i) { /* :97-158 */
+  onode* nd = &o->nodes[i];
+  o->g_v = 1;
+  o->g_n = 0;
+  nd->leader = 0;
+  nd->block_num = 0;
+  o->g_nround = 0;
+  sched_timer(o, i, TM_PBFT_BLOCK, o->pbft_period); /* :155 */
+}
+
+static int pbft_idx_ok(bcsim_oracle* o, int32_t idx) {
+  if (idx < 0) {
+    set_err(o, BCSIM_E_ENCODING);
+    return 0;
+  }
+  if ((uint32_t)idx >= o->cfg.pbft_seq_cap) {
+    set_err(o, BCSIM_E_INDEX);
+    return 0;
+  }
+  return 1;
+}
+
+static void pbft_view_change(bcsim_oracle* o, uint32_t i) { /* :293-303 */
+  onode* nd = &o->nodes[i];
+  nd->leader = (nd->leader + 1) % (int32_t)o->N;
+  o->g_v += 1;
+  omsg m = mk(P_VIEW_CHANGE, enc(o, o->g_v), enc(o, nd->leader), 0, 0);
+  bcast(o, i, &m);
+}
+
+static void pbft_send_block(bcsim_oracle* o, const oev* e, uint32_t i) {
+  onode* nd = &o->nodes[i]; /* :371-411 */
+  /* generateTX(num): header '1', v, n, n (:79-95) */
+  omsg blk = mk(P_PRE_PREPARE, enc(o, o->g_v), enc(o, o->g_n), enc(o, o->g_n), 1);
+  if ((int32_t)i == nd->leader) {
+    emit(o, e, i, BCSIM_TR_PBFT_BLOCK, o->g_n, o->g_v, 0); /* :387 */
+    bcast(o, i, &blk);                                      /* :389-396 */
+    o->g_nround++;
+    o->g_n++;
+    if (o->cfg.pbft_view_change) {
+      int32_t r = draw(o, i); /* :401 */
+      if (r % 100 == 5) pbft_view_change(o, i);
+    }
+  }
+  nd->block_ev = sched_timer(o, i, TM_PBFT_BLOCK, o->pbft_period); /* :406 */
+  if (o->g_nround == (int32_t)o->cfg.pbft_rounds) {
+    emit(o, e, i, BCSIM_TR_PBFT_STOP, o->g_nround, 0, 0); /* :408 */
+    cancel_timer(o, i, nd->block_ev);
+  }
+}
+
+static void pbft_recv(bcsim_oracle* o, const oev* e, uint32_t i) {
+  onode* nd = &o->nodes[i]; /* HandleRead :166-291 */
+  const omsg* m = &e->m;
+  int32_t* tv = o->tx_val + (size_t)i * o->cfg.pbft_seq_cap;
+  int32_t* tp = o->tx_pv + (size_t)i * o->cfg.pbft_seq_cap;
+  int32_t* tc = o->tx_cv + (size_t)i * o->cfg.pbft_seq_cap;
+  switch (dec(mchar(m, 0))) {
+    case P_PRE_PREPARE: { /* :193-211 */
+      omsg r = mk(P_PREPARE, mchar(m, 1), mchar(m, 2), mchar(m, 3), 0);
+      int32_t num = dec(mchar(m, 2));
+      if (!pbft_idx_ok(o, num)) return;
+      tv[num] = dec(mchar(m, 3));
+      bcast(o, i, &r);
+      break;
+    }
+    case P_PREPARE: { /* :212-222 */
+      omsg r = mk(P_PREPARE_RES, mchar(m, 1), mchar(m, 2), enc(o, 0), 0);
+      unicast(o, i, e->aux, &r);
+      break;
+    }
+    case P_PREPARE_RES: { /* :223-240 */
+      int32_t idx = dec(mchar(m, 2));
+      if (!pbft_idx_ok(o, idx)) return;
+      if (dec(mchar(m, 3)) == 0) tp[idx]++;
+      if (tp[idx] >= (int32_t)o->N / 2) {
+        omsg r = mk(P_COMMIT, mchar(m, 1), mchar(m, 2), 0, 0);
+        bcast(o, i, &r);
+        tp[idx] = 0;
+      }
+      break;
+    }
+    case P_COMMIT: { /* :241-265 */
+      int32_t idx = dec(mchar(m, 2));
+      if (!pbft_idx_ok(o, idx)) return;
+      tc[idx]++;
+      if (tc[idx] > (int32_t)o->N / 2) {
+        tc[idx] = 0;
+        emit(o, e, i, BCSIM_TR_PBFT_COMMIT, o->g_v, nd->block_num, tv[idx]);
+        nd->block_num++;
+      }
+      break;
+    }
+    case P_VIEW_CHANGE: { /* :271-286, falls through to default */
+      int32_t vt = dec(mchar(m, 1));
+      int32_t lt = dec(mchar(m, 2));
+      o->g_v = vt;
+      nd->leader = lt;
+      if ((int32_t)i == nd->leader) emit(o, e, i, BCSIM_TR_PBFT_VIEW, o->g_v, lt, 0);
+      o->cnt.wrong_msgs++;
+      break;
+    }
+    default:
+      o->cnt.wrong_msgs++;
+      break;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Raft (raft/raft-node.cc) */
+enum { R_VOTE_REQ = 2, R_VOTE_RES = 3, R_HEARTBEAT = 4, R_HEARTBEAT_RES = 5 };
+
+static int64_t raft_election_timeout(bcsim_oracle* o, uint32_t i) { /* :69-72 */
+  int32_t r = draw(o, i);
+  return o->raft_elec[r % 150];
+}
+
+static void raft_start(bcsim_oracle* o, uint32_t i) { /* :75-115 */
+  onode* nd = &o->nodes[i];
+  nd->m_value = 0;
+  nd->vote_success = 0;
+  nd->vote_failed = 0;
+  nd->has_voted = 0;
+  nd->add_change_value = 0;
+  nd->is_leader = 0;
+  nd->round = 0;
+  nd->blockNum = 0;
+  int64_t to = raft_election_timeout(o, i);
+  nd->next_election = sched_timer(o, i, TM_RAFT_ELECTION, to); /* :114 */
+}
+
+static void raft_send_vote(bcsim_oracle* o, const oev* e, uint32_t i) {
+  onode* nd = &o->nodes[i]; /* :391-401 */
+  nd->has_voted = 1;
+  omsg m = mk(R_VOTE_REQ, enc(o, (int32_t)i), 0, 0, 0);
+  bcast(o, i, &m);
+  emit(o, e, i, BCSIM_TR_RAFT_ELECTION, 0, 0, 0);
+  int64_t to = raft_election_timeout(o, i);
+  nd->next_election = sched_timer(o, i, TM_RAFT_ELECTION, to);
+}
+
+static void raft_heartbeat(bcsim_oracle* o, const oev* e, uint32_t i) {
+  onode* nd = &o->nodes[i]; /* sendHeartBeat :404-429 */
+  nd->has_voted = 1;
+  if (nd->add_change_value == 1) {
+    nd->next_heartbeat = sched_timer(o, i, TM_RAFT_HEARTBEAT, o->raft_hb);
+    /* SendTX :340-366; generateTX: '4','1','1',... (:323-336) */
+    emit(o, e, i, BCSIM_TR_RAFT_PROPOSAL, nd->round, 0, 0);
+    omsg m = mk(R_HEARTBEAT, enc(o, 1), '1', '1', 1);
+    bcast(o, i, &m);
+    nd->round++;
+    if (nd->round == (int32_t)o->cfg.raft_proposal_rounds) nd->add_change_value = 0;
+  } else {
+    nd->next_heartbeat = sched_timer(o, i, TM_RAFT_HEARTBEAT, o->raft_hb);
+    omsg m = mk(R_HEARTBEAT, enc(o, 0), 0, 0, 0);
+    bcast(o, i, &m);
+  }
+}
+
+static void raft_recv(bcsim_oracle* o, const oev* e, uint32_t i) {
+  onode* nd = &o->nodes[i]; /* HandleRead :127-276 */
+  const omsg* m = &e->m;
+  int32_t N = (int32_t)o->N;
+  switch (dec(mchar(m, 0))) {
+    case R_VOTE_REQ: { /* :154-168 */
+      int32_t st;
+      if (nd->has_voted == 0) {
+        st = 0;
+        nd->has_voted = 1;
+      } else {
+        st = 1;
+      }
+      omsg r = mk(R_VOTE_RES, enc(o, st), 0, 0, 0);
+      unicast(o, i, e->aux, &r);
+      break;
+    }
+    case R_HEARTBEAT: { /* :170-194 */
+      int32_t type = dec(mchar(m, 1));
+      int32_t d1;
+      if (type == 0) {
+        d1 = enc(o, 0);
+        cancel_timer(o, i, nd->next_election);
+      } else {
+        d1 = enc(o, 1);
+        nd->m_value = dec(mchar(m, 2));
+        cancel_timer(o, i, nd->next_election);
+      }
+      omsg r = mk(R_HEARTBEAT_RES, d1, enc(o, 0), 0, 0);
+      unicast(o, i, e->aux, &r);
+      break;
+    }
+    case R_VOTE_RES: { /* :196-232 */
+      if (!nd->is_leader) {
+        int32_t st = dec(mchar(m, 1));
+        if (st == 0)
+          nd->vote_success += 1;
+        else
+          nd->vote_failed += 1;
+        if (nd->vote_success + 1 > N / 2) {
+          nd->vote_success = 0;
+          nd->vote_failed = 0;
+          emit(o, e, i, BCSIM_TR_RAFT_LEADER, 0, 0, 0);
+          cancel_timer(o, i, nd->next_election);
+          sched_timer(o, i, TM_RAFT_PROPOSAL, o->cfg.raft_proposal_delay_ns);
+          raft_heartbeat(o, e, i);
+          nd->is_leader = 1;
+        } else if (nd->vote_failed >= N / 2) {
+          nd->vote_success = 0;
+          nd->vote_failed = 0;
+          nd->has_voted = 0;
+        }
+      }
+      break;
+    }
+    case R_HEARTBEAT_RES: { /* :233-266 */
+      int32_t type = dec(mchar(m, 1));
+      if (type == 1) {
+        if (dec(mchar(m, 2)) == 0)
+          nd->vote_success += 1;
+        else
+          nd->vote_failed += 1;
+        if (nd->vote_success + nd->vote_failed == N - 1) {
+          if (nd->vote_success + 1 > N / 2) {
+            nd->vote_success = 0;
+            nd->vote_failed = 0;
+            emit(o, e, i, BCSIM_TR_RAFT_BLOCK, nd->blockNum, 0, 0);
+            nd->blockNum += 1;
+            if (nd->blockNum >= (int32_t)o->cfg.raft_blocks) {
+              emit(o, e, i, BCSIM_TR_RAFT_DONE, nd->blockNum, 0, 0);
+              cancel_timer(o, i, nd->next_heartbeat);
+            }
+          } else {
+            nd->vote_success = 0;
+            nd->vote_failed = 0;
+          }
+        }
+      }
+      break;
+    }
+    default:
+      o->cnt.wrong_msgs++;
+      break;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Paxos (paxos/paxos-node.cc) */
+enum {
+  X_REQ_TICKET = 0, X_REQ_PROPOSE = 1, X_REQ_COMMIT = 2, X_RES_TICKET = 3,
+  X_RES_PROPOSE = 4, X_RES_COMMIT = 5, X_CLIENT_PROPOSE = 6
+};
+
+static void paxos_require_ticket(bcsim_oracle* o, const oev* e, uint32_t i) {
+  onode* nd = &o->nodes[i]; /* :510-522 */
+  nd->ticket += 1;
+  omsg m = mk(X_REQ_TICKET, enc(o, nd->ticket), 0, 0, 0);
+  bcast_paxos(o, i, &m);
+  emit(o, e, i, BCSIM_TR_PAXOS_TICKET, nd->ticket, 0, 0);
+}
+
+static void paxos_start(bcsim_oracle* o, uint32_t i) { /* :58-139 */
+  onode* nd = &o->nodes[i];
+  nd->t_max = 0;
+  nd->command = 'e';
+  nd->t_store = 0;
+  nd->ticket = 0;
+  nd->isCommit = 0;
+  nd->proposal = as_char(o, (int32_t)i + '0');
+  nd->vote_success = 0;
+  nd->vote_failed = 0;
+  nd->round = 0;
+  if (i < o->cfg.paxos_proposers) sched_timer(o, i, TM_PAXOS_TICKET, 0);
+}
+
+static void paxos_recv(bcsim_oracle* o, const oev* e, uint32_t i) {
+  onode* nd = &o->nodes[i]; /* HandleRead :148-372 */
+  const omsg* m = &e->m;
+  int32_t N = (int32_t)o->N;
+  switch (dec(mchar(m, 0))) {
+    case X_REQ_TICKET: { /* :177-198 */
+      int32_t t = dec(mchar(m, 1));
+      omsg r;
+      if (t > nd->t_max) {
+        nd->t_max = t;
+        r = mk(X_RES_TICKET, enc(o, 0), nd->command, 0, 0);
+      } else {
+        r = mk(X_RES_TICKET, enc(o, 1), 0, 0, 0);
+      }
+      unicast(o, i, e->aux, &r);
+      break;
+    }
+    case X_REQ_PROPOSE: { /* :199-221 */
+      int32_t t = dec(mchar(m, 1));
+      int32_t st;
+      if (t == nd->t_max) {
+        nd->command = mchar(m, 2);
+        nd->t_store = t;
+        st = 0;
+      } else {
+        st = 1;
+      }
+      omsg r = mk(X_RES_PROPOSE, enc(o, st), 0, 0, 0);
+      unicast(o, i, e->aux, &r);
+      break;
+    }
+    case X_REQ_COMMIT: { /* :222-247 */
+      int32_t t = dec(mchar(m, 1));
+      int32_t c = mchar(m, 2);
+      int32_t st;
+      if (t == nd->t_store && c == nd->command) {
+        nd->isCommit = 1;
+        st = 0;
+      } else {
+        st = 1;
+      }
+      omsg r = mk(X_RES_COMMIT, enc(o, st), 0, 0, 0);
+      unicast(o, i, e->aux, &r);
+      break;
+    }
+    case X_RES_TICKET:
+    case X_RES_PROPOSE:
+    case X_RES_COMMIT: { /* :248-353 */
+      int32_t ty = dec(mchar(m, 0));
+      int32_t st = dec(mchar(m, 1));
+      if (st == 0)
+        nd->vote_success += 1;
+      else
+        nd->vote_failed += 1;
+      if (nd->vote_success + nd->vote_failed == N - 2) {
+        if (nd->vote_success >= N / 2) {
+          nd->vote_success = 0;
+          nd->vote_failed = 0;
+          if (ty == X_RES_TICKET) {
+            if (mchar(m, 2) != 'e') nd->proposal = mchar(m, 2);
+            omsg r = mk(X_REQ_PROPOSE, enc(o, nd->ticket), nd->proposal, 0, 0);
+            bcast_paxos(o, i, &r);
+          } else if (ty == X_RES_PROPOSE) {
+            omsg r = mk(X_REQ_COMMIT, enc(o, nd->ticket), nd->proposal, 0, 0);
+            bcast_paxos(o, i, &r);
+          } else {
+            emit(o, e, i, BCSIM_TR_PAXOS_COMMIT, nd->ticket, 0, 0);
+          }
+        } else {
+          nd->vote_success = 0;
+          nd->vote_failed = 0;
+          paxos_require_ticket(o, e, i);
+        }
+      }
+      break;
+    }
+    case X_CLIENT_PROPOSE: /* :357-361 */
+      paxos_require_ticket(o, e, i);
+      break;
+    default:
+      o->cnt.wrong_msgs++;
+      break;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* driver */
+static void exec_event(bcsim_oracle* o, const oev* e) {
+  uint32_t i = e->target;
+  onode* nd = &o->nodes[i];
+  switch (e->kind) {
+    case EV_START:
+      o->cnt.events++;
+      if (o->cfg.protocol == BCSIM_PBFT)
+        pbft_start(o, i);
+      else if (o->cfg.protocol == BCSIM_RAFT)
+        raft_start(o, i);
+      else
+        paxos_start(o, i);
+      break;
+    case EV_STOP: /* Application::StopApplication */
+      o->cnt.events++;
+      if (o->cfg.protocol == BCSIM_RAFT && nd->is_leader == 1)
+        emit(o, e, i, BCSIM_TR_RAFT_STOP, nd->blockNum, nd->round, 0);
+      break;
+    case EV_TIMER:
+      if (take_cancelled(nd, e->sub)) break;
+      o->cnt.events++;
+      switch (e->aux) {
+        case TM_PBFT_BLOCK:
+          pbft_send_block(o, e, i);
+          break;
+        case TM_RAFT_ELECTION:
+          raft_send_vote(o, e, i);
+          break;
+        case TM_RAFT_HEARTBEAT:
+          raft_heartbeat(o, e, i);
+          break;
+        case TM_RAFT_PROPOSAL: /* setProposal :432-435 */
+          nd->add_change_value = 1;
+          break;
+        case TM_PAXOS_TICKET:
+          paxos_require_ticket(o, e, i);
+          break;
+      }
+      break;
+    case EV_SEND: { /* SendPacket :323-325 -> socket->Send -> p2p device */
+      o->cnt.sends++;
+      if (e->aux == UINT32_MAX) {
+        o->cnt.dropped++;
+        break;
+      }
+      oev r;
+      memset(&r, 0, sizeof r);
+      int64_t tsl;
+      r.t = link_xmit(o, e->aux, e->m.big, &tsl);
+      r.ts = tsl;
+      r.origin = i;
+      r.sub = e->sub;
+      r.target = o->col[e->aux];
+      r.kind = EV_RECV;
+      r.aux = e->aux;
+      r.m = e->m;
+      int rc = heap_push(&o->heap, &r);
+      if (rc) set_err(o, rc);
+      break;
+    }
+    case EV_RECV: {
+      o->cnt.events++;
+      int ty = e->m.type;
+      if (ty >= 0 && ty < BCSIM_MSG_TYPES) o->cnt.delivered[ty]++;
+      o->cnt.delivered_total++;
+      if (o->cfg.echo) { /* socket->SendTo(packet, 0, from) :175 */
+        int64_t tsl;
+        (void)link_xmit(o, o->rev[e->aux], e->m.big, &tsl);
+        o->cnt.echoes++;
+      }
+      if (o->cfg.protocol == BCSIM_PBFT)
+        pbft_recv(o, e, i);
+      else if (o->cfg.protocol == BCSIM_RAFT)
+        raft_recv(o, e, i);
+      else
+        paxos_recv(o, e, i);
+      break;
+    }
+  }
+}
+
+static int build_full_mesh(bcsim_oracle* o) {
+  uint32_t N = o->N;
+  uint64_t E = (uint64_t)N * (N - 1);
+  uint32_t* row = (uint32_t*)malloc((N + 1) * sizeof(uint32_t));
+  uint32_t* col = (uint32_t*)malloc((E ? E : 1) * sizeof(uint32_t));
+  if (!row || !col) {
+    free(row);
+    free(col);
+    return BCSIM_E_NOMEM;
+  }
+  uint64_t k = 0;
+  for (uint32_t i = 0; i < N; ++i) { /* blockchain-simulator.cc:34-51 order */
+    row[i] = (uint32_t)k;
+    for (uint32_t j = 0; j < N; ++j)
+      if (j != i) col[k++] = j;
+  }
+  row[N] = (uint32_t)k;
+  int rc = bcsim_oracle_set_topology_csr(o, N, row, col, NULL);
+  free(row);
+  free(col);
+  return rc;
+}
+
+typedef struct {
+  uint32_t a, b, e;
+} etrip;
+static int etrip_cmp(const void* x, const void* y) {
+  const etrip* p = (const etrip*)x;
+  const etrip* q = (const etrip*)y;
+  if (p->a != q->a) return p->a < q->a ? -1 : 1;
+  if (p->b != q->b) return p->b < q->b ? -1 : 1;
+  return 0;
+}
+
+int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
+                                  const uint32_t* row_ptr,
+                                  const uint32_t* col_idx,
+                                  const int64_t* prop_ns) {
+  if (!o || n != o->N || !row_ptr || !col_idx) return BCSIM_E_INVAL;
+  if (o->started) return BCSIM_E_STATE;
+  uint32_t E = row_ptr[n];
+  free(o->row);
+  free(o->col);
+  free(o->rev);
+  free(o->prop);
+  free(o->busy);
+  o->row = (uint32_t*)malloc((n + 1) * sizeof(uint32_t));
+  o->col = (uint32_t*)malloc((E ? E : 1) * sizeof(uint32_t));
+  o->rev = (uint32_t*)malloc((E ? E : 1) * sizeof(uint32_t));
+  o->prop = (int64_t*)malloc((E ? E : 1) * sizeof(int64_t));
+  o->busy = (int64_t*)calloc(E ? E : 1, sizeof(int64_t));
+  if (!o->row || !o->col || !o->rev || !o->prop || !o->busy) return BCSIM_E_NOMEM;
+  memcpy(o->row, row_ptr, (n + 1) * sizeof(uint32_t));
+  memcpy(o->col, col_idx, E * sizeof(uint32_t));
+  for (uint32_t e = 0; e < E; ++e)
+    o->prop[e] = prop_ns ? prop_ns[e] : o->cfg.link_delay_ns;
+  /* reverse edge map: (s,d) -> edge of (d,s) */
+  etrip* t = (etrip*)malloc((E ? E : 1) * sizeof(etrip));
+  if (!t) return BCSIM_E_NOMEM;
+  for (uint32_t s = 0; s < n; ++s)
+    for (uint32_t e = row_ptr[s]; e < row_ptr[s + 1]; ++e) {
+      if (col_idx[e] >= n) {
+        free(t);
+        return BCSIM_E_INVAL;
+      }
+      t[e].a = s;
+      t[e].b = col_idx[e];
+      t[e].e = e;
+    }
+  qsort(t, E, sizeof(etrip), etrip_cmp);
+  for (uint32_t s = 0; s < n; ++s)
+    for (uint32_t e = row_ptr[s]; e < row_ptr[s + 1]; ++e) {
+      etrip key = {col_idx[e], s, 0};
+      etrip* hit = (etrip*)bsearch(&key, t, E, sizeof(etrip), etrip_cmp);
+      if (!hit) {
+        free(t);
+        return BCSIM_E_INVAL; /* asymmetric graph */
+      }
+      o->rev[e] = hit->e;
+    }
+  free(t);
+  o->topo_set = 1;
+  return BCSIM_OK;
+}
+
+int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
+  if (!cfg || !out) return BCSIM_E_INVAL;
+  if (cfg->n_nodes < 2 || cfg->protocol > BCSIM_PAXOS || cfg->link_rate_bps == 0)
+    return BCSIM_E_INVAL;
+  bcsim_oracle* o = (bcsim_oracle*)calloc(1, sizeof(bcsim_oracle));
+  if (!o) return BCSIM_E_NOMEM;
+  o->cfg = *cfg;
+  if (o->cfg.n_replicas == 0) o->cfg.n_replicas = 1;
+  if (o->cfg.mtu == 0) o->cfg.mtu = 1500;
+  if (o->cfg.pbft_seq_cap == 0) o->cfg.pbft_seq_cap = 1000;
+  o->N = cfg->n_nodes;
+  o->R = o->cfg.n_replicas;
+  int mode = (int)o->cfg.time_round;
+  /* message sizes */
+  if (o->cfg.protocol == BCSIM_PBFT) {
+    o->small_bytes = 4; /* Create<Packet>(data, 4) pbft-node.cc:332,354 */
+    uint32_t bb = o->cfg.pbft_block_bytes;
+    if (bb == 0) { /* num = tx_speed / (1000 / (timeout*1000)) :377 */
+      float tmo = o->cfg.pbft_timeout_s;
+      int num = (int)(1000 / (1000 / (tmo * 1000)));
+      bb = (uint32_t)(1000 * num);
+    }
+    o->big_bytes = bb;
+  } else if (o->cfg.protocol == BCSIM_RAFT) {
+    o->small_bytes = 3;
+    uint32_t pb = o->cfg.raft_proposal_bytes;
+    if (pb == 0) { /* raft-node.cc:409, tx_size 200, tx_speed 2000 */
+      float hb = o->cfg.raft_heartbeat_s;
+      int num = (int)(2000 / (1000 / (hb * 1000)));
+      pb = (uint32_t)(200 * num);
+    }
+    o->big_bytes = pb;
+  } else {
+    o->small_bytes = 3;
+    o->big_bytes = 3;
+  }
+  oracle_msg_tx(o->small_bytes, o->cfg.mtu, o->cfg.link_rate_bps, mode,
+                &o->tx_tot[0], &o->tx_last[0], NULL, NULL);
+  oracle_msg_tx(o->big_bytes, o->cfg.mtu, o->cfg.link_rate_bps, mode,
+                &o->tx_tot[1], &o->tx_last[1], NULL, NULL);
+  o->pbft_period = fsec_ns(o->cfg.pbft_timeout_s, mode);
+  o->raft_hb = fsec_ns(o->cfg.raft_heartbeat_s, mode);
+  for (int k = 0; k < 3; ++k) {
+    o->pbft_delay[k] = fsec_ns((float)(((k)*1.0 + 3) / 1000), mode);
+    o->raft_delay[k] = fsec_ns((float)((k)*1.0 / 1000), mode);
+  }
+  for (int k = 0; k < 150; ++k)
+    o->raft_elec[k] = fsec_ns((float)(((k) + 150) * 1.0 / 1000), mode);
+  for (int k = 0; k < 50; ++k) o->paxos_delay[k] = fsec_ns((float)((k)*1.0 / 1000), mode);
+  o->nodes = (onode*)calloc(o->N, sizeof(onode));
+  if (!o->nodes) {
+    bcsim_oracle_destroy(o);
+    return BCSIM_E_NOMEM;
+  }
+  if (o->cfg.protocol == BCSIM_PBFT) {
+    size_t sz = (size_t)o->N * o->cfg.pbft_seq_cap;
+    o->tx_val = (int32_t*)calloc(sz, sizeof(int32_t));
+    o->tx_pv = (int32_t*)calloc(sz, sizeof(int32_t));
+    o->tx_cv = (int32_t*)calloc(sz, sizeof(int32_t));
+    if (!o->tx_val || !o->tx_pv || !o->tx_cv) {
+      bcsim_oracle_destroy(o);
+      return BCSIM_E_NOMEM;
+    }
+  }
+  o->rep_now = (int64_t*)calloc(o->R, sizeof(int64_t));
+  int rc = build_full_mesh(o);
+  if (rc) {
+    bcsim_oracle_destroy(o);
+    return rc;
+  }
+  *out = o;
+  return BCSIM_OK;
+}
+
+static void reset_replica(bcsim_oracle* o, uint32_t rep) {
+  o->cur_rep = rep;
+  for (uint32_t i = 0; i < o->N; ++i) {
+    free(o->nodes[i].cancelled);
+    memset(&o->nodes[i], 0, sizeof(onode));
+    o->nodes[i].sub = 2; /* 0 = START, 1 = STOP */
+  }
+  if (o->tx_val) {
+    size_t sz = (size_t)o->N * o->cfg.pbft_seq_cap * sizeof(int32_t);
+    memset(o->tx_val, 0, sz);
+    memset(o->tx_pv, 0, sz);
+    memset(o->tx_cv, 0, sz);
+  }
+  memset(o->busy, 0, (size_t)o->row[o->N] * sizeof(int64_t));
+  o->heap.n = 0;
+  glibc_seed(&o->grng, (uint32_t)(o->cfg.seed + rep));
+  o->g_v = 1;
+  o->g_n = 0;
+  o->g_nround = 0;
+  /* ApplicationContainer Start(0) / Stop(stop_ns), scheduled at init in
+   * node order (blockchain-simulator.cc:54-55) */
+  for (uint32_t i = 0; i < o->N; ++i) {
+    oev e;
+    memset(&e, 0, sizeof e);
+    e.t = 0;
+    e.ts = -1;
+    e.origin = i;
+    e.sub = 0;
+    e.target = i;
+    e.kind = EV_START;
+    heap_push(&o->heap, &e);
+    if (o->cfg.stop_ns >= 0) {
+      e.t = o->cfg.stop_ns;
+      e.sub = 1;
+      e.kind = EV_STOP;
+      heap_push(&o->heap, &e);
+    }
+  }
+}
+
+/* Replicas are independent; the oracle runs them one after another.  For
+ * R > 1 only t_until = INT64_MAX (run to the end) is supported. */
+int bcsim_oracle_run(bcsim_oracle* o, int64_t t_until_ns) {
+  if (!o) return BCSIM_E_INVAL;
+  if (o->err) return o->err;
+  if (o->R > 1 && t_until_ns != INT64_MAX) return BCSIM_E_UNSUPPORTED;
+  int64_t lim = t_until_ns;
+  if (o->cfg.t_end_ns > 0 && o->cfg.t_end_ns < lim) lim = o->cfg.t_end_ns;
+  if (!o->started) {
+    o->started = 1;
+    reset_replica(o, 0);
+  }
+  for (;;) {
+    while (o->heap.n > 0 && o->heap.a[0].t < lim) {
+      if (o->cfg.max_events && o->cnt.events >= o->cfg.max_events) {
+        set_err(o, BCSIM_E_OVERFLOW);
+        return o->err;
+      }
+      oev e;
+      heap_pop(&o->heap, &e);
+      o->now = e.t;
+      if (e.t > o->cnt.t_last_ns) o->cnt.t_last_ns = e.t;
+      exec_event(o, &e);
+      if (o->err) return o->err;
+    }
+    if (o->R > 1 && o->cur_rep + 1 < o->R) {
+      reset_replica(o, o->cur_rep + 1);
+      continue;
+    }
+    break;
+  }
+  o->now = lim;
+  return BCSIM_OK;
+}
+
+static int trace_cmp(const void* x, const void* y) {
+  const bcsim_trace_rec* p = (const bcsim_trace_rec*)x;
+  const bcsim_trace_rec* q = (const bcsim_trace_rec*)y;
+#define C(f)                                 \
+  if (p->f != q->f) return p->f < q->f ? -1 : 1;
+  C(replica) C(t_ns) C(key_ts) C(key_origin) C(key_sub) C(node) C(kind)
+#undef C
+  return 0;
+}
+
+int bcsim_oracle_read_trace(bcsim_oracle* o, bcsim_trace_rec* buf, uint64_t cap,
+                            uint64_t* n_out) {
+  if (!o || !n_out) return BCSIM_E_INVAL;
+  /* emission order within an event is ascending kind,
+   * so a full sort is canonical */
+  qsort(o->tr, o->ntr, sizeof(bcsim_trace_rec), trace_cmp);
+  *n_out = o->ntr;
+  if (buf) {
+    uint64_t k = o->ntr < cap ? o->ntr : cap;
+    memcpy(buf, o->tr, k * sizeof(bcsim_trace_rec));
+  }
+  return BCSIM_OK;
+}
+
+int bcsim_oracle_read_counters(bcsim_oracle* o, bcsim_counters* out) {
+  if (!o || !out) return BCSIM_E_INVAL;
+  *out = o->cnt;
+  out->trace_records = o->ntr;
+  return BCSIM_OK;
+}
+
+int bcsim_oracle_read_status(bcsim_oracle* o, bcsim_status* out) {
+  if (!o || !out) return BCSIM_E_INVAL;
+  memset(out, 0, sizeof *out);
+  out->now_ns = o->now;
+  out->next_ns = o->heap.n ? o->heap.a[0].t : INT64_MAX;
+  out->quiescent = o->heap.n == 0;
+  out->error = o->err;
+  return BCSIM_OK;
+}
+
+int bcsim_oracle_destroy(bcsim_oracle* o) {
+  if (!o) return BCSIM_OK;
+  if (o->nodes)
+    for (uint32_t i = 0; i < o->N; ++i) free(o->nodes[i].cancelled);
+  free(o->nodes);
+  free(o->tx_val);
+  free(o->tx_pv);
+  free(o->tx_cv);
+  free(o->row);
+  free(o->col);
+  free(o->rev);
+  free(o->prop);
+  free(o->busy);
+  free(o->heap.a);
+  free(o->tr);
+  free(o->rep_now);
+  free(o);
+  return BCSIM_OK;
+}
