@@ -1,0 +1,892 @@
+// bcsim_capi.hip — host orchestration of the windowed engine + the C ABI
+// declared in include/bcsim.h.  One translation unit with the kernels.
+#include "engine.hip"
+
+#include <cstdlib>
+
+namespace bcsim {
+
+static thread_local std::string g_detail;
+
+#define HIPCHK(x)                                                                      \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      g_detail = std::string(#x) + ": " + hipGetErrorString(e_);                       \
+      return BCSIM_E_HIP;                                                              \
+    }                                                                                  \
+  } while (0)
+
+static uint32_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return static_cast<uint32_t>(p);
+}
+
+// control block read back once per cell
+struct Ctl {
+  int32_t err;
+  uint32_t trace_cnt, vlog_cnt, dreq_cnt, ov_cnt;
+  int32_t dbg;
+  long long scal[4];  // next_local, ov_min_cell, n_alive_ticks, spare
+};
+
+struct Sim {
+  bcsim_config cfg{};
+  uint32_t N = 0, R = 0, NT = 0, E = 0, deg_max = 0, B = 0;
+  std::vector<uint32_t> row, col, rev;
+  std::vector<int64_t> prop;
+  bool started = false;
+  int32_t err = 0;
+  int64_t L = 0;
+  int64_t t_done = 0;
+  long long grouped_cell = -1;
+  int64_t next_tick = INT64_MAX;  // PBFT
+  bool start_pending = true;
+  hipStream_t stream = nullptr;
+  KP kp{};
+  std::vector<void*> allocs;
+  // host mirrors
+  Ctl* ctl_h = nullptr;  // pinned
+  uint32_t* bcnt_h = nullptr;
+  void* ctl_d = nullptr;
+  std::vector<uint32_t> bcnt;  // bucket counts (host view)
+  long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
+  long long n_alive = 0;
+  uint64_t cells = 0;
+  // timing
+  double us[4] = {0, 0, 0, 0};
+  uint64_t launches[4] = {0, 0, 0, 0};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  std::vector<int> ev_class;
+  size_t ev_used = 0;
+  // trace cache
+  std::vector<bcsim_trace_rec> trace;
+  bool trace_valid = false;
+  int dev = 0;
+};
+
+template <typename T>
+static int dalloc(Sim& s, T** p, size_t count) {
+  if (count == 0) count = 1;
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, count * sizeof(T));
+  if (e != hipSuccess) {
+    g_detail = std::string("hipMalloc ") + std::to_string(count * sizeof(T)) + " bytes: " +
+               hipGetErrorString(e);
+    return BCSIM_E_NOMEM;
+  }
+  s.allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return BCSIM_OK;
+}
+
+static int ev_begin(Sim& s, int cls) {
+  if (s.ev_used == s.ev_pool.size()) {
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    s.ev_pool.push_back({a, b});
+    s.ev_class.push_back(cls);
+  }
+  s.ev_class[s.ev_used] = cls;
+  HIPCHK(hipEventRecord(s.ev_pool[s.ev_used].first, s.stream));
+  return BCSIM_OK;
+}
+static int ev_end(Sim& s) {
+  HIPCHK(hipEventRecord(s.ev_pool[s.ev_used].second, s.stream));
+  s.launches[s.ev_class[s.ev_used]]++;
+  ++s.ev_used;
+  return BCSIM_OK;
+}
+static int ev_collect(Sim& s) {
+  for (size_t k = 0; k < s.ev_used; ++k) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, s.ev_pool[k].first, s.ev_pool[k].second));
+    s.us[s.ev_class[k]] += 1000.0 * ms;
+  }
+  s.ev_used = 0;
+  return BCSIM_OK;
+}
+
+static int validate(const bcsim_config& c) {
+  if (c.abi_version != BCSIM_ABI_VERSION) return BCSIM_E_INVAL;
+  if (c.protocol > BCSIM_PAXOS || c.n_nodes < 2 || c.link_rate_bps == 0) return BCSIM_E_INVAL;
+  if (c.mtu < 68) return BCSIM_E_INVAL;
+  if (c.delay_mode == BCSIM_DELAY_RANDOM && c.rng_mode == BCSIM_RNG_GLIBC) {
+    // the global glibc stream is consumed at every send in event order; only
+    // the oracle replays that serially
+    return BCSIM_E_UNSUPPORTED;
+  }
+  return BCSIM_OK;
+}
+
+static int build_mesh(Sim& s) {
+  s.row.assign(s.N + 1, 0);
+  s.col.clear();
+  s.col.reserve(static_cast<size_t>(s.N) * (s.N - 1));
+  for (uint32_t i = 0; i < s.N; ++i) {  // blockchain-simulator.cc:34-51 peer order
+    s.row[i] = static_cast<uint32_t>(s.col.size());
+    for (uint32_t j = 0; j < s.N; ++j)
+      if (j != i) s.col.push_back(j);
+  }
+  s.row[s.N] = static_cast<uint32_t>(s.col.size());
+  s.prop.assign(s.col.size(), s.cfg.link_delay_ns);
+  return BCSIM_OK;
+}
+
+static int build_rev(Sim& s) {
+  const uint32_t E = s.row[s.N];
+  s.rev.assign(E, kInvalid);
+  std::vector<uint64_t> keys(E);
+  std::vector<uint32_t> idx(E);
+  for (uint32_t a = 0; a < s.N; ++a)
+    for (uint32_t e = s.row[a]; e < s.row[a + 1]; ++e) {
+      if (s.col[e] >= s.N || s.col[e] == a) return BCSIM_E_INVAL;
+      keys[e] = (static_cast<uint64_t>(a) << 32) | s.col[e];
+      idx[e] = e;
+    }
+  std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return keys[x] < keys[y]; });
+  for (uint32_t k = 1; k < E; ++k)
+    if (keys[idx[k]] == keys[idx[k - 1]]) return BCSIM_E_INVAL;  // duplicate edge
+  for (uint32_t e = 0; e < E; ++e) {
+    const uint64_t want = (static_cast<uint64_t>(keys[e] & 0xFFFFFFFFu) << 32) | (keys[e] >> 32);
+    auto it = std::lower_bound(idx.begin(), idx.end(), want,
+                               [&](uint32_t x, uint64_t v) { return keys[x] < v; });
+    if (it == idx.end() || keys[*it] != want) return BCSIM_E_INVAL;  // asymmetric
+    s.rev[e] = *it;
+  }
+  return BCSIM_OK;
+}
+
+// allocate + initialise device state (first run)
+static int setup_device(Sim& s) {
+  bcsim_config& c = s.cfg;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    g_detail = "no HIP device";
+    return BCSIM_E_NODEVICE;
+  }
+  s.dev = static_cast<int>(c.device) % ndev;
+  HIPCHK(hipSetDevice(s.dev));
+  HIPCHK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  KP& p = s.kp;
+  const uint32_t tr = c.time_round;
+  p.N = s.N;
+  p.R = s.R;
+  p.NT = s.NT;
+  p.E = s.E;
+  p.protocol = c.protocol;
+  p.delay_mode = c.delay_mode;
+  p.rng_mode = c.rng_mode;
+  p.encoding = c.encoding;
+  p.echo = c.echo;
+  p.deg_max = s.deg_max;
+  p.app_delay = c.app_delay_ns;
+  // message sizes
+  uint32_t small = 3, big = 3;
+  if (c.protocol == BCSIM_PBFT) {
+    small = 4;  // Create<Packet>(data, 4)
+    big = c.pbft_block_bytes;
+    if (big == 0) {  // tx_size * (tx_speed / (1000 / (timeout * 1000))) pbft-node.cc:377-380
+      const float tmo = c.pbft_timeout_s;
+      const int num = static_cast<int>(1000 / (1000 / (tmo * 1000)));
+      big = static_cast<uint32_t>(1000 * num);
+    }
+  } else if (c.protocol == BCSIM_RAFT) {
+    big = c.raft_proposal_bytes;
+    if (big == 0) {  // raft-node.cc:409 with tx_size 200, tx_speed 2000
+      const float hb = c.raft_heartbeat_s;
+      const int num = static_cast<int>(2000 / (1000 / (hb * 1000)));
+      big = static_cast<uint32_t>(200 * num);
+    }
+  }
+  const MsgTx ms = message_tx(small, c.mtu, c.link_rate_bps, tr);
+  const MsgTx mb = message_tx(big, c.mtu, c.link_rate_bps, tr);
+  p.tx_tot[0] = ms.total;
+  p.tx_last[0] = ms.last;
+  p.tx_tot[1] = mb.total;
+  p.tx_last[1] = mb.last;
+  p.pbft_period = fsec_to_ns(c.pbft_timeout_s, tr);
+  p.raft_hb = fsec_to_ns(c.raft_heartbeat_s, tr);
+  p.raft_prop_delay = c.raft_proposal_delay_ns;
+  p.stop_ns = c.stop_ns;
+  p.pbft_rounds = c.pbft_rounds;
+  p.pbft_seq_cap = c.pbft_seq_cap ? c.pbft_seq_cap : 1000;
+  p.pbft_view_change = c.pbft_view_change;
+  p.raft_blocks = c.raft_blocks;
+  p.raft_prop_rounds = c.raft_proposal_rounds;
+  p.paxos_proposers = c.paxos_proposers;
+  p.seed = c.seed;
+  int64_t pmin = INT64_MAX;
+  for (int64_t v : s.prop) pmin = std::min(pmin, v);
+  if (pmin < 0) return BCSIM_E_INVAL;
+  s.L = pmin + ms.total;  // lookahead: nothing arrives sooner than this after its send
+  if (s.L <= 0 || s.L >= (1ll << 32)) {
+    g_detail = "lookahead out of range";
+    return BCSIM_E_UNSUPPORTED;
+  }
+  if (c.protocol == BCSIM_PBFT && p.pbft_period <= 0) return BCSIM_E_INVAL;
+  p.L = s.L;
+  // delay tables (float seconds -> ns), pbft-node.cc:68, raft-node.cc:65,71, paxos-node.cc:399
+  std::vector<int64_t> dpb(3), drf(3), del(150), dpx(50);
+  for (int k = 0; k < 3; ++k) {
+    dpb[k] = fsec_to_ns(static_cast<float>((k * 1.0 + 3) / 1000), tr);
+    drf[k] = fsec_to_ns(static_cast<float>(k * 1.0 / 1000), tr);
+  }
+  for (int k = 0; k < 150; ++k) del[k] = fsec_to_ns(static_cast<float>((k + 150) * 1.0 / 1000), tr);
+  for (int k = 0; k < 50; ++k) dpx[k] = fsec_to_ns(static_cast<float>(k * 1.0 / 1000), tr);
+  int64_t* tables = nullptr;
+  int rc;
+  if ((rc = dalloc(s, &tables, 256))) return rc;
+  std::vector<int64_t> tab(256, 0);
+  std::copy(dpb.begin(), dpb.end(), tab.begin());
+  std::copy(drf.begin(), drf.end(), tab.begin() + 4);
+  std::copy(del.begin(), del.end(), tab.begin() + 8);
+  std::copy(dpx.begin(), dpx.end(), tab.begin() + 160);
+  HIPCHK(hipMemcpy(tables, tab.data(), 256 * sizeof(int64_t), hipMemcpyHostToDevice));
+  p.pbft_delay = tables;
+  p.raft_delay = tables + 4;
+  p.raft_elec = tables + 8;
+  p.paxos_delay = tables + 160;
+
+  // topology
+  uint32_t *row, *col, *rev;
+  int64_t* prop;
+  if ((rc = dalloc(s, &row, s.N + 1)) || (rc = dalloc(s, &col, s.E)) || (rc = dalloc(s, &rev, s.E)) ||
+      (rc = dalloc(s, &prop, s.E)))
+    return rc;
+  HIPCHK(hipMemcpy(row, s.row.data(), (s.N + 1) * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(col, s.col.data(), static_cast<size_t>(s.E) * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(rev, s.rev.data(), static_cast<size_t>(s.E) * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(prop, s.prop.data(), static_cast<size_t>(s.E) * 8, hipMemcpyHostToDevice));
+  p.row = row;
+  p.col = col;
+  p.rev = rev;
+  p.prop = prop;
+
+  // capacities
+  const uint64_t NT = s.NT;
+  p.cap_arr = std::min<uint32_t>(8192, next_pow2(std::max<uint64_t>(64, 2ull * s.deg_max + 64)));
+  p.cap_timers = c.cap_timers_per_node ? c.cap_timers_per_node : 8;
+  if (p.cap_timers > 64) p.cap_timers = 64;
+  p.cap_ops = c.cap_ops_per_node ? c.cap_ops_per_node : std::max<uint32_t>(1024, 2 * p.cap_arr + 256);
+  const size_t lds_link = (2ull * (s.deg_max + 1) + p.cap_ops) * 4;
+  if (lds_link > 150 * 1024) {
+    g_detail = "node degree / op capacity exceed the LDS budget of k_link";
+    return BCSIM_E_UNSUPPORTED;
+  }
+  s.B = c.n_buckets ? c.n_buckets : 0;
+  uint64_t cap_b = c.cap_bucket_records;
+  if (cap_b == 0) cap_b = std::max<uint64_t>(4096, NT * (static_cast<uint64_t>(s.deg_max) + 8) * 2);
+  if (cap_b > 0xFFFFFFF0ull) cap_b = 0xFFFFFFF0ull;
+  if (s.B == 0) {  // as many buckets as ~8 GB allows, 8..256
+    const uint64_t per = cap_b * sizeof(Rec);
+    uint64_t nb = per ? (8ull << 30) / per : 256;
+    s.B = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(256, nb)));
+  }
+  if (s.B < 2) s.B = 2;
+  p.n_buckets = s.B;
+  p.cap_bucket = static_cast<uint32_t>(cap_b);
+  p.cap_ov = static_cast<uint32_t>(std::min<uint64_t>(cap_b * 4, 1ull << 24));
+  p.cap_trace = static_cast<uint32_t>(std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1u << 20, NT * 256)));
+  p.cap_vlog = 1u << 20;
+  p.cap_dreq = static_cast<uint32_t>(std::max<uint64_t>(4096, 4 * NT));
+  p.cap_E = static_cast<uint64_t>(s.R) * s.E;
+
+  // state
+  if ((rc = dalloc(s, &p.sub, NT)) || (rc = dalloc(s, &p.draws, NT))) return rc;
+  if ((rc = dalloc(s, &p.leader, NT)) || (rc = dalloc(s, &p.block_num, NT)) ||
+      (rc = dalloc(s, &p.tick_alive, NT)) || (rc = dalloc(s, &p.tick_sub, NT)) ||
+      (rc = dalloc(s, &p.g_n, s.R)) || (rc = dalloc(s, &p.g_nround, s.R)))
+    return rc;
+  const size_t txn = c.protocol == BCSIM_PBFT ? NT * p.pbft_seq_cap : 1;
+  p.cap_txn = txn;
+  if ((rc = dalloc(s, &p.tx_val, txn)) || (rc = dalloc(s, &p.tx_pv, txn)) || (rc = dalloc(s, &p.tx_cv, txn)))
+    return rc;
+  int32_t* ibuf = nullptr;
+  const size_t nint = 14;
+  if ((rc = dalloc(s, &ibuf, NT * nint))) return rc;
+  p.is_leader = ibuf;
+  p.has_voted = ibuf + NT;
+  p.m_value = ibuf + 2 * NT;
+  p.vote_s = ibuf + 3 * NT;
+  p.vote_f = ibuf + 4 * NT;
+  p.acv = ibuf + 5 * NT;
+  p.blockNum = ibuf + 6 * NT;
+  p.round = ibuf + 7 * NT;
+  p.t_max = ibuf + 8 * NT;
+  p.command = ibuf + 9 * NT;
+  p.t_store = ibuf + 10 * NT;
+  p.ticket = ibuf + 11 * NT;
+  p.is_commit = ibuf + 12 * NT;
+  p.proposal = ibuf + 13 * NT;
+  if ((rc = dalloc(s, &p.next_election, NT)) || (rc = dalloc(s, &p.next_heartbeat, NT))) return rc;
+  if ((rc = dalloc(s, &p.timers, NT * p.cap_timers)) || (rc = dalloc(s, &p.ops, NT * p.cap_ops)) ||
+      (rc = dalloc(s, &p.n_ops, NT)))
+    return rc;
+  if ((rc = dalloc(s, &p.busy, static_cast<size_t>(s.R) * s.E))) return rc;
+  if ((rc = dalloc(s, &p.bucket, static_cast<size_t>(s.B) * p.cap_bucket)) ||
+      (rc = dalloc(s, &p.ov, p.cap_ov)) || (rc = dalloc(s, &p.grp, p.cap_bucket)))
+    return rc;
+  if ((rc = dalloc(s, &p.seg_cnt, NT)) || (rc = dalloc(s, &p.seg_off, NT + 1)) ||
+      (rc = dalloc(s, &p.cursor, NT)))
+    return rc;
+  if ((rc = dalloc(s, &p.trace, p.cap_trace)) || (rc = dalloc(s, &p.vlog, p.cap_vlog)) ||
+      (rc = dalloc(s, &p.dreq, p.cap_dreq)))
+    return rc;
+  if ((rc = dalloc(s, &p.counters, static_cast<size_t>(s.R) * CNT_N)) || (rc = dalloc(s, &p.kstat, 8)))
+    return rc;
+  if ((rc = dalloc(s, &p.node_tnext, NT)) || (rc = dalloc(s, &p.node_onext, NT))) return rc;
+  // control block: Ctl + bucket counts, contiguous for one read-back
+  char* ctl = nullptr;
+  if ((rc = dalloc(s, &ctl, sizeof(Ctl) + 4ull * s.B))) return rc;
+  s.ctl_d = ctl;
+  Ctl* cd = reinterpret_cast<Ctl*>(ctl);
+  p.err = &cd->err;
+  p.dbg = &cd->dbg;
+  p.trace_cnt = &cd->trace_cnt;
+  p.vlog_cnt = &cd->vlog_cnt;
+  p.dreq_cnt = &cd->dreq_cnt;
+  p.ov_cnt = &cd->ov_cnt;
+  p.scal = cd->scal;
+  p.bucket_cnt = reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), sizeof(Ctl) + 4ull * s.B));
+  s.bcnt_h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.ctl_h) + sizeof(Ctl));
+
+  // glibc stream tables
+  const bool need_glibc = c.rng_mode == BCSIM_RNG_GLIBC &&
+                          (c.protocol == BCSIM_RAFT || (c.protocol == BCSIM_PBFT && c.pbft_view_change));
+  p.glibc_len = need_glibc ? (1u << 20) : 1;
+  int32_t* gl = nullptr;
+  if ((rc = dalloc(s, &gl, static_cast<size_t>(s.R) * p.glibc_len)) || (rc = dalloc(s, &p.glibc_pos, s.R)))
+    return rc;
+  p.glibc = gl;
+  p.cap_glibc = static_cast<uint64_t>(s.R) * p.glibc_len;
+  if (need_glibc) {
+    if (s.R > 64) return BCSIM_E_UNSUPPORTED;
+    for (uint32_t r = 0; r < s.R; ++r) {
+      std::vector<int32_t> st = glibc_stream(static_cast<uint32_t>(c.seed + r), p.glibc_len);
+      HIPCHK(hipMemcpy(gl + static_cast<size_t>(r) * p.glibc_len, st.data(), 4ull * p.glibc_len,
+                       hipMemcpyHostToDevice));
+    }
+  }
+  std::vector<uint32_t> gpos(s.R, c.protocol == BCSIM_RAFT ? s.N : 0);
+  HIPCHK(hipMemcpy(p.glibc_pos, gpos.data(), 4ull * s.R, hipMemcpyHostToDevice));
+
+  // zero / initial values
+  HIPCHK(hipMemset(ibuf, 0, NT * nint * 4));
+  std::vector<uint32_t> sub0(NT, 2);  // 0 = START, 1 = STOP
+  HIPCHK(hipMemcpy(p.sub, sub0.data(), NT * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(p.draws, 0, NT * 8));
+  HIPCHK(hipMemset(p.leader, 0, NT * 4));
+  HIPCHK(hipMemset(p.block_num, 0, NT * 4));
+  HIPCHK(hipMemset(p.tick_alive, 0, NT));
+  HIPCHK(hipMemset(p.tick_sub, 0, NT * 4));
+  HIPCHK(hipMemset(p.g_n, 0, s.R * 4));
+  HIPCHK(hipMemset(p.g_nround, 0, s.R * 4));
+  HIPCHK(hipMemset(p.tx_val, 0, txn * 4));
+  HIPCHK(hipMemset(p.tx_pv, 0, txn * 4));
+  HIPCHK(hipMemset(p.tx_cv, 0, txn * 4));
+  HIPCHK(hipMemset(p.next_election, 0, NT * 4));
+  HIPCHK(hipMemset(p.next_heartbeat, 0, NT * 4));
+  HIPCHK(hipMemset(p.timers, 0, NT * p.cap_timers * sizeof(TimerEnt)));
+  HIPCHK(hipMemset(p.n_ops, 0, NT * 4));
+  HIPCHK(hipMemset(p.busy, 0, static_cast<size_t>(s.R) * s.E * 8));
+  HIPCHK(hipMemset(p.seg_cnt, 0, NT * 4));
+  HIPCHK(hipMemset(p.seg_off, 0, (NT + 1) * 4));
+  HIPCHK(hipMemset(p.cursor, 0, NT * 4));
+  HIPCHK(hipMemset(p.counters, 0, static_cast<size_t>(s.R) * CNT_N * 8));
+  HIPCHK(hipMemset(p.kstat, 0, 64));
+  std::vector<long long> big_ll(NT, LLONG_MAX);
+  HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(p.node_onext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(s.ctl_d, 0, sizeof(Ctl) + 4ull * s.B));
+  long long sc0[4] = {LLONG_MAX, LLONG_MAX, 0, 0};
+  HIPCHK(hipMemcpy(p.scal, sc0, sizeof sc0, hipMemcpyHostToDevice));
+  // counters' t_last slot starts at 0 (max)
+  HIPCHK(hipDeviceSynchronize());
+  s.bcnt.assign(s.B, 0);
+  s.next_tick = (c.protocol == BCSIM_PBFT) ? p.pbft_period : INT64_MAX;
+  s.n_alive = (c.protocol == BCSIM_PBFT) ? 1 : 0;  // STARTs arm the ticks
+  return BCSIM_OK;
+}
+
+static bool sync_each() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("BCSIM_SYNC_EACH");
+    v = (e && *e && *e != '0') ? 1 : 0;
+  }
+  return v == 1;
+}
+
+template <typename K, typename... Args>
+static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, dim3 block, size_t lds,
+                        Args... args) {
+  int rc = ev_begin(s, cls);
+  if (rc) return rc;
+  hipLaunchKernelGGL(kernel, grid, block, lds, s.stream, args...);
+  HIPCHK(hipGetLastError());
+  rc = ev_end(s);
+  if (rc) return rc;
+  if (sync_each()) {  // debugging aid: pin a failure to one launch
+    hipError_t e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) {
+      g_detail = std::string(name) + " cell " + std::to_string(s.cells) + ": " + hipGetErrorString(e);
+      return BCSIM_E_HIP;
+    }
+    Ctl c;
+    HIPCHK(hipMemcpy(&c, s.ctl_d, sizeof c, hipMemcpyDeviceToHost));
+    if (c.err) {
+      g_detail = std::string(name) + " cell " + std::to_string(s.cells) + " err " + std::to_string(c.err) +
+                 (c.dbg ? " at engine.hip:" + std::to_string(c.dbg) : std::string());
+      return c.err;
+    }
+  }
+  return BCSIM_OK;
+}
+#define launch(s, cls, kernel, ...) launch_named(s, #kernel, cls, kernel, __VA_ARGS__)
+
+static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs) {
+  const size_t lds = 16 + static_cast<size_t>(s.kp.cap_arr) * sizeof(SKey) + s.kp.cap_timers * sizeof(TimerEnt);
+  dim3 grid(s.NT), block(256);
+  int rc;
+  if (s.cfg.protocol == BCSIM_PBFT)
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_PBFT>, grid, block, lds, s.kp, cell, lo, hi, cs);
+  else if (s.cfg.protocol == BCSIM_RAFT)
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_RAFT>, grid, block, lds, s.kp, cell, lo, hi, cs);
+  else
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp, cell, lo, hi, cs);
+  if (rc) return rc;
+  const size_t lds_link = (2ull * (s.deg_max + 1) + s.kp.cap_ops) * 4;
+  return launch(s, KS_LINK, k_link, grid, block, lds_link, s.kp, cell, hi);
+}
+
+static int group_cell(Sim& s, long long cell) {
+  const uint32_t b = static_cast<uint32_t>(cell % s.B);
+  // rebin far-future arrivals first
+  if (s.ov_min <= cell + static_cast<long long>(s.B) - 1) {
+    uint32_t nov = 0;
+    HIPCHK(hipMemcpyAsync(&nov, s.kp.ov_cnt, 4, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    long long big = LLONG_MAX;
+    HIPCHK(hipMemcpyAsync(s.kp.scal + 1, &big, 8, hipMemcpyHostToDevice, s.stream));
+    if (nov) {
+      int rc = launch(s, KS_GROUP, k_rebin, dim3((nov + 255) / 256), dim3(256), 0, s.kp, cell, nov);
+      if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(s.bcnt_h, s.kp.bucket_cnt, 4ull * s.B, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipMemcpyAsync(&s.ov_min, s.kp.scal + 1, 8, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    for (uint32_t k = 0; k < s.B; ++k) s.bcnt[k] = s.bcnt_h[k];
+    if (s.ov_min == LLONG_MAX && nov > (s.kp.cap_ov / 2)) {
+      // everything rebinned: reset the overflow list
+      HIPCHK(hipMemsetAsync(s.kp.ov_cnt, 0, 4, s.stream));
+    }
+  }
+  const uint32_t n = s.bcnt[b];
+  if (n > s.kp.cap_bucket) return BCSIM_E_OVERFLOW;
+  HIPCHK(hipMemsetAsync(s.kp.seg_cnt, 0, s.NT * 4ull, s.stream));
+  HIPCHK(hipMemsetAsync(s.kp.cursor, 0, s.NT * 4ull, s.stream));
+  int rc;
+  if (n) {
+    if ((rc = launch(s, KS_GROUP, k_count, dim3((n + 255) / 256), dim3(256), 0, s.kp, b, n))) return rc;
+  }
+  if ((rc = launch(s, KS_GROUP, k_offsets, dim3(1), dim3(1024), 0, s.kp))) return rc;
+  if (n) {
+    if ((rc = launch(s, KS_GROUP, k_place, dim3((n + 255) / 256), dim3(256), 0, s.kp, b, n))) return rc;
+  }
+  s.grouped_cell = cell;
+  return BCSIM_OK;
+}
+
+static int readback(Sim& s) {
+  HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, sizeof(Ctl) + 4ull * s.B, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipStreamSynchronize(s.stream));
+  int rc = ev_collect(s);
+  if (rc) return rc;
+  for (uint32_t k = 0; k < s.B; ++k) s.bcnt[k] = s.bcnt_h[k];
+  s.next_local = s.ctl_h->scal[0];
+  s.ov_min = s.ctl_h->scal[1];
+  if (s.ctl_h->err) {
+    if (s.ctl_h->dbg) g_detail = "checked build: out-of-range access at engine.hip:" + std::to_string(s.ctl_h->dbg);
+    return s.ctl_h->err;
+  }
+  return BCSIM_OK;
+}
+
+static int run(Sim& s, int64_t t_until) {
+  int rc;
+  if (!s.started) {
+    if ((rc = setup_device(s))) return rc;
+    s.started = true;
+  }
+  HIPCHK(hipSetDevice(s.dev));
+  int64_t lim = t_until;
+  if (s.cfg.t_end_ns > 0 && s.cfg.t_end_ns < lim) lim = s.cfg.t_end_ns;
+  s.trace_valid = false;
+  const long long L = s.L;
+  for (;;) {
+    // earliest cell with work
+    long long c = LLONG_MAX;
+    const long long cdone = s.t_done / L;
+    if (s.start_pending) c = 0;
+    if (s.grouped_cell >= 0) c = std::min(c, s.grouped_cell);  // partially processed cell
+    for (uint32_t b = 0; b < s.B; ++b) {
+      if (!s.bcnt[b]) continue;
+      // bucket b holds the cell c == b (mod B) in [cdone, cdone + B)
+      const long long cb = cdone + ((static_cast<long long>(b) - cdone % s.B) % s.B + s.B) % s.B;
+      c = std::min(c, cb);
+    }
+    if (s.next_local != LLONG_MAX) c = std::min(c, std::max<long long>(s.next_local, s.t_done) / L);
+    if (s.ov_min != LLONG_MAX) c = std::min(c, s.ov_min);
+    if (s.n_alive > 0 && s.next_tick != INT64_MAX) c = std::min(c, s.next_tick / L);
+    if (c == LLONG_MAX || c * L >= lim) {
+      if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
+      break;
+    }
+    const long long cs = c * L, ce = cs + L;
+    const long long lo = std::max<long long>(cs, s.t_done);
+    const long long hi = std::min<long long>(ce, lim);
+    if (s.grouped_cell != c) {
+      if ((rc = group_cell(s, c))) return rc;
+    }
+    const bool tick = s.cfg.protocol == BCSIM_PBFT && s.n_alive > 0 && s.next_tick >= lo && s.next_tick < hi;
+    if (tick) {
+      const long long tk = s.next_tick;
+      if (tk > lo) {
+        if ((rc = do_scan(s, c, lo, tk, cs))) return rc;
+      }
+      HIPCHK(hipMemsetAsync(s.kp.scal + 2, 0, 8, s.stream));
+      if ((rc = launch(s, KS_AUX, k_pbft_tick, dim3(s.R), dim3(1024), static_cast<size_t>(s.N), s.kp, tk)))
+        return rc;
+      if ((rc = do_scan(s, c, tk, hi, cs))) return rc;
+    } else {
+      if ((rc = do_scan(s, c, lo, hi, cs))) return rc;
+    }
+    if (s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC) {
+      if ((rc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp, 0u))) return rc;
+    }
+    if ((rc = launch(s, KS_AUX, k_next, dim3(1), dim3(1024), 0, s.kp))) return rc;
+    if (hi == ce) {
+      // cell finished: its bucket is free again
+      HIPCHK(hipMemsetAsync(s.kp.bucket_cnt + (c % s.B), 0, 4, s.stream));
+    }
+    if ((rc = readback(s))) return rc;
+    if (tick) {
+      s.n_alive = s.ctl_h->scal[2];
+      s.next_tick += s.kp.pbft_period;
+    }
+    s.start_pending = false;
+    s.t_done = hi;
+    ++s.cells;
+    if (hi == ce) {
+      s.grouped_cell = -1;
+      s.bcnt[c % s.B] = 0;
+    }
+  }
+  return BCSIM_OK;
+}
+
+static int fetch_trace(Sim& s) {
+  if (s.trace_valid) return BCSIM_OK;
+  s.trace.clear();
+  if (!s.started) {
+    s.trace_valid = true;
+    return BCSIM_OK;
+  }
+  Ctl ctl;
+  HIPCHK(hipMemcpy(&ctl, s.ctl_d, sizeof ctl, hipMemcpyDeviceToHost));
+  const uint32_t n = std::min(ctl.trace_cnt, s.kp.cap_trace);
+  s.trace.resize(n);
+  if (n) HIPCHK(hipMemcpy(s.trace.data(), s.kp.trace, n * sizeof(bcsim_trace_rec), hipMemcpyDeviceToHost));
+  // resolve the PBFT global `v` of commit lines from the v-log
+  if (s.cfg.protocol == BCSIM_PBFT) {
+    const uint32_t nv = std::min(ctl.vlog_cnt, s.kp.cap_vlog);
+    std::vector<VLog> vl(nv);
+    if (nv) HIPCHK(hipMemcpy(vl.data(), s.kp.vlog, nv * sizeof(VLog), hipMemcpyDeviceToHost));
+    auto vless = [](const VLog& a, const VLog& b) {
+      if (a.rep != b.rep) return a.rep < b.rep;
+      if (a.t != b.t) return a.t < b.t;
+      if (a.ts != b.ts) return a.ts < b.ts;
+      if (a.origin != b.origin) return a.origin < b.origin;
+      if (a.sub != b.sub) return a.sub < b.sub;
+      return a.target < b.target;
+    };
+    std::sort(vl.begin(), vl.end(), vless);
+    for (auto& r : s.trace) {
+      if (r.kind != BCSIM_TR_PBFT_COMMIT || r.a != INT32_MIN) continue;
+      VLog key{};
+      key.rep = r.replica;
+      key.t = r.t_ns;
+      key.ts = r.key_ts;
+      key.origin = r.key_origin;
+      key.sub = r.key_sub;
+      key.target = r.node;
+      auto it = std::lower_bound(vl.begin(), vl.end(), key, vless);  // first >= key
+      int32_t v = 1;
+      if (it != vl.begin()) {
+        auto prev = it - 1;
+        if (prev->rep == r.replica) v = prev->v;
+      }
+      r.a = v;
+    }
+  }
+  std::sort(s.trace.begin(), s.trace.end(), [](const bcsim_trace_rec& a, const bcsim_trace_rec& b) {
+    if (a.replica != b.replica) return a.replica < b.replica;
+    if (a.t_ns != b.t_ns) return a.t_ns < b.t_ns;
+    if (a.key_ts != b.key_ts) return a.key_ts < b.key_ts;
+    if (a.key_origin != b.key_origin) return a.key_origin < b.key_origin;
+    if (a.key_sub != b.key_sub) return a.key_sub < b.key_sub;
+    if (a.node != b.node) return a.node < b.node;
+    return a.kind < b.kind;
+  });
+  s.trace_valid = true;
+  return BCSIM_OK;
+}
+
+static int read_counters(Sim& s, bcsim_counters* out) {
+  std::memset(out, 0, sizeof *out);
+  if (!s.started) return BCSIM_OK;
+  std::vector<unsigned long long> c(static_cast<size_t>(s.R) * CNT_N);
+  HIPCHK(hipMemcpy(c.data(), s.kp.counters, c.size() * 8, hipMemcpyDeviceToHost));
+  Ctl ctl;
+  HIPCHK(hipMemcpy(&ctl, s.ctl_d, sizeof ctl, hipMemcpyDeviceToHost));
+  for (uint32_t r = 0; r < s.R; ++r) {
+    const unsigned long long* x = &c[static_cast<size_t>(r) * CNT_N];
+    for (int k = 0; k < BCSIM_MSG_TYPES; ++k) out->delivered[k] += x[CNT_DELIV + k];
+    out->delivered_total += x[CNT_DELIV_TOTAL];
+    out->echoes += x[CNT_ECHOES];
+    out->sends += x[CNT_SENDS];
+    out->dropped += x[CNT_DROPPED];
+    out->wrong_msgs += x[CNT_WRONG];
+    out->events += x[CNT_EVENTS];
+    out->t_last_ns = std::max<int64_t>(out->t_last_ns, static_cast<int64_t>(x[CNT_TLAST]));
+  }
+  out->trace_records = std::min(ctl.trace_cnt, s.kp.cap_trace);
+  return BCSIM_OK;
+}
+
+static void destroy(Sim* s) {
+  if (!s) return;
+  if (s->started) (void)hipSetDevice(s->dev);
+  for (void* q : s->allocs) (void)hipFree(q);
+  for (auto& e : s->ev_pool) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (s->ctl_h) (void)hipHostFree(s->ctl_h);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+}  // namespace bcsim
+
+// ===========================================================================
+// C ABI (include/bcsim.h)
+using bcsim::Sim;
+
+struct bcsim_sim {
+  Sim* s;
+};
+
+extern "C" {
+
+int bcsim_config_default(bcsim_config* c, uint32_t protocol, uint32_t n_nodes) {
+  if (!c || protocol > BCSIM_PAXOS) return BCSIM_E_INVAL;
+  std::memset(c, 0, sizeof *c);
+  c->abi_version = BCSIM_ABI_VERSION;
+  c->protocol = protocol;
+  c->n_nodes = n_nodes;
+  c->n_replicas = 1;
+  c->link_rate_bps = 3000000;       // blockchain-simulator.cc:23 "3Mbps"
+  c->link_delay_ns = 3000000;       // :24 "3ms"
+  c->mtu = 1500;
+  c->delay_mode = BCSIM_DELAY_RANDOM;
+  c->app_delay_ns = 0;
+  c->rng_mode = BCSIM_RNG_GLIBC;
+  c->time_round = BCSIM_TIME_ROUND;
+  c->seed = 1;                      // rand() is never seeded: srand(1)
+  c->encoding = BCSIM_ENC_EXTENDED;
+  c->echo = 1;
+  c->t_end_ns = 0;
+  c->stop_ns = 10000000000ll;       // :55 Stop(Seconds(10.0))
+  c->pbft_rounds = 40;              // pbft-node.cc:407
+  c->pbft_block_bytes = 0;
+  c->pbft_timeout_s = 0.05f;        // :106
+  c->pbft_view_change = 1;
+  c->pbft_seq_cap = 1000;           // TX tx[1000]
+  c->raft_blocks = 50;              // raft-node.cc:248
+  c->raft_proposal_bytes = 0;
+  c->raft_heartbeat_s = 0.05f;      // :80
+  c->raft_proposal_rounds = 50;     // :361
+  c->raft_proposal_delay_ns = 1000000000ll;  // :216 Seconds(1)
+  c->paxos_proposers = 3;           // paxos-node.cc:136
+  return BCSIM_OK;
+}
+
+int bcsim_create(const bcsim_config* cfg, bcsim_sim** out) {
+  if (!cfg || !out) return BCSIM_E_INVAL;
+  int rc = bcsim::validate(*cfg);
+  if (rc) return rc;
+  Sim* s = new (std::nothrow) Sim();
+  if (!s) return BCSIM_E_NOMEM;
+  s->cfg = *cfg;
+  if (s->cfg.n_replicas == 0) s->cfg.n_replicas = 1;
+  if (s->cfg.pbft_seq_cap == 0) s->cfg.pbft_seq_cap = 1000;
+  s->N = cfg->n_nodes;
+  s->R = s->cfg.n_replicas;
+  if (static_cast<uint64_t>(s->N) * s->R > 0xFFFFFFF0ull) {
+    delete s;
+    return BCSIM_E_UNSUPPORTED;
+  }
+  s->NT = s->N * s->R;
+  bcsim::build_mesh(*s);
+  if ((rc = bcsim::build_rev(*s))) {
+    delete s;
+    return rc;
+  }
+  s->E = s->row[s->N];
+  s->deg_max = 0;
+  for (uint32_t i = 0; i < s->N; ++i) s->deg_max = std::max(s->deg_max, s->row[i + 1] - s->row[i]);
+  bcsim_sim* h = new (std::nothrow) bcsim_sim{s};
+  if (!h) {
+    delete s;
+    return BCSIM_E_NOMEM;
+  }
+  *out = h;
+  return BCSIM_OK;
+}
+
+int bcsim_set_topology_csr(bcsim_sim* h, uint32_t n, const uint32_t* row_ptr, const uint32_t* col_idx,
+                           const int64_t* prop_ns) {
+  if (!h || !row_ptr || !col_idx || n != h->s->N) return BCSIM_E_INVAL;
+  Sim& s = *h->s;
+  if (s.started) return BCSIM_E_STATE;
+  const uint32_t E = row_ptr[n];
+  s.row.assign(row_ptr, row_ptr + n + 1);
+  s.col.assign(col_idx, col_idx + E);
+  if (prop_ns)
+    s.prop.assign(prop_ns, prop_ns + E);
+  else
+    s.prop.assign(E, s.cfg.link_delay_ns);
+  for (uint32_t i = 0; i < n; ++i)
+    if (s.row[i + 1] < s.row[i]) return BCSIM_E_INVAL;
+  int rc = bcsim::build_rev(s);
+  if (rc) return rc;
+  s.E = E;
+  s.deg_max = 0;
+  for (uint32_t i = 0; i < n; ++i) s.deg_max = std::max(s.deg_max, s.row[i + 1] - s.row[i]);
+  return BCSIM_OK;
+}
+
+int bcsim_run(bcsim_sim* h, int64_t t_until_ns) {
+  if (!h) return BCSIM_E_INVAL;
+  Sim& s = *h->s;
+  if (s.err) return s.err;
+  int rc = bcsim::run(s, t_until_ns);
+  if (rc) s.err = rc;
+  return rc;
+}
+
+int bcsim_read_trace(bcsim_sim* h, bcsim_trace_rec* buf, uint64_t cap, uint64_t* n_out) {
+  if (!h || !n_out) return BCSIM_E_INVAL;
+  int rc = bcsim::fetch_trace(*h->s);
+  if (rc) return rc;
+  const auto& t = h->s->trace;
+  *n_out = t.size();
+  if (buf) std::memcpy(buf, t.data(), std::min<uint64_t>(cap, t.size()) * sizeof(bcsim_trace_rec));
+  return BCSIM_OK;
+}
+
+int bcsim_read_counters(bcsim_sim* h, bcsim_counters* out) {
+  if (!h || !out) return BCSIM_E_INVAL;
+  return bcsim::read_counters(*h->s, out);
+}
+
+int bcsim_read_status(bcsim_sim* h, bcsim_status* out) {
+  if (!h || !out) return BCSIM_E_INVAL;
+  Sim& s = *h->s;
+  std::memset(out, 0, sizeof *out);
+  out->now_ns = s.t_done;
+  long long nx = LLONG_MAX;
+  if (s.started) {
+    for (uint32_t b = 0; b < s.B; ++b)
+      if (s.bcnt[b]) nx = std::min<long long>(nx, s.t_done);  // cell granularity
+    nx = std::min(nx, s.next_local);
+    if (s.ov_min != LLONG_MAX) nx = std::min<long long>(nx, s.ov_min * s.L);
+    if (s.n_alive > 0) nx = std::min<long long>(nx, s.next_tick);
+  } else {
+    nx = 0;
+  }
+  out->next_ns = nx;
+  out->cells = s.cells;
+  out->quiescent = nx == LLONG_MAX;
+  out->error = s.err;
+  out->lookahead_ns = s.L;
+  return BCSIM_OK;
+}
+
+int bcsim_destroy(bcsim_sim* h) {
+  if (!h) return BCSIM_OK;
+  bcsim::destroy(h->s);
+  delete h;
+  return BCSIM_OK;
+}
+
+const char* bcsim_strerror(int code) {
+  switch (code) {
+    case BCSIM_OK: return "ok";
+    case BCSIM_E_INVAL: return "invalid argument";
+    case BCSIM_E_NOMEM: return "out of memory";
+    case BCSIM_E_HIP: return "HIP runtime error";
+    case BCSIM_E_OVERFLOW: return "engine buffer capacity exceeded";
+    case BCSIM_E_UNSUPPORTED: return "configuration not supported by the GPU engine";
+    case BCSIM_E_ENCODING: return "compat encoding hit reference undefined behaviour";
+    case BCSIM_E_TIE: return "tie-order precondition violated";
+    case BCSIM_E_NODEVICE: return "no HIP device";
+    case BCSIM_E_STATE: return "call out of order";
+    case BCSIM_E_INDEX: return "PBFT tx[] index out of range";
+    default: return "unknown error";
+  }
+}
+
+const char* bcsim_last_error_detail(void) { return bcsim::g_detail.c_str(); }
+
+int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, uint64_t* launches_out4) {
+  if (!h) return BCSIM_E_INVAL;
+  Sim& s = *h->s;
+  unsigned long long ks[8] = {0};
+  if (s.started) {
+    hipError_t e = hipMemcpy(ks, s.kp.kstat, sizeof ks, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return BCSIM_E_HIP;
+  }
+  for (int k = 0; k < 4; ++k) {
+    if (us_out4) us_out4[k] = s.us[k];
+    if (launches_out4) launches_out4[k] = s.launches[k];
+  }
+  if (bytes_out4) {
+    // k_link algorithmic bytes: 32 B per op read, 32 B per
+    // record written, 16 B per touched edge (busy_until read + write),
+    // 32 B per op kept (compaction write)
+    bytes_out4[bcsim::KS_LINK] = 32.0 * ks[1] + 32.0 * ks[0] + 16.0 * ks[2] + 32.0 * ks[3];
+    bytes_out4[bcsim::KS_SCAN] = 0;
+    bytes_out4[bcsim::KS_GROUP] = 0;
+    bytes_out4[bcsim::KS_AUX] = static_cast<double>(ks[0]);  // records emitted
+  }
+  return BCSIM_OK;
+}
+
+int bcsim_reset_kernel_stats(bcsim_sim* h) {
+  if (!h) return BCSIM_E_INVAL;
+  Sim& s = *h->s;
+  for (int k = 0; k < 4; ++k) {
+    s.us[k] = 0;
+    s.launches[k] = 0;
+  }
+  if (s.started && hipMemset(s.kp.kstat, 0, 64) != hipSuccess) return BCSIM_E_HIP;
+  return BCSIM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+// engine.h — device data layout of the MI355X consensus-propagation engine.
+//
+// Layout in HBM:
+//   node state      SoA, one slot per (replica, node) = "gnode" g = rep*N + i
+//   link state      busy_until[rep*E + e], sender-major CSR edge order
+//   arrivals        B time buckets (cells of length L = lookahead) of 32-byte
+//                   Rec records, appended in per-workgroup chunks; regrouped
+//                   by destination each cell (counting sort) into `grp`
+//   pending ops     per gnode list of 32-byte Op (echo / unicast / broadcast)
+//   timers          per gnode list of TimerEnt
+#pragma once
+#include <stdint.h>
+
+#include "../../include/bcsim.h"
+
+namespace bcsim {
+
+constexpr uint32_t kInvalid = 0xFFFFFFFFu;
+
+// 32-byte arrival record (a packet delivered to a listener socket).
+struct __attribute__((aligned(16))) Rec {
+  uint32_t t_off;   // arrival time - cell start of the arrival cell
+  uint32_t dt;      // arrival time - t_sched (transmit start of last frame)
+  uint32_t dest;    // gnode of the receiver; kInvalid = padding slot
+  uint32_t origin;  // sender node id (within replica)
+  uint32_t sub;     // sender's schedule counter of the SendPacket
+  uint32_t edge;    // edge index (s->d) within the replica
+  int16_t f0, f1;   // raw payload chars data[1], data[2]
+  int16_t f2;       // data[3]
+  uint8_t type;     // charToInt(data[0])
+  uint8_t big;      // 1 = block / proposal sized payload
+};
+static_assert(sizeof(Rec) == 32, "Rec must be 32 bytes");
+
+// Far-future arrival (beyond the bucket ring).
+struct __attribute__((aligned(16))) OvRec {
+  int64_t cell;
+  int64_t pad;
+  Rec r;
+};
+
+// op kinds
+enum : uint8_t { OP_ECHO = 0, OP_SEND = 1, OP_BCAST = 2, OP_BCAST_J = 3 };
+// op flags (Op::flags)
+enum : uint8_t {
+  OPF_BIG = 1,       // big payload
+  OPF_PAXOS = 2,     // Paxos broadcast (skip peers[0], drop *end())
+  OPF_DONE = 4       // expanded broadcast (jitter) -- consumed
+};
+
+// 32-byte pending link operation.
+struct __attribute__((aligned(16))) Op {
+  int64_t t;        // execution time (SendPacket / echo time)
+  uint32_t dt;      // t - t_sched
+  uint32_t origin;  // key origin (node itself; ECHO: the received packet's sender)
+  uint32_t sub;     // key sub (BCAST: first edge's sub; edge k gets sub+k)
+  uint32_t edge;    // edge index within replica (SEND/ECHO); BCAST_J: draw base lo
+  int16_t f0, f1;
+  int16_t f2;
+  uint8_t type;
+  uint8_t kind_flags;  // kind (2 bits) | flags << 2
+};
+static_assert(sizeof(Op) == 32, "Op must be 32 bytes");
+
+__host__ __device__ inline uint8_t op_kind(const Op& o) { return o.kind_flags & 3; }
+__host__ __device__ inline uint8_t op_flags(const Op& o) { return o.kind_flags >> 2; }
+
+// timer kinds
+enum : uint8_t {
+  TM_RAFT_ELECTION = 1,
+  TM_RAFT_HEARTBEAT = 2,
+  TM_RAFT_PROPOSAL = 3,
+  TM_PAXOS_TICKET = 4
+};
+
+struct __attribute__((aligned(8))) TimerEnt {
+  int64_t t;      // fire time (INT64_MAX while a glibc draw is pending)
+  int64_t ts;     // t_sched
+  uint32_t sub;   // schedule counter (= EventId)
+  uint8_t kind;
+  uint8_t alive;  // 0 = cancelled / fired (slot free)
+  uint8_t pending_draw;
+  uint8_t pad;
+};
+static_assert(sizeof(TimerEnt) == 24, "TimerEnt");
+
+// glibc draw request (Raft election timeout in GLIBC mode), resolved in
+// canonical global order at the end of the cell.
+struct DrawReq {
+  int64_t t;
+  int64_t ts;
+  uint32_t origin, sub, target;  // event key (target = node)
+  uint32_t rep;
+  uint32_t timer_sub;            // timer entry to fill
+  uint32_t pad;
+};
+
+// PBFT global v write log (file-scope `v`, pbft-node.cc:26)
+struct VLog {
+  int64_t t, ts;
+  uint32_t origin, sub, target, rep;
+  int32_t v;
+  int32_t pad;
+};
+
+// per-replica counters layout in the device counter array
+enum {
+  CNT_DELIV = 0,        // 16 entries
+  CNT_DELIV_TOTAL = 16,
+  CNT_ECHOES,
+  CNT_SENDS,
+  CNT_DROPPED,
+  CNT_WRONG,
+  CNT_EVENTS,
+  CNT_TLAST,            // max event time (atomicMax)
+  CNT_N
+};
+
+// kernel-class timing slots
+enum { KS_SCAN = 0, KS_LINK = 1, KS_GROUP = 2, KS_AUX = 3 };
+
+}  // namespace bcsim

@@ -204,6 +204,7 @@ const char* bcsim_last_error_detail(void);
  * microseconds measured with hipEvents on the engine stream.  kinds:
  * 0 scan, 1 link (fan-out scatter), 2 group, 3 tick/aux.  Also the
  * algorithmic bytes moved by each class. */
+int bcsim_reset_kernel_stats(bcsim_sim* s);
 int bcsim_read_kernel_stats(bcsim_sim* s, double* us_out4, double* bytes_out4,
                             uint64_t* launches_out4);
 

@@ -1,0 +1,70 @@
+"""Shared parity cases: each returns a bcsim Config (and optional topology).
+
+Every case runs through the HIP engine (bcsim) and the CPU oracle and the
+traces / counters must be identical (tests/test_gpu_parity.py).
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "blockchain-simulator_amd"))
+from bcsim import _abi  # noqa: E402
+
+
+def _cfg(proto, n, **kw):
+    c = _abi.default_config(proto, n)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def cases():
+    P, R, X = _abi.PBFT, _abi.RAFT, _abi.PAXOS
+    F, J = _abi.DELAY_FIXED, _abi.DELAY_RANDOM
+    G, K = _abi.RNG_GLIBC, _abi.RNG_COUNTER
+    return {
+        # C1: PBFT n=16, fixed 3 ms app delay, 100 client requests (view change at block 61)
+        "pbft16_fixed_100": _cfg(P, 16, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=100),
+        # the reference's own default shape: N=8, 40 rounds, glibc lottery
+        "pbft8_fixed_40": _cfg(P, 8, delay_mode=F, app_delay_ns=3_000_000),
+        # small blocks: unsaturated links
+        "pbft16_small_blocks": _cfg(P, 16, delay_mode=F, app_delay_ns=4_000_000, pbft_rounds=30,
+                                    pbft_block_bytes=1000),
+        "pbft5_odd": _cfg(P, 5, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=20),
+        "pbft12_jitter_ctr": _cfg(P, 12, delay_mode=J, rng_mode=K, seed=7, pbft_rounds=25),
+        "pbft8_trunc": _cfg(P, 8, delay_mode=F, app_delay_ns=5_000_000, time_round=_abi.TIME_TRUNC,
+                            pbft_rounds=15),
+        "pbft8_compat": _cfg(P, 8, delay_mode=F, app_delay_ns=3_000_000, encoding=_abi.ENC_COMPAT,
+                             pbft_rounds=30),
+        "pbft8_noecho": _cfg(P, 8, delay_mode=F, app_delay_ns=3_000_000, echo=0, pbft_rounds=20),
+        # Raft: fixed delays, glibc election timeouts (N=8 -> node 2 at 177 ms)
+        "raft8_fixed": _cfg(R, 8, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=5_000_000_000),
+        "raft8_fixed0": _cfg(R, 8, delay_mode=F, app_delay_ns=0, t_end_ns=4_000_000_000),
+        "raft64_fixed": _cfg(R, 64, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=4_000_000_000),
+        "raft16_jitter_ctr": _cfg(R, 16, delay_mode=J, rng_mode=K, seed=3, t_end_ns=4_000_000_000),
+        # Paxos: single decree, proposers 0,1,2
+        "paxos8_fixed": _cfg(X, 8, delay_mode=F, app_delay_ns=2_000_000),
+        "paxos8_fixed0": _cfg(X, 8, delay_mode=F, app_delay_ns=0),
+        "paxos32_jitter_ctr": _cfg(X, 32, delay_mode=J, rng_mode=K, seed=11),
+        "paxos16_jitter_rep4": _cfg(X, 16, delay_mode=J, rng_mode=K, seed=5, n_replicas=4),
+        "pbft8_rep3_ctr": _cfg(P, 8, delay_mode=F, app_delay_ns=3_000_000, rng_mode=K, n_replicas=3,
+                               pbft_rounds=20, pbft_block_bytes=2000),
+    }
+
+
+def compare(a, b):
+    """Return None if (trace, counters) agree, else a short diff string."""
+    ta, ca = a[0], a[1]
+    tb, cb = b[0], b[1]
+    msgs = []
+    if len(ta) != len(tb):
+        msgs.append(f"trace length {len(ta)} != {len(tb)}")
+    for k, (x, y) in enumerate(zip(ta, tb)):
+        if x != y:
+            msgs.append(f"first trace diff at {k}: {x} != {y}")
+            break
+    for key in ("delivered", "delivered_total", "echoes", "sends", "dropped", "wrong_msgs", "events",
+                "t_last_ns", "trace_records"):
+        if ca[key] != cb[key]:
+            msgs.append(f"counter {key}: {ca[key]} != {cb[key]}")
+    return "; ".join(msgs) if msgs else None
