@@ -294,6 +294,26 @@ static int setup_device(Sim& s) {
   p.cap_dreq = static_cast<uint32_t>(std::max<uint64_t>(4096, 4 * NT));
   p.cap_E = static_cast<uint64_t>(s.R) * s.E;
 
+  // dynamic LDS above the 64 KiB default needs an explicit opt-in (160 KiB per CU on gfx950)
+  {
+    const size_t lds_scan = 16 + static_cast<size_t>(p.cap_arr) * sizeof(SKey) + p.cap_timers * sizeof(TimerEnt);
+    if (lds_scan > 160 * 1024 - 64) {
+      g_detail = "k_scan LDS request too large";
+      return BCSIM_E_UNSUPPORTED;
+    }
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_RAFT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_link),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_link)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_pbft_tick),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(s.N)));
+  }
+  if (s.N > 60 * 1024) return BCSIM_E_UNSUPPORTED;  // k_pbft_tick keeps one flag per node in LDS
+
   // state
   if ((rc = dalloc(s, &p.sub, NT)) || (rc = dalloc(s, &p.draws, NT))) return rc;
   if ((rc = dalloc(s, &p.leader, NT)) || (rc = dalloc(s, &p.block_num, NT)) ||
