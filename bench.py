@@ -60,6 +60,18 @@ def cpu_baseline(n_nodes, budget_s):
                        f"({cnt['delivered_total']} msgs, {cpu:.1f} s CPU, {wall:.1f} s wall)")
 
 
+def aggregate(dist, device, dt, msgs, trace_delta):
+    """Whole-job numbers over ranks: max wall time, summed work (replicas)."""
+    if dist is None:
+        return dt, msgs, trace_delta
+    import torch
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    m = torch.tensor([float(msgs), float(trace_delta)], dtype=torch.float64, device=device)
+    dist.all_reduce(m, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(m[0].item()), int(m[1].item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,13 +121,7 @@ def main():
     ks = sim.kernel_stats()
     msgs = c1["delivered_total"] - c0["delivered_total"]
     trace_delta = c1["trace_records"] - tr0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        m = torch.tensor([msgs, trace_delta], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(m, op=dist.ReduceOp.SUM)
-        msgs, trace_delta = int(m[0].item()), int(m[1].item())
+    dt, msgs, trace_delta = aggregate(dist, f"cuda:{local}", dt, msgs, trace_delta)
     sim.close()
 
     if rank == 0:

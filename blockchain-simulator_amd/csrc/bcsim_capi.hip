@@ -43,8 +43,10 @@ struct Sim {
   long long grouped_cell = -1;
   int64_t next_tick = INT64_MAX;  // PBFT
   bool start_pending = true;
+  bool stop_pending = true;   // Application::Stop at cfg.stop_ns (if >= 0)
   hipStream_t stream = nullptr;
   KP kp{};
+  KP* kp_dev = nullptr;  // device copy of kp passed to every kernel
   std::vector<void*> allocs;
   // host mirrors
   Ctl* ctl_h = nullptr;  // pinned
@@ -64,7 +66,21 @@ struct Sim {
   std::vector<bcsim_trace_rec> trace;
   bool trace_valid = false;
   int dev = 0;
+  unsigned long long* trail_h = nullptr;  // checked builds: host view of breadcrumbs
 };
+
+static std::string trail_dump(const Sim& s) {
+  std::string out;
+  if (!s.trail_h) return out;
+  int shown = 0;
+  for (uint32_t g = 0; g < s.NT && shown < 64; ++g) {
+    const unsigned long long v = s.trail_h[g];
+    if (!v) continue;
+    out += " [g" + std::to_string(g) + ":L" + std::to_string(v & 0xFFFFFFFFull) + "]";
+    ++shown;
+  }
+  return out;
+}
 
 template <typename T>
 static int dalloc(Sim& s, T** p, size_t count) {
@@ -418,6 +434,20 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemset(p.cursor, 0, NT * 4));
   HIPCHK(hipMemset(p.counters, 0, static_cast<size_t>(s.R) * CNT_N * 8));
   HIPCHK(hipMemset(p.kstat, 0, 64));
+#ifdef BCSIM_CHECKED
+  {
+    const char* tv = std::getenv("BCSIM_TRAIL");
+    if (tv && *tv && *tv != '0') {
+      void* hp = nullptr;
+      HIPCHK(hipHostMalloc(&hp, NT * 8, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(hp, 0, NT * 8);
+      void* dp = nullptr;
+      HIPCHK(hipHostGetDevicePointer(&dp, hp, 0));
+      s.trail_h = static_cast<unsigned long long*>(hp);
+      p.trail = static_cast<unsigned long long*>(dp);
+    }
+  }
+#endif
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p.node_onext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -426,6 +456,8 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemcpy(p.scal, sc0, sizeof sc0, hipMemcpyHostToDevice));
   // counters' t_last slot starts at 0 (max)
   HIPCHK(hipDeviceSynchronize());
+  if ((rc = dalloc(s, &s.kp_dev, 1))) return rc;
+  HIPCHK(hipMemcpy(s.kp_dev, &s.kp, sizeof(KP), hipMemcpyHostToDevice));
   s.bcnt.assign(s.B, 0);
   s.next_tick = (c.protocol == BCSIM_PBFT) ? p.pbft_period : INT64_MAX;
   s.n_alive = (c.protocol == BCSIM_PBFT) ? 1 : 0;  // STARTs arm the ticks
@@ -453,9 +485,11 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
   if (sync_each()) {  // debugging aid: pin a failure to one launch
     hipError_t e = hipStreamSynchronize(s.stream);
     if (e != hipSuccess) {
-      g_detail = std::string(name) + " cell " + std::to_string(s.cells) + ": " + hipGetErrorString(e);
+      g_detail = std::string(name) + " cell " + std::to_string(s.cells) + ": " + hipGetErrorString(e) +
+                 " trail:" + trail_dump(s);
       return BCSIM_E_HIP;
     }
+    if (s.trail_h) std::memset(s.trail_h, 0, s.NT * 8ull);
     Ctl c;
     HIPCHK(hipMemcpy(&c, s.ctl_d, sizeof c, hipMemcpyDeviceToHost));
     if (c.err) {
@@ -473,14 +507,14 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   dim3 grid(s.NT), block(256);
   int rc;
   if (s.cfg.protocol == BCSIM_PBFT)
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_PBFT>, grid, block, lds, s.kp, cell, lo, hi, cs);
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_PBFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs);
   else if (s.cfg.protocol == BCSIM_RAFT)
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_RAFT>, grid, block, lds, s.kp, cell, lo, hi, cs);
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_RAFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs);
   else
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp, cell, lo, hi, cs);
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp_dev, cell, lo, hi, cs);
   if (rc) return rc;
   const size_t lds_link = (2ull * (s.deg_max + 1) + s.kp.cap_ops) * 4;
-  return launch(s, KS_LINK, k_link, grid, block, lds_link, s.kp, cell, hi);
+  return launch(s, KS_LINK, k_link, grid, block, lds_link, s.kp_dev, cell, hi);
 }
 
 static int group_cell(Sim& s, long long cell) {
@@ -493,14 +527,14 @@ static int group_cell(Sim& s, long long cell) {
     long long big = LLONG_MAX;
     HIPCHK(hipMemcpyAsync(s.kp.scal + 1, &big, 8, hipMemcpyHostToDevice, s.stream));
     if (nov) {
-      int rc = launch(s, KS_GROUP, k_rebin, dim3((nov + 255) / 256), dim3(256), 0, s.kp, cell, nov);
+      int rc = launch(s, KS_GROUP, k_rebin, dim3((nov + 255) / 256), dim3(256), 0, s.kp_dev, cell, nov);
       if (rc) return rc;
     }
     HIPCHK(hipMemcpyAsync(s.bcnt_h, s.kp.bucket_cnt, 4ull * s.B, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipMemcpyAsync(&s.ov_min, s.kp.scal + 1, 8, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipStreamSynchronize(s.stream));
     for (uint32_t k = 0; k < s.B; ++k) s.bcnt[k] = s.bcnt_h[k];
-    if (s.ov_min == LLONG_MAX && nov > (s.kp.cap_ov / 2)) {
+    if (s.ov_min == LLONG_MAX) {
       // everything rebinned: reset the overflow list
       HIPCHK(hipMemsetAsync(s.kp.ov_cnt, 0, 4, s.stream));
     }
@@ -511,11 +545,11 @@ static int group_cell(Sim& s, long long cell) {
   HIPCHK(hipMemsetAsync(s.kp.cursor, 0, s.NT * 4ull, s.stream));
   int rc;
   if (n) {
-    if ((rc = launch(s, KS_GROUP, k_count, dim3((n + 255) / 256), dim3(256), 0, s.kp, b, n))) return rc;
+    if ((rc = launch(s, KS_GROUP, k_count, dim3((n + 255) / 256), dim3(256), 0, s.kp_dev, b, n))) return rc;
   }
-  if ((rc = launch(s, KS_GROUP, k_offsets, dim3(1), dim3(1024), 0, s.kp))) return rc;
+  if ((rc = launch(s, KS_GROUP, k_offsets, dim3(1), dim3(1024), 0, s.kp_dev))) return rc;
   if (n) {
-    if ((rc = launch(s, KS_GROUP, k_place, dim3((n + 255) / 256), dim3(256), 0, s.kp, b, n))) return rc;
+    if ((rc = launch(s, KS_GROUP, k_place, dim3((n + 255) / 256), dim3(256), 0, s.kp_dev, b, n))) return rc;
   }
   s.grouped_cell = cell;
   return BCSIM_OK;
@@ -562,6 +596,7 @@ static int run(Sim& s, int64_t t_until) {
     if (s.next_local != LLONG_MAX) c = std::min(c, std::max<long long>(s.next_local, s.t_done) / L);
     if (s.ov_min != LLONG_MAX) c = std::min(c, s.ov_min);
     if (s.n_alive > 0 && s.next_tick != INT64_MAX) c = std::min(c, s.next_tick / L);
+    if (s.stop_pending && s.cfg.stop_ns >= 0 && s.cfg.stop_ns >= s.t_done) c = std::min(c, s.cfg.stop_ns / L);
     if (c == LLONG_MAX || c * L >= lim) {
       if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
       break;
@@ -569,6 +604,10 @@ static int run(Sim& s, int64_t t_until) {
     const long long cs = c * L, ce = cs + L;
     const long long lo = std::max<long long>(cs, s.t_done);
     const long long hi = std::min<long long>(ce, lim);
+    if (lo >= hi) {  // nothing left before the limit inside this cell
+      if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
+      break;
+    }
     if (s.grouped_cell != c) {
       if ((rc = group_cell(s, c))) return rc;
     }
@@ -579,16 +618,16 @@ static int run(Sim& s, int64_t t_until) {
         if ((rc = do_scan(s, c, lo, tk, cs))) return rc;
       }
       HIPCHK(hipMemsetAsync(s.kp.scal + 2, 0, 8, s.stream));
-      if ((rc = launch(s, KS_AUX, k_pbft_tick, dim3(s.R), dim3(1024), static_cast<size_t>(s.N), s.kp, tk)))
+      if ((rc = launch(s, KS_AUX, k_pbft_tick, dim3(s.R), dim3(1024), static_cast<size_t>(s.N), s.kp_dev, tk)))
         return rc;
       if ((rc = do_scan(s, c, tk, hi, cs))) return rc;
     } else {
       if ((rc = do_scan(s, c, lo, hi, cs))) return rc;
     }
     if (s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC) {
-      if ((rc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp, 0u))) return rc;
+      if ((rc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp_dev, 0u))) return rc;
     }
-    if ((rc = launch(s, KS_AUX, k_next, dim3(1), dim3(1024), 0, s.kp))) return rc;
+    if ((rc = launch(s, KS_AUX, k_next, dim3(1), dim3(1024), 0, s.kp_dev))) return rc;
     if (hi == ce) {
       // cell finished: its bucket is free again
       HIPCHK(hipMemsetAsync(s.kp.bucket_cnt + (c % s.B), 0, 4, s.stream));
@@ -599,6 +638,7 @@ static int run(Sim& s, int64_t t_until) {
       s.next_tick += s.kp.pbft_period;
     }
     s.start_pending = false;
+    if (s.cfg.stop_ns >= 0 && s.cfg.stop_ns < hi) s.stop_pending = false;
     s.t_done = hi;
     ++s.cells;
     if (hi == ce) {
@@ -837,6 +877,7 @@ int bcsim_read_status(bcsim_sim* h, bcsim_status* out) {
     nx = std::min(nx, s.next_local);
     if (s.ov_min != LLONG_MAX) nx = std::min<long long>(nx, s.ov_min * s.L);
     if (s.n_alive > 0) nx = std::min<long long>(nx, s.next_tick);
+    if (s.stop_pending && s.cfg.stop_ns >= s.t_done) nx = std::min<long long>(nx, s.cfg.stop_ns);
   } else {
     nx = 0;
   }

@@ -108,6 +108,7 @@ struct KP {
   unsigned long long* kstat;     // link kernel algorithmic counters
   int32_t* err;
   int32_t* dbg;  // BCSIM_CHECKED builds: first out-of-bounds source line
+  unsigned long long* trail;  // BCSIM_CHECKED + BCSIM_TRAIL: host-mapped breadcrumbs
   uint64_t cap_E, cap_EB, cap_txn, cap_glibc;
   long long *node_tnext, *node_onext;
   long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks
@@ -145,6 +146,19 @@ __device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int l
   do {                \
   } while (0)
 #endif
+#ifdef BCSIM_CHECKED
+#define TRAIL_AT(pp, g)                                                                        \
+  do {                                                                                         \
+    if ((pp).trail)                                                                            \
+      __hip_atomic_store(&(pp).trail[g], (static_cast<unsigned long long>(g) << 32) | __LINE__, \
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                          \
+  } while (0)
+#else
+#define TRAIL_AT(pp, g) \
+  do {                  \
+  } while (0)
+#endif
+#define TRAIL(c) TRAIL_AT(*(c).p, (c).g)
 #define AT(arr, idx, cap) at_(p, (arr), static_cast<uint64_t>(idx), static_cast<uint64_t>(cap), __LINE__)
 
 struct Key {
@@ -206,7 +220,8 @@ __device__ inline int32_t c2i(int32_t c) { return c - '0'; }
 
 // ---------------------------------------------------------------------------
 // grouping: counting sort of bucket records by destination node
-__global__ void k_count(KP p, uint32_t b, uint32_t n) {
+__global__ void k_count(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
+  const KP& p = *pk;
   BAIL_IF_ERR();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
@@ -215,7 +230,8 @@ __global__ void k_count(KP p, uint32_t b, uint32_t n) {
 }
 
 // single-block exclusive scan of seg_cnt[0..NT) -> seg_off[0..NT]
-__global__ __launch_bounds__(1024) void k_offsets(KP p) {
+__global__ __launch_bounds__(1024) void k_offsets(const KP* __restrict__ pk) {
+  const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t carry;
@@ -252,7 +268,8 @@ __global__ __launch_bounds__(1024) void k_offsets(KP p) {
   if (tid == 0) AT(p.seg_off, p.NT, p.NT + 1) = carry;
 }
 
-__global__ void k_place(KP p, uint32_t b, uint32_t n) {
+__global__ void k_place(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
+  const KP& p = *pk;
   BAIL_IF_ERR();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
@@ -263,7 +280,8 @@ __global__ void k_place(KP p, uint32_t b, uint32_t n) {
 }
 
 // move far-future arrivals whose cell entered the ring into their bucket
-__global__ void k_rebin(KP p, long long g_cur, uint32_t n) {
+__global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) {
+  const KP& p = *pk;
   BAIL_IF_ERR();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
@@ -301,6 +319,7 @@ struct Ctx {
 
 __device__ inline void ctx_trace(Ctx& c, uint32_t kind, int32_t a, int32_t b, int32_t cc) {
   const KP& p = *c.p;
+  TRAIL(c);
   const uint32_t pos = atomicAdd(p.trace_cnt, 1u);
   if (pos >= p.cap_trace) {
     set_err(p, BCSIM_E_OVERFLOW);
@@ -322,6 +341,7 @@ __device__ inline void ctx_trace(Ctx& c, uint32_t kind, int32_t a, int32_t b, in
 
 __device__ inline void ctx_op(Ctx& c, const Op& o) {
   const KP& p = *c.p;
+  TRAIL(c);
   if (c.nops >= c.p->cap_ops) {
     set_err(*c.p, BCSIM_E_OVERFLOW);
     return;
@@ -347,6 +367,7 @@ __device__ inline Op mk_op(const KP& p, int64_t t, uint32_t dt, uint32_t origin,
 
 __device__ inline int32_t ctx_draw(Ctx& c) {
   const KP& p = *c.p;
+  TRAIL(c);
   if (p.rng_mode == BCSIM_RNG_COUNTER) return ctr_rand(p.seed, c.rep, c.i, c.draws++);
   set_err(p, BCSIM_E_UNSUPPORTED);  // glibc draws inside a cell: unsupported
   return 0;
@@ -355,6 +376,7 @@ __device__ inline int32_t ctx_draw(Ctx& c) {
 // Simulator::Schedule(Seconds(getRandomDelay()), SendPacket, ...) x peers
 __device__ void ctx_bcast(Ctx& c, const Msg& m, bool paxos) {
   const KP& p = *c.p;
+  TRAIL(c);
   const uint8_t fl = paxos ? OPF_PAXOS : 0;
   if (p.delay_mode == BCSIM_DELAY_FIXED) {
     ctx_op(c, mk_op(p, c.cur.t + p.app_delay, static_cast<uint32_t>(p.app_delay), c.i, c.sub, 0, m,
@@ -371,7 +393,9 @@ __device__ void ctx_bcast(Ctx& c, const Msg& m, bool paxos) {
 // Send(data, from): reply on the reverse edge of the arrival
 __device__ void ctx_unicast(Ctx& c, uint32_t in_edge, const Msg& m) {
   const KP& p = *c.p;
+  TRAIL(c);
   const int64_t d = p.delay_mode == BCSIM_DELAY_FIXED ? p.app_delay : delay_from_draw(p, ctx_draw(c));
+  TRAIL(c);
   ctx_op(c, mk_op(p, c.cur.t + d, static_cast<uint32_t>(d), c.i, c.sub++, AT(p.rev, in_edge, p.E), m,
                   OP_SEND, 0));
 }
@@ -649,6 +673,7 @@ __device__ void paxos_ticket(Ctx& c, PaxosState& s) {  // requireTicket :510-522
 
 __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t in_edge) {
   const KP& p = *c.p;
+  TRAIL(c);
   const int32_t N = static_cast<int32_t>(p.N);
   const int32_t ty = c2i(mch(m, 0));
   switch (ty) {
@@ -737,8 +762,9 @@ __device__ inline bool skey_gt(const SKey& a, const SKey& b) {
 }
 
 template <int PROTO>
-__global__ __launch_bounds__(256) void k_scan(KP p, long long cell, long long t_lo, long long t_hi,
+__global__ __launch_bounds__(256) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
                                              long long cs) {
+  const KP& p = *pk;
   BAIL_IF_ERR();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint32_t& n_valid = *reinterpret_cast<uint32_t*>(smem);  // 16-byte control slot
@@ -800,7 +826,7 @@ __global__ __launch_bounds__(256) void k_scan(KP p, long long cell, long long t_
   // ---- serial state machine (one lane) ----
   const uint32_t rep = g / p.N, i = g % p.N;
   Ctx c;
-  c.p = &p;
+  c.p = pk;
   c.g = g;
   c.rep = rep;
   c.i = i;
@@ -843,6 +869,7 @@ __global__ __launch_bounds__(256) void k_scan(KP p, long long cell, long long t_
   }
 
   const uint32_t mv = n_valid;
+  TRAIL(c);
   uint32_t ai = 0;
   bool start_pending = has_start, stop_pending = has_stop;
   long long tmax_ev = LLONG_MIN;
@@ -884,6 +911,7 @@ __global__ __launch_bounds__(256) void k_scan(KP p, long long cell, long long t_
         which = 3;
       }
     }
+    TRAIL(c);
     if (which < 0) break;
     c.cur = best;
     if (best.t > tmax_ev) tmax_ev = best.t;
@@ -897,6 +925,7 @@ __global__ __launch_bounds__(256) void k_scan(KP p, long long cell, long long t_
       msg.f[2] = rec.f2;
       msg.big = rec.big;
       if (rec.type < BCSIM_MSG_TYPES) ++c.deliv[rec.type];
+      TRAIL(c);
       if (p.echo) {  // socket->SendTo(packet, 0, from): reverse-link occupancy
         Op e = mk_op(p, best.t, rec.dt, rec.origin, rec.sub, AT(p.rev, rec.edge, p.E), msg, OP_ECHO, 0);
         ctx_op(c, e);
@@ -969,6 +998,7 @@ __global__ __launch_bounds__(256) void k_scan(KP p, long long cell, long long t_
   }
 
   // write back
+  TRAIL(c);
   AT(p.sub, g, p.NT) = c.sub;
   AT(p.draws, g, p.NT) = c.draws;
   AT(p.n_ops, g, p.NT) = c.nops;
@@ -1084,7 +1114,8 @@ __device__ inline void edge_ops(const KP& p, const Op* ops, const uint32_t* eidx
   }
 }
 
-__global__ __launch_bounds__(256) void k_link(KP p, long long cell, long long t_hi) {
+__global__ __launch_bounds__(256) void k_link(const KP* __restrict__ pk, long long cell, long long t_hi) {
+  const KP& p = *pk;
   BAIL_IF_ERR();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ LinkLds L;
@@ -1349,11 +1380,12 @@ __global__ __launch_bounds__(256) void k_link(KP p, long long cell, long long t_
 // PBFT SendBlock tick (pbft-node.cc:371-411) for every node of a replica.
 // One workgroup per replica; nodes tick in id order (canonical key order of
 // equal-time timers scheduled at the same time).
-__global__ __launch_bounds__(1024) void k_pbft_tick(KP p, long long tk) {
+__global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, long long tk) {
+  const KP& p = *pk;
   BAIL_IF_ERR();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint8_t* lead = reinterpret_cast<uint8_t*>(smem);  // N flags
-  __shared__ int32_t v_cur, nround0, n_alive;
+  __shared__ int32_t v_cur, nround0, n_alive, n_ticked;
   __shared__ long long vk_t, vk_ts;
   __shared__ uint32_t vk_o, vk_s, vk_tg;
   const uint32_t rep = blockIdx.x, tid = threadIdx.x;
@@ -1387,6 +1419,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(KP p, long long tk) {
     }
     nround0 = AT(p.g_nround, rep, p.R);
     n_alive = 0;
+    n_ticked = 0;
   }
   __syncthreads();
   for (uint32_t i = tid; i < N; i += blockDim.x) {
@@ -1509,6 +1542,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(KP p, long long tk) {
         const uint32_t s = AT(p.sub, g, p.NT);
         AT(p.tick_sub, g, p.NT) = s;  // blockEvent = Schedule(Seconds(timeout), SendBlock) :406
         AT(p.sub, g, p.NT) = s + 1;
+        atomicAdd(&n_ticked, 1);
         if (nr == static_cast<int32_t>(p.pbft_rounds)) {  // :407-410
           const uint32_t pos = atomicAdd(p.trace_cnt, 1u);
           if (pos < p.cap_trace) {
@@ -1537,13 +1571,20 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(KP p, long long tk) {
     if (tid == blockDim.x - 1) chunk_base += sc[tid];
     __syncthreads();
   }
-  if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&p.scal[2]),
-                          static_cast<unsigned long long>(n_alive));
+  if (tid == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&p.scal[2]), static_cast<unsigned long long>(n_alive));
+    if (n_ticked > 0) {
+      unsigned long long* cnt = &AT(p.counters, static_cast<size_t>(rep) * CNT_N, static_cast<uint64_t>(p.R) * CNT_N);
+      atomicAdd(&cnt[CNT_EVENTS], static_cast<unsigned long long>(n_ticked));
+      atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), tk);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
 // glibc election-timeout draws (Raft), canonical global order per replica.
-__global__ void k_draws(KP p, uint32_t) {
+__global__ void k_draws(const KP* __restrict__ pk, uint32_t) {
+  const KP& p = *pk;
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const uint32_t n = min(*p.dreq_cnt, p.cap_dreq);
   if (n == 0) return;
@@ -1587,7 +1628,8 @@ __global__ void k_draws(KP p, uint32_t) {
 }
 
 // global min over node_tnext / node_onext
-__global__ __launch_bounds__(1024) void k_next(KP p) {
+__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk) {
+  const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ long long red[1024];
   long long m = LLONG_MAX;

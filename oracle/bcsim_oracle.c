@@ -1142,8 +1142,10 @@ int bcsim_oracle_run(bcsim_oracle* o, int64_t t_until_ns) {
       oev e;
       heap_pop(&o->heap, &e);
       o->now = e.t;
-      if (e.t > o->cnt.t_last_ns) o->cnt.t_last_ns = e.t;
+      const uint64_t ev0 = o->cnt.events;
       exec_event(o, &e);
+      /* t_last: latest protocol event (START/STOP/timer/delivery), sends excluded */
+      if (o->cnt.events != ev0 && e.t > o->cnt.t_last_ns) o->cnt.t_last_ns = e.t;
       if (o->err) return o->err;
     }
     if (o->R > 1 && o->cur_rep + 1 < o->R) {

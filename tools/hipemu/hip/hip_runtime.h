@@ -1,0 +1,124 @@
+// hipemu — DEBUG-ONLY host emulation of the small HIP subset used by
+// blockchain-simulator_amd/csrc, so kernels can run under AddressSanitizer on
+// the CPU when a GPU fault must be located without faulting a GPU.  Never used
+// by the product, tests or bench (tools/hipemu/README.md).
+#pragma once
+#include <atomic>
+#include <barrier>
+#include <climits>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+#include <type_traits>
+#include <vector>
+
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __shared__ static
+
+struct dim3 {
+  unsigned x = 1, y = 1, z = 1;
+  dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+struct hipemu_ctx {
+  dim3 tid, bid, bdim, gdim;
+  std::barrier<>* bar;
+  unsigned long long* shfl;  // per-block shuffle exchange
+};
+extern thread_local hipemu_ctx hipemu_t;
+#define threadIdx (hipemu_t.tid)
+#define blockIdx (hipemu_t.bid)
+#define blockDim (hipemu_t.bdim)
+#define gridDim (hipemu_t.gdim)
+struct hipemu_exit {};
+inline void __syncthreads() { hipemu_t.bar->arrive_and_wait(); }
+inline void __builtin_amdgcn_endpgm() { throw hipemu_exit{}; }
+char* hipemu_dyn_smem();
+
+template <typename T>
+inline T __shfl_up(T v, unsigned d, int width = 64) {
+  unsigned t = hipemu_t.tid.x;
+  hipemu_t.shfl[t] = static_cast<unsigned long long>(v);
+  __syncthreads();
+  unsigned lane = t % width;
+  T r = lane >= d ? static_cast<T>(hipemu_t.shfl[t - d]) : v;
+  __syncthreads();
+  return r;
+}
+
+template <typename T, typename U>
+inline T atomicAdd(T* p, U v) { return __atomic_fetch_add(p, static_cast<T>(v), __ATOMIC_SEQ_CST); }
+template <typename T, typename U, typename V>
+inline T atomicCAS(T* p, U cmp_, V v_) {
+  T cmp = static_cast<T>(cmp_), v = static_cast<T>(v_);
+  __atomic_compare_exchange_n(p, &cmp, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
+  return cmp;
+}
+template <typename T, typename U>
+inline T atomicMin(T* p, U v_) {
+  T v = static_cast<T>(v_);
+  T o = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+  while (v < o && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
+  }
+  return o;
+}
+template <typename T, typename U>
+inline T atomicMax(T* p, U v_) {
+  T v = static_cast<T>(v_);
+  T o = __atomic_load_n(p, __ATOMIC_SEQ_CST);
+  while (v > o && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST)) {
+  }
+  return o;
+}
+template <typename A, typename B>
+inline std::common_type_t<A, B> min(A a, B b) { return a < b ? a : b; }
+template <typename A, typename B>
+inline std::common_type_t<A, B> max(A a, B b) { return a < b ? b : a; }
+
+#define __ATOMIC_RELAXED_ __ATOMIC_RELAXED
+#define __HIP_MEMORY_SCOPE_SYSTEM 0
+template <typename T, typename U>
+inline void __hip_atomic_store(T* p, U v, int, int) { __atomic_store_n(p, static_cast<T>(v), __ATOMIC_RELAXED); }
+
+// ---- runtime API subset ----
+typedef int hipError_t;
+enum { hipSuccess = 0, hipErrorUnknown = 999 };
+typedef struct hipemu_stream* hipStream_t;
+typedef struct hipemu_event* hipEvent_t;
+enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice, hipMemcpyDefault };
+enum { hipStreamNonBlocking = 1, hipFuncAttributeMaxDynamicSharedMemorySize = 8 };
+typedef int hipFuncAttribute;
+const char* hipGetErrorString(hipError_t);
+hipError_t hipGetDeviceCount(int*);
+hipError_t hipSetDevice(int);
+hipError_t hipStreamCreateWithFlags(hipStream_t*, unsigned);
+hipError_t hipStreamDestroy(hipStream_t);
+hipError_t hipStreamSynchronize(hipStream_t);
+hipError_t hipDeviceSynchronize();
+hipError_t hipMalloc(void**, size_t);
+hipError_t hipFree(void*);
+hipError_t hipHostMalloc(void**, size_t, unsigned = 0);
+hipError_t hipHostGetDevicePointer(void**, void*, unsigned);
+enum { hipHostMallocMapped = 2, hipHostMallocCoherent = 0x40000000 };
+hipError_t hipHostFree(void*);
+hipError_t hipMemcpy(void*, const void*, size_t, hipMemcpyKind);
+hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t);
+hipError_t hipMemset(void*, int, size_t);
+hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t);
+hipError_t hipEventCreate(hipEvent_t*);
+hipError_t hipEventDestroy(hipEvent_t);
+hipError_t hipEventRecord(hipEvent_t, hipStream_t);
+hipError_t hipEventElapsedTime(float*, hipEvent_t, hipEvent_t);
+hipError_t hipGetLastError();
+hipError_t hipFuncSetAttribute(const void*, hipFuncAttribute, int);
+
+void hipemu_launch(dim3 grid, dim3 block, size_t lds, const std::function<void()>& body);
+#define hipLaunchKernelGGL(K, G, B, S, ST, ...) hipemu_launch(dim3(G), dim3(B), (S), [=]() { K(__VA_ARGS__); })
