@@ -104,9 +104,13 @@ def main():
 
     # warmup: fill the pipeline (first block needs ~135 ms to serialize)
     t_sim = 0
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
         t_sim += period
+        w = time.perf_counter()
         sim.run(t_sim)
+        if rank == 0:
+            print(f"[bench] warmup {k}: {time.perf_counter() - w:.2f}s msgs={sim.counters()['delivered_total']}",
+                  file=sys.stderr, flush=True)
     c0 = sim.counters()
     tr0 = c0["trace_records"]
     sim.reset_kernel_stats()

@@ -265,6 +265,8 @@ static int setup_device(Sim& s) {
   p.raft_delay = tables + 4;
   p.raft_elec = tables + 8;
   p.paxos_delay = tables + 160;
+  p.jit_delay = c.protocol == BCSIM_PBFT ? p.pbft_delay : c.protocol == BCSIM_RAFT ? p.raft_delay : p.paxos_delay;
+  p.jit_mod = c.protocol == BCSIM_PAXOS ? 50 : 3;
 
   // topology
   uint32_t *row, *col, *rev;

@@ -57,6 +57,8 @@ struct KP {
   uint32_t raft_prop_rounds, paxos_proposers;
   uint64_t seed;
   int64_t *pbft_delay, *raft_delay, *raft_elec, *paxos_delay;
+  int64_t* jit_delay;  // the running protocol's getRandomDelay table
+  uint32_t jit_mod;
   // topology (per replica, shared)
   const uint32_t *row, *col, *rev;
   const int64_t* prop;
@@ -187,10 +189,13 @@ __device__ inline int32_t ctr_rand(uint64_t seed, uint32_t rep, uint32_t node, u
   return static_cast<int32_t>(h >> 33);
 }
 
+// getRandomDelay() of the running protocol: jit_delay/jit_mod are chosen on
+// the host (pbft-node.cc:68 / raft-node.cc:65 / paxos-node.cc:399).  A
+// device-side three-way branch on p.protocol here was miscompiled by the
+// ROCm 7.2 compiler in divergent code (the paxos arm used an unset address
+// register -> aperture violation), so there is deliberately no branch.
 __device__ inline int64_t delay_from_draw(const KP& p, int32_t r) {
-  if (p.protocol == BCSIM_PBFT) return AT(p.pbft_delay, r % 3, 3);
-  if (p.protocol == BCSIM_RAFT) return AT(p.raft_delay, r % 3, 3);
-  return AT(p.paxos_delay, r % 50, 50);
+  return AT(p.jit_delay, static_cast<uint32_t>(r) % p.jit_mod, p.jit_mod);
 }
 
 // intToChar through the wire (raw char code); compat = signed char wrap

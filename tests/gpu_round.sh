@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU-box validation, one step at a time; stops at the first failure or fault.
+#   bash tests/gpu_round.sh [steps...]   (default: checked parity smoke bench prof)
+set -o pipefail
+mkdir -p gpurun_out
+faulted() { grep -q "APERTURE\|illegal memory\|Memory access fault\|HSA_STATUS_ERROR" "$1"; }
+run() {
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] || faulted "gpurun_out/$name.log"; then exit 1; fi
+}
+steps=${*:-checked parity smoke bench prof}
+for st in $steps; do
+  case $st in
+    checked) run checked 600 env BCSIM_LIB="$PWD/blockchain-simulator_amd/libbcsim_checked.so" BCSIM_SYNC_EACH=1 python tests/parity_run.py ;;
+    parity)  run parity 900 python -m pytest tests -m gpu -x -q ;;
+    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench1k) run bench1k 600 python bench.py --nodes 1024 --cpu-budget 5 ;;
+    bench)   run bench 900 python bench.py ;;
+    prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python bench.py --no-cpu-baseline ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done

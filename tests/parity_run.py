@@ -17,3 +17,4 @@ for name, cfg in sorted(cases().items()):
         if "E_HIP" in str(e) or "illegal" in str(e):
             sys.exit(3)
 print("passed", ok)
+sys.exit(0 if ok == sum(1 for n in cases() if not sel or n in sel) else 1)
