@@ -82,6 +82,10 @@ static std::string trail_dump(const Sim& s) {
   return out;
 }
 
+static size_t scan_lds_bytes(const KP& p) {
+  return 64 + static_cast<size_t>(p.cap_arr) * sizeof(Rec) + p.cap_timers * sizeof(TimerEnt);
+}
+
 template <typename T>
 static int dalloc(Sim& s, T** p, size_t count) {
   if (count == 0) count = 1;
@@ -285,10 +289,14 @@ static int setup_device(Sim& s) {
 
   // capacities
   const uint64_t NT = s.NT;
-  p.cap_arr = std::min<uint32_t>(8192, next_pow2(std::max<uint64_t>(64, 2ull * s.deg_max + 64)));
+  // k_scan stages up to cap_arr arrivals per window in LDS (32 B each); a
+  // cell with more is split into windows, so cap_arr only bounds one instant
+  const uint64_t arr_want = next_pow2(std::max<uint64_t>(64, 2ull * s.deg_max + 64));
+  p.cap_arr = static_cast<uint32_t>(std::min<uint64_t>(kScanMaxArr, arr_want));
   p.cap_timers = c.cap_timers_per_node ? c.cap_timers_per_node : 8;
   if (p.cap_timers > 64) p.cap_timers = 64;
-  p.cap_ops = c.cap_ops_per_node ? c.cap_ops_per_node : std::max<uint32_t>(1024, 2 * p.cap_arr + 256);
+  p.cap_ops = c.cap_ops_per_node ? c.cap_ops_per_node
+                                 : static_cast<uint32_t>(std::max<uint64_t>(1024, 2 * arr_want + 256));
   const size_t lds_link = (2ull * (s.deg_max + 1) + p.cap_ops) * 4;
   if (lds_link > 150 * 1024) {
     g_detail = "node degree / op capacity exceed the LDS budget of k_link";
@@ -314,7 +322,7 @@ static int setup_device(Sim& s) {
 
   // dynamic LDS above the 64 KiB default needs an explicit opt-in (160 KiB per CU on gfx950)
   {
-    const size_t lds_scan = 16 + static_cast<size_t>(p.cap_arr) * sizeof(SKey) + p.cap_timers * sizeof(TimerEnt);
+    const size_t lds_scan = scan_lds_bytes(p);
     if (lds_scan > 160 * 1024 - 64) {
       g_detail = "k_scan LDS request too large";
       return BCSIM_E_UNSUPPORTED;
@@ -505,8 +513,8 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
 #define launch(s, cls, kernel, ...) launch_named(s, #kernel, cls, kernel, __VA_ARGS__)
 
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs) {
-  const size_t lds = 16 + static_cast<size_t>(s.kp.cap_arr) * sizeof(SKey) + s.kp.cap_timers * sizeof(TimerEnt);
-  dim3 grid(s.NT), block(256);
+  const size_t lds = scan_lds_bytes(s.kp);
+  dim3 grid(s.NT), block(kScanThreads);
   int rc;
   if (s.cfg.protocol == BCSIM_PBFT)
     rc = launch(s, KS_SCAN, k_scan<BCSIM_PBFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs);
@@ -566,7 +574,8 @@ static int readback(Sim& s) {
   s.next_local = s.ctl_h->scal[0];
   s.ov_min = s.ctl_h->scal[1];
   if (s.ctl_h->err) {
-    if (s.ctl_h->dbg) g_detail = "checked build: out-of-range access at engine.hip:" + std::to_string(s.ctl_h->dbg);
+    g_detail = std::string(bcsim_strerror(s.ctl_h->err)) + " raised at engine.hip:" + std::to_string(s.ctl_h->dbg) +
+               " (cell " + std::to_string(s.cells) + ")";
     return s.ctl_h->err;
   }
   return BCSIM_OK;

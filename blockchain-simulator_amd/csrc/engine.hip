@@ -118,9 +118,12 @@ struct KP {
 
 // ---------------------------------------------------------------------------
 // device helpers
-__device__ inline void set_err(const KP& p, int32_t code) {
-  atomicCAS(p.err, 0, code);
+// First error wins; its source line goes to p.dbg so the host can name the
+// exact capacity or invariant that failed (bcsim_last_error_detail).
+__device__ inline void set_err_(const KP& p, int32_t code, int line) {
+  if (atomicCAS(p.err, 0, code) == 0) atomicCAS(p.dbg, 0, line);
 }
+#define set_err(pp, code) set_err_((pp), (code), __LINE__)
 
 __device__ __attribute__((aligned(64))) char g_dummy[256];
 
@@ -396,12 +399,14 @@ __device__ void ctx_bcast(Ctx& c, const Msg& m, bool paxos) {
 }
 
 // Send(data, from): reply on the reverse edge of the arrival
-__device__ void ctx_unicast(Ctx& c, uint32_t in_edge, const Msg& m) {
+// out_edge = the reverse of the arrival's edge (resolved when the arrival was
+// staged into LDS)
+__device__ void ctx_unicast(Ctx& c, uint32_t out_edge, const Msg& m) {
   const KP& p = *c.p;
   TRAIL(c);
   const int64_t d = p.delay_mode == BCSIM_DELAY_FIXED ? p.app_delay : delay_from_draw(p, ctx_draw(c));
   TRAIL(c);
-  ctx_op(c, mk_op(p, c.cur.t + d, static_cast<uint32_t>(d), c.i, c.sub++, AT(p.rev, in_edge, p.E), m,
+  ctx_op(c, mk_op(p, c.cur.t + d, static_cast<uint32_t>(d), c.i, c.sub++, out_edge, m,
                   OP_SEND, 0));
 }
 
@@ -458,7 +463,7 @@ __device__ bool pbft_index(const KP& p, int32_t idx) {
   return true;
 }
 
-__device__ void pbft_recv(Ctx& c, PbftState& s, const Msg& m, uint32_t in_edge) {
+__device__ void pbft_recv(Ctx& c, PbftState& s, const Msg& m, uint32_t back_edge) {
   const KP& p = *c.p;
   const size_t base = static_cast<size_t>(c.g) * p.pbft_seq_cap;
   const int32_t N = static_cast<int32_t>(p.N);
@@ -473,7 +478,7 @@ __device__ void pbft_recv(Ctx& c, PbftState& s, const Msg& m, uint32_t in_edge) 
     }
     case PB_PREPARE: {  // :212-222
       const Msg r = mkmsg(PB_PREPARE_RES, mch(m, 1), mch(m, 2), enc_raw(p, 0), 0);
-      ctx_unicast(c, in_edge, r);
+      ctx_unicast(c, back_edge, r);
       break;
     }
     case PB_PREPARE_RES: {  // :223-240
@@ -580,7 +585,7 @@ __device__ void raft_heartbeat(Ctx& c, RaftState& s) {  // sendHeartBeat :404-42
   }
 }
 
-__device__ void raft_recv(Ctx& c, RaftState& s, const Msg& m, uint32_t in_edge) {
+__device__ void raft_recv(Ctx& c, RaftState& s, const Msg& m, uint32_t back_edge) {
   const KP& p = *c.p;
   const int32_t N = static_cast<int32_t>(p.N);
   switch (c2i(mch(m, 0))) {
@@ -590,7 +595,7 @@ __device__ void raft_recv(Ctx& c, RaftState& s, const Msg& m, uint32_t in_edge) 
         st = 0;
         s.has_voted = 1;
       }
-      ctx_unicast(c, in_edge, mkmsg(RF_VOTE_RES, enc_raw(p, st), 0, 0, 0));
+      ctx_unicast(c, back_edge, mkmsg(RF_VOTE_RES, enc_raw(p, st), 0, 0, 0));
       break;
     }
     case RF_HEARTBEAT: {  // :170-194
@@ -603,7 +608,7 @@ __device__ void raft_recv(Ctx& c, RaftState& s, const Msg& m, uint32_t in_edge) 
         s.m_value = c2i(mch(m, 2));
       }
       ctx_cancel(c, s.next_election);
-      ctx_unicast(c, in_edge, mkmsg(RF_HEARTBEAT_RES, d1, enc_raw(p, 0), 0, 0));
+      ctx_unicast(c, back_edge, mkmsg(RF_HEARTBEAT_RES, d1, enc_raw(p, 0), 0, 0));
       break;
     }
     case RF_VOTE_RES: {  // :196-232
@@ -676,7 +681,7 @@ __device__ void paxos_ticket(Ctx& c, PaxosState& s) {  // requireTicket :510-522
   ctx_trace(c, BCSIM_TR_PAXOS_TICKET, s.ticket, 0, 0);
 }
 
-__device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t in_edge) {
+__device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t back_edge) {
   const KP& p = *c.p;
   TRAIL(c);
   const int32_t N = static_cast<int32_t>(p.N);
@@ -691,7 +696,7 @@ __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t in_edge
       } else {
         r = mkmsg(PX_RES_TICKET, enc_raw(p, 1), 0, 0, 0);
       }
-      ctx_unicast(c, in_edge, r);
+      ctx_unicast(c, back_edge, r);
       break;
     }
     case PX_REQ_PROPOSE: {  // :199-221
@@ -702,7 +707,7 @@ __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t in_edge
         s.t_store = t;
         st = 0;
       }
-      ctx_unicast(c, in_edge, mkmsg(PX_RES_PROPOSE, enc_raw(p, st), 0, 0, 0));
+      ctx_unicast(c, back_edge, mkmsg(PX_RES_PROPOSE, enc_raw(p, st), 0, 0, 0));
       break;
     }
     case PX_REQ_COMMIT: {  // :222-247
@@ -713,7 +718,7 @@ __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t in_edge
         s.is_commit = 1;
         st = 0;
       }
-      ctx_unicast(c, in_edge, mkmsg(PX_RES_COMMIT, enc_raw(p, st), 0, 0, 0));
+      ctx_unicast(c, back_edge, mkmsg(PX_RES_COMMIT, enc_raw(p, st), 0, 0, 0));
       break;
     }
     case PX_RES_TICKET:
@@ -756,6 +761,10 @@ __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t in_edge
 // k_scan: one workgroup per node.  Sort the node's arrivals of [t_lo, t_hi)
 // by (t, t_sched, origin) in LDS, then run the state machine in canonical
 // key order merged with the node's timers and START/STOP.
+constexpr int kScanThreads = 256;
+constexpr int kScanMaxArr = 4096;  // LDS window: 32 B per staged arrival
+constexpr int kScanPerThread = kScanMaxArr / kScanThreads;
+
 struct SKey {
   uint64_t hi;  // t_off << 32 | ~dt
   uint32_t lo;  // origin
@@ -766,15 +775,35 @@ __device__ inline bool skey_gt(const SKey& a, const SKey& b) {
   return a.hi > b.hi || (a.hi == b.hi && a.lo > b.lo);
 }
 
+// Count this node's arrivals with t in [a, b) (all threads; block-uniform result).
+__device__ inline uint32_t scan_count(const KP& p, uint32_t* slot, uint32_t seg_b, uint32_t m, long long cs,
+                                      long long a, long long b) {
+  const uint32_t tid = threadIdx.x;
+  __syncthreads();
+  if (tid == 0) *slot = 0;
+  __syncthreads();
+  uint32_t mine = 0;
+  for (uint32_t k = tid; k < m; k += blockDim.x) {
+    const long long t = cs + AT(p.grp, seg_b + k, p.cap_bucket).t_off;
+    mine += (t >= a && t < b);
+  }
+  if (mine) atomicAdd(slot, mine);
+  __syncthreads();
+  return *slot;
+}
+
 template <int PROTO>
-__global__ __launch_bounds__(256) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
-                                             long long cs) {
+__global__ __launch_bounds__(kScanThreads) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                      long long t_hi, long long cs) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  // LDS: [0,64) control | cap_arr x Rec (sorted window; the SKey sort runs in
+  // the same bytes first) | cap_timers x TimerEnt
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint32_t& n_valid = *reinterpret_cast<uint32_t*>(smem);  // 16-byte control slot
-  SKey* keys = reinterpret_cast<SKey*>(smem + 16);
-  TimerEnt* tm = reinterpret_cast<TimerEnt*>(smem + 16 + static_cast<size_t>(p.cap_arr) * sizeof(SKey));
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(smem);
+  SKey* keys = reinterpret_cast<SKey*>(smem + 64);
+  Rec* recs = reinterpret_cast<Rec*>(smem + 64);
+  TimerEnt* tm = reinterpret_cast<TimerEnt*>(smem + 64 + static_cast<size_t>(p.cap_arr) * sizeof(Rec));
 
   const uint32_t g = blockIdx.x;
   if (g >= p.NT) return;
@@ -784,224 +813,280 @@ __global__ __launch_bounds__(256) void k_scan(const KP* __restrict__ pk, long lo
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
   if (m == 0 && AT(p.node_tnext, g, p.NT) >= t_hi && !has_start && !has_stop) return;
-  if (m > p.cap_arr) {
-    if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
-    return;
-  }
-  uint32_t P2 = 2;
-  while (P2 < m) P2 <<= 1;
-  if (tid == 0) n_valid = 0;
-  __syncthreads();
-  for (uint32_t k = tid; k < P2; k += blockDim.x) {
-    SKey s;
-    s.hi = ~0ull;
-    s.lo = ~0u;
-    s.idx = k;
-    if (k < m) {
-      const Rec r = AT(p.grp, seg_b + k, p.cap_bucket);
-      const long long t = cs + r.t_off;
-      if (t >= t_lo && t < t_hi) {
-        s.hi = (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~r.dt);
-        s.lo = r.origin;
-        atomicAdd(&n_valid, 1u);
-      }
-    }
-    keys[k] = s;
-  }
-  if (tid < p.cap_timers) tm[tid] = AT(p.timers, static_cast<size_t>(g) * p.cap_timers + tid, static_cast<uint64_t>(p.NT) * p.cap_timers);
-  __syncthreads();
-  for (uint32_t k2 = 2; k2 <= P2; k2 <<= 1) {
-    for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
-      for (uint32_t t = tid; t < P2; t += blockDim.x) {
-        const uint32_t ixj = t ^ j;
-        if (ixj > t) {
-          const SKey a = keys[t], b = keys[ixj];
-          const bool up = (t & k2) == 0;
-          if (up ? skey_gt(a, b) : skey_gt(b, a)) {
-            keys[t] = b;
-            keys[ixj] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  if (tid != 0) return;
+  if (tid < p.cap_timers)
+    tm[tid] = AT(p.timers, static_cast<size_t>(g) * p.cap_timers + tid, static_cast<uint64_t>(p.NT) * p.cap_timers);
 
-  // ---- serial state machine (one lane) ----
+  // ---- serial state (lane 0 only) ----
   const uint32_t rep = g / p.N, i = g % p.N;
   Ctx c;
-  c.p = pk;
-  c.g = g;
-  c.rep = rep;
-  c.i = i;
-  c.deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
-  c.sub = AT(p.sub, g, p.NT);
-  c.draws = AT(p.draws, g, p.NT);
-  c.ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
-  c.nops = AT(p.n_ops, g, p.NT);
-  c.tm = tm;
-  c.cap_t = p.cap_timers;
-  for (int k = 0; k < BCSIM_MSG_TYPES; ++k) c.deliv[k] = 0;
-  c.echoes = c.wrong = c.events = 0;
-
   PbftState ps{};
   RaftState rs{};
   PaxosState xs{};
-  if (PROTO == BCSIM_PBFT) {
-    ps.leader = AT(p.leader, g, p.NT);
-    ps.block_num = AT(p.block_num, g, p.NT);
-  } else if (PROTO == BCSIM_RAFT) {
-    rs.is_leader = AT(p.is_leader, g, p.NT);
-    rs.has_voted = AT(p.has_voted, g, p.NT);
-    rs.m_value = AT(p.m_value, g, p.NT);
-    rs.vs = AT(p.vote_s, g, p.NT);
-    rs.vf = AT(p.vote_f, g, p.NT);
-    rs.acv = AT(p.acv, g, p.NT);
-    rs.blockNum = AT(p.blockNum, g, p.NT);
-    rs.round = AT(p.round, g, p.NT);
-    rs.next_election = AT(p.next_election, g, p.NT);
-    rs.next_heartbeat = AT(p.next_heartbeat, g, p.NT);
-  } else {
-    xs.t_max = AT(p.t_max, g, p.NT);
-    xs.command = AT(p.command, g, p.NT);
-    xs.t_store = AT(p.t_store, g, p.NT);
-    xs.ticket = AT(p.ticket, g, p.NT);
-    xs.is_commit = AT(p.is_commit, g, p.NT);
-    xs.proposal = AT(p.proposal, g, p.NT);
-    xs.vs = AT(p.vote_s, g, p.NT);
-    xs.vf = AT(p.vote_f, g, p.NT);
-  }
-
-  const uint32_t mv = n_valid;
-  TRAIL(c);
-  uint32_t ai = 0;
   bool start_pending = has_start, stop_pending = has_stop;
-  long long tmax_ev = LLONG_MIN;
-  for (;;) {
-    // candidates
-    int which = -1;  // 0 arrival, 1 timer, 2 start, 3 stop
-    Key best{};
-    Rec rec{};
-    int tsel = -1;
-    if (ai < mv) {
-      rec = AT(p.grp, seg_b + keys[ai].idx, p.cap_bucket);
-      best.t = cs + rec.t_off;
-      best.ts = best.t - rec.dt;
-      best.origin = rec.origin;
-      best.sub = rec.sub;
-      which = 0;
-    }
-    for (uint32_t k = 0; k < c.cap_t; ++k) {
-      const TimerEnt& te = tm[k];
-      if (!te.alive || te.pending_draw || te.t >= t_hi || te.t < t_lo) continue;
-      const Key kk{te.t, te.ts, i, te.sub};
-      if (which < 0 || key_less(kk, best)) {
-        best = kk;
-        which = 1;
-        tsel = static_cast<int>(k);
-      }
-    }
-    if (start_pending) {
-      const Key kk{0, -1, i, 0};
-      if (which < 0 || key_less(kk, best)) {
-        best = kk;
-        which = 2;
-      }
-    }
-    if (stop_pending) {
-      const Key kk{p.stop_ns, -1, i, 1};
-      if (which < 0 || key_less(kk, best)) {
-        best = kk;
-        which = 3;
-      }
+  if (tid == 0) {
+    c.p = pk;
+    c.g = g;
+    c.rep = rep;
+    c.i = i;
+    c.deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
+    c.sub = AT(p.sub, g, p.NT);
+    c.draws = AT(p.draws, g, p.NT);
+    c.ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
+    c.nops = AT(p.n_ops, g, p.NT);
+    c.tm = tm;
+    c.cap_t = p.cap_timers;
+    for (int k = 0; k < BCSIM_MSG_TYPES; ++k) c.deliv[k] = 0;
+    c.echoes = c.wrong = c.events = 0;
+    if (PROTO == BCSIM_PBFT) {
+      ps.leader = AT(p.leader, g, p.NT);
+      ps.block_num = AT(p.block_num, g, p.NT);
+    } else if (PROTO == BCSIM_RAFT) {
+      rs.is_leader = AT(p.is_leader, g, p.NT);
+      rs.has_voted = AT(p.has_voted, g, p.NT);
+      rs.m_value = AT(p.m_value, g, p.NT);
+      rs.vs = AT(p.vote_s, g, p.NT);
+      rs.vf = AT(p.vote_f, g, p.NT);
+      rs.acv = AT(p.acv, g, p.NT);
+      rs.blockNum = AT(p.blockNum, g, p.NT);
+      rs.round = AT(p.round, g, p.NT);
+      rs.next_election = AT(p.next_election, g, p.NT);
+      rs.next_heartbeat = AT(p.next_heartbeat, g, p.NT);
+    } else {
+      xs.t_max = AT(p.t_max, g, p.NT);
+      xs.command = AT(p.command, g, p.NT);
+      xs.t_store = AT(p.t_store, g, p.NT);
+      xs.ticket = AT(p.ticket, g, p.NT);
+      xs.is_commit = AT(p.is_commit, g, p.NT);
+      xs.proposal = AT(p.proposal, g, p.NT);
+      xs.vs = AT(p.vote_s, g, p.NT);
+      xs.vf = AT(p.vote_f, g, p.NT);
     }
     TRAIL(c);
-    if (which < 0) break;
-    c.cur = best;
-    if (best.t > tmax_ev) tmax_ev = best.t;
-    ++c.events;
-    if (which == 0) {
-      ++ai;
-      Msg msg;
-      msg.type = rec.type;
-      msg.f[0] = rec.f0;
-      msg.f[1] = rec.f1;
-      msg.f[2] = rec.f2;
-      msg.big = rec.big;
-      if (rec.type < BCSIM_MSG_TYPES) ++c.deliv[rec.type];
-      TRAIL(c);
-      if (p.echo) {  // socket->SendTo(packet, 0, from): reverse-link occupancy
-        Op e = mk_op(p, best.t, rec.dt, rec.origin, rec.sub, AT(p.rev, rec.edge, p.E), msg, OP_ECHO, 0);
-        ctx_op(c, e);
-        ++c.echoes;
-      }
-      if (PROTO == BCSIM_PBFT) {
-        if (best.t == ((best.t / p.pbft_period) * p.pbft_period) && best.ts <= best.t - p.pbft_period)
-          set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
-        pbft_recv(c, ps, msg, rec.edge);
-      } else if (PROTO == BCSIM_RAFT) {
-        raft_recv(c, rs, msg, rec.edge);
-      } else {
-        paxos_recv(c, xs, msg, rec.edge);
-      }
-    } else if (which == 1) {
-      TimerEnt& te = tm[tsel];
-      te.alive = 0;
-      if (PROTO == BCSIM_RAFT) {
-        if (te.kind == TM_RAFT_ELECTION) {  // sendVote :391-401
-          rs.has_voted = 1;
-          ctx_bcast(c, mkmsg(RF_VOTE_REQ, enc_raw(p, static_cast<int32_t>(i)), 0, 0, 0), false);
-          ctx_trace(c, BCSIM_TR_RAFT_ELECTION, 0, 0, 0);
-          raft_arm_election(c, rs);
-        } else if (te.kind == TM_RAFT_HEARTBEAT) {
-          raft_heartbeat(c, rs);
-        } else if (te.kind == TM_RAFT_PROPOSAL) {  // setProposal :432-435
-          rs.acv = 1;
-        }
-      } else if (PROTO == BCSIM_PAXOS) {
-        if (te.kind == TM_PAXOS_TICKET) paxos_ticket(c, xs);
-      }
-    } else if (which == 2) {  // StartApplication
-      start_pending = false;
-      if (PROTO == BCSIM_PBFT) {  // :97-158; globals reset host-side
-        ps.leader = 0;
-        ps.block_num = 0;
-        AT(p.tick_sub, g, p.NT) = c.sub++;  // Schedule(Seconds(timeout), SendBlock) :155
-        AT(p.tick_alive, g, p.NT) = 1;
-      } else if (PROTO == BCSIM_RAFT) {  // :75-115
-        rs.m_value = 0;
-        rs.vs = 0;
-        rs.vf = 0;
-        rs.has_voted = 0;
-        rs.acv = 0;
-        rs.is_leader = 0;
-        rs.round = 0;
-        rs.blockNum = 0;
-        if (p.rng_mode == BCSIM_RNG_COUNTER) {
-          raft_arm_election(c, rs);
-        } else {  // START draws run in node order at t=0: stream index = node id
-          const int32_t r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + i, p.cap_glibc);
-          rs.next_election = ctx_timer(c, TM_RAFT_ELECTION, AT(p.raft_elec, r % 150, 150));
-        }
-      } else {  // :58-139
-        xs.t_max = 0;
-        xs.command = 'e';
-        xs.t_store = 0;
-        xs.ticket = 0;
-        xs.is_commit = 0;
-        xs.proposal = enc_raw(p, static_cast<int32_t>(i));
-        xs.vs = 0;
-        xs.vf = 0;
-        if (i < p.paxos_proposers) (void)ctx_timer(c, TM_PAXOS_TICKET, 0);
-      }
-    } else {  // StopApplication
-      stop_pending = false;
-      if (PROTO == BCSIM_RAFT && rs.is_leader == 1)
-        ctx_trace(c, BCSIM_TR_RAFT_STOP, rs.blockNum, rs.round, 0);
-    }
   }
 
+  // ---- windows: [t_lo, t_hi) split so that each holds <= cap_arr arrivals.
+  // At one instant a node receives at most one record per in-edge (links are
+  // FIFO and serialise), and cap_arr > deg, so every window is non-empty.
+  long long tmax_ev = LLONG_MIN;
+  long long wa = t_lo;
+  for (;;) {
+    long long wb = t_hi;
+    uint32_t n;
+    if (m > p.cap_arr && scan_count(p, &ctl[1], seg_b, m, cs, wa, t_hi) > p.cap_arr) {
+      long long lo = wa, hi = t_hi;  // count(lo) <= cap < count(hi)
+      while (hi - lo > 1) {
+        const long long mid = lo + (hi - lo) / 2;
+        if (scan_count(p, &ctl[1], seg_b, m, cs, wa, mid) <= p.cap_arr)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      wb = lo;
+      if (wb == wa) {  // > cap_arr arrivals at one instant (cap_arr <= deg)
+        if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
+        return;
+      }
+    }
+    // select this window's arrivals and sort them by (t, t_sched, origin)
+    __syncthreads();
+    if (tid == 0) ctl[0] = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < m; k += blockDim.x) {
+      const Rec r = AT(p.grp, seg_b + k, p.cap_bucket);
+      const long long t = cs + r.t_off;
+      if (t >= wa && t < wb) {
+        const uint32_t slot = atomicAdd(&ctl[0], 1u);
+        if (slot < p.cap_arr) {
+          SKey s;
+          s.hi = (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~r.dt);
+          s.lo = r.origin;
+          s.idx = k;
+          keys[slot] = s;
+        }
+      }
+    }
+    __syncthreads();
+    n = ctl[0];
+    if (n > p.cap_arr) {  // unreachable by construction
+      if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
+      return;
+    }
+    uint32_t P2 = 2;
+    while (P2 < n) P2 <<= 1;
+    for (uint32_t k = n + tid; k < P2; k += blockDim.x) {
+      SKey s;
+      s.hi = ~0ull;
+      s.lo = ~0u;
+      s.idx = 0;
+      keys[k] = s;
+    }
+    __syncthreads();
+    for (uint32_t k2 = 2; k2 <= P2; k2 <<= 1) {
+      for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+        for (uint32_t t = tid; t < P2; t += blockDim.x) {
+          const uint32_t ixj = t ^ j;
+          if (ixj > t) {
+            const SKey a = keys[t], b = keys[ixj];
+            const bool up = (t & k2) == 0;
+            if (up ? skey_gt(a, b) : skey_gt(b, a)) {
+              keys[t] = b;
+              keys[ixj] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // gather the records in key order into LDS (same bytes as the keys:
+    // indices go through registers first); edge -> reverse edge here
+    uint32_t ix[kScanPerThread];
+#pragma unroll
+    for (int j = 0; j < kScanPerThread; ++j) {
+      const uint32_t k = tid + j * kScanThreads;
+      ix[j] = k < n ? keys[k].idx : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kScanPerThread; ++j) {
+      const uint32_t k = tid + j * kScanThreads;
+      if (k < n) {
+        Rec r = AT(p.grp, seg_b + ix[j], p.cap_bucket);
+        r.edge = AT(p.rev, r.edge, p.E);
+        recs[k] = r;
+      }
+    }
+    __syncthreads();
+
+    if (tid == 0) {
+      uint32_t ai = 0;
+      for (;;) {
+        // candidates
+        int which = -1;  // 0 arrival, 1 timer, 2 start, 3 stop
+        Key best{};
+        Rec rec{};
+        int tsel = -1;
+        if (ai < n) {
+          rec = recs[ai];
+          best.t = cs + rec.t_off;
+          best.ts = best.t - rec.dt;
+          best.origin = rec.origin;
+          best.sub = rec.sub;
+          which = 0;
+        }
+        for (uint32_t k = 0; k < c.cap_t; ++k) {
+          const TimerEnt& te = tm[k];
+          if (!te.alive || te.pending_draw || te.t >= wb || te.t < t_lo) continue;
+          const Key kk{te.t, te.ts, i, te.sub};
+          if (which < 0 || key_less(kk, best)) {
+            best = kk;
+            which = 1;
+            tsel = static_cast<int>(k);
+          }
+        }
+        if (start_pending && 0 < wb) {
+          const Key kk{0, -1, i, 0};
+          if (which < 0 || key_less(kk, best)) {
+            best = kk;
+            which = 2;
+          }
+        }
+        if (stop_pending && p.stop_ns < wb) {
+          const Key kk{p.stop_ns, -1, i, 1};
+          if (which < 0 || key_less(kk, best)) {
+            best = kk;
+            which = 3;
+          }
+        }
+        TRAIL(c);
+        if (which < 0) break;
+        c.cur = best;
+        if (best.t > tmax_ev) tmax_ev = best.t;
+        ++c.events;
+        if (which == 0) {
+          ++ai;
+          Msg msg;
+          msg.type = rec.type;
+          msg.f[0] = rec.f0;
+          msg.f[1] = rec.f1;
+          msg.f[2] = rec.f2;
+          msg.big = rec.big;
+          if (rec.type < BCSIM_MSG_TYPES) ++c.deliv[rec.type];
+          TRAIL(c);
+          // rec.edge is the reverse edge (receiver -> sender) from the gather
+          if (p.echo) {  // socket->SendTo(packet, 0, from): reverse-link occupancy
+            ctx_op(c, mk_op(p, best.t, rec.dt, rec.origin, rec.sub, rec.edge, msg, OP_ECHO, 0));
+            ++c.echoes;
+          }
+          if (PROTO == BCSIM_PBFT) {
+            if (best.t == ((best.t / p.pbft_period) * p.pbft_period) && best.ts <= best.t - p.pbft_period)
+              set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
+            pbft_recv(c, ps, msg, rec.edge);
+          } else if (PROTO == BCSIM_RAFT) {
+            raft_recv(c, rs, msg, rec.edge);
+          } else {
+            paxos_recv(c, xs, msg, rec.edge);
+          }
+        } else if (which == 1) {
+          TimerEnt& te = tm[tsel];
+          te.alive = 0;
+          if (PROTO == BCSIM_RAFT) {
+            if (te.kind == TM_RAFT_ELECTION) {  // sendVote :391-401
+              rs.has_voted = 1;
+              ctx_bcast(c, mkmsg(RF_VOTE_REQ, enc_raw(p, static_cast<int32_t>(i)), 0, 0, 0), false);
+              ctx_trace(c, BCSIM_TR_RAFT_ELECTION, 0, 0, 0);
+              raft_arm_election(c, rs);
+            } else if (te.kind == TM_RAFT_HEARTBEAT) {
+              raft_heartbeat(c, rs);
+            } else if (te.kind == TM_RAFT_PROPOSAL) {  // setProposal :432-435
+              rs.acv = 1;
+            }
+          } else if (PROTO == BCSIM_PAXOS) {
+            if (te.kind == TM_PAXOS_TICKET) paxos_ticket(c, xs);
+          }
+        } else if (which == 2) {  // StartApplication
+          start_pending = false;
+          if (PROTO == BCSIM_PBFT) {  // :97-158; globals reset host-side
+            ps.leader = 0;
+            ps.block_num = 0;
+            AT(p.tick_sub, g, p.NT) = c.sub++;  // Schedule(Seconds(timeout), SendBlock) :155
+            AT(p.tick_alive, g, p.NT) = 1;
+          } else if (PROTO == BCSIM_RAFT) {  // :75-115
+            rs.m_value = 0;
+            rs.vs = 0;
+            rs.vf = 0;
+            rs.has_voted = 0;
+            rs.acv = 0;
+            rs.is_leader = 0;
+            rs.round = 0;
+            rs.blockNum = 0;
+            if (p.rng_mode == BCSIM_RNG_COUNTER) {
+              raft_arm_election(c, rs);
+            } else {  // START draws run in node order at t=0: stream index = node id
+              const int32_t r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + i, p.cap_glibc);
+              rs.next_election = ctx_timer(c, TM_RAFT_ELECTION, AT(p.raft_elec, r % 150, 150));
+            }
+          } else {  // :58-139
+            xs.t_max = 0;
+            xs.command = 'e';
+            xs.t_store = 0;
+            xs.ticket = 0;
+            xs.is_commit = 0;
+            xs.proposal = enc_raw(p, static_cast<int32_t>(i));
+            xs.vs = 0;
+            xs.vf = 0;
+            if (i < p.paxos_proposers) (void)ctx_timer(c, TM_PAXOS_TICKET, 0);
+          }
+        } else {  // StopApplication
+          stop_pending = false;
+          if (PROTO == BCSIM_RAFT && rs.is_leader == 1)
+            ctx_trace(c, BCSIM_TR_RAFT_STOP, rs.blockNum, rs.round, 0);
+        }
+      }
+    }
+    if (wb >= t_hi) break;
+    wa = wb;
+  }
+  if (tid != 0) return;
   // write back
   TRAIL(c);
   AT(p.sub, g, p.NT) = c.sub;
