@@ -17,10 +17,10 @@ run() {
 steps=${*:-checked parity smoke bench prof}
 for st in $steps; do
   case $st in
-    checked) run checked 600 env BCSIM_LIB="$PWD/blockchain-simulator_amd/libbcsim_checked.so" BCSIM_SYNC_EACH=1 python tests/parity_run.py ;;
-    parity)  run parity 900 python -m pytest tests -m gpu -x -q ;;
-    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench1k) run bench1k 600 python bench.py --nodes 1024 --cpu-budget 5 ;;
+    checked) run checked 240 env BCSIM_LIB="$PWD/blockchain-simulator_amd/libbcsim_checked.so" BCSIM_SYNC_EACH=1 python tests/parity_run.py ;;
+    parity)  run parity 300 python -m pytest tests -m gpu -x -q ;;
+    smoke)   run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench1k) run bench1k 300 python bench.py --nodes 1024 --cpu-budget 5 ;;
     bench)   run bench 900 python bench.py ;;
     prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python bench.py --no-cpu-baseline ;;
     *) echo "unknown step $st"; exit 2 ;;
