@@ -29,6 +29,7 @@ struct Ctl {
   uint32_t trace_cnt, vlog_cnt, dreq_cnt, ov_cnt;
   int32_t dbg;
   long long scal[4];  // next_local, ov_min_cell, n_alive_ticks, spare
+  // followed by bucket_cnt[B] and x_cnt[B]
 };
 
 struct Sim {
@@ -51,8 +52,12 @@ struct Sim {
   // host mirrors
   Ctl* ctl_h = nullptr;  // pinned
   uint32_t* bcnt_h = nullptr;
+  uint32_t* xcnt_h = nullptr;
   void* ctl_d = nullptr;
   std::vector<uint32_t> bcnt;  // bucket counts (host view)
+  std::vector<uint32_t> xcnt;  // extras counts (host view)
+  int x_active = 0;            // extras of the grouped cell are in xgrp
+  uint32_t bs_scan = 64, bs_link = 64;
   long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
   long long n_alive = 0;
   uint64_t cells = 0;
@@ -82,9 +87,11 @@ static std::string trail_dump(const Sim& s) {
   return out;
 }
 
+// k_scan dynamic LDS: akey u64 | asec u32 | arec Rec | acls u32 per staged arrival + timers
 static size_t scan_lds_bytes(const KP& p) {
-  return 64 + static_cast<size_t>(p.cap_arr) * sizeof(Rec) + p.cap_timers * sizeof(TimerEnt);
+  return static_cast<size_t>(p.cap_arr) * (8 + 4 + sizeof(Rec) + 4) + p.cap_timers * sizeof(TimerEnt);
 }
+static size_t link_lds_bytes(const KP& p) { return (2ull * (p.deg_max + 1) + p.cap_ops) * 4; }
 
 template <typename T>
 static int dalloc(Sim& s, T** p, size_t count) {
@@ -163,6 +170,13 @@ static int build_rev(Sim& s) {
   for (uint32_t a = 0; a < s.N; ++a)
     for (uint32_t e = s.row[a]; e < s.row[a + 1]; ++e) {
       if (s.col[e] >= s.N || s.col[e] == a) return BCSIM_E_INVAL;
+      // rows list peers in ascending id order (the reference's peer order,
+      // blockchain-simulator.cc:34-51): a receiver's inbox row is then in
+      // canonical origin order
+      if (e > s.row[a] && s.col[e] <= s.col[e - 1]) {
+        g_detail = "CSR rows must list peers in ascending id order";
+        return BCSIM_E_INVAL;
+      }
       keys[e] = (static_cast<uint64_t>(a) << 32) | s.col[e];
       idx[e] = e;
     }
@@ -274,56 +288,78 @@ static int setup_device(Sim& s) {
 
   // topology
   uint32_t *row, *col, *rev;
-  int64_t* prop;
+  int64_t *prop, *prop_in;
   if ((rc = dalloc(s, &row, s.N + 1)) || (rc = dalloc(s, &col, s.E)) || (rc = dalloc(s, &rev, s.E)) ||
-      (rc = dalloc(s, &prop, s.E)))
+      (rc = dalloc(s, &prop, s.E)) || (rc = dalloc(s, &prop_in, s.E)))
     return rc;
+  std::vector<int64_t> pin(s.E);
+  int64_t dt_max = 0;
+  for (uint32_t q = 0; q < s.E; ++q) {
+    pin[q] = s.prop[s.rev[q]];  // arrival at in-slot q travelled edge rev[q]
+    dt_max = std::max(dt_max, pin[q] + std::max(p.tx_last[0], p.tx_last[1]));
+  }
+  if (dt_max >= (1ll << 32)) {
+    g_detail = "propagation + frame time must be < 2^32 ns";
+    return BCSIM_E_UNSUPPORTED;
+  }
   HIPCHK(hipMemcpy(row, s.row.data(), (s.N + 1) * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(col, s.col.data(), static_cast<size_t>(s.E) * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(rev, s.rev.data(), static_cast<size_t>(s.E) * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(prop, s.prop.data(), static_cast<size_t>(s.E) * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(prop_in, pin.data(), static_cast<size_t>(s.E) * 8, hipMemcpyHostToDevice));
   p.row = row;
   p.col = col;
   p.rev = rev;
   p.prop = prop;
+  p.prop_in = prop_in;
 
   // capacities
   const uint64_t NT = s.NT;
   // k_scan stages up to cap_arr arrivals per window in LDS (32 B each); a
   // cell with more is split into windows, so cap_arr only bounds one instant
-  const uint64_t arr_want = next_pow2(std::max<uint64_t>(64, 2ull * s.deg_max + 64));
-  p.cap_arr = static_cast<uint32_t>(std::min<uint64_t>(kScanMaxArr, arr_want));
+  p.cap_arr = static_cast<uint32_t>(std::min<uint64_t>(kScanMaxArr, next_pow2(std::max<uint64_t>(64, s.deg_max + 64))));
+  if (p.cap_arr <= s.deg_max && s.deg_max >= kScanMaxArr) {
+    g_detail = "node degree exceeds the k_scan LDS window";
+    return BCSIM_E_UNSUPPORTED;
+  }
   p.cap_timers = c.cap_timers_per_node ? c.cap_timers_per_node : 8;
   if (p.cap_timers > 64) p.cap_timers = 64;
   p.cap_ops = c.cap_ops_per_node ? c.cap_ops_per_node
-                                 : static_cast<uint32_t>(std::max<uint64_t>(1024, 2 * arr_want + 256));
-  const size_t lds_link = (2ull * (s.deg_max + 1) + p.cap_ops) * 4;
-  if (lds_link > 150 * 1024) {
+                                 : static_cast<uint32_t>(std::max<uint64_t>(1024, 4ull * s.deg_max + 256));
+  if (link_lds_bytes(p) > 150 * 1024) {
     g_detail = "node degree / op capacity exceed the LDS budget of k_link";
     return BCSIM_E_UNSUPPORTED;
   }
+  s.bs_scan = static_cast<uint32_t>(std::min<uint64_t>(1024, std::max<uint64_t>(64, next_pow2(s.deg_max + 1))));
+  s.bs_link = s.bs_scan;
+  // inbox ring: one 16-byte slot per (bucket, replica, edge); as many buckets
+  // as ~8 GiB allows, 8..64
+  const uint64_t per_bucket = static_cast<uint64_t>(s.R) * s.E * sizeof(Rec);
   s.B = c.n_buckets ? c.n_buckets : 0;
-  uint64_t cap_b = c.cap_bucket_records;
-  if (cap_b == 0) cap_b = std::max<uint64_t>(4096, NT * (static_cast<uint64_t>(s.deg_max) + 8) * 2);
-  if (cap_b > 0xFFFFFFF0ull) cap_b = 0xFFFFFFF0ull;
-  if (s.B == 0) {  // as many buckets as ~8 GB allows, 8..256
-    const uint64_t per = cap_b * sizeof(Rec);
-    uint64_t nb = per ? (8ull << 30) / per : 256;
-    s.B = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(256, nb)));
+  if (s.B == 0) {
+    const uint64_t nb = per_bucket ? (8ull << 30) / per_bucket : kMaxBuckets;
+    s.B = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(kMaxBuckets, nb)));
   }
-  if (s.B < 2) s.B = 2;
+  if (s.B < 2 || s.B > static_cast<uint32_t>(kMaxBuckets)) {
+    g_detail = "n_buckets must be in [2, 64]";
+    return BCSIM_E_INVAL;
+  }
   p.n_buckets = s.B;
-  p.cap_bucket = static_cast<uint32_t>(cap_b);
-  p.cap_ov = static_cast<uint32_t>(std::min<uint64_t>(cap_b * 4, 1ull << 24));
+  uint64_t cap_x = c.cap_bucket_records;
+  if (cap_x == 0) cap_x = std::max<uint64_t>(65536, NT * 8);
+  p.cap_x = static_cast<uint32_t>(std::min<uint64_t>(cap_x, 1ull << 26));
+  p.cap_ov = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(1ull << 20, NT * 256), 1ull << 26));
   p.cap_trace = static_cast<uint32_t>(std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1u << 20, NT * 256)));
   p.cap_vlog = 1u << 20;
   p.cap_dreq = static_cast<uint32_t>(std::max<uint64_t>(4096, 4 * NT));
   p.cap_E = static_cast<uint64_t>(s.R) * s.E;
+  p.cap_inbox = static_cast<uint64_t>(s.B) * s.R * s.E;
+  p.cap_xbuf = static_cast<uint64_t>(s.B) * p.cap_x;
 
   // dynamic LDS above the 64 KiB default needs an explicit opt-in (160 KiB per CU on gfx950)
   {
     const size_t lds_scan = scan_lds_bytes(p);
-    if (lds_scan > 160 * 1024 - 64) {
+    if (lds_scan + sizeof(ScanShared) > 160 * 1024) {
       g_detail = "k_scan LDS request too large";
       return BCSIM_E_UNSUPPORTED;
     }
@@ -334,7 +370,7 @@ static int setup_device(Sim& s) {
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_link),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_link)));
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(link_lds_bytes(p))));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_pbft_tick),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(s.N)));
   }
@@ -371,9 +407,12 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.timers, NT * p.cap_timers)) || (rc = dalloc(s, &p.ops, NT * p.cap_ops)) ||
       (rc = dalloc(s, &p.n_ops, NT)))
     return rc;
-  if ((rc = dalloc(s, &p.busy, static_cast<size_t>(s.R) * s.E))) return rc;
-  if ((rc = dalloc(s, &p.bucket, static_cast<size_t>(s.B) * p.cap_bucket)) ||
-      (rc = dalloc(s, &p.ov, p.cap_ov)) || (rc = dalloc(s, &p.grp, p.cap_bucket)))
+  if ((rc = dalloc(s, &p.busy, static_cast<size_t>(s.R) * s.E)) ||
+      (rc = dalloc(s, &p.lastc, static_cast<size_t>(s.R) * s.E)))
+    return rc;
+  if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
+      (rc = dalloc(s, &p.xbuf, p.cap_xbuf)) || (rc = dalloc(s, &p.xgrp, p.cap_x)) ||
+      (rc = dalloc(s, &p.ov, p.cap_ov)))
     return rc;
   if ((rc = dalloc(s, &p.seg_cnt, NT)) || (rc = dalloc(s, &p.seg_off, NT + 1)) ||
       (rc = dalloc(s, &p.cursor, NT)))
@@ -384,9 +423,10 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.counters, static_cast<size_t>(s.R) * CNT_N)) || (rc = dalloc(s, &p.kstat, 8)))
     return rc;
   if ((rc = dalloc(s, &p.node_tnext, NT)) || (rc = dalloc(s, &p.node_onext, NT))) return rc;
-  // control block: Ctl + bucket counts, contiguous for one read-back
+  // control block: Ctl + bucket counts + extras counts, contiguous for one read-back
+  const size_t ctl_bytes = sizeof(Ctl) + 8ull * s.B;
   char* ctl = nullptr;
-  if ((rc = dalloc(s, &ctl, sizeof(Ctl) + 4ull * s.B))) return rc;
+  if ((rc = dalloc(s, &ctl, ctl_bytes))) return rc;
   s.ctl_d = ctl;
   Ctl* cd = reinterpret_cast<Ctl*>(ctl);
   p.err = &cd->err;
@@ -397,8 +437,10 @@ static int setup_device(Sim& s) {
   p.ov_cnt = &cd->ov_cnt;
   p.scal = cd->scal;
   p.bucket_cnt = reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl));
-  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), sizeof(Ctl) + 4ull * s.B));
+  p.x_cnt = p.bucket_cnt + s.B;
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), ctl_bytes));
   s.bcnt_h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.ctl_h) + sizeof(Ctl));
+  s.xcnt_h = s.bcnt_h + s.B;
 
   // glibc stream tables
   const bool need_glibc = c.rng_mode == BCSIM_RNG_GLIBC &&
@@ -439,6 +481,9 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemset(p.timers, 0, NT * p.cap_timers * sizeof(TimerEnt)));
   HIPCHK(hipMemset(p.n_ops, 0, NT * 4));
   HIPCHK(hipMemset(p.busy, 0, static_cast<size_t>(s.R) * s.E * 8));
+  HIPCHK(hipMemset(p.lastc, 0xFF, static_cast<size_t>(s.R) * s.E * 8));  // -1: no record yet
+  HIPCHK(hipMemset(p.inbox, 0, p.cap_inbox * sizeof(Rec)));
+  HIPCHK(hipMemset(p.iflag, 0, static_cast<size_t>(s.B) * NT));
   HIPCHK(hipMemset(p.seg_cnt, 0, NT * 4));
   HIPCHK(hipMemset(p.seg_off, 0, (NT + 1) * 4));
   HIPCHK(hipMemset(p.cursor, 0, NT * 4));
@@ -461,7 +506,7 @@ static int setup_device(Sim& s) {
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p.node_onext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(s.ctl_d, 0, sizeof(Ctl) + 4ull * s.B));
+  HIPCHK(hipMemset(s.ctl_d, 0, ctl_bytes));
   long long sc0[4] = {LLONG_MAX, LLONG_MAX, 0, 0};
   HIPCHK(hipMemcpy(p.scal, sc0, sizeof sc0, hipMemcpyHostToDevice));
   // counters' t_last slot starts at 0 (max)
@@ -469,6 +514,7 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &s.kp_dev, 1))) return rc;
   HIPCHK(hipMemcpy(s.kp_dev, &s.kp, sizeof(KP), hipMemcpyHostToDevice));
   s.bcnt.assign(s.B, 0);
+  s.xcnt.assign(s.B, 0);
   s.next_tick = (c.protocol == BCSIM_PBFT) ? p.pbft_period : INT64_MAX;
   s.n_alive = (c.protocol == BCSIM_PBFT) ? 1 : 0;  // STARTs arm the ticks
   return BCSIM_OK;
@@ -512,24 +558,26 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
 }
 #define launch(s, cls, kernel, ...) launch_named(s, #kernel, cls, kernel, __VA_ARGS__)
 
-static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs) {
+static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
-  dim3 grid(s.NT), block(kScanThreads);
+  dim3 grid(s.NT), block(s.bs_scan);
+  const int fw = final_win ? 1 : 0, xa = s.x_active;
   int rc;
   if (s.cfg.protocol == BCSIM_PBFT)
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_PBFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs);
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_PBFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   else if (s.cfg.protocol == BCSIM_RAFT)
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_RAFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs);
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_RAFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   else
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp_dev, cell, lo, hi, cs);
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   if (rc) return rc;
-  const size_t lds_link = (2ull * (s.deg_max + 1) + s.kp.cap_ops) * 4;
-  return launch(s, KS_LINK, k_link, grid, block, lds_link, s.kp_dev, cell, hi);
+  return launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, hi);
 }
 
+// Prepare cell `cell`: move overflow records whose cell entered the ring into
+// the inbox, and group the cell's extras (second records of one edge) by
+// receiver.
 static int group_cell(Sim& s, long long cell) {
   const uint32_t b = static_cast<uint32_t>(cell % s.B);
-  // rebin far-future arrivals first
   if (s.ov_min <= cell + static_cast<long long>(s.B) - 1) {
     uint32_t nov = 0;
     HIPCHK(hipMemcpyAsync(&nov, s.kp.ov_cnt, 4, hipMemcpyDeviceToHost, s.stream));
@@ -540,37 +588,46 @@ static int group_cell(Sim& s, long long cell) {
       int rc = launch(s, KS_GROUP, k_rebin, dim3((nov + 255) / 256), dim3(256), 0, s.kp_dev, cell, nov);
       if (rc) return rc;
     }
-    HIPCHK(hipMemcpyAsync(s.bcnt_h, s.kp.bucket_cnt, 4ull * s.B, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipMemcpyAsync(s.bcnt_h, s.kp.bucket_cnt, 8ull * s.B, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipMemcpyAsync(&s.ov_min, s.kp.scal + 1, 8, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipStreamSynchronize(s.stream));
-    for (uint32_t k = 0; k < s.B; ++k) s.bcnt[k] = s.bcnt_h[k];
+    for (uint32_t k = 0; k < s.B; ++k) {
+      s.bcnt[k] = s.bcnt_h[k];
+      s.xcnt[k] = s.xcnt_h[k];
+    }
     if (s.ov_min == LLONG_MAX) {
       // everything rebinned: reset the overflow list
       HIPCHK(hipMemsetAsync(s.kp.ov_cnt, 0, 4, s.stream));
     }
   }
-  const uint32_t n = s.bcnt[b];
-  if (n > s.kp.cap_bucket) return BCSIM_E_OVERFLOW;
-  HIPCHK(hipMemsetAsync(s.kp.seg_cnt, 0, s.NT * 4ull, s.stream));
-  HIPCHK(hipMemsetAsync(s.kp.cursor, 0, s.NT * 4ull, s.stream));
-  int rc;
-  if (n) {
-    if ((rc = launch(s, KS_GROUP, k_count, dim3((n + 255) / 256), dim3(256), 0, s.kp_dev, b, n))) return rc;
+  const uint32_t nx = s.xcnt[b];
+  if (nx > s.kp.cap_x) {
+    g_detail = "extras list of a cell overflowed (cap_bucket_records)";
+    return BCSIM_E_OVERFLOW;
   }
-  if ((rc = launch(s, KS_GROUP, k_offsets, dim3(1), dim3(1024), 0, s.kp_dev))) return rc;
-  if (n) {
-    if ((rc = launch(s, KS_GROUP, k_place, dim3((n + 255) / 256), dim3(256), 0, s.kp_dev, b, n))) return rc;
+  s.x_active = 0;
+  if (nx) {
+    HIPCHK(hipMemsetAsync(s.kp.seg_cnt, 0, s.NT * 4ull, s.stream));
+    HIPCHK(hipMemsetAsync(s.kp.cursor, 0, s.NT * 4ull, s.stream));
+    int rc;
+    if ((rc = launch(s, KS_GROUP, k_xcount, dim3((nx + 255) / 256), dim3(256), 0, s.kp_dev, b, nx))) return rc;
+    if ((rc = launch(s, KS_GROUP, k_offsets, dim3(1), dim3(1024), 0, s.kp_dev))) return rc;
+    if ((rc = launch(s, KS_GROUP, k_xplace, dim3((nx + 255) / 256), dim3(256), 0, s.kp_dev, b, nx))) return rc;
+    s.x_active = 1;
   }
   s.grouped_cell = cell;
   return BCSIM_OK;
 }
 
 static int readback(Sim& s) {
-  HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, sizeof(Ctl) + 4ull * s.B, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, sizeof(Ctl) + 8ull * s.B, hipMemcpyDeviceToHost, s.stream));
   HIPCHK(hipStreamSynchronize(s.stream));
   int rc = ev_collect(s);
   if (rc) return rc;
-  for (uint32_t k = 0; k < s.B; ++k) s.bcnt[k] = s.bcnt_h[k];
+  for (uint32_t k = 0; k < s.B; ++k) {
+    s.bcnt[k] = s.bcnt_h[k];
+    s.xcnt[k] = s.xcnt_h[k];
+  }
   s.next_local = s.ctl_h->scal[0];
   s.ov_min = s.ctl_h->scal[1];
   if (s.ctl_h->err) {
@@ -626,14 +683,14 @@ static int run(Sim& s, int64_t t_until) {
     if (tick) {
       const long long tk = s.next_tick;
       if (tk > lo) {
-        if ((rc = do_scan(s, c, lo, tk, cs))) return rc;
+        if ((rc = do_scan(s, c, lo, tk, cs, false))) return rc;
       }
       HIPCHK(hipMemsetAsync(s.kp.scal + 2, 0, 8, s.stream));
       if ((rc = launch(s, KS_AUX, k_pbft_tick, dim3(s.R), dim3(1024), static_cast<size_t>(s.N), s.kp_dev, tk)))
         return rc;
-      if ((rc = do_scan(s, c, tk, hi, cs))) return rc;
+      if ((rc = do_scan(s, c, tk, hi, cs, hi == ce))) return rc;
     } else {
-      if ((rc = do_scan(s, c, lo, hi, cs))) return rc;
+      if ((rc = do_scan(s, c, lo, hi, cs, hi == ce))) return rc;
     }
     if (s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC) {
       if ((rc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp_dev, 0u))) return rc;
@@ -642,6 +699,7 @@ static int run(Sim& s, int64_t t_until) {
     if (hi == ce) {
       // cell finished: its bucket is free again
       HIPCHK(hipMemsetAsync(s.kp.bucket_cnt + (c % s.B), 0, 4, s.stream));
+      HIPCHK(hipMemsetAsync(s.kp.x_cnt + (c % s.B), 0, 4, s.stream));
     }
     if ((rc = readback(s))) return rc;
     if (tick) {
@@ -655,6 +713,8 @@ static int run(Sim& s, int64_t t_until) {
     if (hi == ce) {
       s.grouped_cell = -1;
       s.bcnt[c % s.B] = 0;
+      s.xcnt[c % s.B] = 0;
+      s.x_active = 0;
     }
   }
   return BCSIM_OK;
@@ -939,13 +999,15 @@ int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, u
     if (launches_out4) launches_out4[k] = s.launches[k];
   }
   if (bytes_out4) {
-    // k_link algorithmic bytes: 32 B per op read, 32 B per
-    // record written, 16 B per touched edge (busy_until read + write),
-    // 32 B per op kept (compaction write)
-    bytes_out4[bcsim::KS_LINK] = 32.0 * ks[1] + 32.0 * ks[0] + 16.0 * ks[2] + 32.0 * ks[3];
-    bytes_out4[bcsim::KS_SCAN] = 0;
+    // algorithmic bytes.  k_link: 32 B per due op read, 16 B
+    // per record scattered, 32 B per touched edge (busy_until + last_cell
+    // read + write), 32 B per op kept (compaction write).  k_scan: 16 B per
+    // record read + 16 B slot release, 32 B per op written (echo + reply).
+    bytes_out4[bcsim::KS_LINK] = 32.0 * ks[bcsim::KST_OPS] + 16.0 * ks[bcsim::KST_REC] +
+                                 32.0 * ks[bcsim::KST_EDGES] + 32.0 * ks[bcsim::KST_KEPT];
+    bytes_out4[bcsim::KS_SCAN] = 32.0 * ks[bcsim::KST_DELIV];
     bytes_out4[bcsim::KS_GROUP] = 0;
-    bytes_out4[bcsim::KS_AUX] = static_cast<double>(ks[0]);  // records emitted
+    bytes_out4[bcsim::KS_AUX] = static_cast<double>(ks[bcsim::KST_REC]);  // records emitted
   }
   return BCSIM_OK;
 }

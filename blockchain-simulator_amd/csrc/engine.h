@@ -2,12 +2,18 @@
 //
 // Layout in HBM:
 //   node state      SoA, one slot per (replica, node) = "gnode" g = rep*N + i
-//   link state      busy_until[rep*E + e], sender-major CSR edge order
-//   arrivals        B time buckets (cells of length L = lookahead) of 32-byte
-//                   Rec records, appended in per-workgroup chunks; regrouped
-//                   by destination each cell (counting sort) into `grp`
+//   link state      busy_until[rep*E + e] and last_cell[rep*E + e], sender-major
+//                   CSR edge order (edge e = i -> col[e], rows ascending)
+//   inbox           B time buckets; bucket b holds cell c (c % B == b) as one
+//                   16-byte Rec per directed edge, stored at the RECEIVER's
+//                   in-slot: the arrival on edge i->s lives at index rev[e]
+//                   (= the edge s->i, inside s's CSR row), so a receiver reads
+//                   its arrivals as one contiguous row, already in ascending
+//                   origin order (the canonical tie order).  A second record on
+//                   the same edge in the same cell goes to the bucket's extras
+//                   list; arrivals beyond the ring go to the overflow list.
 //   pending ops     per gnode list of 32-byte Op (echo / unicast / broadcast)
-//   timers          per gnode list of TimerEnt
+//   timers          per gnode list of TimerEnt (Raft / Paxos)
 #pragma once
 #include <stdint.h>
 
@@ -17,27 +23,35 @@ namespace bcsim {
 
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;
 
-// 32-byte arrival record (a packet delivered to a listener socket).
+// Rec::flags
+enum : uint8_t {
+  RF_VALID = 1,  // slot holds an undelivered packet
+  RF_BIG = 2,    // block / proposal sized payload
+  RF_OWNER = 4   // (overflow list only) first record of its (edge, cell): goes to the slot
+};
+
+// 16-byte arrival record: one packet delivered to a listener socket.  The
+// sender (col[slot]), the edge and dt = t - t_sched (= propagation + last
+// frame serialisation) are implied by the slot it is stored at.
 struct __attribute__((aligned(16))) Rec {
-  uint32_t t_off;   // arrival time - cell start of the arrival cell
-  uint32_t dt;      // arrival time - t_sched (transmit start of last frame)
-  uint32_t dest;    // gnode of the receiver; kInvalid = padding slot
-  uint32_t origin;  // sender node id (within replica)
+  uint32_t t_off;   // arrival time - start of the arrival cell
   uint32_t sub;     // sender's schedule counter of the SendPacket
-  uint32_t edge;    // edge index (s->d) within the replica
   int16_t f0, f1;   // raw payload chars data[1], data[2]
   int16_t f2;       // data[3]
   uint8_t type;     // charToInt(data[0])
-  uint8_t big;      // 1 = block / proposal sized payload
+  uint8_t flags;    // RF_*
 };
-static_assert(sizeof(Rec) == 32, "Rec must be 32 bytes");
+static_assert(sizeof(Rec) == 16, "Rec must be 16 bytes");
 
-// Far-future arrival (beyond the bucket ring).
-struct __attribute__((aligned(16))) OvRec {
-  int64_t cell;
-  int64_t pad;
+// Extras / overflow entry: a record that does not own its slot, or whose
+// cell is beyond the bucket ring.
+struct __attribute__((aligned(16))) XRec {
   Rec r;
+  int64_t cell;   // arrival cell (overflow list); -1 once rebinned
+  uint32_t slot;  // in-slot: edge index within the replica, in the receiver's row
+  uint32_t g;     // receiver gnode
 };
+static_assert(sizeof(XRec) == 32, "XRec must be 32 bytes");
 
 // op kinds
 enum : uint8_t { OP_ECHO = 0, OP_SEND = 1, OP_BCAST = 2, OP_BCAST_J = 3 };
@@ -118,5 +132,8 @@ enum {
 
 // kernel-class timing slots
 enum { KS_SCAN = 0, KS_LINK = 1, KS_GROUP = 2, KS_AUX = 3 };
+
+// link-kernel algorithmic counters (KP::kstat)
+enum { KST_REC = 0, KST_OPS = 1, KST_EDGES = 2, KST_KEPT = 3, KST_DELIV = 4, KST_SCAN_OPS = 5 };
 
 }  // namespace bcsim

@@ -10,22 +10,22 @@
 //   independent of every other node's and are processed in parallel:
 //
 //   per cell g:
-//     k_count / k_offsets / k_place   group the arrivals of cell g (bucket
-//                                     g % B) by destination node
-//     k_scan<P>                       one workgroup per node: LDS bitonic sort
-//                                     of its arrivals by the canonical key,
-//                                     then the protocol state machine in key
-//                                     order; emits link ops, timers, traces
-//     k_link                          one workgroup per node: per out-edge FIFO
-//                                     (busy_until), serialization + propagation,
-//                                     scatter of 32-byte arrival records into
-//                                     the time-bucketed inboxes (chunked,
-//                                     workgroup-aggregated atomics)
-//     (PBFT) k_pbft_tick              the 50 ms SendBlock tick of every node,
-//                                     which touches the file-scope globals
-//                                     n, n_round, v (pbft-node.cc:24-30)
-//     (Raft, glibc rng) k_draws       election-timeout draws in canonical
-//                                     global order
+//     (extras / overflow only) k_rebin, k_xcount/k_offsets/k_xplace
+//     k_scan<P>     one workgroup per node: stage the node's inbox row (one
+//                   16-byte slot per in-edge, ascending origin = canonical tie
+//                   order) in LDS, sort by the canonical key only if needed,
+//                   run the protocol:
+//                     PBFT   data-parallel: wave-ballot quorum ranks per
+//                            (phase, sequence), block scans for the schedule
+//                            counter / rand() draw / commit prefixes, every
+//                            lane emits its own echo / reply ops
+//                     Raft, Paxos  serial state machine in key order (lane 0)
+//     k_link        one workgroup per node: per out-edge FIFO (busy_until) in
+//                   canonical key order, serialization + propagation, and the
+//                   scatter of 16-byte records into the receivers' inbox
+//                   slots of the arrival cell
+//     (PBFT) k_pbft_tick   SendBlock tick of every node (globals n, n_round, v)
+//     (Raft, glibc rng) k_draws   election-timeout draws in canonical order
 //
 // Semantics are specified in DESIGN.md §2 and restated serially by oracle/
 // (the parity checker).  No code here calls the oracle.
@@ -44,7 +44,7 @@
 namespace bcsim {
 
 // ---------------------------------------------------------------------------
-// kernel parameter block (passed by value)
+// kernel parameter block (device-resident, one per simulation)
 struct KP {
   uint32_t N, R, NT, E;
   uint32_t protocol, delay_mode, rng_mode, encoding, echo;
@@ -61,7 +61,8 @@ struct KP {
   uint32_t jit_mod;
   // topology (per replica, shared)
   const uint32_t *row, *col, *rev;
-  const int64_t* prop;
+  const int64_t* prop;     // per edge (sender-major)
+  const int64_t* prop_in;  // per in-slot q: prop[rev[q]]
   // common node state
   uint32_t* sub;
   uint64_t* draws;
@@ -83,16 +84,21 @@ struct KP {
   uint32_t cap_ops;
   // links
   int64_t* busy;
-  // buckets / grouping
-  Rec* bucket;
-  uint32_t* bucket_cnt;
-  uint32_t n_buckets, cap_bucket;
-  OvRec* ov;
+  int64_t* lastc;  // cell of the last record emitted on the edge (-1: none)
+  // inbox
+  Rec* inbox;            // [B][R][E]
+  uint8_t* iflag;        // [B][NT] node has records in the bucket
+  uint32_t* bucket_cnt;  // [B] records in the bucket (slots + extras)
+  uint32_t* x_cnt;       // [B] extras in the bucket
+  uint32_t n_buckets;
+  XRec* xbuf;            // [B][cap_x]
+  uint32_t cap_x;
+  XRec* xgrp;            // extras of the current cell grouped by receiver
+  XRec* ov;
   uint32_t* ov_cnt;
   uint32_t cap_ov;
   uint32_t *seg_cnt, *seg_off, *cursor;
-  Rec* grp;
-  uint32_t cap_arr;  // LDS sort capacity (power of two)
+  uint32_t cap_arr;  // LDS staging capacity of k_scan (power of two, <= 4096)
   // outputs
   bcsim_trace_rec* trace;
   uint32_t* trace_cnt;
@@ -107,11 +113,11 @@ struct KP {
   uint32_t glibc_len;
   uint32_t* glibc_pos;  // per replica
   unsigned long long* counters;  // R * CNT_N
-  unsigned long long* kstat;     // link kernel algorithmic counters
+  unsigned long long* kstat;     // link / scan algorithmic counters (KST_*)
   int32_t* err;
-  int32_t* dbg;  // BCSIM_CHECKED builds: first out-of-bounds source line
+  int32_t* dbg;  // first error's source line
   unsigned long long* trail;  // BCSIM_CHECKED + BCSIM_TRAIL: host-mapped breadcrumbs
-  uint64_t cap_E, cap_EB, cap_txn, cap_glibc;
+  uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   long long *node_tnext, *node_onext;
   long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks
 };
@@ -125,11 +131,9 @@ __device__ inline void set_err_(const KP& p, int32_t code, int line) {
 }
 #define set_err(pp, code) set_err_((pp), (code), __LINE__)
 
-__device__ __attribute__((aligned(64))) char g_dummy[256];
-
 // Checked array access.  In BCSIM_CHECKED builds an out-of-range index is
-// recorded (source line in p.dbg, BCSIM_E_OVERFLOW in p.err) and redirected
-// to a per-thread dummy element instead of faulting the GPU.
+// recorded (source line in p.dbg, BCSIM_E_OVERFLOW in p.err) and the wave
+// stops instead of faulting the GPU.
 template <typename T>
 __device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int line) {
 #ifdef BCSIM_CHECKED
@@ -146,12 +150,6 @@ __device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int l
   do {                \
     if (*p.err) return; \
   } while (0)
-#else
-#define BAIL_IF_ERR() \
-  do {                \
-  } while (0)
-#endif
-#ifdef BCSIM_CHECKED
 #define TRAIL_AT(pp, g)                                                                        \
   do {                                                                                         \
     if ((pp).trail)                                                                            \
@@ -159,12 +157,23 @@ __device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int l
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                          \
   } while (0)
 #else
+#define BAIL_IF_ERR() \
+  do {                \
+  } while (0)
 #define TRAIL_AT(pp, g) \
   do {                  \
   } while (0)
 #endif
 #define TRAIL(c) TRAIL_AT(*(c).p, (c).g)
 #define AT(arr, idx, cap) at_(p, (arr), static_cast<uint64_t>(idx), static_cast<uint64_t>(cap), __LINE__)
+
+// Workgroups are dispatched round-robin over the 8 XCDs; give each XCD a
+// contiguous range of nodes so that concurrently running senders write
+// neighbouring inbox slots (same L2) and receivers read their own rows.
+__device__ inline uint32_t xcd_map(uint32_t b, uint32_t n) {
+  const uint32_t x = b & 7u, k = b >> 3, per = n >> 3, rem = n & 7u;
+  return x * per + min(x, rem) + k;
+}
 
 struct Key {
   int64_t t, ts;
@@ -195,8 +204,7 @@ __device__ inline int32_t ctr_rand(uint64_t seed, uint32_t rep, uint32_t node, u
 // getRandomDelay() of the running protocol: jit_delay/jit_mod are chosen on
 // the host (pbft-node.cc:68 / raft-node.cc:65 / paxos-node.cc:399).  A
 // device-side three-way branch on p.protocol here was miscompiled by the
-// ROCm 7.2 compiler in divergent code (the paxos arm used an unset address
-// register -> aperture violation), so there is deliberately no branch.
+// ROCm 7.2 compiler in divergent code, so there is no branch.
 __device__ inline int64_t delay_from_draw(const KP& p, int32_t r) {
   return AT(p.jit_delay, static_cast<uint32_t>(r) % p.jit_mod, p.jit_mod);
 }
@@ -225,16 +233,187 @@ __device__ inline int32_t mch(const Msg& m, int i) {
   return m.f[i - 1];
 }
 __device__ inline int32_t c2i(int32_t c) { return c - '0'; }
+__device__ inline Msg rec_msg(const Rec& r) {
+  Msg m;
+  m.type = r.type;
+  m.f[0] = r.f0;
+  m.f[1] = r.f1;
+  m.f[2] = r.f2;
+  m.big = (r.flags & RF_BIG) ? 1 : 0;
+  return m;
+}
+__device__ inline Msg mkmsg(int32_t type, int32_t f0, int32_t f1, int32_t f2, int32_t big) {
+  Msg m;
+  m.type = type;
+  m.f[0] = f0;
+  m.f[1] = f1;
+  m.f[2] = f2;
+  m.big = big;
+  return m;
+}
+
+__device__ inline Op mk_op(const KP& p, int64_t t, uint32_t dt, uint32_t origin, uint32_t sub,
+                           uint32_t edge, const Msg& m, uint8_t kind, uint8_t flags) {
+  Op o;
+  o.t = t;
+  o.dt = dt;
+  o.origin = origin;
+  o.sub = sub;
+  o.edge = edge;
+  o.f0 = to16(p, m.f[0]);
+  o.f1 = to16(p, m.f[1]);
+  o.f2 = to16(p, m.f[2]);
+  o.type = static_cast<uint8_t>(m.type);
+  o.kind_flags = static_cast<uint8_t>(kind | ((flags | (m.big ? OPF_BIG : 0)) << 2));
+  return o;
+}
+
+__device__ inline void emit_trace(const KP& p, const Key& k, uint32_t rep, uint32_t node, uint32_t kind,
+                                  int32_t a, int32_t b, int32_t c) {
+  const uint32_t pos = atomicAdd(p.trace_cnt, 1u);
+  if (pos >= p.cap_trace) {
+    set_err(p, BCSIM_E_OVERFLOW);
+    return;
+  }
+  bcsim_trace_rec r;
+  r.t_ns = k.t;
+  r.key_ts = k.ts;
+  r.key_origin = k.origin;
+  r.key_sub = k.sub;
+  r.replica = rep;
+  r.node = node;
+  r.kind = kind;
+  r.a = a;
+  r.b = b;
+  r.c = c;
+  AT(p.trace, pos, p.cap_trace) = r;
+}
+
+__device__ inline void emit_vlog(const KP& p, const Key& k, uint32_t rep, uint32_t node, int32_t v) {
+  const uint32_t pos = atomicAdd(p.vlog_cnt, 1u);
+  if (pos >= p.cap_vlog) {
+    set_err(p, BCSIM_E_OVERFLOW);
+    return;
+  }
+  VLog e;
+  e.t = k.t;
+  e.ts = k.ts;
+  e.origin = k.origin;
+  e.sub = k.sub;
+  e.target = node;
+  e.rep = rep;
+  e.v = v;
+  e.pad = 0;
+  AT(p.vlog, pos, p.cap_vlog) = e;
+}
+
+// ---- block-wide primitives (blockDim.x a multiple of 64, <= 1024) ----------
+constexpr int kMaxWaves = 16;
+
+// Ordered compaction rank: exclusive position of this thread's flag among
+// the block's set flags in thread order; `total` = number of set flags.
+__device__ inline uint32_t block_rank(bool f, uint32_t* wcnt, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const unsigned long long m = __ballot(f);
+  const uint32_t below = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
+  if (lane == 0) wcnt[w] = static_cast<uint32_t>(__popcll(m));
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+  for (uint32_t k = 0; k < nw; ++k) {
+    const uint32_t c = wcnt[k];
+    if (k < w) off += c;
+    tot += c;
+  }
+  __syncthreads();
+  total = tot;
+  return off + below;
+}
+
+// Exclusive block scan of four u32 lanes at once; totals in `tot`.
+__device__ inline uint4 block_scan4(uint4 v, uint4* wsum, uint4& tot) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint4 x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t a = __shfl_up(x.x, off, 64), b = __shfl_up(x.y, off, 64);
+    const uint32_t c = __shfl_up(x.z, off, 64), d = __shfl_up(x.w, off, 64);
+    if (lane >= static_cast<uint32_t>(off)) {
+      x.x += a;
+      x.y += b;
+      x.z += c;
+      x.w += d;
+    }
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint4 base = make_uint4(0, 0, 0, 0), t = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = 0; k < nw; ++k) {
+    const uint4 s = wsum[k];
+    if (k < w) {
+      base.x += s.x;
+      base.y += s.y;
+      base.z += s.z;
+      base.w += s.w;
+    }
+    t.x += s.x;
+    t.y += s.y;
+    t.z += s.z;
+    t.w += s.w;
+  }
+  __syncthreads();
+  tot = t;
+  return make_uint4(base.x + x.x - v.x, base.y + x.y - v.y, base.z + x.z - v.z, base.w + x.w - v.w);
+}
+
+// In-place exclusive scan of a[0..n) (LDS) with contiguous per-thread runs;
+// returns the total.  All threads must call it.
+__device__ inline uint32_t block_scan_array(uint32_t* a, uint32_t n, uint4* wsum) {
+  const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
+  const uint32_t b0 = min(n, threadIdx.x * per), b1 = min(n, b0 + per);
+  uint32_t s = 0;
+  for (uint32_t k = b0; k < b1; ++k) s += a[k];
+  uint4 tot;
+  const uint4 ex = block_scan4(make_uint4(s, 0, 0, 0), wsum, tot);
+  uint32_t acc = ex.x;
+  for (uint32_t k = b0; k < b1; ++k) {
+    const uint32_t v = a[k];
+    a[k] = acc;
+    acc += v;
+  }
+  __syncthreads();
+  return tot.x;
+}
+
+// Add `inc` to lds[key] once per distinct key of the wave (wave-aggregated
+// LDS atomics; all lanes of the wave must call it).
+__device__ inline void wave_add_by_key(bool act, uint32_t key, uint32_t inc, unsigned long long* lds) {
+  unsigned long long rem = __ballot(act);
+  const uint32_t lane = threadIdx.x & 63u;
+  while (rem) {
+    const int ld = __ffsll(static_cast<long long>(rem)) - 1;
+    const uint32_t kl = __shfl(key, ld, 64);
+    const bool mine = act && key == kl;
+    const unsigned long long same = __ballot(mine);
+    unsigned long long sum = 0;
+    // sum of inc over `same` lanes
+    uint32_t v = mine ? inc : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    sum = v;
+    if (lane == static_cast<uint32_t>(ld)) atomicAdd(&lds[kl], sum);
+    rem &= ~same;
+  }
+}
 
 // ---------------------------------------------------------------------------
-// grouping: counting sort of bucket records by destination node
-__global__ void k_count(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
+// extras grouping: counting sort of the cell's extras by receiver gnode
+__global__ void k_xcount(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  const uint32_t d = AT(p.bucket, static_cast<size_t>(b) * p.cap_bucket + k, static_cast<uint64_t>(p.n_buckets) * p.cap_bucket).dest;
-  if (d != kInvalid) atomicAdd(&AT(p.seg_cnt, d, p.NT), 1u);
+  const uint32_t g = AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf).g;
+  atomicAdd(&AT(p.seg_cnt, g, p.NT), 1u);
 }
 
 // single-block exclusive scan of seg_cnt[0..NT) -> seg_off[0..NT]
@@ -249,7 +428,6 @@ __global__ __launch_bounds__(1024) void k_offsets(const KP* __restrict__ pk) {
   for (uint32_t base = 0; base < p.NT; base += 1024) {
     const uint32_t idx = base + tid;
     const uint32_t v = idx < p.NT ? AT(p.seg_cnt, idx, p.NT) : 0u;
-    // inclusive wave scan
     uint32_t x = v;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -276,15 +454,14 @@ __global__ __launch_bounds__(1024) void k_offsets(const KP* __restrict__ pk) {
   if (tid == 0) AT(p.seg_off, p.NT, p.NT + 1) = carry;
 }
 
-__global__ void k_place(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
+__global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  const Rec r = AT(p.bucket, static_cast<size_t>(b) * p.cap_bucket + k, static_cast<uint64_t>(p.n_buckets) * p.cap_bucket);
-  if (r.dest == kInvalid) return;
-  const uint32_t pos = AT(p.seg_off, r.dest, p.NT + 1) + atomicAdd(&AT(p.cursor, r.dest, p.NT), 1u);
-  AT(p.grp, pos, p.cap_bucket) = r;
+  const XRec x = AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf);
+  const uint32_t pos = AT(p.seg_off, x.g, p.NT + 1) + atomicAdd(&AT(p.cursor, x.g, p.NT), 1u);
+  AT(p.xgrp, pos, p.cap_x) = x;
 }
 
 // move far-future arrivals whose cell entered the ring into their bucket
@@ -293,16 +470,26 @@ __global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) 
   BAIL_IF_ERR();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  OvRec& o = AT(p.ov, k, p.cap_ov);
+  XRec& o = AT(p.ov, k, p.cap_ov);
   if (o.cell < 0) return;
   if (o.cell < g_cur + static_cast<long long>(p.n_buckets)) {
     const uint32_t b = static_cast<uint32_t>(o.cell % p.n_buckets);
-    const uint32_t pos = atomicAdd(&p.bucket_cnt[b], 1u);
-    if (pos >= p.cap_bucket) {
-      set_err(p, BCSIM_E_OVERFLOW);
-      return;
+    const uint32_t rep = o.g / p.N;
+    XRec x = o;
+    const bool owner = (x.r.flags & RF_OWNER) != 0;
+    x.r.flags = static_cast<uint8_t>(x.r.flags & ~RF_OWNER);
+    if (owner) {
+      AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox) = x.r;
+    } else {
+      const uint32_t pos = atomicAdd(&p.x_cnt[b], 1u);
+      if (pos >= p.cap_x) {
+        set_err(p, BCSIM_E_OVERFLOW);
+        return;
+      }
+      AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
     }
-    AT(p.bucket, static_cast<size_t>(b) * p.cap_bucket + pos, static_cast<uint64_t>(p.n_buckets) * p.cap_bucket) = o.r;
+    AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(p.n_buckets) * p.NT) = 1;
+    atomicAdd(&p.bucket_cnt[b], 1u);
     o.cell = -1;
   } else {
     atomicMin(&p.scal[1], o.cell);
@@ -310,7 +497,7 @@ __global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) 
 }
 
 // ---------------------------------------------------------------------------
-// per-node serial protocol context (thread 0 of the node's workgroup)
+// per-node serial protocol context (Raft / Paxos: lane 0 of the node's workgroup)
 struct Ctx {
   const KP* p;
   uint32_t g, rep, i, deg;
@@ -326,56 +513,22 @@ struct Ctx {
 };
 
 __device__ inline void ctx_trace(Ctx& c, uint32_t kind, int32_t a, int32_t b, int32_t cc) {
-  const KP& p = *c.p;
   TRAIL(c);
-  const uint32_t pos = atomicAdd(p.trace_cnt, 1u);
-  if (pos >= p.cap_trace) {
-    set_err(p, BCSIM_E_OVERFLOW);
-    return;
-  }
-  bcsim_trace_rec r;
-  r.t_ns = c.cur.t;
-  r.key_ts = c.cur.ts;
-  r.key_origin = c.cur.origin;
-  r.key_sub = c.cur.sub;
-  r.replica = c.rep;
-  r.node = c.i;
-  r.kind = kind;
-  r.a = a;
-  r.b = b;
-  r.c = cc;
-  AT(p.trace, pos, p.cap_trace) = r;
+  emit_trace(*c.p, c.cur, c.rep, c.i, kind, a, b, cc);
 }
 
 __device__ inline void ctx_op(Ctx& c, const Op& o) {
   const KP& p = *c.p;
   TRAIL(c);
-  if (c.nops >= c.p->cap_ops) {
-    set_err(*c.p, BCSIM_E_OVERFLOW);
+  if (c.nops >= p.cap_ops) {
+    set_err(p, BCSIM_E_OVERFLOW);
     return;
   }
   AT(c.ops, c.nops++, p.cap_ops) = o;
 }
 
-__device__ inline Op mk_op(const KP& p, int64_t t, uint32_t dt, uint32_t origin, uint32_t sub,
-                           uint32_t edge, const Msg& m, uint8_t kind, uint8_t flags) {
-  Op o;
-  o.t = t;
-  o.dt = dt;
-  o.origin = origin;
-  o.sub = sub;
-  o.edge = edge;
-  o.f0 = to16(p, m.f[0]);
-  o.f1 = to16(p, m.f[1]);
-  o.f2 = to16(p, m.f[2]);
-  o.type = static_cast<uint8_t>(m.type);
-  o.kind_flags = static_cast<uint8_t>(kind | ((flags | (m.big ? OPF_BIG : 0)) << 2));
-  return o;
-}
-
 __device__ inline int32_t ctx_draw(Ctx& c) {
   const KP& p = *c.p;
-  TRAIL(c);
   if (p.rng_mode == BCSIM_RNG_COUNTER) return ctr_rand(p.seed, c.rep, c.i, c.draws++);
   set_err(p, BCSIM_E_UNSUPPORTED);  // glibc draws inside a cell: unsupported
   return 0;
@@ -384,30 +537,23 @@ __device__ inline int32_t ctx_draw(Ctx& c) {
 // Simulator::Schedule(Seconds(getRandomDelay()), SendPacket, ...) x peers
 __device__ void ctx_bcast(Ctx& c, const Msg& m, bool paxos) {
   const KP& p = *c.p;
-  TRAIL(c);
   const uint8_t fl = paxos ? OPF_PAXOS : 0;
   if (p.delay_mode == BCSIM_DELAY_FIXED) {
     ctx_op(c, mk_op(p, c.cur.t + p.app_delay, static_cast<uint32_t>(p.app_delay), c.i, c.sub, 0, m,
                     OP_BCAST, fl));
   } else {
     // jitter: expanded per edge by k_link; edge field carries the draw base
-    Op o = mk_op(p, c.cur.t, 0, c.i, c.sub, static_cast<uint32_t>(c.draws), m, OP_BCAST_J, fl);
-    ctx_op(c, o);
+    ctx_op(c, mk_op(p, c.cur.t, 0, c.i, c.sub, static_cast<uint32_t>(c.draws), m, OP_BCAST_J, fl));
     c.draws += c.deg;
   }
   c.sub += c.deg;
 }
 
-// Send(data, from): reply on the reverse edge of the arrival
-// out_edge = the reverse of the arrival's edge (resolved when the arrival was
-// staged into LDS)
+// Send(data, from): reply on the reverse edge of the arrival (= its in-slot)
 __device__ void ctx_unicast(Ctx& c, uint32_t out_edge, const Msg& m) {
   const KP& p = *c.p;
-  TRAIL(c);
   const int64_t d = p.delay_mode == BCSIM_DELAY_FIXED ? p.app_delay : delay_from_draw(p, ctx_draw(c));
-  TRAIL(c);
-  ctx_op(c, mk_op(p, c.cur.t + d, static_cast<uint32_t>(d), c.i, c.sub++, out_edge, m,
-                  OP_SEND, 0));
+  ctx_op(c, mk_op(p, c.cur.t + d, static_cast<uint32_t>(d), c.i, c.sub++, out_edge, m, OP_SEND, 0));
 }
 
 __device__ uint32_t ctx_timer(Ctx& c, uint8_t kind, int64_t delay, bool pending = false) {
@@ -433,23 +579,9 @@ __device__ void ctx_cancel(Ctx& c, uint32_t id) {
     if (c.tm[k].alive && c.tm[k].sub == id) c.tm[k].alive = 0;
 }
 
-__device__ inline Msg mkmsg(int32_t type, int32_t f0, int32_t f1, int32_t f2, int32_t big) {
-  Msg m;
-  m.type = type;
-  m.f[0] = f0;
-  m.f[1] = f1;
-  m.f[2] = f2;
-  m.big = big;
-  return m;
-}
-
 // ---------------------------------------------------------------------------
-// PBFT handlers (pbft/pbft-node.cc).  Message types pbft-node.h:80-91.
+// PBFT message types (pbft-node.h:80-91)
 enum { PB_PRE_PREPARE = 1, PB_PREPARE = 2, PB_COMMIT = 3, PB_PREPARE_RES = 5, PB_VIEW_CHANGE = 8 };
-
-struct PbftState {
-  int32_t leader, block_num;
-};
 
 __device__ bool pbft_index(const KP& p, int32_t idx) {
   if (idx < 0) {
@@ -461,79 +593,6 @@ __device__ bool pbft_index(const KP& p, int32_t idx) {
     return false;
   }
   return true;
-}
-
-__device__ void pbft_recv(Ctx& c, PbftState& s, const Msg& m, uint32_t back_edge) {
-  const KP& p = *c.p;
-  const size_t base = static_cast<size_t>(c.g) * p.pbft_seq_cap;
-  const int32_t N = static_cast<int32_t>(p.N);
-  switch (c2i(mch(m, 0))) {
-    case PB_PRE_PREPARE: {  // :193-211
-      const Msg r = mkmsg(PB_PREPARE, mch(m, 1), mch(m, 2), mch(m, 3), 0);
-      const int32_t num = c2i(mch(m, 2));
-      if (!pbft_index(p, num)) return;
-      AT(p.tx_val, base + num, p.cap_txn) = c2i(mch(m, 3));
-      ctx_bcast(c, r, false);
-      break;
-    }
-    case PB_PREPARE: {  // :212-222
-      const Msg r = mkmsg(PB_PREPARE_RES, mch(m, 1), mch(m, 2), enc_raw(p, 0), 0);
-      ctx_unicast(c, back_edge, r);
-      break;
-    }
-    case PB_PREPARE_RES: {  // :223-240
-      const int32_t idx = c2i(mch(m, 2));
-      if (!pbft_index(p, idx)) return;
-      int32_t v = AT(p.tx_pv, base + idx, p.cap_txn);
-      if (c2i(mch(m, 3)) == 0) ++v;
-      if (v >= N / 2) {
-        const Msg r = mkmsg(PB_COMMIT, mch(m, 1), mch(m, 2), 0, 0);
-        ctx_bcast(c, r, false);
-        v = 0;
-      }
-      AT(p.tx_pv, base + idx, p.cap_txn) = v;
-      break;
-    }
-    case PB_COMMIT: {  // :241-265
-      const int32_t idx = c2i(mch(m, 2));
-      if (!pbft_index(p, idx)) return;
-      int32_t v = AT(p.tx_cv, base + idx, p.cap_txn) + 1;
-      if (v > N / 2) {
-        v = 0;
-        // a = global v, resolved from the v-log on the host (INT32_MIN marker)
-        ctx_trace(c, BCSIM_TR_PBFT_COMMIT, INT32_MIN, s.block_num, AT(p.tx_val, base + idx, p.cap_txn));
-        ++s.block_num;
-      }
-      AT(p.tx_cv, base + idx, p.cap_txn) = v;
-      break;
-    }
-    case PB_VIEW_CHANGE: {  // :271-286 (falls through to "Wrong msg")
-      const int32_t vt = c2i(mch(m, 1));
-      const int32_t lt = c2i(mch(m, 2));
-      const uint32_t pos = atomicAdd(p.vlog_cnt, 1u);
-      if (pos < p.cap_vlog) {
-        VLog e;
-        e.t = c.cur.t;
-        e.ts = c.cur.ts;
-        e.origin = c.cur.origin;
-        e.sub = c.cur.sub;
-        e.target = c.i;
-        e.rep = c.rep;
-        e.v = vt;
-        e.pad = 0;
-        AT(p.vlog, pos, p.cap_vlog) = e;
-      } else {
-        set_err(p, BCSIM_E_OVERFLOW);
-      }
-      s.leader = lt;
-      if (static_cast<int32_t>(c.i) == lt) ctx_trace(c, BCSIM_TR_PBFT_VIEW, vt, lt, 0);
-      ++c.wrong;
-      break;
-    }
-    default:
-      ++c.wrong;
-      break;
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -683,7 +742,6 @@ __device__ void paxos_ticket(Ctx& c, PaxosState& s) {  // requireTicket :510-522
 
 __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t back_edge) {
   const KP& p = *c.p;
-  TRAIL(c);
   const int32_t N = static_cast<int32_t>(p.N);
   const int32_t ty = c2i(mch(m, 0));
   switch (ty) {
@@ -758,89 +816,457 @@ __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t back_ed
 }
 
 // ---------------------------------------------------------------------------
-// k_scan: one workgroup per node.  Sort the node's arrivals of [t_lo, t_hi)
-// by (t, t_sched, origin) in LDS, then run the state machine in canonical
-// key order merged with the node's timers and START/STOP.
-constexpr int kScanThreads = 256;
-constexpr int kScanMaxArr = 4096;  // LDS window: 32 B per staged arrival
-constexpr int kScanPerThread = kScanMaxArr / kScanThreads;
+// k_scan: one workgroup per node.
+//
+// The node's arrivals of [t_lo, t_hi) are staged from its inbox row (+ the
+// cell's extras) into LDS in slot order = ascending origin.  Sort key per
+// arrival: (t_off << 32 | ~dt, slot): t, then t_sched = t - dt ascending,
+// then origin — the canonical key (t, t_sched, origin, sub); sub never
+// decides between two arrivals at one receiver (one edge cannot deliver
+// twice at the same instant).  The common full-mesh case (all arrivals of a
+// phase at one instant) is already sorted and skips the LDS bitonic sort.
+constexpr int kScanMaxArr = 4096;  // LDS staging window (28 B per arrival)
+constexpr int kRidxBits = 12;
+constexpr uint32_t kRidxMask = (1u << kRidxBits) - 1u;
+constexpr int kQuorumTab = 256;    // distinct (phase, sequence) pairs per window
 
-struct SKey {
-  uint64_t hi;  // t_off << 32 | ~dt
-  uint32_t lo;  // origin
-  uint32_t idx;
+// PBFT class word per staged arrival (acls): bits 30-31 class, 29 crossing, 0-28 index
+constexpr uint32_t kClsPres = 1u << 30, kClsCommit = 2u << 30, kCross = 1u << 29;
+constexpr uint32_t kIdxMask = kCross - 1u;
+
+struct ScanShared {
+  uint32_t wcnt[kMaxWaves];
+  uint4 wsum[kMaxWaves];
+  uint32_t n, n_main, unsorted, cnt;
+  // PBFT window state
+  uint32_t sub, nops, tn, npp, last_vc;
+  uint64_t draws;
+  int32_t block_num, leader;
+  uint32_t tkey[kQuorumTab];
+  uint32_t tcnt[kQuorumTab];
+  uint32_t pp_r[64];
+  int32_t pp_idx[64], pp_val[64];
+  unsigned long long deliv[BCSIM_MSG_TYPES];
+  unsigned long long wrong;
+  long long tmax;
 };
 
-__device__ inline bool skey_gt(const SKey& a, const SKey& b) {
-  return a.hi > b.hi || (a.hi == b.hi && a.lo > b.lo);
+__device__ inline uint64_t arr_key(const KP& p, const Rec& r, uint32_t q) {
+  const uint32_t dt = static_cast<uint32_t>(AT(p.prop_in, q, p.E) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
+  return (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~dt);
 }
 
-// Count this node's arrivals with t in [a, b) (all threads; block-uniform result).
-__device__ inline uint32_t scan_count(const KP& p, uint32_t* slot, uint32_t seg_b, uint32_t m, long long cs,
-                                      long long a, long long b) {
+// Stage this node's arrivals with t in [wa, wb): main row first (slot order),
+// then extras.  Returns the total count (entries beyond cap are not stored).
+__device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, uint32_t e0, uint32_t deg,
+                                 const XRec* xs, uint32_t xn, long long cs, long long wa, long long wb,
+                                 uint64_t* akey, uint32_t* asec, Rec* arec, bool store) {
   const uint32_t tid = threadIdx.x;
-  __syncthreads();
-  if (tid == 0) *slot = 0;
-  __syncthreads();
-  uint32_t mine = 0;
-  for (uint32_t k = tid; k < m; k += blockDim.x) {
-    const long long t = cs + AT(p.grp, seg_b + k, p.cap_bucket).t_off;
-    mine += (t >= a && t < b);
+  uint32_t n = 0;
+  for (uint32_t base = 0; base < deg; base += blockDim.x) {
+    const uint32_t k = base + tid;
+    Rec r{};
+    bool v = false;
+    if (k < deg) {
+      r = slots[k];
+      const long long t = cs + r.t_off;
+      v = (r.flags & RF_VALID) && t >= wa && t < wb;
+    }
+    uint32_t tot;
+    const uint32_t pos = n + block_rank(v, S.wcnt, tot);
+    if (store && v && pos < p.cap_arr) {
+      arec[pos] = r;
+      asec[pos] = (k << kRidxBits) | pos;
+      akey[pos] = arr_key(p, r, e0 + k);
+    }
+    n += tot;
   }
-  if (mine) atomicAdd(slot, mine);
+  const uint32_t n_main = n;
+  for (uint32_t base = 0; base < xn; base += blockDim.x) {
+    const uint32_t k = base + tid;
+    XRec x{};
+    bool v = false;
+    if (k < xn) {
+      x = xs[k];
+      const long long t = cs + x.r.t_off;
+      v = t >= wa && t < wb;
+    }
+    uint32_t tot;
+    const uint32_t pos = n + block_rank(v, S.wcnt, tot);
+    if (store && v && pos < p.cap_arr) {
+      arec[pos] = x.r;
+      asec[pos] = ((x.slot - e0) << kRidxBits) | pos;
+      akey[pos] = arr_key(p, x.r, x.slot);
+    }
+    n += tot;
+  }
+  if (tid == 0) S.n_main = n_main;
   __syncthreads();
-  return *slot;
+  return n;
+}
+
+__device__ inline bool sec_less(uint64_t ka, uint32_t sa, uint64_t kb, uint32_t sb) {
+  return ka < kb || (ka == kb && sa < sb);
+}
+
+// Sort (akey, asec) pairs of [0, n) unless already ordered.
+__device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec) {
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) S.unsorted = 0;
+  __syncthreads();
+  bool bad = false;
+  for (uint32_t r = tid; r + 1 < n; r += blockDim.x)
+    if (sec_less(akey[r + 1], asec[r + 1], akey[r], asec[r])) bad = true;
+  if (__ballot(bad) && (tid & 63) == 0) S.unsorted = 1;
+  __syncthreads();
+  if (!S.unsorted) return;
+  uint32_t P2 = 2;
+  while (P2 < n) P2 <<= 1;
+  for (uint32_t k = n + tid; k < P2; k += blockDim.x) {
+    akey[k] = ~0ull;
+    asec[k] = ~0u;
+  }
+  __syncthreads();
+  for (uint32_t k2 = 2; k2 <= P2; k2 <<= 1) {
+    for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = tid; t < P2 / 2; t += blockDim.x) {
+        const uint32_t lo = 2 * t - (t & (j - 1)), hi = lo + j;
+        const bool up = (lo & k2) == 0;
+        const uint64_t ka = akey[lo], kb = akey[hi];
+        const uint32_t sa = asec[lo], sb = asec[hi];
+        if (up == sec_less(kb, sb, ka, sa)) {
+          akey[lo] = kb;
+          akey[hi] = ka;
+          asec[lo] = sb;
+          asec[hi] = sa;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---- PBFT, data parallel (pbft-node.cc:166-291) ----------------------------
+// One window of sorted arrivals.  Sequential semantics restated as prefixes:
+//   PRE_PREPARE   tx[n].val = val; bcast PREPARE          sub += deg
+//   PREPARE       reply PREPARE_RES (unicast)             sub += 1
+//   PREPARE_RES   ++prepare_vote; crossing (every N/2-th increment) -> bcast COMMIT
+//   COMMIT        ++commit_vote; crossing (every (N/2+1)-th) -> commit, block_num++
+//   VIEW_CHANGE   leader = msg (last one wins), "Wrong msg"
+// Crossings are ranks within each (phase, sequence) group: wave 0 walks the
+// window 64 arrivals at a time, grouping lanes by ballot.
+__device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep, uint32_t i, uint32_t e0,
+                            uint32_t deg, uint32_t n, long long cs, const uint64_t* akey, const uint32_t* asec,
+                            const Rec* arec, uint32_t* acls) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const size_t base = static_cast<size_t>(g) * p.pbft_seq_cap;
+  const int32_t N = static_cast<int32_t>(p.N);
+  const uint32_t T1 = static_cast<uint32_t>(N / 2), T2 = T1 + 1;
+  const bool fixed = p.delay_mode == BCSIM_DELAY_FIXED;
+  // ---- A: classify ----
+  if (tid == 0) {
+    S.tn = 0;
+    S.npp = 0;
+    S.last_vc = 0;
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += blockDim.x) {
+    const Rec rec = arec[asec[r] & kRidxMask];
+    const Msg m = rec_msg(rec);
+    uint32_t w = 0;
+    switch (rec.type) {
+      case PB_PRE_PREPARE: {
+        const int32_t num = c2i(mch(m, 2));
+        if (pbft_index(p, num)) {
+          const uint32_t k = atomicAdd(&S.npp, 1u);
+          if (k < 64) {
+            S.pp_r[k] = r;
+            S.pp_idx[k] = num;
+            S.pp_val[k] = c2i(mch(m, 3));
+          } else {
+            set_err(p, BCSIM_E_OVERFLOW);
+          }
+        }
+        break;
+      }
+      case PB_PREPARE_RES: {
+        const int32_t idx = c2i(mch(m, 2));
+        if (pbft_index(p, idx) && c2i(mch(m, 3)) == 0) w = kClsPres | static_cast<uint32_t>(idx);
+        break;
+      }
+      case PB_COMMIT: {
+        const int32_t idx = c2i(mch(m, 2));
+        if (pbft_index(p, idx)) w = kClsCommit | static_cast<uint32_t>(idx);
+        break;
+      }
+      case PB_VIEW_CHANGE:
+        atomicMax(&S.last_vc, r + 1);
+        break;
+      default:
+        break;
+    }
+    acls[r] = w;
+  }
+  __syncthreads();
+  // ---- B: quorum ranks (wave 0) ----
+  if (tid < 64) {
+    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+      const uint32_t r = b0 + lane;
+      const uint32_t w = r < n ? acls[r] : 0u;
+      unsigned long long rem = __ballot(w != 0);
+      while (rem) {
+        const int ld = __ffsll(static_cast<long long>(rem)) - 1;
+        const uint32_t wl = __shfl(w, ld, 64);
+        const bool mine = (w == wl);
+        const unsigned long long same = __ballot(mine);
+        uint32_t cnt = 0;
+        if (lane == static_cast<uint32_t>(ld)) {
+          int e = -1;
+          for (uint32_t k = 0; k < S.tn; ++k)
+            if (S.tkey[k] == wl) {
+              e = static_cast<int>(k);
+              break;
+            }
+          if (e < 0) {
+            if (S.tn >= static_cast<uint32_t>(kQuorumTab)) {
+              set_err(p, BCSIM_E_OVERFLOW);
+              e = kQuorumTab - 1;
+            } else {
+              e = static_cast<int>(S.tn++);
+              S.tkey[e] = wl;
+              const uint32_t idx = wl & kIdxMask;
+              S.tcnt[e] = static_cast<uint32_t>((wl >> 30) == 1u ? AT(p.tx_pv, base + idx, p.cap_txn)
+                                                                  : AT(p.tx_cv, base + idx, p.cap_txn));
+            }
+          }
+          cnt = S.tcnt[e];
+          S.tcnt[e] = cnt + static_cast<uint32_t>(__popcll(same));
+        }
+        cnt = __shfl(cnt, ld, 64);
+        if (mine) {
+          const uint32_t v = cnt + static_cast<uint32_t>(__popcll(same & ((1ull << lane) - 1ull))) + 1u;
+          const bool cross = (w >> 30) == 1u ? (v % T1 == 0) : (v % T2 == 0);
+          if (cross) acls[r] = w | kCross;
+        }
+        rem &= ~same;
+      }
+    }
+    // write back the vote counters (tx[idx].prepare_vote / commit_vote)
+    for (uint32_t k = lane; k < S.tn; k += 64) {
+      const uint32_t wl = S.tkey[k], idx = wl & kIdxMask;
+      if ((wl >> 30) == 1u)
+        AT(p.tx_pv, base + idx, p.cap_txn) = static_cast<int32_t>(S.tcnt[k] % T1);
+      else
+        AT(p.tx_cv, base + idx, p.cap_txn) = static_cast<int32_t>(S.tcnt[k] % T2);
+    }
+  }
+  __syncthreads();
+  // ---- C: per-arrival increments over contiguous runs, block scan ----
+  const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
+  const uint32_t r0 = min(n, tid * per), r1 = min(n, r0 + per);
+  const uint32_t ech = p.echo ? 1u : 0u;
+  uint4 loc = make_uint4(0, 0, 0, 0);  // sub, draws, commits, ops
+  for (uint32_t r = r0; r < r1; ++r) {
+    const Rec rec = arec[asec[r] & kRidxMask];
+    const uint32_t w = acls[r];
+    const bool cross = (w & kCross) != 0;
+    uint32_t si = 0, di = 0, ci = 0, oi = ech;
+    if (rec.type == PB_PRE_PREPARE) {
+      si = deg;
+      di = fixed ? 0u : deg;
+      oi += 1;
+    } else if (rec.type == PB_PREPARE) {
+      si = 1;
+      di = fixed ? 0u : 1u;
+      oi += 1;
+    } else if (rec.type == PB_PREPARE_RES && cross) {
+      si = deg;
+      di = fixed ? 0u : deg;
+      oi += 1;
+    } else if (rec.type == PB_COMMIT && cross) {
+      ci = 1;
+    }
+    loc.x += si;
+    loc.y += di;
+    loc.z += ci;
+    loc.w += oi;
+  }
+  uint4 tot;
+  const uint4 ex = block_scan4(loc, S.wsum, tot);
+  // ---- D: outputs ----
+  const uint32_t sub0 = S.sub, nops0 = S.nops;
+  const uint64_t draws0 = S.draws;
+  const int32_t bn0 = S.block_num;
+  if (nops0 + tot.w > p.cap_ops) {
+    if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
+    return;
+  }
+  Op* ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
+  uint32_t sp = sub0 + ex.x, op = nops0 + ex.w, cp = ex.z;
+  uint64_t dp = draws0 + ex.y;
+  unsigned long long wrong = 0;
+  for (uint32_t r = r0; r < r1; ++r) {
+    const uint32_t sec = asec[r];
+    const Rec rec = arec[sec & kRidxMask];
+    const uint32_t q = e0 + (sec >> kRidxBits);  // in-slot = reverse (reply) edge
+    const uint32_t w = acls[r];
+    const bool cross = (w & kCross) != 0;
+    const Msg m = rec_msg(rec);
+    const int64_t t = cs + rec.t_off;
+    const uint32_t dt = static_cast<uint32_t>(AT(p.prop_in, q, p.E) + p.tx_last[m.big]);
+    const uint32_t origin = AT(p.col, q, p.E);
+    const Key key{t, t - static_cast<int64_t>(dt), origin, rec.sub};
+    if (t == ((t / p.pbft_period) * p.pbft_period) && key.ts <= t - p.pbft_period)
+      set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
+    if (ech) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);  // pbft-node.cc:175
+    switch (rec.type) {
+      case PB_PRE_PREPARE: {  // :193-211
+        const Msg rr = mkmsg(PB_PREPARE, mch(m, 1), mch(m, 2), mch(m, 3), 0);
+        ops[op++] = fixed ? mk_op(p, t + p.app_delay, static_cast<uint32_t>(p.app_delay), i, sp, 0, rr, OP_BCAST, 0)
+                          : mk_op(p, t, 0, i, sp, static_cast<uint32_t>(dp), rr, OP_BCAST_J, 0);
+        sp += deg;
+        if (!fixed) dp += deg;
+        break;
+      }
+      case PB_PREPARE: {  // :212-222
+        const Msg rr = mkmsg(PB_PREPARE_RES, mch(m, 1), mch(m, 2), enc_raw(p, 0), 0);
+        int64_t d = p.app_delay;
+        if (!fixed) d = delay_from_draw(p, ctr_rand(p.seed, rep, i, dp++));
+        ops[op++] = mk_op(p, t + d, static_cast<uint32_t>(d), i, sp++, q, rr, OP_SEND, 0);
+        break;
+      }
+      case PB_PREPARE_RES:  // :223-240
+        if (cross) {
+          const Msg rr = mkmsg(PB_COMMIT, mch(m, 1), mch(m, 2), 0, 0);
+          ops[op++] = fixed ? mk_op(p, t + p.app_delay, static_cast<uint32_t>(p.app_delay), i, sp, 0, rr, OP_BCAST, 0)
+                            : mk_op(p, t, 0, i, sp, static_cast<uint32_t>(dp), rr, OP_BCAST_J, 0);
+          sp += deg;
+          if (!fixed) dp += deg;
+        }
+        break;
+      case PB_COMMIT:  // :241-265
+        if (cross) {
+          const int32_t idx = static_cast<int32_t>(w & kIdxMask);
+          // tx[idx].val as of this event: the latest PRE_PREPARE of the window before it
+          int32_t val = 0;
+          int32_t best = -1;
+          for (uint32_t k = 0; k < min(S.npp, 64u); ++k)
+            if (S.pp_idx[k] == idx && S.pp_r[k] < r && static_cast<int32_t>(S.pp_r[k]) > best) {
+              best = static_cast<int32_t>(S.pp_r[k]);
+              val = S.pp_val[k];
+            }
+          if (best < 0) val = AT(p.tx_val, base + idx, p.cap_txn);
+          // a = global v, resolved from the v-log on the host (INT32_MIN marker)
+          emit_trace(p, key, rep, i, BCSIM_TR_PBFT_COMMIT, INT32_MIN, bn0 + static_cast<int32_t>(cp), val);
+          ++cp;
+        }
+        break;
+      case PB_VIEW_CHANGE: {  // :271-286 (falls through to "Wrong msg")
+        const int32_t vt = c2i(mch(m, 1));
+        const int32_t lt = c2i(mch(m, 2));
+        emit_vlog(p, key, rep, i, vt);
+        if (static_cast<int32_t>(i) == lt) emit_trace(p, key, rep, i, BCSIM_TR_PBFT_VIEW, vt, lt, 0);
+        if (r + 1 == S.last_vc) S.leader = lt;
+        ++wrong;
+        break;
+      }
+      default:
+        ++wrong;
+        break;
+    }
+  }
+  // delivery counters by type (wave-aggregated)
+  for (uint32_t j = 0; j < per; ++j) {
+    const uint32_t r = r0 + j;
+    const bool act = r < r1;
+    const uint32_t ty = act ? arec[asec[r] & kRidxMask].type : 0u;
+    wave_add_by_key(act && ty < BCSIM_MSG_TYPES, ty, 1u, S.deliv);
+  }
+  if (wrong) atomicAdd(&S.wrong, wrong);
+  __syncthreads();
+  // ---- E: tx[n].val of the window's PRE_PREPAREs (last one per index wins) ----
+  for (uint32_t k = tid; k < min(S.npp, 64u); k += blockDim.x) {
+    bool last = true;
+    for (uint32_t k2 = 0; k2 < min(S.npp, 64u); ++k2)
+      if (S.pp_idx[k2] == S.pp_idx[k] && S.pp_r[k2] > S.pp_r[k]) last = false;
+    if (last) AT(p.tx_val, base + S.pp_idx[k], p.cap_txn) = S.pp_val[k];
+  }
+  if (tid == 0) {
+    S.sub += tot.x;
+    S.draws += tot.y;
+    S.block_num += static_cast<int32_t>(tot.z);
+    S.nops += tot.w;
+    if (n) S.tmax = max(S.tmax, cs + static_cast<long long>(akey[n - 1] >> 32));
+  }
+  __syncthreads();
 }
 
 template <int PROTO>
-__global__ __launch_bounds__(kScanThreads) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                      long long t_hi, long long cs) {
+__global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                               long long t_hi, long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  // LDS: [0,64) control | cap_arr x Rec (sorted window; the SKey sort runs in
-  // the same bytes first) | cap_timers x TimerEnt
+  // LDS: akey[cap] u64 | asec[cap] u32 | arec[cap] Rec | acls[cap] u32 | timers
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint32_t* ctl = reinterpret_cast<uint32_t*>(smem);
-  SKey* keys = reinterpret_cast<SKey*>(smem + 64);
-  Rec* recs = reinterpret_cast<Rec*>(smem + 64);
-  TimerEnt* tm = reinterpret_cast<TimerEnt*>(smem + 64 + static_cast<size_t>(p.cap_arr) * sizeof(Rec));
+  __shared__ ScanShared S;
+  const uint32_t cap = p.cap_arr;
+  uint64_t* akey = reinterpret_cast<uint64_t*>(smem);
+  uint32_t* asec = reinterpret_cast<uint32_t*>(akey + cap);
+  Rec* arec = reinterpret_cast<Rec*>(asec + cap);
+  uint32_t* acls = reinterpret_cast<uint32_t*>(arec + cap);
+  TimerEnt* tm = reinterpret_cast<TimerEnt*>(acls + cap);
 
-  const uint32_t g = blockIdx.x;
+  const uint32_t g = xcd_map(blockIdx.x, p.NT);
   if (g >= p.NT) return;
   const uint32_t tid = threadIdx.x;
-  const uint32_t seg_b = AT(p.seg_off, g, p.NT + 1);
-  const uint32_t m = AT(p.seg_off, g + 1, p.NT + 1) - seg_b;
+  const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
-  if (m == 0 && AT(p.node_tnext, g, p.NT) >= t_hi && !has_start && !has_stop) return;
-  if (tid < p.cap_timers)
+  const size_t fidx = static_cast<size_t>(b) * p.NT + g;
+  const bool flag = AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) != 0;
+  if (!flag && AT(p.node_tnext, g, p.NT) >= t_hi && !has_start && !has_stop) return;
+
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
+  const Rec* slots = p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0;
+  uint32_t xn = 0;
+  const XRec* xs = p.xgrp;
+  if (x_active) {
+    const uint32_t xb = AT(p.seg_off, g, p.NT + 1);
+    xn = AT(p.seg_off, g + 1, p.NT + 1) - xb;
+    xs = p.xgrp + xb;
+  }
+  if (PROTO != BCSIM_PBFT && tid < p.cap_timers)
     tm[tid] = AT(p.timers, static_cast<size_t>(g) * p.cap_timers + tid, static_cast<uint64_t>(p.NT) * p.cap_timers);
 
-  // ---- serial state (lane 0 only) ----
-  const uint32_t rep = g / p.N, i = g % p.N;
-  Ctx c;
-  PbftState ps{};
-  RaftState rs{};
-  PaxosState xs{};
-  bool start_pending = has_start, stop_pending = has_stop;
+  // ---- node state ----
   if (tid == 0) {
+    S.sub = AT(p.sub, g, p.NT);
+    S.draws = AT(p.draws, g, p.NT);
+    S.nops = AT(p.n_ops, g, p.NT);
+    S.block_num = PROTO == BCSIM_PBFT ? AT(p.block_num, g, p.NT) : 0;
+    S.leader = PROTO == BCSIM_PBFT ? AT(p.leader, g, p.NT) : 0;
+    for (int k = 0; k < BCSIM_MSG_TYPES; ++k) S.deliv[k] = 0;
+    S.wrong = 0;
+    S.tmax = LLONG_MIN;
+  }
+  Ctx c;
+  RaftState rs{};
+  PaxosState xs_{};
+  unsigned long long events = 0;
+  bool start_pending = has_start, stop_pending = has_stop;
+  if (PROTO != BCSIM_PBFT && tid == 0) {
     c.p = pk;
     c.g = g;
     c.rep = rep;
     c.i = i;
-    c.deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
-    c.sub = AT(p.sub, g, p.NT);
-    c.draws = AT(p.draws, g, p.NT);
+    c.deg = deg;
     c.ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
-    c.nops = AT(p.n_ops, g, p.NT);
     c.tm = tm;
     c.cap_t = p.cap_timers;
     for (int k = 0; k < BCSIM_MSG_TYPES; ++k) c.deliv[k] = 0;
     c.echoes = c.wrong = c.events = 0;
-    if (PROTO == BCSIM_PBFT) {
-      ps.leader = AT(p.leader, g, p.NT);
-      ps.block_num = AT(p.block_num, g, p.NT);
-    } else if (PROTO == BCSIM_RAFT) {
+    if (PROTO == BCSIM_RAFT) {
       rs.is_leader = AT(p.is_leader, g, p.NT);
       rs.has_voted = AT(p.has_voted, g, p.NT);
       rs.m_value = AT(p.m_value, g, p.NT);
@@ -852,124 +1278,75 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const KP* __restrict__ pk
       rs.next_election = AT(p.next_election, g, p.NT);
       rs.next_heartbeat = AT(p.next_heartbeat, g, p.NT);
     } else {
-      xs.t_max = AT(p.t_max, g, p.NT);
-      xs.command = AT(p.command, g, p.NT);
-      xs.t_store = AT(p.t_store, g, p.NT);
-      xs.ticket = AT(p.ticket, g, p.NT);
-      xs.is_commit = AT(p.is_commit, g, p.NT);
-      xs.proposal = AT(p.proposal, g, p.NT);
-      xs.vs = AT(p.vote_s, g, p.NT);
-      xs.vf = AT(p.vote_f, g, p.NT);
+      xs_.t_max = AT(p.t_max, g, p.NT);
+      xs_.command = AT(p.command, g, p.NT);
+      xs_.t_store = AT(p.t_store, g, p.NT);
+      xs_.ticket = AT(p.ticket, g, p.NT);
+      xs_.is_commit = AT(p.is_commit, g, p.NT);
+      xs_.proposal = AT(p.proposal, g, p.NT);
+      xs_.vs = AT(p.vote_s, g, p.NT);
+      xs_.vf = AT(p.vote_f, g, p.NT);
     }
-    TRAIL(c);
+  }
+  __syncthreads();
+  if (PROTO == BCSIM_PBFT && has_start && tid == 0) {  // StartApplication pbft-node.cc:97-158
+    S.leader = 0;
+    S.block_num = 0;
+    AT(p.tick_sub, g, p.NT) = S.sub++;  // Schedule(Seconds(timeout), SendBlock) :155
+    AT(p.tick_alive, g, p.NT) = 1;
+    S.tmax = 0;
+  }
+  if (PROTO == BCSIM_PBFT) {
+    events += (has_start ? 1 : 0) + (has_stop ? 1 : 0);
+    if (has_stop && tid == 0) S.tmax = max(S.tmax, static_cast<long long>(p.stop_ns));
   }
 
-  // ---- windows: [t_lo, t_hi) split so that each holds <= cap_arr arrivals.
-  // At one instant a node receives at most one record per in-edge (links are
-  // FIFO and serialise), and cap_arr > deg, so every window is non-empty.
-  long long tmax_ev = LLONG_MIN;
+  // ---- windows of <= cap arrivals ----
   long long wa = t_lo;
   for (;;) {
     long long wb = t_hi;
-    uint32_t n;
-    if (m > p.cap_arr && scan_count(p, &ctl[1], seg_b, m, cs, wa, t_hi) > p.cap_arr) {
+    uint32_t n = flag ? stage_window(p, S, slots, e0, deg, xs, xn, cs, wa, wb, akey, asec, arec, true) : 0u;
+    if (n > cap) {  // more than cap arrivals: shrink the window (rare)
       long long lo = wa, hi = t_hi;  // count(lo) <= cap < count(hi)
       while (hi - lo > 1) {
         const long long mid = lo + (hi - lo) / 2;
-        if (scan_count(p, &ctl[1], seg_b, m, cs, wa, mid) <= p.cap_arr)
+        if (stage_window(p, S, slots, e0, deg, xs, xn, cs, wa, mid, akey, asec, arec, false) <= cap)
           lo = mid;
         else
           hi = mid;
       }
       wb = lo;
-      if (wb == wa) {  // > cap_arr arrivals at one instant (cap_arr <= deg)
+      if (wb == wa) {  // > cap arrivals at one instant
         if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
         return;
       }
+      n = stage_window(p, S, slots, e0, deg, xs, xn, cs, wa, wb, akey, asec, arec, true);
     }
-    // select this window's arrivals and sort them by (t, t_sched, origin)
-    __syncthreads();
-    if (tid == 0) ctl[0] = 0;
-    __syncthreads();
-    for (uint32_t k = tid; k < m; k += blockDim.x) {
-      const Rec r = AT(p.grp, seg_b + k, p.cap_bucket);
-      const long long t = cs + r.t_off;
-      if (t >= wa && t < wb) {
-        const uint32_t slot = atomicAdd(&ctl[0], 1u);
-        if (slot < p.cap_arr) {
-          SKey s;
-          s.hi = (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~r.dt);
-          s.lo = r.origin;
-          s.idx = k;
-          keys[slot] = s;
-        }
-      }
-    }
-    __syncthreads();
-    n = ctl[0];
-    if (n > p.cap_arr) {  // unreachable by construction
-      if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
-      return;
-    }
-    uint32_t P2 = 2;
-    while (P2 < n) P2 <<= 1;
-    for (uint32_t k = n + tid; k < P2; k += blockDim.x) {
-      SKey s;
-      s.hi = ~0ull;
-      s.lo = ~0u;
-      s.idx = 0;
-      keys[k] = s;
-    }
-    __syncthreads();
-    for (uint32_t k2 = 2; k2 <= P2; k2 <<= 1) {
-      for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
-        for (uint32_t t = tid; t < P2; t += blockDim.x) {
-          const uint32_t ixj = t ^ j;
-          if (ixj > t) {
-            const SKey a = keys[t], b = keys[ixj];
-            const bool up = (t & k2) == 0;
-            if (up ? skey_gt(a, b) : skey_gt(b, a)) {
-              keys[t] = b;
-              keys[ixj] = a;
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    // gather the records in key order into LDS (same bytes as the keys:
-    // indices go through registers first); edge -> reverse edge here
-    uint32_t ix[kScanPerThread];
-#pragma unroll
-    for (int j = 0; j < kScanPerThread; ++j) {
-      const uint32_t k = tid + j * kScanThreads;
-      ix[j] = k < n ? keys[k].idx : 0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kScanPerThread; ++j) {
-      const uint32_t k = tid + j * kScanThreads;
-      if (k < n) {
-        Rec r = AT(p.grp, seg_b + ix[j], p.cap_bucket);
-        r.edge = AT(p.rev, r.edge, p.E);
-        recs[k] = r;
-      }
-    }
-    __syncthreads();
+    const uint32_t n_main = S.n_main;
+    sort_window(S, n, akey, asec);
 
-    if (tid == 0) {
+    if (PROTO == BCSIM_PBFT) {
+      pbft_window(p, S, g, rep, i, e0, deg, n, cs, akey, asec, arec, acls);
+      events += (tid == 0) ? n : 0;
+    } else if (tid == 0) {
+      c.sub = S.sub;
+      c.draws = S.draws;
+      c.nops = S.nops;
       uint32_t ai = 0;
       for (;;) {
-        // candidates
         int which = -1;  // 0 arrival, 1 timer, 2 start, 3 stop
         Key best{};
         Rec rec{};
+        uint32_t q = 0;
         int tsel = -1;
         if (ai < n) {
-          rec = recs[ai];
+          const uint32_t sec = asec[ai];
+          rec = arec[sec & kRidxMask];
+          q = e0 + (sec >> kRidxBits);
+          const uint32_t dt = static_cast<uint32_t>(AT(p.prop_in, q, p.E) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
           best.t = cs + rec.t_off;
-          best.ts = best.t - rec.dt;
-          best.origin = rec.origin;
+          best.ts = best.t - dt;
+          best.origin = AT(p.col, q, p.E);
           best.sub = rec.sub;
           which = 0;
         }
@@ -1000,32 +1377,21 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const KP* __restrict__ pk
         TRAIL(c);
         if (which < 0) break;
         c.cur = best;
-        if (best.t > tmax_ev) tmax_ev = best.t;
+        if (best.t > S.tmax) S.tmax = best.t;
         ++c.events;
         if (which == 0) {
           ++ai;
-          Msg msg;
-          msg.type = rec.type;
-          msg.f[0] = rec.f0;
-          msg.f[1] = rec.f1;
-          msg.f[2] = rec.f2;
-          msg.big = rec.big;
+          const Msg msg = rec_msg(rec);
           if (rec.type < BCSIM_MSG_TYPES) ++c.deliv[rec.type];
-          TRAIL(c);
-          // rec.edge is the reverse edge (receiver -> sender) from the gather
           if (p.echo) {  // socket->SendTo(packet, 0, from): reverse-link occupancy
-            ctx_op(c, mk_op(p, best.t, rec.dt, rec.origin, rec.sub, rec.edge, msg, OP_ECHO, 0));
+            ctx_op(c, mk_op(p, best.t, static_cast<uint32_t>(best.t - best.ts), best.origin, rec.sub, q, msg,
+                            OP_ECHO, 0));
             ++c.echoes;
           }
-          if (PROTO == BCSIM_PBFT) {
-            if (best.t == ((best.t / p.pbft_period) * p.pbft_period) && best.ts <= best.t - p.pbft_period)
-              set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
-            pbft_recv(c, ps, msg, rec.edge);
-          } else if (PROTO == BCSIM_RAFT) {
-            raft_recv(c, rs, msg, rec.edge);
-          } else {
-            paxos_recv(c, xs, msg, rec.edge);
-          }
+          if (PROTO == BCSIM_RAFT)
+            raft_recv(c, rs, msg, q);
+          else
+            paxos_recv(c, xs_, msg, q);
         } else if (which == 1) {
           TimerEnt& te = tm[tsel];
           te.alive = 0;
@@ -1040,17 +1406,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const KP* __restrict__ pk
             } else if (te.kind == TM_RAFT_PROPOSAL) {  // setProposal :432-435
               rs.acv = 1;
             }
-          } else if (PROTO == BCSIM_PAXOS) {
-            if (te.kind == TM_PAXOS_TICKET) paxos_ticket(c, xs);
+          } else {
+            if (te.kind == TM_PAXOS_TICKET) paxos_ticket(c, xs_);
           }
         } else if (which == 2) {  // StartApplication
           start_pending = false;
-          if (PROTO == BCSIM_PBFT) {  // :97-158; globals reset host-side
-            ps.leader = 0;
-            ps.block_num = 0;
-            AT(p.tick_sub, g, p.NT) = c.sub++;  // Schedule(Seconds(timeout), SendBlock) :155
-            AT(p.tick_alive, g, p.NT) = 1;
-          } else if (PROTO == BCSIM_RAFT) {  // :75-115
+          if (PROTO == BCSIM_RAFT) {  // :75-115
             rs.m_value = 0;
             rs.vs = 0;
             rs.vf = 0;
@@ -1065,84 +1426,114 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const KP* __restrict__ pk
               const int32_t r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + i, p.cap_glibc);
               rs.next_election = ctx_timer(c, TM_RAFT_ELECTION, AT(p.raft_elec, r % 150, 150));
             }
-          } else {  // :58-139
-            xs.t_max = 0;
-            xs.command = 'e';
-            xs.t_store = 0;
-            xs.ticket = 0;
-            xs.is_commit = 0;
-            xs.proposal = enc_raw(p, static_cast<int32_t>(i));
-            xs.vs = 0;
-            xs.vf = 0;
+          } else {  // paxos-node.cc:58-139
+            xs_.t_max = 0;
+            xs_.command = 'e';
+            xs_.t_store = 0;
+            xs_.ticket = 0;
+            xs_.is_commit = 0;
+            xs_.proposal = enc_raw(p, static_cast<int32_t>(i));
+            xs_.vs = 0;
+            xs_.vf = 0;
             if (i < p.paxos_proposers) (void)ctx_timer(c, TM_PAXOS_TICKET, 0);
           }
         } else {  // StopApplication
           stop_pending = false;
-          if (PROTO == BCSIM_RAFT && rs.is_leader == 1)
-            ctx_trace(c, BCSIM_TR_RAFT_STOP, rs.blockNum, rs.round, 0);
+          if (PROTO == BCSIM_RAFT && rs.is_leader == 1) ctx_trace(c, BCSIM_TR_RAFT_STOP, rs.blockNum, rs.round, 0);
         }
       }
+      S.sub = c.sub;
+      S.draws = c.draws;
+      S.nops = c.nops;
     }
+    __syncthreads();
+    // consumed slots are free again
+    for (uint32_t r = tid; r < n; r += blockDim.x) {
+      const uint32_t sec = asec[r];
+      if ((sec & kRidxMask) < n_main) const_cast<Rec*>(slots)[sec >> kRidxBits] = Rec{};
+    }
+    __syncthreads();
     if (wb >= t_hi) break;
     wa = wb;
   }
-  if (tid != 0) return;
-  // write back
-  TRAIL(c);
-  AT(p.sub, g, p.NT) = c.sub;
-  AT(p.draws, g, p.NT) = c.draws;
-  AT(p.n_ops, g, p.NT) = c.nops;
-  long long tnext = LLONG_MAX;
-  for (uint32_t k = 0; k < c.cap_t; ++k) {
-    AT(p.timers, static_cast<size_t>(g) * p.cap_timers + k, static_cast<uint64_t>(p.NT) * p.cap_timers) = tm[k];
-    if (tm[k].alive && tm[k].t < tnext) tnext = tm[k].t;
-  }
-  AT(p.node_tnext, g, p.NT) = tnext;
-  if (c.nops > 0) AT(p.node_onext, g, p.NT) = LLONG_MIN;  // link stage recomputes
-  if (PROTO == BCSIM_PBFT) {
-    AT(p.leader, g, p.NT) = ps.leader;
-    AT(p.block_num, g, p.NT) = ps.block_num;
-  } else if (PROTO == BCSIM_RAFT) {
-    AT(p.is_leader, g, p.NT) = rs.is_leader;
-    AT(p.has_voted, g, p.NT) = rs.has_voted;
-    AT(p.m_value, g, p.NT) = rs.m_value;
-    AT(p.vote_s, g, p.NT) = rs.vs;
-    AT(p.vote_f, g, p.NT) = rs.vf;
-    AT(p.acv, g, p.NT) = rs.acv;
-    AT(p.blockNum, g, p.NT) = rs.blockNum;
-    AT(p.round, g, p.NT) = rs.round;
-    AT(p.next_election, g, p.NT) = rs.next_election;
-    AT(p.next_heartbeat, g, p.NT) = rs.next_heartbeat;
-  } else {
-    AT(p.t_max, g, p.NT) = xs.t_max;
-    AT(p.command, g, p.NT) = xs.command;
-    AT(p.t_store, g, p.NT) = xs.t_store;
-    AT(p.ticket, g, p.NT) = xs.ticket;
-    AT(p.is_commit, g, p.NT) = xs.is_commit;
-    AT(p.proposal, g, p.NT) = xs.proposal;
-    AT(p.vote_s, g, p.NT) = xs.vs;
-    AT(p.vote_f, g, p.NT) = xs.vf;
-  }
+  if (final_win && flag && tid == 0) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
+
+  // ---- write back ----
   unsigned long long* cnt = &AT(p.counters, static_cast<size_t>(rep) * CNT_N, static_cast<uint64_t>(p.R) * CNT_N);
+  if (tid != 0) return;
+  const uint32_t nops_in = AT(p.n_ops, g, p.NT);
+  AT(p.sub, g, p.NT) = S.sub;
+  AT(p.draws, g, p.NT) = S.draws;
+  AT(p.n_ops, g, p.NT) = S.nops;
+  if (S.nops > nops_in) AT(p.node_onext, g, p.NT) = LLONG_MIN;  // link stage recomputes
   unsigned long long tot = 0;
-  for (int k = 0; k < BCSIM_MSG_TYPES; ++k)
-    if (c.deliv[k]) {
-      atomicAdd(&cnt[CNT_DELIV + k], c.deliv[k]);
-      tot += c.deliv[k];
+  if (PROTO == BCSIM_PBFT) {
+    AT(p.leader, g, p.NT) = S.leader;
+    AT(p.block_num, g, p.NT) = S.block_num;
+    for (int k = 0; k < BCSIM_MSG_TYPES; ++k)
+      if (S.deliv[k]) {
+        atomicAdd(&cnt[CNT_DELIV + k], S.deliv[k]);
+        tot += S.deliv[k];
+      }
+    if (tot) {
+      atomicAdd(&cnt[CNT_DELIV_TOTAL], tot);
+      if (p.echo) atomicAdd(&cnt[CNT_ECHOES], tot);
+      atomicAdd(&p.kstat[KST_DELIV], tot);
     }
-  if (tot) atomicAdd(&cnt[CNT_DELIV_TOTAL], tot);
-  if (c.echoes) atomicAdd(&cnt[CNT_ECHOES], c.echoes);
-  if (c.wrong) atomicAdd(&cnt[CNT_WRONG], c.wrong);
-  if (c.events) atomicAdd(&cnt[CNT_EVENTS], c.events);
-  if (tmax_ev > LLONG_MIN) atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), tmax_ev);
+    if (S.wrong) atomicAdd(&cnt[CNT_WRONG], S.wrong);
+    if (events) atomicAdd(&cnt[CNT_EVENTS], events);
+  } else {
+    long long tnext = LLONG_MAX;
+    for (uint32_t k = 0; k < c.cap_t; ++k) {
+      AT(p.timers, static_cast<size_t>(g) * p.cap_timers + k, static_cast<uint64_t>(p.NT) * p.cap_timers) = tm[k];
+      if (tm[k].alive && tm[k].t < tnext) tnext = tm[k].t;
+    }
+    AT(p.node_tnext, g, p.NT) = tnext;
+    if (PROTO == BCSIM_RAFT) {
+      AT(p.is_leader, g, p.NT) = rs.is_leader;
+      AT(p.has_voted, g, p.NT) = rs.has_voted;
+      AT(p.m_value, g, p.NT) = rs.m_value;
+      AT(p.vote_s, g, p.NT) = rs.vs;
+      AT(p.vote_f, g, p.NT) = rs.vf;
+      AT(p.acv, g, p.NT) = rs.acv;
+      AT(p.blockNum, g, p.NT) = rs.blockNum;
+      AT(p.round, g, p.NT) = rs.round;
+      AT(p.next_election, g, p.NT) = rs.next_election;
+      AT(p.next_heartbeat, g, p.NT) = rs.next_heartbeat;
+    } else {
+      AT(p.t_max, g, p.NT) = xs_.t_max;
+      AT(p.command, g, p.NT) = xs_.command;
+      AT(p.t_store, g, p.NT) = xs_.t_store;
+      AT(p.ticket, g, p.NT) = xs_.ticket;
+      AT(p.is_commit, g, p.NT) = xs_.is_commit;
+      AT(p.proposal, g, p.NT) = xs_.proposal;
+      AT(p.vote_s, g, p.NT) = xs_.vs;
+      AT(p.vote_f, g, p.NT) = xs_.vf;
+    }
+    for (int k = 0; k < BCSIM_MSG_TYPES; ++k)
+      if (c.deliv[k]) {
+        atomicAdd(&cnt[CNT_DELIV + k], c.deliv[k]);
+        tot += c.deliv[k];
+      }
+    if (tot) {
+      atomicAdd(&cnt[CNT_DELIV_TOTAL], tot);
+      atomicAdd(&p.kstat[KST_DELIV], tot);
+    }
+    if (c.echoes) atomicAdd(&cnt[CNT_ECHOES], c.echoes);
+    if (c.wrong) atomicAdd(&cnt[CNT_WRONG], c.wrong);
+    if (c.events) atomicAdd(&cnt[CNT_EVENTS], c.events);
+  }
+  if (S.tmax > LLONG_MIN) atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), S.tmax);
 }
 
 // ---------------------------------------------------------------------------
 // k_link: per-node link stage.  Ops due in [.., t_hi) are applied to their
 // out-edge's FIFO in canonical key order; every non-echo op produces one
-// 32-byte arrival record, scattered into the bucket of its arrival cell.
-constexpr int kHot = 8;       // arrival cells g+1 .. g+kHot get chunked appends
-constexpr int kBcastCap = 64; // due broadcasts per node per cell
+// 16-byte arrival record, stored in the receiver's inbox slot of the arrival
+// cell (a second record of the same edge and cell goes to the extras list,
+// a cell beyond the ring to the overflow list).
+constexpr int kBcastCap = 64;  // due broadcasts per node per cell
+constexpr int kMaxBuckets = 64;
 
 __device__ inline bool op_key_less(const Op& a, uint32_t sa, const Op& b, uint32_t sb) {
   if (a.t != b.t) return a.t < b.t;
@@ -1152,64 +1543,20 @@ __device__ inline bool op_key_less(const Op& a, uint32_t sa, const Op& b, uint32
   return sa < sb;
 }
 
-struct LinkLds {
-  uint32_t n_bc;
-  uint32_t n_due;
-  uint32_t n_keep;
-  uint32_t hot_cnt[kHot];
-  uint32_t hot_base[kHot];
-  uint32_t hot_fill[kHot];
+struct LinkShared {
+  uint32_t n_bc, n_keep;
   uint32_t bc[kBcastCap];
+  uint32_t lcnt[kMaxBuckets];
+  uint4 wsum[kMaxWaves];
+  long long omin;
 };
 
-// iterate the ops of edge `le` of node i in key order, calling f(op, sub, is_echo, dropped)
-template <typename F>
-__device__ inline void edge_ops(const KP& p, const Op* ops, const uint32_t* eidx, uint32_t eb,
-                                uint32_t ee, const uint32_t* bc, uint32_t n_bc, uint32_t le,
-                                uint32_t deg, F&& f) {
-  // eidx[eb..ee) are this edge's SEND/ECHO op indices, sorted by key already
-  uint32_t a = eb, b = 0;
-  for (;;) {
-    // next bcast that targets this edge
-    while (b < n_bc) {
-      const Op& o = AT(ops, bc[b], p.cap_ops);
-      const bool paxos = (op_flags(o) & OPF_PAXOS) != 0;
-      if (paxos && le == 0) {
-        ++b;
-        continue;
-      }
-      break;
-    }
-    const bool ha = a < ee, hb = b < n_bc;
-    if (!ha && !hb) break;
-    bool take_a;
-    uint32_t sub_b = 0;
-    if (hb) {
-      const Op& ob = AT(ops, bc[b], p.cap_ops);
-      const bool paxos = (op_flags(ob) & OPF_PAXOS) != 0;
-      sub_b = ob.sub + (paxos ? le - 1 : le);
-    }
-    if (ha && hb) {
-      const Op& oa = AT(ops, eidx[a], p.cap_ops);
-      take_a = op_key_less(oa, oa.sub, AT(ops, bc[b], p.cap_ops), sub_b);
-    } else {
-      take_a = ha;
-    }
-    if (take_a) {
-      const Op& oa = AT(ops, eidx[a++], p.cap_ops);
-      f(oa, oa.sub, op_kind(oa) == OP_ECHO);
-    } else {
-      f(AT(ops, bc[b++], p.cap_ops), sub_b, false);
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void k_link(const KP* __restrict__ pk, long long cell, long long t_hi) {
+__global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_hi) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ LinkLds L;
-  const uint32_t g = blockIdx.x;
+  __shared__ LinkShared L;
+  const uint32_t g = xcd_map(blockIdx.x, p.NT);
   if (g >= p.NT) return;
   uint32_t n = AT(p.n_ops, g, p.NT);
   if (n == 0) return;
@@ -1220,9 +1567,12 @@ __global__ __launch_bounds__(256) void k_link(const KP* __restrict__ pk, long lo
   uint32_t* ecnt = reinterpret_cast<uint32_t*>(smem);   // deg+1
   uint32_t* efill = ecnt + (p.deg_max + 1);              // deg
   uint32_t* eidx = efill + p.deg_max;                    // cap_ops
-  int64_t* busy = p.busy + static_cast<size_t>(rep) * p.E + e0;
+  const size_t eb0 = static_cast<size_t>(rep) * p.E + e0;
+  int64_t* busy = p.busy + eb0;
+  int64_t* lastc = p.lastc + eb0;
   const int64_t* prop = p.prop + e0;
   unsigned long long* cnt = &AT(p.counters, static_cast<size_t>(rep) * CNT_N, static_cast<uint64_t>(p.R) * CNT_N);
+  const uint32_t B = p.n_buckets;
 
   // ---- 0. expand jitter broadcasts into per-edge SEND ops ----
   if (p.delay_mode != BCSIM_DELAY_FIXED) {
@@ -1253,24 +1603,21 @@ __global__ __launch_bounds__(256) void k_link(const KP* __restrict__ pk, long lo
     }
   }
 
-  // ---- 1. classify due ops ----
+  // ---- 1. classify due ops: per-edge counts, broadcast list ----
   for (uint32_t k = tid; k <= deg; k += blockDim.x) ecnt[k] = 0;
+  for (uint32_t k = tid; k < deg; k += blockDim.x) efill[k] = 0;
+  for (uint32_t k = tid; k < B; k += blockDim.x) L.lcnt[k] = 0;
   if (tid == 0) {
     L.n_bc = 0;
-    L.n_due = 0;
-    for (int h = 0; h < kHot; ++h) {
-      L.hot_cnt[h] = 0;
-      L.hot_fill[h] = 0;
-    }
+    L.n_keep = 0;
+    L.omin = LLONG_MAX;
   }
   __syncthreads();
-  unsigned long long dropped = 0, sends = 0;
-  unsigned long long st_rec = 0, st_ops = 0, st_edges = 0;
+  unsigned long long dropped = 0, sends = 0, st_ops = 0;
   for (uint32_t k = tid; k < n; k += blockDim.x) {
-    const Op& o = AT(ops, k, p.cap_ops);
+    const Op& o = ops[k];
     const uint8_t kind = op_kind(o);
-    if (kind == OP_BCAST_J) continue;  // expanded (done) marker
-    if (o.t >= t_hi) continue;
+    if (kind == OP_BCAST_J || o.t >= t_hi) continue;
     ++st_ops;
     if (kind == OP_BCAST) {
       const uint32_t pos = atomicAdd(&L.n_bc, 1u);
@@ -1290,30 +1637,27 @@ __global__ __launch_bounds__(256) void k_link(const KP* __restrict__ pk, long lo
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
     return;
   }
-  // exclusive scan of ecnt[0..deg] (single thread; deg is small next to the op count)
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (uint32_t k = 0; k <= deg; ++k) {
-      const uint32_t v = ecnt[k];
-      ecnt[k] = acc;
-      acc += v;
-    }
-    L.n_due = acc;
-    // sort the broadcasts by key (insertion sort, few)
+  const uint32_t n_due = block_scan_array(ecnt, deg + 1, L.wsum);
+  if (n_due > p.cap_ops) {  // unreachable: n_due <= n <= cap_ops
+    if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
+    return;
+  }
+  if (tid == 0) {  // sort the broadcasts by key (insertion sort, few)
     for (uint32_t a = 1; a < L.n_bc; ++a) {
       const uint32_t x = L.bc[a];
+      const Op ox = ops[x];
       uint32_t b2 = a;
-      while (b2 > 0 && op_key_less(AT(ops, x, p.cap_ops), AT(ops, x, p.cap_ops).sub, AT(ops, L.bc[b2 - 1], p.cap_ops), AT(ops, L.bc[b2 - 1], p.cap_ops).sub)) {
+      while (b2 > 0) {
+        const Op& oy = ops[L.bc[b2 - 1]];
+        if (!op_key_less(ox, ox.sub, oy, oy.sub)) break;
         L.bc[b2] = L.bc[b2 - 1];
         --b2;
       }
       L.bc[b2] = x;
     }
   }
-  for (uint32_t k = tid; k < deg; k += blockDim.x) efill[k] = 0;
-  __syncthreads();
   for (uint32_t k = tid; k < n; k += blockDim.x) {
-    const Op& o = AT(ops, k, p.cap_ops);
+    const Op& o = ops[k];
     const uint8_t kind = op_kind(o);
     if (kind == OP_BCAST_J || kind == OP_BCAST || o.t >= t_hi || o.edge == kInvalid) continue;
     const uint32_t le = o.edge - e0;
@@ -1322,114 +1666,122 @@ __global__ __launch_bounds__(256) void k_link(const KP* __restrict__ pk, long lo
   __syncthreads();
   const uint32_t n_bc = L.n_bc;
 
-  // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO ----
-  // pass A counts arrivals per hot cell; pass B writes.
-  for (int pass = 0; pass < 2; ++pass) {
-    for (uint32_t le = tid; le < deg; le += blockDim.x) {
-      const uint32_t eb = ecnt[le], ee = ecnt[le + 1];
-      if (pass == 0) {  // insertion sort this edge's op indices by key
-        for (uint32_t a = eb + 1; a < ee; ++a) {
-          const uint32_t x = eidx[a];
-          uint32_t b2 = a;
-          while (b2 > eb && op_key_less(AT(ops, x, p.cap_ops), AT(ops, x, p.cap_ops).sub, AT(ops, eidx[b2 - 1], p.cap_ops), AT(ops, eidx[b2 - 1], p.cap_ops).sub)) {
-            eidx[b2] = eidx[b2 - 1];
-            --b2;
+  // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO, emit ----
+  unsigned long long st_rec = 0, st_edges = 0;
+  for (uint32_t le = tid; le < deg; le += blockDim.x) {
+    const uint32_t eb = ecnt[le], ee = ecnt[le + 1];
+    if (ee == eb && n_bc == 0) continue;
+    for (uint32_t a = eb + 1; a < ee; ++a) {  // insertion sort of this edge's ops (few)
+      const uint32_t x = eidx[a];
+      const Op ox = ops[x];
+      uint32_t b2 = a;
+      while (b2 > eb) {
+        const Op& oy = ops[eidx[b2 - 1]];
+        if (!op_key_less(ox, ox.sub, oy, oy.sub)) break;
+        eidx[b2] = eidx[b2 - 1];
+        --b2;
+      }
+      eidx[b2] = x;
+    }
+    ++st_edges;
+    const uint32_t e = e0 + le;
+    int64_t bu = busy[le];
+    int64_t lc = lastc[le];
+    const int64_t pr = prop[le];
+    const uint32_t s = AT(p.col, e, p.E);
+    const uint32_t slot = AT(p.rev, e, p.E);
+    const uint32_t dg = rep * p.N + s;
+    uint32_t a = eb, bi = 0;
+    for (;;) {
+      // next broadcast that targets this edge (Paxos broadcasts skip peers[0])
+      while (bi < n_bc && (op_flags(ops[L.bc[bi]]) & OPF_PAXOS) && le == 0) ++bi;
+      const bool ha = a < ee, hb = bi < n_bc;
+      if (!ha && !hb) break;
+      uint32_t sub_b = 0;
+      if (hb) {
+        const Op& ob = ops[L.bc[bi]];
+        sub_b = ob.sub + ((op_flags(ob) & OPF_PAXOS) ? le - 1 : le);
+      }
+      bool take_a = ha;
+      if (ha && hb) {
+        const Op& oa = ops[eidx[a]];
+        take_a = op_key_less(oa, oa.sub, ops[L.bc[bi]], sub_b);
+      }
+      const Op o = take_a ? ops[eidx[a++]] : ops[L.bc[bi++]];
+      const uint32_t sub = take_a ? o.sub : sub_b;
+      const bool is_echo = take_a && op_kind(o) == OP_ECHO;
+      const int big = (op_flags(o) & OPF_BIG) ? 1 : 0;
+      const int64_t start = bu > o.t ? bu : o.t;
+      const int64_t end = start + p.tx_tot[big];
+      bu = end;
+      if (is_echo) continue;
+      const int64_t ta = end + pr;
+      const long long ca = ta / p.L;
+      const long long rel = ca - cell;
+      if (rel < 1) {
+        set_err(p, BCSIM_E_TIE);  // lookahead violated
+        continue;
+      }
+      ++st_rec;
+      Rec r;
+      r.t_off = static_cast<uint32_t>(ta - ca * p.L);
+      r.sub = sub;
+      r.f0 = o.f0;
+      r.f1 = o.f1;
+      r.f2 = o.f2;
+      r.type = o.type;
+      r.flags = static_cast<uint8_t>(RF_VALID | (big ? RF_BIG : 0));
+      const bool owner = lc != ca;
+      lc = ca;
+      if (rel < static_cast<long long>(B)) {
+        const uint32_t bk = static_cast<uint32_t>(ca % B);
+        if (owner) {
+          AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox) = r;
+        } else {
+          const uint32_t pos = atomicAdd(&p.x_cnt[bk], 1u);
+          if (pos >= p.cap_x) {
+            set_err(p, BCSIM_E_OVERFLOW);
+            continue;
           }
-          eidx[b2] = x;
+          XRec x;
+          x.r = r;
+          x.cell = ca;
+          x.slot = slot;
+          x.g = dg;
+          AT(p.xbuf, static_cast<size_t>(bk) * p.cap_x + pos, p.cap_xbuf) = x;
         }
-      }
-      if (ee == eb && n_bc == 0) continue;
-      if (pass == 1) ++st_edges;
-      int64_t bu = AT(busy, le, p.cap_E - (static_cast<uint64_t>(rep) * p.E + e0));
-      const int64_t pr = prop[le];
-      const uint32_t dest = rep * p.N + AT(p.col, e0 + le, p.E);
-      edge_ops(p, ops, eidx, eb, ee, L.bc, n_bc, le, deg,
-               [&](const Op& o, uint32_t sub, bool is_echo) {
-                 const int big = (op_flags(o) & OPF_BIG) ? 1 : 0;
-                 const int64_t start = bu > o.t ? bu : o.t;
-                 const int64_t end = start + p.tx_tot[big];
-                 bu = end;
-                 if (is_echo) return;
-                 const int64_t ta = end + pr;
-                 const long long ca = ta / p.L;
-                 const long long rel = ca - cell;
-                 if (pass == 0) {
-                   if (rel >= 1 && rel <= kHot && rel < static_cast<long long>(p.n_buckets))
-                     atomicAdd(&L.hot_cnt[rel - 1], 1u);
-                   return;
-                 }
-                 ++st_rec;
-                 Rec r;
-                 r.t_off = static_cast<uint32_t>(ta - ca * p.L);
-                 r.dt = static_cast<uint32_t>(ta - (end - p.tx_last[big]));
-                 r.dest = dest;
-                 r.origin = i;
-                 r.sub = sub;
-                 r.edge = e0 + le;
-                 r.f0 = o.f0;
-                 r.f1 = o.f1;
-                 r.f2 = o.f2;
-                 r.type = o.type;
-                 r.big = static_cast<uint8_t>(big);
-                 if (rel >= 1 && rel <= kHot && rel < static_cast<long long>(p.n_buckets)) {
-                   const uint32_t h = static_cast<uint32_t>(rel - 1);
-                   const uint32_t pos = L.hot_base[h] + atomicAdd(&L.hot_fill[h], 1u);
-                   const uint32_t b = static_cast<uint32_t>(ca % p.n_buckets);
-                   AT(p.bucket, static_cast<size_t>(b) * p.cap_bucket + pos, static_cast<uint64_t>(p.n_buckets) * p.cap_bucket) = r;
-                 } else if (rel >= 1 && rel < static_cast<long long>(p.n_buckets)) {
-                   const uint32_t b = static_cast<uint32_t>(ca % p.n_buckets);
-                   const uint32_t pos = atomicAdd(&p.bucket_cnt[b], 1u);
-                   if (pos >= p.cap_bucket) {
-                     set_err(p, BCSIM_E_OVERFLOW);
-                     return;
-                   }
-                   AT(p.bucket, static_cast<size_t>(b) * p.cap_bucket + pos, static_cast<uint64_t>(p.n_buckets) * p.cap_bucket) = r;
-                 } else if (rel >= 1) {
-                   const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
-                   if (pos >= p.cap_ov) {
-                     set_err(p, BCSIM_E_OVERFLOW);
-                     return;
-                   }
-                   OvRec ovr;
-                   ovr.cell = ca;
-                   ovr.pad = 0;
-                   ovr.r = r;
-                   AT(p.ov, pos, p.cap_ov) = ovr;
-                   atomicMin(&p.scal[1], ca);
-                 } else {
-                   set_err(p, BCSIM_E_TIE);  // lookahead violated
-                 }
-               });
-      if (pass == 1) AT(busy, le, p.cap_E - (static_cast<uint64_t>(rep) * p.E + e0)) = bu;
-    }
-    __syncthreads();
-    if (pass == 0 && tid == 0) {
-      for (int h = 0; h < kHot; ++h) {
-        if (L.hot_cnt[h] == 0) continue;
-        const long long ca = cell + 1 + h;
-        const uint32_t b = static_cast<uint32_t>(ca % p.n_buckets);
-        const uint32_t base = atomicAdd(&p.bucket_cnt[b], L.hot_cnt[h]);
-        if (base + L.hot_cnt[h] > p.cap_bucket) set_err(p, BCSIM_E_OVERFLOW);
-        L.hot_base[h] = base;
+        AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
+        atomicAdd(&L.lcnt[bk], 1u);
+      } else {
+        const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+        if (pos >= p.cap_ov) {
+          set_err(p, BCSIM_E_OVERFLOW);
+          continue;
+        }
+        XRec x;
+        x.r = r;
+        if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+        x.cell = ca;
+        x.slot = slot;
+        x.g = dg;
+        AT(p.ov, pos, p.cap_ov) = x;
+        atomicMin(&p.scal[1], ca);
       }
     }
-    __syncthreads();
-    if (*p.err) return;
+    busy[le] = bu;
+    lastc[le] = lc;
   }
+  __syncthreads();
 
   // ---- 3. compact the ops that are not due yet ----
-  if (tid == 0) L.n_keep = 0;
-  __syncthreads();
   long long omin = LLONG_MAX;
-  // stable enough: order inside the list is irrelevant (ops are re-sorted)
   Op keep[4];
-  uint32_t nk = 0;
   for (uint32_t k0 = 0; k0 < n; k0 += blockDim.x * 4) {
-    nk = 0;
+    uint32_t nk = 0;
     for (uint32_t u = 0; u < 4; ++u) {
       const uint32_t k = k0 + u * blockDim.x + tid;
       if (k >= n) continue;
-      const Op o = AT(ops, k, p.cap_ops);
+      const Op o = ops[k];
       const uint8_t kind = op_kind(o);
       if (kind == OP_BCAST_J) {
         if (op_flags(o) & OPF_DONE) continue;
@@ -1446,23 +1798,19 @@ __global__ __launch_bounds__(256) void k_link(const KP* __restrict__ pk, long lo
     for (uint32_t u = 0; u < nk; ++u) AT(ops, base + u, p.cap_ops) = keep[u];
     __syncthreads();
   }
-  // min over lanes of omin
-  __shared__ long long omin_s;
-  if (tid == 0) omin_s = LLONG_MAX;
-  __syncthreads();
-  if (omin != LLONG_MAX) atomicMin(&omin_s, omin);
+  if (omin != LLONG_MAX) atomicMin(&L.omin, omin);
   if (dropped) atomicAdd(&cnt[CNT_DROPPED], dropped);
   if (sends) atomicAdd(&cnt[CNT_SENDS], sends);
-  if (st_rec | st_ops | st_edges) {
-    atomicAdd(&p.kstat[0], st_rec);
-    atomicAdd(&p.kstat[1], st_ops);
-    atomicAdd(&p.kstat[2], st_edges);
-  }
+  if (st_rec) atomicAdd(&p.kstat[KST_REC], st_rec);
+  if (st_ops) atomicAdd(&p.kstat[KST_OPS], st_ops);
+  if (st_edges) atomicAdd(&p.kstat[KST_EDGES], st_edges);
   __syncthreads();
+  for (uint32_t k = tid; k < B; k += blockDim.x)
+    if (L.lcnt[k]) atomicAdd(&p.bucket_cnt[k], L.lcnt[k]);
   if (tid == 0) {
     AT(p.n_ops, g, p.NT) = L.n_keep;
-    AT(p.node_onext, g, p.NT) = omin_s;
-    atomicAdd(&p.kstat[3], static_cast<unsigned long long>(L.n_keep));
+    AT(p.node_onext, g, p.NT) = L.omin;
+    atomicAdd(&p.kstat[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
   }
 }
 
@@ -1525,26 +1873,9 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
       const uint32_t g = rep * N + i;
       uint32_t sub = AT(p.sub, g, p.NT);
       const uint32_t deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
-      bcsim_trace_rec tr;
-      tr.t_ns = tk;
-      tr.key_ts = ts_tick;
-      tr.key_origin = i;
-      tr.key_sub = AT(p.tick_sub, g, p.NT);
-      tr.replica = rep;
-      tr.node = i;
       const int32_t n_seq = AT(p.g_n, rep, p.R);
-      {  // :387 leader log
-        const uint32_t pos = atomicAdd(p.trace_cnt, 1u);
-        if (pos < p.cap_trace) {
-          tr.kind = BCSIM_TR_PBFT_BLOCK;
-          tr.a = n_seq;
-          tr.b = v_cur;
-          tr.c = 0;
-          AT(p.trace, pos, p.cap_trace) = tr;
-        } else {
-          set_err(p, BCSIM_E_OVERFLOW);
-        }
-      }
+      const Key tkey{tk, ts_tick, i, AT(p.tick_sub, g, p.NT)};
+      emit_trace(p, tkey, rep, i, BCSIM_TR_PBFT_BLOCK, n_seq, v_cur, 0);  // :387 leader log
       // block = generateTX header '1', v, n, n (:79-95)
       Msg blk = mkmsg(PB_PRE_PREPARE, enc_raw(p, v_cur), enc_raw(p, n_seq), enc_raw(p, n_seq), 1);
       uint32_t nops = AT(p.n_ops, g, p.NT);
@@ -1557,7 +1888,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
         }
         if (p.delay_mode == BCSIM_DELAY_FIXED) {
           AT(ops, nops++, p.cap_ops) = mk_op(p, tk + p.app_delay, static_cast<uint32_t>(p.app_delay), i, sub, 0, m,
-                              OP_BCAST, 0);
+                                             OP_BCAST, 0);
         } else {
           AT(ops, nops++, p.cap_ops) = mk_op(p, tk, 0, i, sub, static_cast<uint32_t>(draws), m, OP_BCAST_J, 0);
           draws += deg;
@@ -1580,21 +1911,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
           const int32_t nl = (AT(p.leader, g, p.NT) + 1) % static_cast<int32_t>(N);
           AT(p.leader, g, p.NT) = nl;
           v_cur += 1;
-          const uint32_t pos = atomicAdd(p.vlog_cnt, 1u);
-          if (pos < p.cap_vlog) {
-            VLog e;
-            e.t = tk;
-            e.ts = ts_tick;
-            e.origin = i;
-            e.sub = AT(p.tick_sub, g, p.NT);
-            e.target = i;
-            e.rep = rep;
-            e.v = v_cur;
-            e.pad = 0;
-            AT(p.vlog, pos, p.cap_vlog) = e;
-          } else {
-            set_err(p, BCSIM_E_OVERFLOW);
-          }
+          emit_vlog(p, tkey, rep, i, v_cur);
           push_bcast(mkmsg(PB_VIEW_CHANGE, enc_raw(p, v_cur), enc_raw(p, nl), 0, 0));
         }
       }
@@ -1609,13 +1926,12 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
   // every alive node: n_round seen = n_round0 + #leaders with id <= i
   // (prefix over the leader flags), reschedule, stop check.
   __shared__ int32_t chunk_base;
+  __shared__ int32_t sc[1024];
   if (tid == 0) chunk_base = 0;
   __syncthreads();
   for (uint32_t base = 0; base < N; base += blockDim.x) {
     const uint32_t i = base + tid;
     const uint32_t f = (i < N) ? lead[i] : 0u;
-    // block inclusive prefix of f
-    __shared__ int32_t sc[1024];
     sc[tid] = static_cast<int32_t>(f);
     __syncthreads();
     for (uint32_t off = 1; off < blockDim.x; off <<= 1) {
@@ -1634,23 +1950,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
         AT(p.sub, g, p.NT) = s + 1;
         atomicAdd(&n_ticked, 1);
         if (nr == static_cast<int32_t>(p.pbft_rounds)) {  // :407-410
-          const uint32_t pos = atomicAdd(p.trace_cnt, 1u);
-          if (pos < p.cap_trace) {
-            bcsim_trace_rec tr;
-            tr.t_ns = tk;
-            tr.key_ts = ts_tick;
-            tr.key_origin = i;
-            tr.key_sub = fired;
-            tr.replica = rep;
-            tr.node = i;
-            tr.kind = BCSIM_TR_PBFT_STOP;
-            tr.a = nr;
-            tr.b = 0;
-            tr.c = 0;
-            AT(p.trace, pos, p.cap_trace) = tr;
-          } else {
-            set_err(p, BCSIM_E_OVERFLOW);
-          }
+          emit_trace(p, Key{tk, ts_tick, i, fired}, rep, i, BCSIM_TR_PBFT_STOP, nr, 0, 0);
           AT(p.tick_alive, g, p.NT) = 0;
         } else {
           atomicAdd(&n_alive, 1);

@@ -21,8 +21,8 @@ for st in $steps; do
     parity)  run parity 300 python -m pytest tests -m gpu -x -q ;;
     smoke)   run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench1k) run bench1k 300 python bench.py --nodes 1024 --cpu-budget 5 ;;
-    bench)   run bench 900 python bench.py ;;
-    prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python bench.py --no-cpu-baseline ;;
+    bench)   run bench 400 python bench.py ;;
+    prof)    run prof 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python bench.py --no-cpu-baseline ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

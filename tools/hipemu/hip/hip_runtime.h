@@ -31,8 +31,13 @@ struct dim3 {
 struct hipemu_ctx {
   dim3 tid, bid, bdim, gdim;
   std::barrier<>* bar;
+  std::barrier<>* wbar;      // per-wave barriers (64 lanes each)
   unsigned long long* shfl;  // per-block shuffle exchange
 };
+struct uint4 {
+  unsigned x, y, z, w;
+};
+inline uint4 make_uint4(unsigned a, unsigned b, unsigned c, unsigned d) { return uint4{a, b, c, d}; }
 extern thread_local hipemu_ctx hipemu_t;
 #define threadIdx (hipemu_t.tid)
 #define blockIdx (hipemu_t.bid)
@@ -43,16 +48,60 @@ inline void __syncthreads() { hipemu_t.bar->arrive_and_wait(); }
 inline void __builtin_amdgcn_endpgm() { throw hipemu_exit{}; }
 char* hipemu_dyn_smem();
 
+// wave-level exchange: every lane of the wave must call (wave64)
+inline void hipemu_wsync() { hipemu_t.wbar[hipemu_t.tid.x / 64].arrive_and_wait(); }
+inline unsigned long long hipemu_xchg_get(unsigned lane) {
+  return hipemu_t.shfl[(hipemu_t.tid.x / 64) * 64 + lane];
+}
 template <typename T>
-inline T __shfl_up(T v, unsigned d, int width = 64) {
-  unsigned t = hipemu_t.tid.x;
-  hipemu_t.shfl[t] = static_cast<unsigned long long>(v);
-  __syncthreads();
-  unsigned lane = t % width;
-  T r = lane >= d ? static_cast<T>(hipemu_t.shfl[t - d]) : v;
-  __syncthreads();
+inline T hipemu_from(unsigned long long v) {
+  T r;
+  std::memcpy(&r, &v, sizeof(T));
   return r;
 }
+template <typename T>
+inline unsigned long long hipemu_to(T v) {
+  unsigned long long r = 0;
+  std::memcpy(&r, &v, sizeof(T));
+  return r;
+}
+template <typename T>
+inline T __shfl(T v, int src, int width = 64) {
+  hipemu_t.shfl[hipemu_t.tid.x] = hipemu_to(v);
+  hipemu_wsync();
+  T r = hipemu_from<T>(hipemu_xchg_get(static_cast<unsigned>(src) & 63u));
+  hipemu_wsync();
+  return r;
+}
+template <typename T>
+inline T __shfl_up(T v, unsigned d, int width = 64) {
+  hipemu_t.shfl[hipemu_t.tid.x] = hipemu_to(v);
+  hipemu_wsync();
+  unsigned lane = hipemu_t.tid.x % 64;
+  T r = lane >= d ? hipemu_from<T>(hipemu_xchg_get(lane - d)) : v;
+  hipemu_wsync();
+  return r;
+}
+template <typename T>
+inline T __shfl_xor(T v, int m, int width = 64) {
+  hipemu_t.shfl[hipemu_t.tid.x] = hipemu_to(v);
+  hipemu_wsync();
+  unsigned lane = hipemu_t.tid.x % 64;
+  T r = hipemu_from<T>(hipemu_xchg_get((lane ^ static_cast<unsigned>(m)) & 63u));
+  hipemu_wsync();
+  return r;
+}
+inline unsigned long long __ballot(int pred) {
+  hipemu_t.shfl[hipemu_t.tid.x] = pred ? 1ull : 0ull;
+  hipemu_wsync();
+  unsigned long long m = 0;
+  for (unsigned l = 0; l < 64; ++l)
+    if (hipemu_xchg_get(l)) m |= 1ull << l;
+  hipemu_wsync();
+  return m;
+}
+inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+inline int __ffsll(long long x) { return __builtin_ffsll(x); }
 
 template <typename T, typename U>
 inline T atomicAdd(T* p, U v) { return __atomic_fetch_add(p, static_cast<T>(v), __ATOMIC_SEQ_CST); }

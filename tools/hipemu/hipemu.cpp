@@ -51,6 +51,7 @@ struct Pool {
   dim3 grid, block;
   unsigned bid = 0, nt = 0;
   std::barrier<>* bar = nullptr;
+  std::barrier<>* wbar = nullptr;
   std::latch* done = nullptr;
   char* smem = nullptr;
   unsigned long long* shfl = nullptr;
@@ -70,10 +71,12 @@ struct Pool {
       hipemu_t.bdim = block;
       hipemu_t.gdim = grid;
       hipemu_t.bar = bar;
+      hipemu_t.wbar = wbar;
       hipemu_t.shfl = shfl;
       t_smem = smem;
       auto* dn = done;
       auto* br = bar;
+      auto* wb = &wbar[t / 64];
       lk.unlock();
       try {
         (*b)();
@@ -81,6 +84,7 @@ struct Pool {
         std::fprintf(stderr, "hipemu: wave ended by s_endpgm (block %u thread %u)\n", hipemu_t.bid.x, t);
       }
       br->arrive_and_drop();
+      wb->arrive_and_drop();
       dn->count_down();
     }
   }
@@ -97,8 +101,13 @@ void hipemu_launch(dim3 grid, dim3 block, size_t lds, const std::function<void()
   if (nt > Pool::kMax) throw std::runtime_error("hipemu: block too large");
   std::vector<char> smem(lds + 64, 0);
   std::vector<unsigned long long> shfl(nt);
+  if (nt % 64) throw std::runtime_error("hipemu: block must be a multiple of 64 threads");
   for (unsigned b = 0; b < grid.x; ++b) {
     std::barrier<> bar(nt);
+    std::allocator<std::barrier<>> wal;
+    const unsigned nw = nt / 64;
+    std::barrier<>* wb = wal.allocate(nw);
+    for (unsigned w = 0; w < nw; ++w) new (&wb[w]) std::barrier<>(64);
     std::latch done(nt);
     {
       std::lock_guard<std::mutex> lk(P.m);
@@ -111,9 +120,12 @@ void hipemu_launch(dim3 grid, dim3 block, size_t lds, const std::function<void()
       P.done = &done;
       P.smem = smem.data();
       P.shfl = shfl.data();
+      P.wbar = wb;
       ++P.gen;
     }
     P.cv.notify_all();
     done.wait();
+    for (unsigned w = 0; w < nw; ++w) wb[w].~barrier();
+    wal.deallocate(wb, nw);
   }
 }
