@@ -334,7 +334,13 @@ static int setup_device(Sim& s) {
   s.bs_link = s.bs_scan;
   // inbox ring: one 16-byte slot per (bucket, replica, edge); as many buckets
   // as ~8 GiB allows, 8..64
-  const uint64_t per_bucket = static_cast<uint64_t>(s.R) * s.E * sizeof(Rec);
+  // full mesh (blockchain-simulator.cc:34-51): records are staged sender-major
+  // and moved to the receivers by the tiled transpose (k_transpose)
+  bool mesh = s.E == static_cast<uint64_t>(s.N) * (s.N - 1) && s.N >= 2;
+  for (uint32_t i = 0; mesh && i <= s.N; ++i) mesh = s.row[i] == static_cast<uint64_t>(i) * (s.N - 1);
+  p.mesh = mesh ? 1u : 0u;
+  p.n_tiles = (s.N + kTile - 1) / kTile;
+  const uint64_t per_bucket = static_cast<uint64_t>(s.R) * s.E * sizeof(Rec) * (mesh ? 2 : 1);
   s.B = c.n_buckets ? c.n_buckets : 0;
   if (s.B == 0) {
     const uint64_t nb = per_bucket ? (8ull << 30) / per_bucket : kMaxBuckets;
@@ -410,6 +416,8 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.busy, static_cast<size_t>(s.R) * s.E)) ||
       (rc = dalloc(s, &p.lastc, static_cast<size_t>(s.R) * s.E)))
     return rc;
+  const size_t n_dirty = p.mesh ? static_cast<size_t>(s.B) * s.R * p.n_tiles * p.n_tiles : 1;
+  if ((rc = dalloc(s, &p.outbox, p.mesh ? p.cap_inbox : 1)) || (rc = dalloc(s, &p.tdirty, n_dirty))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
       (rc = dalloc(s, &p.xbuf, p.cap_xbuf)) || (rc = dalloc(s, &p.xgrp, p.cap_x)) ||
       (rc = dalloc(s, &p.ov, p.cap_ov)))
@@ -483,6 +491,8 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemset(p.busy, 0, static_cast<size_t>(s.R) * s.E * 8));
   HIPCHK(hipMemset(p.lastc, 0xFF, static_cast<size_t>(s.R) * s.E * 8));  // -1: no record yet
   HIPCHK(hipMemset(p.inbox, 0, p.cap_inbox * sizeof(Rec)));
+  if (p.mesh) HIPCHK(hipMemset(p.outbox, 0, p.cap_inbox * sizeof(Rec)));
+  HIPCHK(hipMemset(p.tdirty, 0, n_dirty));
   HIPCHK(hipMemset(p.iflag, 0, static_cast<size_t>(s.B) * NT));
   HIPCHK(hipMemset(p.seg_cnt, 0, NT * 4));
   HIPCHK(hipMemset(p.seg_off, 0, (NT + 1) * 4));
@@ -606,6 +616,11 @@ static int group_cell(Sim& s, long long cell) {
     return BCSIM_E_OVERFLOW;
   }
   s.x_active = 0;
+  if (s.kp.mesh) {  // sender-major outbox -> receiver rows of this cell's bucket
+    const uint32_t nt = s.kp.n_tiles;
+    int rc = launch(s, KS_GROUP, k_transpose, dim3(s.R * nt * nt), dim3(256), 0, s.kp_dev, b);
+    if (rc) return rc;
+  }
   if (nx) {
     HIPCHK(hipMemsetAsync(s.kp.seg_cnt, 0, s.NT * 4ull, s.stream));
     HIPCHK(hipMemsetAsync(s.kp.cursor, 0, s.NT * 4ull, s.stream));

@@ -86,7 +86,10 @@ struct KP {
   int64_t* busy;
   int64_t* lastc;  // cell of the last record emitted on the edge (-1: none)
   // inbox
-  Rec* inbox;            // [B][R][E]
+  Rec* inbox;            // [B][R][E]  receiver-major (in-slot order)
+  Rec* outbox;           // [B][R][E]  sender-major staging (full mesh only)
+  uint8_t* tdirty;       // [B][R][nt][nt] outbox tile holds records (full mesh only)
+  uint32_t mesh, n_tiles;  // full-mesh topology: records go through the tiled transpose
   uint8_t* iflag;        // [B][NT] node has records in the bucket
   uint32_t* bucket_cnt;  // [B] records in the bucket (slots + extras)
   uint32_t* x_cnt;       // [B] extras in the bucket
@@ -329,6 +332,23 @@ __device__ inline uint32_t block_rank(bool f, uint32_t* wcnt, uint32_t& total) {
   return off + below;
 }
 
+// Append one element per ACTIVE lane to a global counter with a single
+// atomic per wave (the returning atomic is the bottleneck when many lanes
+// hit one word).  Call from divergent code: the active lanes participate.
+__device__ inline uint32_t wave_append(uint32_t* counter) {
+#ifdef HIPEMU  // tools/hipemu runs lanes as threads without lockstep: no divergent ballots
+  return atomicAdd(counter, 1u);
+#else
+  const unsigned long long m = __ballot(1);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t first = static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
+  uint32_t base = 0;
+  if (lane == first) base = atomicAdd(counter, static_cast<uint32_t>(__popcll(m)));
+  base = __builtin_amdgcn_readfirstlane(base);
+  return base + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
+#endif
+}
+
 // Exclusive block scan of four u32 lanes at once; totals in `tot`.
 __device__ inline uint4 block_scan4(uint4 v, uint4* wsum, uint4& tot) {
   const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -481,7 +501,7 @@ __global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) 
     if (owner) {
       AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox) = x.r;
     } else {
-      const uint32_t pos = atomicAdd(&p.x_cnt[b], 1u);
+      const uint32_t pos = wave_append(&p.x_cnt[b]);
       if (pos >= p.cap_x) {
         set_err(p, BCSIM_E_OVERFLOW);
         return;
@@ -1548,7 +1568,8 @@ struct LinkShared {
   uint32_t bc[kBcastCap];
   uint32_t lcnt[kMaxBuckets];
   uint4 wsum[kMaxWaves];
-  long long omin;
+  uint32_t wcnt[kMaxWaves];
+  long long omin, ovmin;
 };
 
 __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_hi) {
@@ -1611,6 +1632,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     L.n_bc = 0;
     L.n_keep = 0;
     L.omin = LLONG_MAX;
+    L.ovmin = LLONG_MAX;
   }
   __syncthreads();
   unsigned long long dropped = 0, sends = 0, st_ops = 0;
@@ -1668,6 +1690,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
 
   // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO, emit ----
   unsigned long long st_rec = 0, st_edges = 0;
+  long long ovmin = LLONG_MAX;
   for (uint32_t le = tid; le < deg; le += blockDim.x) {
     const uint32_t eb = ecnt[le], ee = ecnt[le + 1];
     if (ee == eb && n_bc == 0) continue;
@@ -1736,9 +1759,15 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       if (rel < static_cast<long long>(B)) {
         const uint32_t bk = static_cast<uint32_t>(ca % B);
         if (owner) {
-          AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox) = r;
+          if (p.mesh) {  // sender-major staging, moved to the receiver by k_transpose
+            AT(p.outbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + e, p.cap_inbox) = r;
+            AT(p.tdirty, ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (i >> 6)) * p.n_tiles + (s >> 6),
+               static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
+          } else {
+            AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox) = r;
+          }
         } else {
-          const uint32_t pos = atomicAdd(&p.x_cnt[bk], 1u);
+          const uint32_t pos = wave_append(&p.x_cnt[bk]);
           if (pos >= p.cap_x) {
             set_err(p, BCSIM_E_OVERFLOW);
             continue;
@@ -1753,7 +1782,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
         atomicAdd(&L.lcnt[bk], 1u);
       } else {
-        const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+        const uint32_t pos = wave_append(p.ov_cnt);
         if (pos >= p.cap_ov) {
           set_err(p, BCSIM_E_OVERFLOW);
           continue;
@@ -1765,7 +1794,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         x.slot = slot;
         x.g = dg;
         AT(p.ov, pos, p.cap_ov) = x;
-        atomicMin(&p.scal[1], ca);
+        if (ca < ovmin) ovmin = ca;
       }
     }
     busy[le] = bu;
@@ -1774,31 +1803,32 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   __syncthreads();
 
   // ---- 3. compact the ops that are not due yet ----
+  // ordered in-place compaction: an op moves to the count of kept ops before
+  // it (<= its own index); every lane has read its op before any lane writes
   long long omin = LLONG_MAX;
-  Op keep[4];
-  for (uint32_t k0 = 0; k0 < n; k0 += blockDim.x * 4) {
-    uint32_t nk = 0;
-    for (uint32_t u = 0; u < 4; ++u) {
-      const uint32_t k = k0 + u * blockDim.x + tid;
-      if (k >= n) continue;
-      const Op o = ops[k];
+  uint32_t kept = 0;
+  for (uint32_t k0 = 0; k0 < n; k0 += blockDim.x) {
+    const uint32_t k = k0 + tid;
+    Op o{};
+    bool keep = false;
+    if (k < n) {
+      o = ops[k];
       const uint8_t kind = op_kind(o);
-      if (kind == OP_BCAST_J) {
-        if (op_flags(o) & OPF_DONE) continue;
-        keep[nk++] = o;  // unexpanded (fixed mode never creates these)
-        continue;
+      if (kind == OP_BCAST_J)
+        keep = !(op_flags(o) & OPF_DONE);  // unexpanded (fixed mode never creates these)
+      else if (o.t >= t_hi) {
+        keep = true;
+        if (o.t < omin) omin = o.t;
       }
-      if (o.t < t_hi) continue;
-      keep[nk++] = o;
-      if (o.t < omin) omin = o.t;
     }
-    __syncthreads();
-    const uint32_t base = atomicAdd(&L.n_keep, nk);
-    __syncthreads();
-    for (uint32_t u = 0; u < nk; ++u) AT(ops, base + u, p.cap_ops) = keep[u];
-    __syncthreads();
+    uint32_t tot;
+    const uint32_t pos = kept + block_rank(keep, L.wcnt, tot);
+    if (keep) ops[pos] = o;
+    kept += tot;
   }
+  if (tid == 0) L.n_keep = kept;
   if (omin != LLONG_MAX) atomicMin(&L.omin, omin);
+  if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
   if (dropped) atomicAdd(&cnt[CNT_DROPPED], dropped);
   if (sends) atomicAdd(&cnt[CNT_SENDS], sends);
   if (st_rec) atomicAdd(&p.kstat[KST_REC], st_rec);
@@ -1808,10 +1838,56 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   for (uint32_t k = tid; k < B; k += blockDim.x)
     if (L.lcnt[k]) atomicAdd(&p.bucket_cnt[k], L.lcnt[k]);
   if (tid == 0) {
+    if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
     AT(p.n_ops, g, p.NT) = L.n_keep;
     AT(p.node_onext, g, p.NT) = L.omin;
     atomicAdd(&p.kstat[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_transpose (full mesh): move the records of bucket b from the sender-major
+// outbox (coalesced k_link writes) to the receivers' inbox rows (coalesced
+// k_scan reads) through a 64 x 64 LDS tile — the all-to-all transpose of the
+// O(N^2) message matrix.  Edge i->s sits at i*(N-1) + s - (s > i) in the
+// outbox and at s*(N-1) + i - (i > s) in the inbox.  Clean tiles exit.
+constexpr int kTile = 64;
+
+__global__ __launch_bounds__(256) void k_transpose(const KP* __restrict__ pk, uint32_t b) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ Rec tile[kTile][kTile];  // column index XOR row: column reads spread over banks
+  const uint32_t nt = p.n_tiles;
+  const uint32_t tj = blockIdx.x % nt, ti = (blockIdx.x / nt) % nt, rep = blockIdx.x / (nt * nt);
+  const size_t didx = ((static_cast<size_t>(b) * p.R + rep) * nt + ti) * nt + tj;
+  uint8_t& dirty = AT(p.tdirty, didx, static_cast<uint64_t>(p.n_buckets) * p.R * nt * nt);
+  if (!dirty) return;
+  const uint32_t N = p.N, lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const size_t base = (static_cast<size_t>(b) * p.R + rep) * p.E;
+  Rec* ob = p.outbox + base;
+  Rec* ib = p.inbox + base;
+  const uint32_t i0 = ti * kTile, s0 = tj * kTile;
+  // rows of the outbox: sender i, receivers s0 + lane
+  for (uint32_t r = w; r < kTile; r += nw) {
+    const uint32_t i = i0 + r, s = s0 + lane;
+    Rec v{};
+    if (i < N && s < N && s != i) {
+      const size_t e = static_cast<size_t>(i) * (N - 1) + s - (s > i ? 1 : 0);
+      v = AT(ob, e, p.E);
+      if (v.flags) AT(ob, e, p.E) = Rec{};
+    }
+    tile[r][lane ^ r] = v;
+  }
+  __syncthreads();
+  // rows of the inbox: receiver s, senders i0 + lane
+  for (uint32_t c = w; c < kTile; c += nw) {
+    const uint32_t s = s0 + c, i = i0 + lane;
+    if (i < N && s < N && s != i) {
+      const Rec v = tile[lane][c ^ lane];
+      if (v.flags) AT(ib, static_cast<size_t>(s) * (N - 1) + i - (i > s ? 1 : 0), p.E) = v;
+    }
+  }
+  if (threadIdx.x == 0) dirty = 0;
 }
 
 // ---------------------------------------------------------------------------
