@@ -310,6 +310,22 @@ __device__ inline void emit_vlog(const KP& p, const Key& k, uint32_t rep, uint32
   AT(p.vlog, pos, p.cap_vlog) = e;
 }
 
+
+// one 16-byte memory access per record (the compiler otherwise splits the
+// mixed-width struct into byte / short / dwordx3 pieces)
+__device__ inline Rec ld_rec(const Rec* p) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  Rec r;
+  __builtin_memcpy(&r, &v, sizeof r);
+  return r;
+}
+__device__ inline void st_rec(Rec* p, const Rec& r) {
+  uint4 v;
+  __builtin_memcpy(&v, &r, sizeof v);
+  *reinterpret_cast<uint4*>(p) = v;
+}
+__device__ inline void clr_rec(Rec* p) { *reinterpret_cast<uint4*>(p) = make_uint4(0, 0, 0, 0); }
+
 // ---- block-wide primitives (blockDim.x a multiple of 64, <= 1024) ----------
 constexpr int kMaxWaves = 16;
 
@@ -339,7 +355,9 @@ __device__ inline uint32_t wave_append(uint32_t* counter) {
 #ifdef HIPEMU  // tools/hipemu runs lanes as threads without lockstep: no divergent ballots
   return atomicAdd(counter, 1u);
 #else
-  const unsigned long long m = __ballot(1);
+  // active lanes = EXEC (a constant-true __ballot(1) can be folded to the
+  // wave-uniform mask by the compiler, which is wrong in divergent code)
+  const unsigned long long m = __builtin_amdgcn_read_exec();
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t first = static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
   uint32_t base = 0;
@@ -499,7 +517,7 @@ __global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) 
     const bool owner = (x.r.flags & RF_OWNER) != 0;
     x.r.flags = static_cast<uint8_t>(x.r.flags & ~RF_OWNER);
     if (owner) {
-      AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox) = x.r;
+      st_rec(&AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox), x.r);
     } else {
       const uint32_t pos = wave_append(&p.x_cnt[b]);
       if (pos >= p.cap_x) {
@@ -888,7 +906,7 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
     Rec r{};
     bool v = false;
     if (k < deg) {
-      r = slots[k];
+      r = ld_rec(slots + k);
       const long long t = cs + r.t_off;
       v = (r.flags & RF_VALID) && t >= wa && t < wb;
     }
@@ -1470,7 +1488,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     // consumed slots are free again
     for (uint32_t r = tid; r < n; r += blockDim.x) {
       const uint32_t sec = asec[r];
-      if ((sec & kRidxMask) < n_main) const_cast<Rec*>(slots)[sec >> kRidxBits] = Rec{};
+      if ((sec & kRidxMask) < n_main) clr_rec(const_cast<Rec*>(slots) + (sec >> kRidxBits));
     }
     __syncthreads();
     if (wb >= t_hi) break;
@@ -1689,7 +1707,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   const uint32_t n_bc = L.n_bc;
 
   // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO, emit ----
-  unsigned long long st_rec = 0, st_edges = 0;
+  unsigned long long n_rec = 0, st_edges = 0;
   long long ovmin = LLONG_MAX;
   for (uint32_t le = tid; le < deg; le += blockDim.x) {
     const uint32_t eb = ecnt[le], ee = ecnt[le + 1];
@@ -1745,7 +1763,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         set_err(p, BCSIM_E_TIE);  // lookahead violated
         continue;
       }
-      ++st_rec;
+      ++n_rec;
       Rec r;
       r.t_off = static_cast<uint32_t>(ta - ca * p.L);
       r.sub = sub;
@@ -1760,11 +1778,11 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         const uint32_t bk = static_cast<uint32_t>(ca % B);
         if (owner) {
           if (p.mesh) {  // sender-major staging, moved to the receiver by k_transpose
-            AT(p.outbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + e, p.cap_inbox) = r;
+            st_rec(&AT(p.outbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + e, p.cap_inbox), r);
             AT(p.tdirty, ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (i >> 6)) * p.n_tiles + (s >> 6),
                static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
           } else {
-            AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox) = r;
+            st_rec(&AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox), r);
           }
         } else {
           const uint32_t pos = wave_append(&p.x_cnt[bk]);
@@ -1831,7 +1849,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
   if (dropped) atomicAdd(&cnt[CNT_DROPPED], dropped);
   if (sends) atomicAdd(&cnt[CNT_SENDS], sends);
-  if (st_rec) atomicAdd(&p.kstat[KST_REC], st_rec);
+  if (n_rec) atomicAdd(&p.kstat[KST_REC], n_rec);
   if (st_ops) atomicAdd(&p.kstat[KST_OPS], st_ops);
   if (st_edges) atomicAdd(&p.kstat[KST_EDGES], st_edges);
   __syncthreads();
@@ -1873,8 +1891,8 @@ __global__ __launch_bounds__(256) void k_transpose(const KP* __restrict__ pk, ui
     Rec v{};
     if (i < N && s < N && s != i) {
       const size_t e = static_cast<size_t>(i) * (N - 1) + s - (s > i ? 1 : 0);
-      v = AT(ob, e, p.E);
-      if (v.flags) AT(ob, e, p.E) = Rec{};
+      v = ld_rec(&AT(ob, e, p.E));
+      if (v.flags) clr_rec(&AT(ob, e, p.E));
     }
     tile[r][lane ^ r] = v;
   }
@@ -1884,7 +1902,7 @@ __global__ __launch_bounds__(256) void k_transpose(const KP* __restrict__ pk, ui
     const uint32_t s = s0 + c, i = i0 + lane;
     if (i < N && s < N && s != i) {
       const Rec v = tile[lane][c ^ lane];
-      if (v.flags) AT(ib, static_cast<size_t>(s) * (N - 1) + i - (i > s ? 1 : 0), p.E) = v;
+      if (v.flags) st_rec(&AT(ib, static_cast<size_t>(s) * (N - 1) + i - (i > s ? 1 : 0), p.E), v);
     }
   }
   if (threadIdx.x == 0) dirty = 0;
