@@ -338,6 +338,7 @@ static int setup_device(Sim& s) {
   // and moved to the receivers by the tiled transpose (k_transpose)
   bool mesh = s.E == static_cast<uint64_t>(s.N) * (s.N - 1) && s.N >= 2;
   for (uint32_t i = 0; mesh && i <= s.N; ++i) mesh = s.row[i] == static_cast<uint64_t>(i) * (s.N - 1);
+  if (const char* nm = std::getenv("BCSIM_NO_MESH"); nm && *nm == '1') mesh = false;  // debugging aid
   p.mesh = mesh ? 1u : 0u;
   p.n_tiles = (s.N + kTile - 1) / kTile;
   const uint64_t per_bucket = static_cast<uint64_t>(s.R) * s.E * sizeof(Rec) * (mesh ? 2 : 1);
@@ -354,6 +355,7 @@ static int setup_device(Sim& s) {
   uint64_t cap_x = c.cap_bucket_records;
   if (cap_x == 0) cap_x = std::max<uint64_t>(65536, NT * 8);
   p.cap_x = static_cast<uint32_t>(std::min<uint64_t>(cap_x, 1ull << 26));
+  p.cap_stage = static_cast<uint32_t>(2ull * s.deg_max + 256);  // k_link staging per node
   p.cap_ov = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(1ull << 20, NT * 256), 1ull << 26));
   p.cap_trace = static_cast<uint32_t>(std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1u << 20, NT * 256)));
   p.cap_vlog = 1u << 20;
@@ -420,6 +422,7 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.outbox, p.mesh ? p.cap_inbox : 1)) || (rc = dalloc(s, &p.tdirty, n_dirty))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
       (rc = dalloc(s, &p.xbuf, p.cap_xbuf)) || (rc = dalloc(s, &p.xgrp, p.cap_x)) ||
+      (rc = dalloc(s, &p.xstage, NT * p.cap_stage)) || (rc = dalloc(s, &p.xmeta, NT * p.cap_stage)) ||
       (rc = dalloc(s, &p.ov, p.cap_ov)))
     return rc;
   if ((rc = dalloc(s, &p.seg_cnt, NT)) || (rc = dalloc(s, &p.seg_off, NT + 1)) ||
@@ -513,6 +516,10 @@ static int setup_device(Sim& s) {
     }
   }
 #endif
+  if (const char* wv = std::getenv("BCSIM_WGT"); wv && *wv == '1') {  // debug: k_link per-WG timing
+    if ((rc = dalloc(s, &p.wgt, NT * 8))) return rc;
+    HIPCHK(hipMemset(p.wgt, 0, NT * 64));
+  }
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p.node_onext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -580,7 +587,34 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   else
     rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   if (rc) return rc;
-  return launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, hi);
+  rc = launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, hi);
+  if (rc || !s.kp.wgt) return rc;
+  // debug (BCSIM_WGT=1): report the slowest k_link workgroups of this launch
+  std::vector<unsigned long long> w(8ull * s.NT);
+  HIPCHK(hipStreamSynchronize(s.stream));
+  HIPCHK(hipMemcpy(w.data(), s.kp.wgt, w.size() * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(s.kp.wgt, 0, w.size() * 8));
+  std::vector<uint32_t> idx;
+  unsigned long long tmin = ~0ull, tmax = 0;
+  for (uint32_t g = 0; g < s.NT; ++g)
+    if (w[8 * g + 1]) {
+      idx.push_back(g);
+      tmin = std::min(tmin, w[8 * g]);
+      tmax = std::max(tmax, w[8 * g + 1]);
+    }
+  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return w[8 * a + 1] - w[8 * a] > w[8 * b + 1] - w[8 * b]; });
+  if (!idx.empty() && tmax - tmin > 100000) {  // > 1 ms (100 MHz clock)
+    std::fprintf(stderr, "[wgt] cell %lld k_link span %.2f ms, %zu WGs:", cell, (tmax - tmin) / 1e5, idx.size());
+    for (size_t k = 0; k < std::min<size_t>(5, idx.size()); ++k) {
+      const uint32_t g = idx[k];
+      const unsigned long long* q = &w[8 * g];
+      std::fprintf(stderr, " [g%u %.2fms n=%llu kept=%llu classify=%.0f scan+place=%.0f edges=%.0f gap=%.0f compact=%.0f us]", g,
+                   (q[1] - q[0]) / 1e5, q[2] >> 32, q[2] & 0xFFFFFFFFull, (q[3] - q[0]) / 100.0, (q[4] - q[3]) / 100.0,
+                   (q[5] - q[4]) / 100.0, (q[6] - q[5]) / 100.0, (q[1] - q[6]) / 100.0);
+    }
+    std::fprintf(stderr, "\n");
+  }
+  return BCSIM_OK;
 }
 
 // Prepare cell `cell`: move overflow records whose cell entered the ring into

@@ -97,6 +97,9 @@ struct KP {
   XRec* xbuf;            // [B][cap_x]
   uint32_t cap_x;
   XRec* xgrp;            // extras of the current cell grouped by receiver
+  XRec* xstage;          // [NT][cap_stage] k_link staging of extras / overflow records
+  uint32_t* xmeta;       // [NT][cap_stage] (list << 24) | rank within the list
+  uint32_t cap_stage;
   XRec* ov;
   uint32_t* ov_cnt;
   uint32_t cap_ov;
@@ -120,6 +123,7 @@ struct KP {
   int32_t* err;
   int32_t* dbg;  // first error's source line
   unsigned long long* trail;  // BCSIM_CHECKED + BCSIM_TRAIL: host-mapped breadcrumbs
+  unsigned long long* wgt;    // BCSIM_WGT: per-workgroup k_link timing [NT][4] (debug)
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   long long *node_tnext, *node_onext;
   long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks
@@ -348,24 +352,8 @@ __device__ inline uint32_t block_rank(bool f, uint32_t* wcnt, uint32_t& total) {
   return off + below;
 }
 
-// Append one element per ACTIVE lane to a global counter with a single
-// atomic per wave (the returning atomic is the bottleneck when many lanes
-// hit one word).  Call from divergent code: the active lanes participate.
-__device__ inline uint32_t wave_append(uint32_t* counter) {
-#ifdef HIPEMU  // tools/hipemu runs lanes as threads without lockstep: no divergent ballots
-  return atomicAdd(counter, 1u);
-#else
-  // active lanes = EXEC (a constant-true __ballot(1) can be folded to the
-  // wave-uniform mask by the compiler, which is wrong in divergent code)
-  const unsigned long long m = __builtin_amdgcn_read_exec();
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t first = static_cast<uint32_t>(__ffsll(static_cast<long long>(m)) - 1);
-  uint32_t base = 0;
-  if (lane == first) base = atomicAdd(counter, static_cast<uint32_t>(__popcll(m)));
-  base = __builtin_amdgcn_readfirstlane(base);
-  return base + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
-#endif
-}
+// Append one element to a global list (k_rebin: few records per launch).
+__device__ inline uint32_t list_append(uint32_t* counter) { return atomicAdd(counter, 1u); }
 
 // Exclusive block scan of four u32 lanes at once; totals in `tot`.
 __device__ inline uint4 block_scan4(uint4 v, uint4* wsum, uint4& tot) {
@@ -519,7 +507,7 @@ __global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) 
     if (owner) {
       st_rec(&AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox), x.r);
     } else {
-      const uint32_t pos = wave_append(&p.x_cnt[b]);
+      const uint32_t pos = list_append(&p.x_cnt[b]);
       if (pos >= p.cap_x) {
         set_err(p, BCSIM_E_OVERFLOW);
         return;
@@ -1587,8 +1575,40 @@ struct LinkShared {
   uint32_t lcnt[kMaxBuckets];
   uint4 wsum[kMaxWaves];
   uint32_t wcnt[kMaxWaves];
+  uint32_t nst;                      // staged extras / overflow records
+  uint32_t lst[kMaxBuckets + 1];     // per list (bucket extras..., overflow) staged count
+  uint32_t lbase[kMaxBuckets + 1];   // per list base reserved in the global list
   long long omin, ovmin;
 };
+
+// Stage one extras / overflow record of k_link (list = bucket, or B for the
+// overflow list): LDS ranks now, one global atomic per list at the flush.
+// A full staging area falls back to a direct (contended) global append.
+__device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32_t list, const XRec& x) {
+  const uint32_t spos = atomicAdd(&L.nst, 1u);
+  if (spos < p.cap_stage) {
+    const uint32_t rank = atomicAdd(&L.lst[list], 1u);
+    const size_t k = static_cast<size_t>(g) * p.cap_stage + spos;
+    p.xstage[k] = x;
+    p.xmeta[k] = (list << 24) | rank;
+    return;
+  }
+  if (list == p.n_buckets) {
+    const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+    if (pos >= p.cap_ov) {
+      set_err(p, BCSIM_E_OVERFLOW);
+      return;
+    }
+    AT(p.ov, pos, p.cap_ov) = x;
+  } else {
+    const uint32_t pos = atomicAdd(&p.x_cnt[list], 1u);
+    if (pos >= p.cap_x) {
+      set_err(p, BCSIM_E_OVERFLOW);
+      return;
+    }
+    AT(p.xbuf, static_cast<size_t>(list) * p.cap_x + pos, p.cap_xbuf) = x;
+  }
+}
 
 __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_hi) {
   const KP& p = *pk;
@@ -1599,6 +1619,9 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   if (g >= p.NT) return;
   uint32_t n = AT(p.n_ops, g, p.NT);
   if (n == 0) return;
+  const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
+  unsigned long long ph[4] = {0, 0, 0, 0};
+  const uint32_t n_in = n;
   const uint32_t tid = threadIdx.x;
   const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
@@ -1646,9 +1669,11 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   for (uint32_t k = tid; k <= deg; k += blockDim.x) ecnt[k] = 0;
   for (uint32_t k = tid; k < deg; k += blockDim.x) efill[k] = 0;
   for (uint32_t k = tid; k < B; k += blockDim.x) L.lcnt[k] = 0;
+  for (uint32_t k = tid; k <= B; k += blockDim.x) L.lst[k] = 0;
   if (tid == 0) {
     L.n_bc = 0;
     L.n_keep = 0;
+    L.nst = 0;
     L.omin = LLONG_MAX;
     L.ovmin = LLONG_MAX;
   }
@@ -1677,6 +1702,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
     return;
   }
+  if (p.wgt && tid == 0) ph[0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t n_due = block_scan_array(ecnt, deg + 1, L.wsum);
   if (n_due > p.cap_ops) {  // unreachable: n_due <= n <= cap_ops
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
@@ -1706,6 +1732,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   __syncthreads();
   const uint32_t n_bc = L.n_bc;
 
+  if (p.wgt && tid == 0) ph[1] = __builtin_amdgcn_s_memrealtime();
   // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO, emit ----
   unsigned long long n_rec = 0, st_edges = 0;
   long long ovmin = LLONG_MAX;
@@ -1785,33 +1812,23 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
             st_rec(&AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox), r);
           }
         } else {
-          const uint32_t pos = wave_append(&p.x_cnt[bk]);
-          if (pos >= p.cap_x) {
-            set_err(p, BCSIM_E_OVERFLOW);
-            continue;
-          }
           XRec x;
           x.r = r;
           x.cell = ca;
           x.slot = slot;
           x.g = dg;
-          AT(p.xbuf, static_cast<size_t>(bk) * p.cap_x + pos, p.cap_xbuf) = x;
+          link_stage(p, L, g, bk, x);
         }
         AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
         atomicAdd(&L.lcnt[bk], 1u);
       } else {
-        const uint32_t pos = wave_append(p.ov_cnt);
-        if (pos >= p.cap_ov) {
-          set_err(p, BCSIM_E_OVERFLOW);
-          continue;
-        }
         XRec x;
         x.r = r;
         if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
         x.cell = ca;
         x.slot = slot;
         x.g = dg;
-        AT(p.ov, pos, p.cap_ov) = x;
+        link_stage(p, L, g, B, x);
         if (ca < ovmin) ovmin = ca;
       }
     }
@@ -1820,11 +1837,13 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   }
   __syncthreads();
 
+  if (p.wgt && tid == 0) ph[2] = __builtin_amdgcn_s_memrealtime();
   // ---- 3. compact the ops that are not due yet ----
   // ordered in-place compaction: an op moves to the count of kept ops before
   // it (<= its own index); every lane has read its op before any lane writes
   long long omin = LLONG_MAX;
   uint32_t kept = 0;
+  if (p.wgt && tid == 0) ph[3] = __builtin_amdgcn_s_memrealtime();
   for (uint32_t k0 = 0; k0 < n; k0 += blockDim.x) {
     const uint32_t k = k0 + tid;
     Op o{};
@@ -1847,14 +1866,51 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   if (tid == 0) L.n_keep = kept;
   if (omin != LLONG_MAX) atomicMin(&L.omin, omin);
   if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
-  if (dropped) atomicAdd(&cnt[CNT_DROPPED], dropped);
-  if (sends) atomicAdd(&cnt[CNT_SENDS], sends);
-  if (n_rec) atomicAdd(&p.kstat[KST_REC], n_rec);
-  if (st_ops) atomicAdd(&p.kstat[KST_OPS], st_ops);
-  if (st_edges) atomicAdd(&p.kstat[KST_EDGES], st_edges);
+  // ---- 4. flush the staged extras / overflow records: one atomic per list ----
+  for (uint32_t k = tid; k <= B; k += blockDim.x) {
+    const uint32_t c = L.lst[k];
+    if (!c) continue;
+    const bool ov = k == B;
+    const uint32_t base = atomicAdd(ov ? p.ov_cnt : &p.x_cnt[k], c);
+    if (base + c > (ov ? p.cap_ov : p.cap_x)) set_err(p, BCSIM_E_OVERFLOW);
+    L.lbase[k] = base;
+  }
+  __syncthreads();
+  const uint32_t nst = min(L.nst, p.cap_stage);
+  for (uint32_t k = tid; k < nst; k += blockDim.x) {
+    const size_t sidx = static_cast<size_t>(g) * p.cap_stage + k;
+    const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
+    const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
+    if (list == B) {
+      if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
+    } else if (pos < p.cap_x) {
+      p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
+    }
+  }
+  // ---- 5. counters: one global atomic per workgroup ----
+  uint4 t1, t2;
+  (void)block_scan4(make_uint4(static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends),
+                               static_cast<uint32_t>(n_rec), static_cast<uint32_t>(st_ops)), L.wsum, t1);
+  (void)block_scan4(make_uint4(static_cast<uint32_t>(st_edges), 0, 0, 0), L.wsum, t2);
+  if (tid == 0) {
+    if (t1.x) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(t1.x));
+    if (t1.y) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(t1.y));
+    if (t1.z) atomicAdd(&p.kstat[KST_REC], static_cast<unsigned long long>(t1.z));
+    if (t1.w) atomicAdd(&p.kstat[KST_OPS], static_cast<unsigned long long>(t1.w));
+    if (t2.x) atomicAdd(&p.kstat[KST_EDGES], static_cast<unsigned long long>(t2.x));
+  }
   __syncthreads();
   for (uint32_t k = tid; k < B; k += blockDim.x)
     if (L.lcnt[k]) atomicAdd(&p.bucket_cnt[k], L.lcnt[k]);
+  if (p.wgt && tid == 0) {
+    p.wgt[8ull * g] = wg_t0;
+    p.wgt[8ull * g + 1] = __builtin_amdgcn_s_memrealtime();
+    p.wgt[8ull * g + 2] = (static_cast<unsigned long long>(n_in) << 32) | L.n_keep;
+    p.wgt[8ull * g + 3] = ph[0];
+    p.wgt[8ull * g + 4] = ph[1];
+    p.wgt[8ull * g + 5] = ph[2];
+    p.wgt[8ull * g + 6] = ph[3];
+  }
   if (tid == 0) {
     if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
     AT(p.n_ops, g, p.NT) = L.n_keep;

@@ -5,6 +5,7 @@
 #pragma once
 #include <atomic>
 #include <barrier>
+#include <chrono>
 #include <climits>
 #include <cstdint>
 #include <cstdlib>
@@ -101,6 +102,9 @@ inline unsigned long long __ballot(int pred) {
   return m;
 }
 inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+inline unsigned long long __builtin_amdgcn_s_memrealtime() {  // 100 MHz
+  return static_cast<unsigned long long>(std::chrono::steady_clock::now().time_since_epoch().count() / 10);
+}
 inline int __ffsll(long long x) { return __builtin_ffsll(x); }
 
 template <typename T, typename U>
