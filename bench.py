@@ -37,9 +37,21 @@ def make_cfg(n_nodes, rounds, device):
     return c
 
 
+def pmc_traffic(n_nodes, kernel="bcsim::k_link"):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (tools/pmc_summary.py over tests/gpu_prof.sh: FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE), for the same workload; None if absent."""
+    path = os.path.join(REPO, "profiles", f"r01_pmc_pbft{n_nodes}.json")
+    try:
+        with open(path) as f:
+            return json.load(f)["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(n_nodes, budget_s):
     """Serial oracle DES (same semantics) on the host: a bounded time slice of
-    the same workload, run from t=0 in 10 ms slices until budget_s of CPU."""
+    the same workload, run from t=0 in 1 ms slices until budget_s of CPU."""
     import oracle
     cfg = make_cfg(n_nodes, 100, 0)
     o = oracle.OracleSim(cfg)
@@ -47,7 +59,7 @@ def cpu_baseline(n_nodes, budget_s):
     w0 = time.time()
     t = 0
     while time.process_time() - t0 < budget_s:
-        t += 10_000_000
+        t += 1_000_000
         o.run(t)
         if o.status()["quiescent"]:
             break
@@ -134,6 +146,8 @@ def main():
         dom = max(("scan", "link", "group", "aux"), key=lambda k: ks[k]["us"])
         lk = ks["link"]
         ach = (lk["bytes"] / 1e9) / (lk["us"] / 1e6) if lk["us"] > 0 else 0.0
+        traffic = pmc_traffic(args.nodes)
+        lk_launch_bytes = lk["bytes"] / max(1, lk["launches"])
         out = {
             "metric": METRIC,
             "value": msgs / dt,
@@ -153,7 +167,9 @@ def main():
             "committed_rounds_per_s": rounds / dt,
             "roofline": {"kernel": "k_link (inbox scatter)", "bound": "hbm", "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                         "traffic": None, "dominant_kernel_class": dom},
+                         "traffic": traffic, "algorithmic_bytes_per_launch": lk_launch_bytes,
+                         "avg_launch_us": lk["us"] / max(1, lk["launches"]),
+                         "dominant_kernel_class": dom},
             "kernel_us": {k: v["us"] for k, v in ks.items()},
             "kernel_launches": {k: v["launches"] for k, v in ks.items()},
         }
