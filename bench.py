@@ -7,10 +7,14 @@ N=4096 full mesh (16.8 M directed 3 Mbps / 3 ms links), reference block size
 is one PBFT block interval: 50 ms (Seconds(0.05f)) of simulated time in which
 the leader ticks once and every node runs its prepare/commit traffic.
 
-Multi-GPU: one process per GPU; each rank simulates its own independent
-replica of the workload (replicas only in this round), so the
-per-GPU work is fixed ("scaling": "weak") and `value` = the msgs delivered on
-all ranks / max wall time over ranks.
+Multi-GPU (BASELINE configs[3]: "1/2/4/8 MI355X node-partitioned PDES"): one
+process per GPU; by default the SAME n=4096 network is node-partitioned over
+the ranks (contiguous node ranges, cross-rank records exchanged
+by RCCL all-to-all over xGMI once per lookahead cell), so total work is fixed
+("scaling": "strong") and `value` = msgs delivered on all ranks / max wall time
+over ranks.  `--mode replicas` runs one independent replica per rank instead
+("scaling": "weak"); it is also the fallback if the RCCL partition cannot be
+set up (reported in config.parallelism).
 
 Prints ONE JSON line on rank 0 with metric/value/roofline/cpu_baseline.
 """
@@ -73,7 +77,8 @@ def cpu_baseline(n_nodes, budget_s):
 
 
 def aggregate(dist, device, dt, msgs, trace_delta):
-    """Whole-job numbers over ranks: max wall time, summed work (replicas)."""
+    """Whole-job numbers over ranks: max wall time, summed work (the per-rank
+    deliveries of a partitioned run, or of independent replicas)."""
     if dist is None:
         return dt, msgs, trace_delta
     import torch
@@ -92,6 +97,8 @@ def main():
     ap.add_argument("--nodes", type=int, default=4096)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=("pdes", "replicas"), default="pdes",
+                    help="multi-GPU mode (N>1): node-partitioned PDES or independent replicas")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -108,6 +115,23 @@ def main():
     period = 50_000_001  # Seconds(0.05f) in ns (round mode)
     cfg = make_cfg(args.nodes, args.warmup + args.steps + 4, local)
     sim = bcsim.Simulator(cfg)
+    mode = "single"
+    if dist is not None:
+        mode = args.mode
+        if mode == "pdes":
+            err = ""
+            try:
+                sim.set_partition(dist, transport="rccl")
+            except Exception as e:  # every rank must agree before the first collective run
+                err = repr(e)
+            ok = torch.tensor([0 if err else 1], dtype=torch.int64, device=f"cuda:{local}")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if not int(ok.item()):
+                print(f"[bench] rank {rank}: RCCL partition unavailable ({err or 'peer failed'}); "
+                      f"falling back to replicas", file=sys.stderr, flush=True)
+                sim.close()
+                sim = bcsim.Simulator(cfg)
+                mode = "replicas"
 
     def barrier():
         if dist is not None:
@@ -157,13 +181,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1000.0 * dt / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if mode == "pdes" else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, fixed 3 ms app delay)" % args.nodes,
             "config": {"workload": f"PBFT n={args.nodes} full O(n^2) prepare/commit (BASELINE configs[3])",
                        "nodes": args.nodes, "step": "one 50 ms block interval",
-                       "parallelism": f"replicas{world}"},
+                       "parallelism": f"{mode}{world}" if world > 1 else "single"},
             "committed_rounds_per_s": rounds / dt,
             "roofline": {"kernel": "k_link (inbox scatter)", "bound": "hbm", "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,

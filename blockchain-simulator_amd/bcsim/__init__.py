@@ -9,7 +9,7 @@ import ctypes as C
 import os
 import subprocess
 
-from . import _abi
+from . import _abi, partition
 from ._abi import (  # noqa: F401
     PBFT, RAFT, PAXOS, DELAY_FIXED, DELAY_RANDOM, RNG_GLIBC, RNG_COUNTER,
     TIME_ROUND, TIME_TRUNC, ENC_EXTENDED, ENC_COMPAT, TR, INT64_MAX,
@@ -45,6 +45,7 @@ def lib():
         _LIB.bcsim_read_kernel_stats.restype = C.c_int
         _LIB.bcsim_reset_kernel_stats.argtypes = [C.c_void_p]
         _LIB.bcsim_reset_kernel_stats.restype = C.c_int
+        partition.declare(_LIB)
     return _LIB
 
 
@@ -77,6 +78,17 @@ class Simulator(_abi.Handle):
 
     def reset_kernel_stats(self):
         self._call("reset_kernel_stats", self.h)
+
+    def set_partition(self, dist, group=None, transport="rccl"):
+        """Own this rank's node range of a node-partitioned multi-GPU run
+        (DESIGN.md §5): transport "rccl" (device, xGMI) or "host" (callbacks
+        over the torch.distributed group, e.g. gloo)."""
+        if transport == "rccl":
+            partition.partition_rccl(self, dist, group)
+        elif transport == "host":
+            partition.partition_torch(self, dist, group)
+        else:
+            raise ValueError(transport)
 
 
 def run(cfg, t_until=INT64_MAX, topology=None):

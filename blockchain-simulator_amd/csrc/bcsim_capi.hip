@@ -17,6 +17,10 @@ static thread_local std::string g_detail;
     }                                                                                  \
   } while (0)
 
+}  // namespace bcsim
+#include "transport.h"
+namespace bcsim {
+
 static uint32_t next_pow2(uint64_t v) {
   uint64_t p = 1;
   while (p < v) p <<= 1;
@@ -72,6 +76,14 @@ struct Sim {
   bool trace_valid = false;
   int dev = 0;
   unsigned long long* trail_h = nullptr;  // checked builds: host view of breadcrumbs
+  // multi-GPU node partition
+  uint32_t P = 1, prank = 0, nlo = 0, nloc = 0;
+  Xport* xp = nullptr;
+  uint32_t* scnt_h = nullptr;  // host view of the per-rank send counts (control block)
+  XRec* recvbuf = nullptr;
+  uint64_t cap_recv = 0;
+  uint32_t vsync = 0;          // v-log entries already exchanged
+  std::vector<int64_t> lead_w; // leader flags packed for the all-reduce
 };
 
 static std::string trail_dump(const Sim& s) {
@@ -384,6 +396,46 @@ static int setup_device(Sim& s) {
   }
   if (s.N > 60 * 1024) return BCSIM_E_UNSUPPORTED;  // k_pbft_tick keeps one flag per node in LDS
 
+  // node partition: rank prank owns [nlo, nlo + nloc) of every replica
+  if (s.P > 1) {
+    if (s.P > static_cast<uint32_t>(kMaxRanks) || s.N < s.P) return BCSIM_E_INVAL;
+    if (c.protocol == BCSIM_RAFT && c.rng_mode == BCSIM_RNG_GLIBC) {
+      g_detail = "Raft with the global glibc stream is single-GPU only (draws in global order)";
+      return BCSIM_E_UNSUPPORTED;
+    }
+  }
+  s.nlo = static_cast<uint32_t>(static_cast<uint64_t>(s.prank) * s.N / s.P);
+  s.nloc = static_cast<uint32_t>(static_cast<uint64_t>(s.prank + 1) * s.N / s.P) - s.nlo;
+  p.nlo = s.nlo;
+  p.nloc = s.nloc;
+  p.rank = s.prank;
+  p.nranks = s.P;
+  {
+    std::vector<uint16_t> own(s.N);
+    for (uint32_t r = 0; r < s.P; ++r)
+      for (uint64_t i = static_cast<uint64_t>(r) * s.N / s.P; i < static_cast<uint64_t>(r + 1) * s.N / s.P; ++i)
+        own[i] = static_cast<uint16_t>(r);
+    uint16_t* own_d = nullptr;
+    if ((rc = dalloc(s, &own_d, s.N))) return rc;
+    HIPCHK(hipMemcpy(own_d, own.data(), s.N * 2ull, hipMemcpyHostToDevice));
+    p.owner = own_d;
+    // per destination rank: at most one record per (local sender, remote
+    // receiver) edge per cell, plus second records and broadcasts
+    const uint64_t cs = std::max<uint64_t>(65536, 2ull * s.R * s.nloc * std::min<uint64_t>(s.deg_max, s.N) + 4096);
+    p.cap_send = s.xp ? static_cast<uint32_t>(std::min<uint64_t>(cs, 1ull << 28)) : 1;
+    s.cap_recv = static_cast<uint64_t>(p.cap_send) * s.P;
+    uint8_t *la = nullptr, *ll = nullptr;
+    if ((rc = dalloc(s, &p.sendbuf, static_cast<size_t>(p.cap_send) * s.P)) ||
+        (rc = dalloc(s, &s.recvbuf, s.xp ? s.cap_recv : 1)) || (rc = dalloc(s, &la, NT + 8)) ||
+        (rc = dalloc(s, &ll, NT + 8)))
+      return rc;
+    HIPCHK(hipMemset(la, 0, NT + 8));
+    HIPCHK(hipMemset(ll, 0, NT + 8));
+    p.lead_all = la;
+    p.lead_loc = ll;
+    s.lead_w.assign((NT + 7) / 8, 0);
+  }
+
   // state
   if ((rc = dalloc(s, &p.sub, NT)) || (rc = dalloc(s, &p.draws, NT))) return rc;
   if ((rc = dalloc(s, &p.leader, NT)) || (rc = dalloc(s, &p.block_num, NT)) ||
@@ -435,7 +487,7 @@ static int setup_device(Sim& s) {
     return rc;
   if ((rc = dalloc(s, &p.node_tnext, NT)) || (rc = dalloc(s, &p.node_onext, NT))) return rc;
   // control block: Ctl + bucket counts + extras counts, contiguous for one read-back
-  const size_t ctl_bytes = sizeof(Ctl) + 8ull * s.B;
+  const size_t ctl_bytes = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
   char* ctl = nullptr;
   if ((rc = dalloc(s, &ctl, ctl_bytes))) return rc;
   s.ctl_d = ctl;
@@ -449,9 +501,11 @@ static int setup_device(Sim& s) {
   p.scal = cd->scal;
   p.bucket_cnt = reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl));
   p.x_cnt = p.bucket_cnt + s.B;
+  p.send_cnt = p.x_cnt + s.B;
   HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), ctl_bytes));
   s.bcnt_h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.ctl_h) + sizeof(Ctl));
   s.xcnt_h = s.bcnt_h + s.B;
+  s.scnt_h = s.xcnt_h + s.B;
 
   // glibc stream tables
   const bool need_glibc = c.rng_mode == BCSIM_RNG_GLIBC &&
@@ -577,7 +631,7 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
 
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
-  dim3 grid(s.NT), block(s.bs_scan);
+  dim3 grid(s.R * s.nloc), block(s.bs_scan);
   const int fw = final_win ? 1 : 0, xa = s.x_active;
   int rc;
   if (s.cfg.protocol == BCSIM_PBFT)
@@ -669,7 +723,8 @@ static int group_cell(Sim& s, long long cell) {
 }
 
 static int readback(Sim& s) {
-  HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, sizeof(Ctl) + 8ull * s.B, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks, hipMemcpyDeviceToHost,
+                        s.stream));
   HIPCHK(hipStreamSynchronize(s.stream));
   int rc = ev_collect(s);
   if (rc) return rc;
@@ -684,6 +739,88 @@ static int readback(Sim& s) {
                " (cell " + std::to_string(s.cells) + ")";
     return s.ctl_h->err;
   }
+  return BCSIM_OK;
+}
+
+// ---- multi-GPU steps (all ranks call them in the same order) -------------
+// Records for other ranks' receivers, staged by k_link during the cell, go
+// out in one all-to-all; k_import places what came in.
+static int exchange(Sim& s, long long cell) {
+  std::vector<uint64_t> sb(s.P), rb(s.P);
+  for (uint32_t r = 0; r < s.P; ++r) {
+    if (s.scnt_h[r] > s.kp.cap_send) {
+      g_detail = "multi-GPU send list overflowed";
+      return BCSIM_E_OVERFLOW;
+    }
+    sb[r] = static_cast<uint64_t>(s.scnt_h[r]) * sizeof(XRec);
+  }
+  int rc = s.xp->alltoallv_dev(s.stream, reinterpret_cast<const char*>(s.kp.sendbuf),
+                               static_cast<uint64_t>(s.kp.cap_send) * sizeof(XRec), sb.data(),
+                               reinterpret_cast<char*>(s.recvbuf), s.cap_recv * sizeof(XRec), rb.data());
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(s.kp.send_cnt, 0, 4ull * kMaxRanks, s.stream));
+  uint64_t n = 0;
+  for (uint32_t r = 0; r < s.P; ++r) n += rb[r] / sizeof(XRec);
+  if (n) {
+    rc = launch(s, KS_GROUP, k_import, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s.kp_dev, cell,
+                static_cast<const XRec*>(s.recvbuf), static_cast<uint32_t>(n));
+    if (rc) return rc;
+  }
+  return BCSIM_OK;
+}
+
+// Share the v-log entries written since the last sync (PBFT file-scope `v`,
+// pbft-node.cc:26, written by VIEW_CHANGE receipts on every node).
+static int sync_vlog(Sim& s) {
+  uint32_t cnt = 0;
+  HIPCHK(hipMemcpyAsync(&cnt, s.kp.vlog_cnt, 4, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipStreamSynchronize(s.stream));
+  cnt = std::min(cnt, s.kp.cap_vlog);
+  const uint32_t mine = cnt - s.vsync;
+  std::vector<VLog> loc(mine);
+  if (mine) HIPCHK(hipMemcpy(loc.data(), s.kp.vlog + s.vsync, mine * sizeof(VLog), hipMemcpyDeviceToHost));
+  // everyone gets my new entries
+  std::vector<char> snd(static_cast<size_t>(mine) * sizeof(VLog) * s.P);
+  std::vector<uint64_t> sb(s.P, static_cast<uint64_t>(mine) * sizeof(VLog)), rb(s.P);
+  for (uint32_t r = 0; r < s.P; ++r)
+    if (mine) std::memcpy(snd.data() + static_cast<size_t>(r) * mine * sizeof(VLog), loc.data(), mine * sizeof(VLog));
+  int64_t tot = mine;
+  int rc = s.xp->allreduce_i64(s.stream, &tot, 1, 1);
+  if (rc) return rc;
+  std::vector<char> rcv(static_cast<size_t>(tot) * sizeof(VLog) + 16);
+  rc = s.xp->alltoallv_host(s.stream, snd.data(), sb.data(), rcv.data(), rcv.size(), rb.data());
+  if (rc) return rc;
+  std::vector<VLog> add;
+  uint64_t off = 0;
+  for (uint32_t r = 0; r < s.P; ++r) {
+    const uint64_t k = rb[r] / sizeof(VLog);
+    if (r != s.prank)
+      for (uint64_t j = 0; j < k; ++j) add.push_back(reinterpret_cast<const VLog*>(rcv.data() + off)[j]);
+    off += rb[r];
+  }
+  if (cnt + add.size() > s.kp.cap_vlog) return BCSIM_E_OVERFLOW;
+  if (!add.empty()) {
+    HIPCHK(hipMemcpy(s.kp.vlog + cnt, add.data(), add.size() * sizeof(VLog), hipMemcpyHostToDevice));
+    const uint32_t ncnt = cnt + static_cast<uint32_t>(add.size());
+    HIPCHK(hipMemcpy(s.kp.vlog_cnt, &ncnt, 4, hipMemcpyHostToDevice));
+    cnt = ncnt;
+  }
+  s.vsync = cnt;
+  return BCSIM_OK;
+}
+
+// Leader flags of every rank for the PBFT tick (bytes are 0/1 and disjoint
+// across ranks, so an int64 SUM of the packed bytes is their union).
+static int sync_leaders(Sim& s) {
+  int rc = launch(s, KS_AUX, k_lead, dim3(s.R), dim3(1024), 0, s.kp_dev);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(s.lead_w.data(), s.kp.lead_loc, s.NT, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipStreamSynchronize(s.stream));
+  for (size_t k = 0; k < s.lead_w.size(); k += 64) {
+    const uint32_t n = static_cast<uint32_t>(std::min<size_t>(64, s.lead_w.size() - k));
+    if ((rc = s.xp->allreduce_i64(s.stream, s.lead_w.data() + k, n, 1))) return rc;
+  }
+  HIPCHK(hipMemcpyAsync(const_cast<uint8_t*>(s.kp.lead_all), s.lead_w.data(), s.NT, hipMemcpyHostToDevice, s.stream));
   return BCSIM_OK;
 }
 
@@ -714,6 +851,11 @@ static int run(Sim& s, int64_t t_until) {
     if (s.ov_min != LLONG_MAX) c = std::min(c, s.ov_min);
     if (s.n_alive > 0 && s.next_tick != INT64_MAX) c = std::min(c, s.next_tick / L);
     if (s.stop_pending && s.cfg.stop_ns >= 0 && s.cfg.stop_ns >= s.t_done) c = std::min(c, s.cfg.stop_ns / L);
+    if (s.xp) {  // the next cell of the whole system
+      int64_t cv = c;
+      if ((rc = s.xp->allreduce_i64(s.stream, &cv, 1, 0))) return rc;
+      c = cv;
+    }
     if (c == LLONG_MAX || c * L >= lim) {
       if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
       break;
@@ -734,6 +876,9 @@ static int run(Sim& s, int64_t t_until) {
       if (tk > lo) {
         if ((rc = do_scan(s, c, lo, tk, cs, false))) return rc;
       }
+      if (s.xp) {
+        if ((rc = sync_vlog(s)) || (rc = sync_leaders(s))) return rc;
+      }
       HIPCHK(hipMemsetAsync(s.kp.scal + 2, 0, 8, s.stream));
       if ((rc = launch(s, KS_AUX, k_pbft_tick, dim3(s.R), dim3(1024), static_cast<size_t>(s.N), s.kp_dev, tk)))
         return rc;
@@ -752,8 +897,13 @@ static int run(Sim& s, int64_t t_until) {
     }
     if ((rc = readback(s))) return rc;
     if (tick) {
-      s.n_alive = s.ctl_h->scal[2];
+      int64_t na = s.ctl_h->scal[2];
+      if (s.xp && (rc = s.xp->allreduce_i64(s.stream, &na, 1, 1))) return rc;
+      s.n_alive = na;
       s.next_tick += s.kp.pbft_period;
+    }
+    if (s.xp) {  // ship records for other ranks' nodes, place the received ones
+      if ((rc = exchange(s, c)) || (rc = readback(s))) return rc;
     }
     s.start_pending = false;
     if (s.cfg.stop_ns >= 0 && s.cfg.stop_ns < hi) s.stop_pending = false;
@@ -766,6 +916,7 @@ static int run(Sim& s, int64_t t_until) {
       s.x_active = 0;
     }
   }
+  if (s.xp && s.cfg.protocol == BCSIM_PBFT && (rc = sync_vlog(s))) return rc;
   return BCSIM_OK;
 }
 
@@ -858,6 +1009,7 @@ static void destroy(Sim* s) {
   }
   if (s->ctl_h) (void)hipHostFree(s->ctl_h);
   if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s->xp;
   delete s;
 }
 
@@ -922,6 +1074,7 @@ int bcsim_create(const bcsim_config* cfg, bcsim_sim** out) {
     return BCSIM_E_UNSUPPORTED;
   }
   s->NT = s->N * s->R;
+  s->nloc = s->N;
   bcsim::build_mesh(*s);
   if ((rc = bcsim::build_rev(*s))) {
     delete s;
@@ -1059,6 +1212,63 @@ int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, u
     bytes_out4[bcsim::KS_AUX] = static_cast<double>(ks[bcsim::KST_REC]);  // records emitted
   }
   return BCSIM_OK;
+}
+
+int bcsim_set_partition(bcsim_sim* h, uint32_t rank, uint32_t nranks, const bcsim_transport* t) {
+  if (!h || !t || !t->allreduce_i64 || !t->alltoallv || nranks == 0 || rank >= nranks) return BCSIM_E_INVAL;
+  Sim& s = *h->s;
+  if (s.started) return BCSIM_E_STATE;
+  auto* x = new (std::nothrow) bcsim::CbXport();
+  if (!x) return BCSIM_E_NOMEM;
+  x->t = *t;
+  x->rank = rank;
+  x->nranks = nranks;
+  delete s.xp;
+  s.xp = x;
+  s.P = nranks;
+  s.prank = rank;
+  return BCSIM_OK;
+}
+
+int bcsim_rccl_unique_id(void* out, uint64_t cap, uint64_t* n_out) {
+#ifdef HIPEMU
+  return BCSIM_E_UNSUPPORTED;
+#else
+  if (!out || !n_out || cap < sizeof(ncclUniqueId)) return BCSIM_E_INVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return BCSIM_E_HIP;
+  std::memcpy(out, &id, sizeof id);
+  *n_out = sizeof id;
+  return BCSIM_OK;
+#endif
+}
+
+int bcsim_set_partition_rccl(bcsim_sim* h, uint32_t rank, uint32_t nranks, const void* unique_id,
+                             uint64_t id_bytes) {
+#ifdef HIPEMU
+  return BCSIM_E_UNSUPPORTED;
+#else
+  if (!h || !unique_id || id_bytes != sizeof(ncclUniqueId) || nranks == 0 || rank >= nranks) return BCSIM_E_INVAL;
+  Sim& s = *h->s;
+  if (s.started) return BCSIM_E_STATE;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return BCSIM_E_NODEVICE;
+  if (hipSetDevice(static_cast<int>(s.cfg.device) % ndev) != hipSuccess) return BCSIM_E_HIP;
+  auto* x = new (std::nothrow) bcsim::RcclXport();
+  if (!x) return BCSIM_E_NOMEM;
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof id);
+  const int rc = x->init(rank, nranks, id);
+  if (rc) {
+    delete x;
+    return rc;
+  }
+  delete s.xp;
+  s.xp = x;
+  s.P = nranks;
+  s.prank = rank;
+  return BCSIM_OK;
+#endif
 }
 
 int bcsim_reset_kernel_stats(bcsim_sim* h) {

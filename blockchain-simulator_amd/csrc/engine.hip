@@ -127,7 +127,20 @@ struct KP {
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   long long *node_tnext, *node_onext;
   long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks
+  // node partition (multi-GPU PDES): this rank owns nodes
+  // [nlo, nlo + nloc) of every replica; records for other ranks' receivers
+  // are staged in sendbuf and exchanged once per cell
+  uint32_t nlo, nloc, rank, nranks;
+  const uint16_t* owner;    // [N] rank owning node i
+  XRec* sendbuf;            // [nranks][cap_send]
+  uint32_t* send_cnt;       // [nranks] (control block)
+  uint32_t cap_send;
+  const uint8_t* lead_all;  // [R][N] PBFT leader flags gathered from all ranks
+  uint8_t* lead_loc;        // [R][N] this rank's leader flags (k_lead)
 };
+
+constexpr int kMaxRanks = 16;
+
 
 // ---------------------------------------------------------------------------
 // device helpers
@@ -180,6 +193,12 @@ __device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int l
 __device__ inline uint32_t xcd_map(uint32_t b, uint32_t n) {
   const uint32_t x = b & 7u, k = b >> 3, per = n >> 3, rem = n & 7u;
   return x * per + min(x, rem) + k;
+}
+
+// blockIdx -> gnode of this rank's partition (XCD-contiguous ranges)
+__device__ inline uint32_t local_gnode(const KP& p, uint32_t b) {
+  const uint32_t j = xcd_map(b, p.R * p.nloc);
+  return (j / p.nloc) * p.N + p.nlo + j % p.nloc;
 }
 
 struct Key {
@@ -1242,8 +1261,8 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   uint32_t* acls = reinterpret_cast<uint32_t*>(arec + cap);
   TimerEnt* tm = reinterpret_cast<TimerEnt*>(acls + cap);
 
-  const uint32_t g = xcd_map(blockIdx.x, p.NT);
-  if (g >= p.NT) return;
+  if (blockIdx.x >= p.R * p.nloc) return;
+  const uint32_t g = local_gnode(p, blockIdx.x);
   const uint32_t tid = threadIdx.x;
   const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
@@ -1576,8 +1595,8 @@ struct LinkShared {
   uint4 wsum[kMaxWaves];
   uint32_t wcnt[kMaxWaves];
   uint32_t nst;                      // staged extras / overflow records
-  uint32_t lst[kMaxBuckets + 1];     // per list (bucket extras..., overflow) staged count
-  uint32_t lbase[kMaxBuckets + 1];   // per list base reserved in the global list
+  uint32_t lst[kMaxBuckets + 1 + kMaxRanks];    // per list (bucket extras..., overflow, ranks...)
+  uint32_t lbase[kMaxBuckets + 1 + kMaxRanks];  // per list base reserved in the global list
   long long omin, ovmin;
 };
 
@@ -1593,7 +1612,15 @@ __device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32
     p.xmeta[k] = (list << 24) | rank;
     return;
   }
-  if (list == p.n_buckets) {
+  if (list > p.n_buckets) {  // another rank's receiver
+    const uint32_t r = list - p.n_buckets - 1;
+    const uint32_t pos = atomicAdd(&p.send_cnt[r], 1u);
+    if (pos >= p.cap_send) {
+      set_err(p, BCSIM_E_OVERFLOW);
+      return;
+    }
+    p.sendbuf[static_cast<size_t>(r) * p.cap_send + pos] = x;
+  } else if (list == p.n_buckets) {
     const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
     if (pos >= p.cap_ov) {
       set_err(p, BCSIM_E_OVERFLOW);
@@ -1615,8 +1642,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   BAIL_IF_ERR();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ LinkShared L;
-  const uint32_t g = xcd_map(blockIdx.x, p.NT);
-  if (g >= p.NT) return;
+  if (blockIdx.x >= p.R * p.nloc) return;
+  const uint32_t g = local_gnode(p, blockIdx.x);
   uint32_t n = AT(p.n_ops, g, p.NT);
   if (n == 0) return;
   const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1669,7 +1696,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   for (uint32_t k = tid; k <= deg; k += blockDim.x) ecnt[k] = 0;
   for (uint32_t k = tid; k < deg; k += blockDim.x) efill[k] = 0;
   for (uint32_t k = tid; k < B; k += blockDim.x) L.lcnt[k] = 0;
-  for (uint32_t k = tid; k <= B; k += blockDim.x) L.lst[k] = 0;
+  const uint32_t n_lists = B + 1 + (p.nranks > 1 ? p.nranks : 0);
+  for (uint32_t k = tid; k < n_lists; k += blockDim.x) L.lst[k] = 0;
   if (tid == 0) {
     L.n_bc = 0;
     L.n_keep = 0;
@@ -1801,6 +1829,19 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       r.flags = static_cast<uint8_t>(RF_VALID | (big ? RF_BIG : 0));
       const bool owner = lc != ca;
       lc = ca;
+      if (p.nranks > 1) {
+        const uint32_t orank = p.owner[s];
+        if (orank != p.rank) {  // receiver on another GPU: ship the record (k_import places it)
+          XRec x;
+          x.r = r;
+          if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+          x.cell = ca;
+          x.slot = slot;
+          x.g = dg;
+          link_stage(p, L, g, B + 1 + orank, x);
+          continue;
+        }
+      }
       if (rel < static_cast<long long>(B)) {
         const uint32_t bk = static_cast<uint32_t>(ca % B);
         if (owner) {
@@ -1867,12 +1908,13 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   if (omin != LLONG_MAX) atomicMin(&L.omin, omin);
   if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
   // ---- 4. flush the staged extras / overflow records: one atomic per list ----
-  for (uint32_t k = tid; k <= B; k += blockDim.x) {
+  for (uint32_t k = tid; k < n_lists; k += blockDim.x) {
     const uint32_t c = L.lst[k];
     if (!c) continue;
-    const bool ov = k == B;
-    const uint32_t base = atomicAdd(ov ? p.ov_cnt : &p.x_cnt[k], c);
-    if (base + c > (ov ? p.cap_ov : p.cap_x)) set_err(p, BCSIM_E_OVERFLOW);
+    uint32_t* ctr = k < B ? &p.x_cnt[k] : k == B ? p.ov_cnt : &p.send_cnt[k - B - 1];
+    const uint32_t cap = k < B ? p.cap_x : k == B ? p.cap_ov : p.cap_send;
+    const uint32_t base = atomicAdd(ctr, c);
+    if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
     L.lbase[k] = base;
   }
   __syncthreads();
@@ -1881,7 +1923,9 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     const size_t sidx = static_cast<size_t>(g) * p.cap_stage + k;
     const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
     const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
-    if (list == B) {
+    if (list > B) {
+      if (pos < p.cap_send) p.sendbuf[static_cast<size_t>(list - B - 1) * p.cap_send + pos] = p.xstage[sidx];
+    } else if (list == B) {
       if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
     } else if (pos < p.cap_x) {
       p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
@@ -1916,6 +1960,73 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     AT(p.n_ops, g, p.NT) = L.n_keep;
     AT(p.node_onext, g, p.NT) = L.omin;
     atomicAdd(&p.kstat[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_import (multi-GPU): place the records received from other ranks -- the
+// same rules as a local k_link emission (slot owner -> inbox, or outbox +
+// tile flag for the full mesh; second record of an edge -> extras; beyond
+// the ring -> overflow).  g_cur = the cell just processed.
+__global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long long g_cur, const XRec* __restrict__ rx,
+                                                uint32_t n) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ uint32_t lb[kMaxBuckets];
+  __shared__ long long ovmin;
+  const uint32_t B = p.n_buckets;
+  for (uint32_t k = threadIdx.x; k < B; k += blockDim.x) lb[k] = 0;
+  if (threadIdx.x == 0) ovmin = LLONG_MAX;
+  __syncthreads();
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) {
+    XRec x = rx[k];
+    const uint32_t rep = x.g / p.N, s = x.g % p.N;
+    if (x.cell < g_cur + static_cast<long long>(B)) {
+      const uint32_t b = static_cast<uint32_t>(x.cell % B);
+      const bool owner = (x.r.flags & RF_OWNER) != 0;
+      x.r.flags = static_cast<uint8_t>(x.r.flags & ~RF_OWNER);
+      if (owner) {
+        if (p.mesh) {
+          const uint32_t i = AT(p.col, x.slot, p.E);  // the sender: slot = edge s -> i
+          const uint32_t e = AT(p.rev, x.slot, p.E);
+          st_rec(&AT(p.outbox, (static_cast<size_t>(b) * p.R + rep) * p.E + e, p.cap_inbox), x.r);
+          AT(p.tdirty, ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6)) * p.n_tiles + (s >> 6),
+             static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
+        } else {
+          st_rec(&AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox), x.r);
+        }
+      } else {
+        const uint32_t pos = atomicAdd(&p.x_cnt[b], 1u);
+        if (pos < p.cap_x)
+          AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
+        else
+          set_err(p, BCSIM_E_OVERFLOW);
+      }
+      AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(B) * p.NT) = 1;
+      atomicAdd(&lb[b], 1u);
+    } else {
+      const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+      if (pos < p.cap_ov)
+        AT(p.ov, pos, p.cap_ov) = x;
+      else
+        set_err(p, BCSIM_E_OVERFLOW);
+      atomicMin(&ovmin, x.cell);
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < B; q += blockDim.x)
+    if (lb[q]) atomicAdd(&p.bucket_cnt[q], lb[q]);
+  if (threadIdx.x == 0 && ovmin != LLONG_MAX) atomicMin(&p.scal[1], ovmin);
+}
+
+// k_lead (multi-GPU, PBFT): this rank's "ticking leader" flags for k_pbft_tick
+__global__ __launch_bounds__(1024) void k_lead(const KP* __restrict__ pk) {
+  const KP& p = *pk;
+  const uint32_t rep = blockIdx.x;
+  for (uint32_t k = threadIdx.x; k < p.nloc; k += blockDim.x) {
+    const uint32_t i = p.nlo + k, g = rep * p.N + i;
+    p.lead_loc[g] = (p.tick_alive[g] && p.leader[g] == static_cast<int32_t>(i)) ? 1 : 0;
   }
 }
 
@@ -2012,7 +2123,10 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
   __syncthreads();
   for (uint32_t i = tid; i < N; i += blockDim.x) {
     const uint32_t g = rep * N + i;
-    lead[i] = (AT(p.tick_alive, g, p.NT) && AT(p.leader, g, p.NT) == static_cast<int32_t>(i)) ? 1 : 0;
+    if (p.nranks > 1)
+      lead[i] = p.lead_all[g];
+    else
+      lead[i] = (AT(p.tick_alive, g, p.NT) && AT(p.leader, g, p.NT) == static_cast<int32_t>(i)) ? 1 : 0;
   }
   __syncthreads();
   // leaders, serially in node order (rare: normally exactly one)
@@ -2021,6 +2135,18 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
     for (uint32_t i = 0; i < N; ++i) {
       if (!lead[i]) continue;
       const uint32_t g = rep * N + i;
+      if (i < p.nlo || i >= p.nlo + p.nloc) {
+        // another rank's leader: advance the replicated file-scope globals
+        // (n_round, n, glibc stream position, v) exactly as its owner does
+        ++nround;
+        AT(p.g_n, rep, p.R) = AT(p.g_n, rep, p.R) + 1;
+        if (p.pbft_view_change && p.rng_mode == BCSIM_RNG_GLIBC) {
+          const uint32_t pos = AT(p.glibc_pos, rep, p.R)++;
+          const int32_t r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + (pos % p.glibc_len), p.cap_glibc);
+          if (r % 100 == 5) v_cur += 1;
+        }
+        continue;
+      }
       uint32_t sub = AT(p.sub, g, p.NT);
       const uint32_t deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
       const int32_t n_seq = AT(p.g_n, rep, p.R);
@@ -2090,7 +2216,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
       sc[tid] += y;
       __syncthreads();
     }
-    if (i < N) {
+    if (i < N && i >= p.nlo && i < p.nlo + p.nloc) {
       const uint32_t g = rep * N + i;
       if (AT(p.tick_alive, g, p.NT)) {
         const int32_t nr = nround0 + chunk_base + sc[tid];

@@ -200,6 +200,35 @@ const char* bcsim_strerror(int code);
 /* Last HIP/engine diagnostic text (thread-unsafe, for logs). */
 const char* bcsim_last_error_detail(void);
 
+/* ---- multi-GPU: node-partitioned conservative PDES --------
+ * nranks handles (one process and one GPU each) simulate ONE system: rank r
+ * owns a contiguous node range of every replica; records for another rank's
+ * nodes are exchanged once per cell (lookahead window), the next cell is
+ * agreed by an all-reduce MIN, and the PBFT SendBlock tick gathers the
+ * leader flags and the v-log.  No reference counterpart: the reference is
+ * single-threaded ns-3 (blockchain-simulator.cc:57).  Call before the first
+ * bcsim_run; every rank must then call bcsim_run with the same t_until.
+ * Counters and traces are per rank (sum / merge them across ranks). */
+typedef struct bcsim_transport {
+  void* ctx;
+  /* in-place all-reduce of n int64 values on host memory; op 0 = MIN, 1 = SUM */
+  int (*allreduce_i64)(void* ctx, int64_t* v, uint32_t n, int32_t op);
+  /* all-to-all-v of host bytes: send holds nranks consecutive segments of
+   * send_bytes[r] bytes (segment r goes to rank r); recv gets the segments
+   * from ranks 0..nranks-1 back to back, recv_bytes[r] each (<= recv_cap) */
+  int (*alltoallv)(void* ctx, const void* send, const uint64_t* send_bytes, void* recv, uint64_t recv_cap,
+                   uint64_t* recv_bytes);
+} bcsim_transport;
+
+/* Partition over a caller-provided host transport (e.g. torch.distributed
+ * gloo callbacks; used by the tests: several ranks may share one GPU). */
+int bcsim_set_partition(bcsim_sim* s, uint32_t rank, uint32_t nranks, const bcsim_transport* t);
+/* Partition over RCCL (xGMI): device-resident exchange.  unique_id is the
+ * ncclUniqueId made by bcsim_rccl_unique_id on rank 0 and shared by the caller. */
+int bcsim_rccl_unique_id(void* out, uint64_t cap, uint64_t* n_out);
+int bcsim_set_partition_rccl(bcsim_sim* s, uint32_t rank, uint32_t nranks, const void* unique_id,
+                             uint64_t id_bytes);
+
 /* Device timing of the last bcsim_run: per-kernel-class accumulated
  * microseconds measured with hipEvents on the engine stream.  kinds:
  * 0 scan, 1 link (fan-out scatter), 2 group, 3 tick/aux.  Also the

@@ -18,7 +18,8 @@ steps=${*:-checked parity smoke bench prof}
 for st in $steps; do
   case $st in
     checked) run checked 240 env BCSIM_LIB="$PWD/blockchain-simulator_amd/libbcsim_checked.so" BCSIM_SYNC_EACH=1 python tests/parity_run.py ;;
-    parity)  run parity 300 python -m pytest tests -m gpu -x -q ;;
+    parity)  run parity 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    part)    run part 400 python -u -m pytest tests/test_partition.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     smoke)   run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench1k) run bench1k 300 python bench.py --nodes 1024 --cpu-budget 5 ;;
     bench)   run bench 400 python bench.py ;;

@@ -1,0 +1,149 @@
+"""Node-partitioned multi-GPU PDES.
+
+CPU (gloo, world 2): the host-callback transport (bcsim_transport) that the
+engine calls once per lookahead cell, and the per-rank result merge.
+GPU: the same parity cases run partitioned over 2 and 3 ranks sharing the
+one GPU (gloo host transport) -- merged traces and summed counters must be
+bit-identical to the oracle, i.e. to the single-process run -- and the RCCL
+transport at world 1 (the device exchange path with no remote peers).
+"""
+import ctypes as C
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+import oracle
+from parity_cases import cases, compare
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _transport_worker(rank, world, port, q):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "blockchain-simulator_amd"))
+    import torch.distributed as dist
+    from bcsim.partition import TorchTransport
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = TorchTransport(dist)
+    # all-reduce MIN / SUM, called the way the engine calls it (through the C thunk)
+    v = (C.c_int64 * 3)(10 + rank, -rank, 1 << 40)
+    assert tr.struct.allreduce_i64(None, v, 3, 0) == 0
+    mn = list(v)
+    v = (C.c_int64 * 3)(10 + rank, -rank, 1 << 40)
+    assert tr.struct.allreduce_i64(None, v, 3, 1) == 0
+    sm = list(v)
+    # all-to-all-v: rank r sends (r+1)*(d+1) bytes of value 16*r+d to rank d
+    segs = [bytes([16 * rank + d]) * ((rank + 1) * (d + 1)) for d in range(world)]
+    send = b"".join(segs)
+    sb = (C.c_uint64 * world)(*[len(x) for x in segs])
+    rb = (C.c_uint64 * world)()
+    cap = 64
+    recv = (C.c_uint8 * cap)()
+    sbuf = (C.c_uint8 * max(1, len(send))).from_buffer_copy(send or b"\0")
+    assert tr.struct.alltoallv(None, C.cast(sbuf, C.c_void_p), sb, C.cast(recv, C.c_void_p), cap, rb) == 0
+    got = bytes(recv[:sum(rb)])
+    # a receive buffer that is too small is an error, not a truncation
+    small = (C.c_uint8 * 1)()
+    rc_small = tr.struct.alltoallv(None, C.cast(sbuf, C.c_void_p), sb, C.cast(small, C.c_void_p), 1, rb)
+    q.put((rank, mn, sm, list(rb), got, rc_small))
+    dist.destroy_process_group()
+
+
+def test_torch_transport_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_transport_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, mn, sm, rb, got, rc_small in res:
+        assert mn == [10, -1, 1 << 40]
+        assert sm == [21, -1, 2 << 40]
+        want = [(r + 1) * (rank + 1) for r in range(world)]
+        assert rb == want
+        assert got == b"".join(bytes([16 * r + rank]) * want[r] for r in range(world))
+        assert rc_small != 0
+
+
+def test_merge_matches_single_process_shape():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "blockchain-simulator_amd"))
+    from bcsim.partition import merge
+    a = ([(0, 5, 1, 0, 0, 1, 2, 0, 0, 0)], dict(delivered=[1, 2], delivered_total=3, t_last_ns=7, events=4))
+    b = ([(0, 3, 1, 0, 0, 0, 2, 0, 0, 0)], dict(delivered=[0, 5], delivered_total=5, t_last_ns=9, events=1))
+    tr, cnt = merge([a, b])
+    assert [t[1] for t in tr] == [3, 5]
+    assert cnt == dict(delivered=[1, 7], delivered_total=8, t_last_ns=9, events=5)
+
+
+# cases whose RNG is per node (counter) or absent: the glibc global stream of
+# Raft is a single-GPU configuration (bcsim_run returns E_UNSUPPORTED)
+PART_CASES = ["pbft16_fixed_100", "pbft5_odd", "pbft12_jitter_ctr", "pbft8_rep3_ctr", "pbft8_compat",
+              "raft16_jitter_ctr", "paxos8_fixed", "paxos32_jitter_ctr", "paxos16_jitter_rep4"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_matches_oracle(world, engine_lib):
+    import partition_run
+    res = partition_run.run(world, PART_CASES, transport="host", timeout=240)
+    allc = cases()
+    for name in PART_CASES:
+        merged, err = res[name]
+        assert err is None, f"{name} world={world}: {err}"
+        ref = oracle.run(allc[name])
+        d = compare(ref, merged)
+        assert d is None, f"{name} world={world}: {d}"
+
+
+def _rccl1_worker(port, names, q):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "tests"), os.path.join(repo, "blockchain-simulator_amd")]
+    import torch.distributed as dist
+    import bcsim
+    from parity_cases import cases
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    for name in names:
+        with bcsim.Simulator(cases()[name]) as s:
+            s.set_partition(dist, transport="rccl")
+            s.run()
+            q.put((name, s.trace(), s.counters()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_transport_world1(engine_lib):
+    names = ["pbft16_fixed_100", "raft16_jitter_ctr", "paxos16_jitter_rep4"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl1_worker, args=(_free_port(), names, q))
+    p.start()
+    got = {}
+    for _ in names:
+        name, tr, cnt = q.get(timeout=180)
+        got[name] = (tr, cnt)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    allc = cases()
+    for name in names:
+        d = compare(oracle.run(allc[name]), got[name])
+        assert d is None, f"{name}: {d}"
