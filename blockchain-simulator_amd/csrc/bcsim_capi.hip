@@ -324,6 +324,9 @@ static int setup_device(Sim& s) {
   p.rev = rev;
   p.prop = prop;
   p.prop_in = prop_in;
+  p.prop_const = s.E ? s.prop[0] : 0;  // uniform links: k_link skips the per-edge loads
+  for (uint32_t e = 1; e < s.E && p.prop_const >= 0; ++e)
+    if (s.prop[e] != s.prop[0]) p.prop_const = -1;
 
   // capacities
   const uint64_t NT = s.NT;
@@ -467,6 +470,21 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.timers, NT * p.cap_timers)) || (rc = dalloc(s, &p.ops, NT * p.cap_ops)) ||
       (rc = dalloc(s, &p.n_ops, NT)))
     return rc;
+  // per-edge reply slots of main-slot arrivals (kOpRing cells) and implicit
+  // echoes; slots off beyond a 16 GiB budget, both off with BCSIM_NO_SLOTS=1 (A/B aid)
+  {
+    const uint64_t ne = static_cast<uint64_t>(kOpRing) * s.R * s.E;
+    const char* ns = std::getenv("BCSIM_NO_SLOTS");
+    const bool off = ns && *ns == '1';
+    p.impl = off ? 0u : 1u;
+    const bool on = ne * sizeof(Op) <= (16ull << 30) && !off;
+    p.cap_eslot = on ? ne : 1;
+    if ((rc = dalloc(s, &p.eslot, p.cap_eslot)) || (rc = dalloc(s, &p.sflag, static_cast<size_t>(kOpRing) * NT)))
+      return rc;
+    HIPCHK(hipMemset(p.eslot, 0xFF, p.cap_eslot * sizeof(Op)));  // t = -1: no live op
+    HIPCHK(hipMemset(p.sflag, 0, static_cast<size_t>(kOpRing) * NT));
+    if (!on) p.eslot = nullptr;
+  }
   if ((rc = dalloc(s, &p.busy, static_cast<size_t>(s.R) * s.E)) ||
       (rc = dalloc(s, &p.lastc, static_cast<size_t>(s.R) * s.E)))
     return rc;
@@ -641,7 +659,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   else
     rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   if (rc) return rc;
-  rc = launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, hi);
+  rc = launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw);
   if (rc || !s.kp.wgt) return rc;
   // debug (BCSIM_WGT=1): report the slowest k_link workgroups of this launch
   std::vector<unsigned long long> w(8ull * s.NT);
@@ -1206,8 +1224,9 @@ int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, u
     // read + write), 32 B per op kept (compaction write).  k_scan: 16 B per
     // record read + 16 B slot release, 32 B per op written (echo + reply).
     bytes_out4[bcsim::KS_LINK] = 32.0 * ks[bcsim::KST_OPS] + 16.0 * ks[bcsim::KST_REC] +
-                                 32.0 * ks[bcsim::KST_EDGES] + 32.0 * ks[bcsim::KST_KEPT];
-    bytes_out4[bcsim::KS_SCAN] = 32.0 * ks[bcsim::KST_DELIV];
+                                 32.0 * ks[bcsim::KST_EDGES] + 32.0 * ks[bcsim::KST_KEPT] +
+                                 32.0 * ks[bcsim::KST_ECHO];
+    bytes_out4[bcsim::KS_SCAN] = 16.0 * ks[bcsim::KST_DELIV];
     bytes_out4[bcsim::KS_GROUP] = 0;
     bytes_out4[bcsim::KS_AUX] = static_cast<double>(ks[bcsim::KST_REC]);  // records emitted
   }

@@ -82,6 +82,18 @@ struct KP {
   Op* ops;
   uint32_t* n_ops;
   uint32_t cap_ops;
+  // per-edge reply slots: ring of kOpRing cells, one slot per
+  // (replica, edge) for a unicast reply (PBFT PREPARE_RES) of the edge's main
+  // inbox record.  A slot op is live while t >= the current window start;
+  // nullptr = disabled (replies go to the op lists)
+  Op* eslot;             // [kOpRing][R][E]
+  uint8_t* sflag;        // [kOpRing][NT] node has reply-slot ops in the ring cell
+  uint64_t cap_eslot;
+  // implicit echoes: k_link echoes a node's main inbox records itself (the
+  // in-slot index is the reverse out-edge) and releases the slots; k_scan
+  // writes echo ops only for extras records
+  uint32_t impl;
+  int64_t prop_const;    // propagation delay of every edge, or -1 (per-edge array)
   // links
   int64_t* busy;
   int64_t* lastc;  // cell of the last record emitted on the edge (-1: none)
@@ -348,6 +360,39 @@ __device__ inline void st_rec(Rec* p, const Rec& r) {
   *reinterpret_cast<uint4*>(p) = v;
 }
 __device__ inline void clr_rec(Rec* p) { *reinterpret_cast<uint4*>(p) = make_uint4(0, 0, 0, 0); }
+
+// 32-byte ops as two dwordx4 accesses
+__device__ inline Op ld_op(const Op* q) {
+  const uint4* v = reinterpret_cast<const uint4*>(q);
+  const uint4 a = v[0], b = v[1];
+  Op o;
+  __builtin_memcpy(&o, &a, 16);
+  __builtin_memcpy(reinterpret_cast<char*>(&o) + 16, &b, 16);
+  return o;
+}
+__device__ inline void st_op(Op* q, const Op& o) {
+  uint4 a, b;
+  __builtin_memcpy(&a, &o, 16);
+  __builtin_memcpy(&b, reinterpret_cast<const char*>(&o) + 16, 16);
+  uint4* v = reinterpret_cast<uint4*>(q);
+  v[0] = a;
+  v[1] = b;
+}
+
+// per-edge op slots
+constexpr uint32_t kOpRing = 4;
+__device__ inline Op* eslot_at(const KP& p, uint32_t ob, uint32_t rep, uint32_t e) {
+  return &AT(p.eslot, (static_cast<size_t>(ob) * p.R + rep) * p.E + e, p.cap_eslot);
+}
+// may the reply of a main-slot arrival, due at t_r, sit in its edge's slot 1?
+// (within the ring, and the slot holds no live op: live = t >= t_lo)
+__device__ inline bool reply_slot_free(const KP& p, long long cell, long long t_lo, int64_t t_r, uint32_t rep,
+                                       uint32_t q) {
+  const long long dc = t_r / p.L - cell;
+  if (dc < 0 || dc >= static_cast<long long>(kOpRing)) return false;
+  const uint32_t ob = static_cast<uint32_t>((t_r / p.L) % kOpRing);
+  return eslot_at(p, ob, rep, q)->t < t_lo;
+}
 
 // ---- block-wide primitives (blockDim.x a multiple of 64, <= 1024) ----------
 constexpr int kMaxWaves = 16;
@@ -894,6 +939,7 @@ struct ScanShared {
   unsigned long long deliv[BCSIM_MSG_TYPES];
   unsigned long long wrong;
   long long tmax;
+  uint32_t ocnt[kOpRing];  // reply-slot ops written, by due cell - cell
 };
 
 __device__ inline uint64_t arr_key(const KP& p, const Rec& r, uint32_t q) {
@@ -1001,8 +1047,8 @@ __device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t*
 // Crossings are ranks within each (phase, sequence) group: wave 0 walks the
 // window 64 arrivals at a time, grouping lanes by ballot.
 __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep, uint32_t i, uint32_t e0,
-                            uint32_t deg, uint32_t n, long long cs, const uint64_t* akey, const uint32_t* asec,
-                            const Rec* arec, uint32_t* acls) {
+                            uint32_t deg, uint32_t n, uint32_t n_main, long long cell, long long cs, long long t_lo,
+                            const uint64_t* akey, const uint32_t* asec, const Rec* arec, uint32_t* acls) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const size_t base = static_cast<size_t>(g) * p.pbft_seq_cap;
   const int32_t N = static_cast<int32_t>(p.N);
@@ -1110,12 +1156,17 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
   const uint32_t r0 = min(n, tid * per), r1 = min(n, r0 + per);
   const uint32_t ech = p.echo ? 1u : 0u;
+  const bool slots = p.eslot != nullptr;
   uint4 loc = make_uint4(0, 0, 0, 0);  // sub, draws, commits, ops
+  uint32_t rslot = 0;                   // bit j: reply of arrival r0 + j goes to its edge slot
   for (uint32_t r = r0; r < r1; ++r) {
-    const Rec rec = arec[asec[r] & kRidxMask];
+    const uint32_t sec = asec[r];
+    const Rec rec = arec[sec & kRidxMask];
     const uint32_t w = acls[r];
     const bool cross = (w & kCross) != 0;
-    uint32_t si = 0, di = 0, ci = 0, oi = ech;
+    const bool main_rec = (sec & kRidxMask) < n_main;
+    const bool main_slot = slots && main_rec;
+    uint32_t si = 0, di = 0, ci = 0, oi = (p.impl && main_rec) ? 0u : ech;
     if (rec.type == PB_PRE_PREPARE) {
       si = deg;
       di = fixed ? 0u : deg;
@@ -1123,7 +1174,11 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
     } else if (rec.type == PB_PREPARE) {
       si = 1;
       di = fixed ? 0u : 1u;
-      oi += 1;
+      const uint32_t q = e0 + (sec >> kRidxBits);
+      if (main_slot && fixed && r - r0 < 32 && reply_slot_free(p, cell, t_lo, cs + rec.t_off + p.app_delay, rep, q))
+        rslot |= 1u << (r - r0);
+      else
+        oi += 1;
     } else if (rec.type == PB_PREPARE_RES && cross) {
       si = deg;
       di = fixed ? 0u : deg;
@@ -1150,6 +1205,7 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   uint32_t sp = sub0 + ex.x, op = nops0 + ex.w, cp = ex.z;
   uint64_t dp = draws0 + ex.y;
   unsigned long long wrong = 0;
+  uint32_t n_slot[kOpRing] = {0, 0, 0, 0};
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
     const Rec rec = arec[sec & kRidxMask];
@@ -1163,7 +1219,8 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
     const Key key{t, t - static_cast<int64_t>(dt), origin, rec.sub};
     if (t == ((t / p.pbft_period) * p.pbft_period) && key.ts <= t - p.pbft_period)
       set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
-    if (ech) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);  // pbft-node.cc:175
+    // pbft-node.cc:175 echo: implicit for main-slot records (k_link), listed otherwise
+    if (ech && !(p.impl && (sec & kRidxMask) < n_main)) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);
     switch (rec.type) {
       case PB_PRE_PREPARE: {  // :193-211
         const Msg rr = mkmsg(PB_PREPARE, mch(m, 1), mch(m, 2), mch(m, 3), 0);
@@ -1177,7 +1234,14 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
         const Msg rr = mkmsg(PB_PREPARE_RES, mch(m, 1), mch(m, 2), enc_raw(p, 0), 0);
         int64_t d = p.app_delay;
         if (!fixed) d = delay_from_draw(p, ctr_rand(p.seed, rep, i, dp++));
-        ops[op++] = mk_op(p, t + d, static_cast<uint32_t>(d), i, sp++, q, rr, OP_SEND, 0);
+        const Op ro = mk_op(p, t + d, static_cast<uint32_t>(d), i, sp++, q, rr, OP_SEND, 0);
+        if (rslot & (1u << (r - r0))) {
+          const long long dc = ro.t / p.L;
+          st_op(eslot_at(p, static_cast<uint32_t>(dc % kOpRing), rep, q), ro);
+          ++n_slot[dc - cell];
+        } else {
+          ops[op++] = ro;
+        }
         break;
       }
       case PB_PREPARE_RES:  // :223-240
@@ -1228,6 +1292,8 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
     wave_add_by_key(act && ty < BCSIM_MSG_TYPES, ty, 1u, S.deliv);
   }
   if (wrong) atomicAdd(&S.wrong, wrong);
+  for (uint32_t k = 0; k < kOpRing; ++k)
+    if (n_slot[k]) atomicAdd(&S.ocnt[k], n_slot[k]);
   __syncthreads();
   // ---- E: tx[n].val of the window's PRE_PREPAREs (last one per index wins) ----
   for (uint32_t k = tid; k < min(S.npp, 64u); k += blockDim.x) {
@@ -1292,6 +1358,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     S.block_num = PROTO == BCSIM_PBFT ? AT(p.block_num, g, p.NT) : 0;
     S.leader = PROTO == BCSIM_PBFT ? AT(p.leader, g, p.NT) : 0;
     for (int k = 0; k < BCSIM_MSG_TYPES; ++k) S.deliv[k] = 0;
+    for (uint32_t k = 0; k < kOpRing; ++k) S.ocnt[k] = 0;
     S.wrong = 0;
     S.tmax = LLONG_MIN;
   }
@@ -1371,7 +1438,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     sort_window(S, n, akey, asec);
 
     if (PROTO == BCSIM_PBFT) {
-      pbft_window(p, S, g, rep, i, e0, deg, n, cs, akey, asec, arec, acls);
+      pbft_window(p, S, g, rep, i, e0, deg, n, n_main, cell, cs, t_lo, akey, asec, arec, acls);
       events += (tid == 0) ? n : 0;
     } else if (tid == 0) {
       c.sub = S.sub;
@@ -1429,8 +1496,9 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
           const Msg msg = rec_msg(rec);
           if (rec.type < BCSIM_MSG_TYPES) ++c.deliv[rec.type];
           if (p.echo) {  // socket->SendTo(packet, 0, from): reverse-link occupancy
-            ctx_op(c, mk_op(p, best.t, static_cast<uint32_t>(best.t - best.ts), best.origin, rec.sub, q, msg,
-                            OP_ECHO, 0));
+            const Op eo = mk_op(p, best.t, static_cast<uint32_t>(best.t - best.ts), best.origin, rec.sub, q, msg,
+                                OP_ECHO, 0);
+            if (!(p.impl && (asec[ai - 1] & kRidxMask) < n_main)) ctx_op(c, eo);  // else implicit (k_link)
             ++c.echoes;
           }
           if (PROTO == BCSIM_RAFT)
@@ -1495,13 +1563,20 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     // consumed slots are free again
     for (uint32_t r = tid; r < n; r += blockDim.x) {
       const uint32_t sec = asec[r];
-      if ((sec & kRidxMask) < n_main) clr_rec(const_cast<Rec*>(slots) + (sec >> kRidxBits));
+      if (!p.impl && (sec & kRidxMask) < n_main) clr_rec(const_cast<Rec*>(slots) + (sec >> kRidxBits));
     }
     __syncthreads();
     if (wb >= t_hi) break;
     wa = wb;
   }
-  if (final_win && flag && tid == 0) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
+  // (implicit echoes: k_link still reads this cell's slots and clears the flag)
+  if (final_win && flag && tid == 0 && !p.impl) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
+  // slot ops make their cells busy (bucket counts) and flag this node for k_link
+  if (tid < kOpRing && S.ocnt[tid]) {
+    const long long dc = cell + tid;
+    atomicAdd(&p.bucket_cnt[dc % p.n_buckets], S.ocnt[tid]);
+    AT(p.sflag, (dc % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 1;
+  }
 
   // ---- write back ----
   unsigned long long* cnt = &AT(p.counters, static_cast<size_t>(rep) * CNT_N, static_cast<uint64_t>(p.R) * CNT_N);
@@ -1578,6 +1653,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
 // cell (a second record of the same edge and cell goes to the extras list,
 // a cell beyond the ring to the overflow list).
 constexpr int kBcastCap = 64;  // due broadcasts per node per cell
+constexpr int kMaxTiles = 1024;  // 64-node tiles of the full-mesh transpose (N <= 65536)
 constexpr int kMaxBuckets = 64;
 
 __device__ inline bool op_key_less(const Op& a, uint32_t sa, const Op& b, uint32_t sb) {
@@ -1598,6 +1674,8 @@ struct LinkShared {
   uint32_t lst[kMaxBuckets + 1 + kMaxRanks];    // per list (bucket extras..., overflow, ranks...)
   uint32_t lbase[kMaxBuckets + 1 + kMaxRanks];  // per list base reserved in the global list
   long long omin, ovmin;
+  uint8_t tflag[kMaxTiles];  // full mesh: receiver tiles this sender wrote in this launch
+  uint32_t tbk;              // (the bucket of those records; one per launch in practice)
 };
 
 // Stage one extras / overflow record of k_link (list = bucket, or B for the
@@ -1637,7 +1715,8 @@ __device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32
   }
 }
 
-__global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_hi) {
+__global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                              long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1645,7 +1724,12 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   if (blockIdx.x >= p.R * p.nloc) return;
   const uint32_t g = local_gnode(p, blockIdx.x);
   uint32_t n = AT(p.n_ops, g, p.NT);
-  if (n == 0) return;
+  const uint32_t ob = static_cast<uint32_t>(cell % kOpRing);
+  const bool sl = p.eslot && AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT);
+  const uint32_t ib = static_cast<uint32_t>(cell % p.n_buckets);
+  const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
+  const bool rx = p.impl && AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT);
+  if (n == 0 && !sl && !rx) return;
   const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
   unsigned long long ph[4] = {0, 0, 0, 0};
   const uint32_t n_in = n;
@@ -1698,15 +1782,20 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   for (uint32_t k = tid; k < B; k += blockDim.x) L.lcnt[k] = 0;
   const uint32_t n_lists = B + 1 + (p.nranks > 1 ? p.nranks : 0);
   for (uint32_t k = tid; k < n_lists; k += blockDim.x) L.lst[k] = 0;
+  const bool tmap = p.mesh && p.n_tiles <= static_cast<uint32_t>(kMaxTiles);
+  if (tmap)
+    for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x) L.tflag[k] = 0;
   if (tid == 0) {
     L.n_bc = 0;
     L.n_keep = 0;
     L.nst = 0;
     L.omin = LLONG_MAX;
     L.ovmin = LLONG_MAX;
+    L.tbk = kInvalid;
   }
   __syncthreads();
   unsigned long long dropped = 0, sends = 0, st_ops = 0;
+  uint32_t cb = kInvalid, cbn = 0;  // run-length bucket count of this thread's records
   for (uint32_t k = tid; k < n; k += blockDim.x) {
     const Op& o = ops[k];
     const uint8_t kind = op_kind(o);
@@ -1762,11 +1851,47 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
 
   if (p.wgt && tid == 0) ph[1] = __builtin_amdgcn_s_memrealtime();
   // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO, emit ----
-  unsigned long long n_rec = 0, st_edges = 0;
+  unsigned long long n_rec = 0, st_edges = 0, st_echo = 0;
   long long ovmin = LLONG_MAX;
+  const long long cs = cell * p.L;
+  const Rec* in_row = p.inbox + (static_cast<size_t>(ib) * p.R + rep) * p.E;
   for (uint32_t le = tid; le < deg; le += blockDim.x) {
     const uint32_t eb = ecnt[le], ee = ecnt[le + 1];
-    if (ee == eb && n_bc == 0) continue;
+    const uint32_t e = e0 + le;
+    // full mesh: peers ascending without self (validated on the host)
+    const uint32_t s = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e, p.E);
+    // implicit echo: this node's main inbox record of in-slot le, delivered in
+    // [t_lo, t_hi), goes back out on out-edge le (the same peer); release the slot
+    bool he = false;
+    Op eo;
+    if (rx) {
+      Rec* ir = const_cast<Rec*>(in_row) + e;
+      const Rec r0 = ld_rec(ir);
+      const long long ta0 = cs + r0.t_off;
+      if ((r0.flags & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
+        clr_rec(ir);
+        if (p.echo) {
+          const int bg = (r0.flags & RF_BIG) ? 1 : 0;
+          const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
+          eo.t = ta0;
+          eo.dt = static_cast<uint32_t>(pin + p.tx_last[bg]);
+          eo.origin = s;
+          eo.sub = r0.sub;
+          eo.kind_flags = static_cast<uint8_t>(OP_ECHO | (bg ? (OPF_BIG << 2) : 0));
+          he = true;
+          ++st_echo;
+        }
+      }
+    }
+    // this edge's reply-slot op due in [t_lo, t_hi)
+    bool hr = false;
+    Op ro;
+    if (sl) {
+      ro = ld_op(eslot_at(p, ob, rep, e));
+      hr = ro.t >= t_lo && ro.t < t_hi;
+      if (hr) ++st_ops;
+    }
+    if (ee == eb && n_bc == 0 && !he && !hr) continue;
     for (uint32_t a = eb + 1; a < ee; ++a) {  // insertion sort of this edge's ops (few)
       const uint32_t x = eidx[a];
       const Op ox = ops[x];
@@ -1780,32 +1905,55 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       eidx[b2] = x;
     }
     ++st_edges;
-    const uint32_t e = e0 + le;
     int64_t bu = busy[le];
     int64_t lc = lastc[le];
-    const int64_t pr = prop[le];
-    const uint32_t s = AT(p.col, e, p.E);
-    const uint32_t slot = AT(p.rev, e, p.E);
+    const int64_t pr = p.prop_const >= 0 ? p.prop_const : prop[le];
+    // in-slot of this edge in the receiver's row (full mesh: arithmetic)
+    const uint32_t slot = p.mesh ? s * (p.N - 1) + (i < s ? i : i - 1) : AT(p.rev, e, p.E);
     const uint32_t dg = rep * p.N + s;
     uint32_t a = eb, bi = 0;
     for (;;) {
       // next broadcast that targets this edge (Paxos broadcasts skip peers[0])
       while (bi < n_bc && (op_flags(ops[L.bc[bi]]) & OPF_PAXOS) && le == 0) ++bi;
-      const bool ha = a < ee, hb = bi < n_bc;
-      if (!ha && !hb) break;
-      uint32_t sub_b = 0;
-      if (hb) {
-        const Op& ob = ops[L.bc[bi]];
-        sub_b = ob.sub + ((op_flags(ob) & OPF_PAXOS) ? le - 1 : le);
+      // four sorted sources, each applied in canonical key order: broadcasts
+      // (1), this edge's listed ops (0), the reply slot (2), the implicit echo (3)
+      int src = -1;
+      Op o;
+      uint32_t sub = 0;
+      if (bi < n_bc) {
+        o = ops[L.bc[bi]];
+        sub = o.sub + ((op_flags(o) & OPF_PAXOS) ? le - 1 : le);
+        src = 1;
       }
-      bool take_a = ha;
-      if (ha && hb) {
-        const Op& oa = ops[eidx[a]];
-        take_a = op_key_less(oa, oa.sub, ops[L.bc[bi]], sub_b);
+      if (a < ee) {
+        const Op oa = ops[eidx[a]];
+        if (src < 0 || op_key_less(oa, oa.sub, o, sub)) {
+          o = oa;
+          sub = oa.sub;
+          src = 0;
+        }
       }
-      const Op o = take_a ? ops[eidx[a++]] : ops[L.bc[bi++]];
-      const uint32_t sub = take_a ? o.sub : sub_b;
-      const bool is_echo = take_a && op_kind(o) == OP_ECHO;
+      if (hr && (src < 0 || op_key_less(ro, ro.sub, o, sub))) {
+        o = ro;
+        sub = ro.sub;
+        src = 2;
+      }
+      if (he && (src < 0 || op_key_less(eo, eo.sub, o, sub))) {
+        o = eo;
+        sub = eo.sub;
+        src = 3;
+      }
+      if (src < 0) break;
+      if (src == 0)
+        ++a;
+      else if (src == 1)
+        ++bi;
+      else if (src == 2)
+        hr = false;
+      else
+        he = false;
+      if (src == 2 && op_kind(o) == OP_SEND) ++sends;
+      const bool is_echo = src != 1 && op_kind(o) == OP_ECHO;
       const int big = (op_flags(o) & OPF_BIG) ? 1 : 0;
       const int64_t start = bu > o.t ? bu : o.t;
       const int64_t end = start + p.tx_tot[big];
@@ -1844,11 +1992,27 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       }
       if (rel < static_cast<long long>(B)) {
         const uint32_t bk = static_cast<uint32_t>(ca % B);
+        bool flag_rx = true;
         if (owner) {
           if (p.mesh) {  // sender-major staging, moved to the receiver by k_transpose
             st_rec(&AT(p.outbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + e, p.cap_inbox), r);
-            AT(p.tdirty, ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (i >> 6)) * p.n_tiles + (s >> 6),
-               static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
+            // tile flag: one LDS byte per receiver tile, flushed once per workgroup
+            // (k_transpose then sets the receivers' iflag once per tile)
+            uint32_t tb = kInvalid;
+            if (tmap) {  // the first bucket seen owns the LDS map; others flag directly
+              tb = L.tbk;
+              if (tb == kInvalid) {
+                const uint32_t old = atomicCAS(&L.tbk, kInvalid, bk);
+                tb = old == kInvalid ? bk : old;
+              }
+            }
+            if (tb == bk) {
+              L.tflag[s >> 6] = 1;
+            } else {
+              AT(p.tdirty, ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (i >> 6)) * p.n_tiles + (s >> 6),
+                 static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
+            }
+            flag_rx = false;
           } else {
             st_rec(&AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox), r);
           }
@@ -1860,8 +2024,13 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
           x.g = dg;
           link_stage(p, L, g, bk, x);
         }
-        AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
-        atomicAdd(&L.lcnt[bk], 1u);
+        if (flag_rx) AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
+        if (bk != cb) {
+          if (cbn) atomicAdd(&L.lcnt[cb], cbn);
+          cb = bk;
+          cbn = 0;
+        }
+        ++cbn;
       } else {
         XRec x;
         x.r = r;
@@ -1876,7 +2045,14 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     busy[le] = bu;
     lastc[le] = lc;
   }
+  if (cbn) atomicAdd(&L.lcnt[cb], cbn);
   __syncthreads();
+  // flush the tile flags of this sender's full-mesh records
+  if (tmap && L.tbk != kInvalid) {
+    const size_t tb = (static_cast<size_t>(L.tbk) * p.R + rep) * p.n_tiles + (i >> 6);
+    for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x)
+      if (L.tflag[k]) AT(p.tdirty, tb * p.n_tiles + k, static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
+  }
 
   if (p.wgt && tid == 0) ph[2] = __builtin_amdgcn_s_memrealtime();
   // ---- 3. compact the ops that are not due yet ----
@@ -1935,13 +2111,14 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   uint4 t1, t2;
   (void)block_scan4(make_uint4(static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends),
                                static_cast<uint32_t>(n_rec), static_cast<uint32_t>(st_ops)), L.wsum, t1);
-  (void)block_scan4(make_uint4(static_cast<uint32_t>(st_edges), 0, 0, 0), L.wsum, t2);
+  (void)block_scan4(make_uint4(static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo), 0, 0), L.wsum, t2);
   if (tid == 0) {
     if (t1.x) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(t1.x));
     if (t1.y) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(t1.y));
     if (t1.z) atomicAdd(&p.kstat[KST_REC], static_cast<unsigned long long>(t1.z));
     if (t1.w) atomicAdd(&p.kstat[KST_OPS], static_cast<unsigned long long>(t1.w));
     if (t2.x) atomicAdd(&p.kstat[KST_EDGES], static_cast<unsigned long long>(t2.x));
+    if (t2.y) atomicAdd(&p.kstat[KST_ECHO], static_cast<unsigned long long>(t2.y));
   }
   __syncthreads();
   for (uint32_t k = tid; k < B; k += blockDim.x)
@@ -1957,6 +2134,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   }
   if (tid == 0) {
     if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
+    if (sl && final_win) AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 0;
+    if (rx && final_win) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
     AT(p.n_ops, g, p.NT) = L.n_keep;
     AT(p.node_onext, g, p.NT) = L.omin;
     atomicAdd(&p.kstat[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
@@ -2067,10 +2246,13 @@ __global__ __launch_bounds__(256) void k_transpose(const KP* __restrict__ pk, ui
   // rows of the inbox: receiver s, senders i0 + lane
   for (uint32_t c = w; c < kTile; c += nw) {
     const uint32_t s = s0 + c, i = i0 + lane;
-    if (i < N && s < N && s != i) {
-      const Rec v = tile[lane][c ^ lane];
-      if (v.flags) st_rec(&AT(ib, static_cast<size_t>(s) * (N - 1) + i - (i > s ? 1 : 0), p.E), v);
-    }
+    const bool ok = i < N && s < N && s != i;
+    const Rec v = tile[lane][c ^ lane];
+    const bool has = ok && v.flags != 0;
+    if (has) st_rec(&AT(ib, static_cast<size_t>(s) * (N - 1) + i - (i > s ? 1 : 0), p.E), v);
+    // receiver s has arrivals in this bucket (k_link leaves the flag to us)
+    if (__ballot(has) && lane == 0)
+      AT(p.iflag, static_cast<size_t>(b) * p.NT + rep * N + s, static_cast<uint64_t>(p.n_buckets) * p.NT) = 1;
   }
   if (threadIdx.x == 0) dirty = 0;
 }

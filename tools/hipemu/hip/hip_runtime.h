@@ -109,6 +109,8 @@ inline int __ffsll(long long x) { return __builtin_ffsll(x); }
 
 template <typename T, typename U>
 inline T atomicAdd(T* p, U v) { return __atomic_fetch_add(p, static_cast<T>(v), __ATOMIC_SEQ_CST); }
+template <typename T, typename U>
+inline T atomicOr(T* p, U v) { return __atomic_fetch_or(p, static_cast<T>(v), __ATOMIC_SEQ_CST); }
 template <typename T, typename U, typename V>
 inline T atomicCAS(T* p, U cmp_, V v_) {
   T cmp = static_cast<T>(cmp_), v = static_cast<T>(v_);
