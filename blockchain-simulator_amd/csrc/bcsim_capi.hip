@@ -589,8 +589,9 @@ static int setup_device(Sim& s) {
   }
 #endif
   if (const char* wv = std::getenv("BCSIM_WGT"); wv && *wv == '1') {  // debug: k_link per-WG timing
-    if ((rc = dalloc(s, &p.wgt, NT * 8))) return rc;
+    if ((rc = dalloc(s, &p.wgt, NT * 8)) || (rc = dalloc(s, &p.wgs, NT * 8))) return rc;
     HIPCHK(hipMemset(p.wgt, 0, NT * 64));
+    HIPCHK(hipMemset(p.wgs, 0, NT * 64));
   }
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -659,6 +660,35 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   else
     rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   if (rc) return rc;
+  if (s.kp.wgs) {  // debug (BCSIM_WGT=1): mean k_scan phase times of a heavy launch
+    std::vector<unsigned long long> w(8ull * s.NT);
+    HIPCHK(hipStreamSynchronize(s.stream));
+    HIPCHK(hipMemcpy(w.data(), s.kp.wgs, w.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(s.kp.wgs, 0, w.size() * 8));
+    double acc[8] = {0};
+    unsigned long long tmin = ~0ull, tmax = 0;
+    uint32_t nw = 0;
+    for (uint32_t g = 0; g < s.NT; ++g) {
+      const unsigned long long* q = &w[8ull * g];
+      if (!q[7] || !q[0]) continue;
+      ++nw;
+      tmin = std::min(tmin, q[0]);
+      tmax = std::max(tmax, q[7]);
+      unsigned long long prev = q[0];
+      for (int k = 1; k < 8; ++k) {
+        if (q[k] >= prev) {
+          acc[k] += static_cast<double>(q[k] - prev);
+          prev = q[k];
+        }
+      }
+      acc[0] += static_cast<double>(q[7] - q[0]);
+    }
+    if (nw && tmax - tmin > 40000) {
+      std::fprintf(stderr, "[wgs] cell %lld k_scan span %.2f ms, %u WGs, mean us: total %.1f stage %.1f sort %.1f A %.1f B %.1f C %.1f D %.1f E+wb %.1f\n",
+                   cell, (tmax - tmin) / 1e5, nw, acc[0] / nw / 100, acc[1] / nw / 100, acc[2] / nw / 100,
+                   acc[3] / nw / 100, acc[4] / nw / 100, acc[5] / nw / 100, acc[6] / nw / 100, acc[7] / nw / 100);
+    }
+  }
   rc = launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw);
   if (rc || !s.kp.wgt) return rc;
   // debug (BCSIM_WGT=1): report the slowest k_link workgroups of this launch

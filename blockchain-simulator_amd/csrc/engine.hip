@@ -135,7 +135,8 @@ struct KP {
   int32_t* err;
   int32_t* dbg;  // first error's source line
   unsigned long long* trail;  // BCSIM_CHECKED + BCSIM_TRAIL: host-mapped breadcrumbs
-  unsigned long long* wgt;    // BCSIM_WGT: per-workgroup k_link timing [NT][4] (debug)
+  unsigned long long* wgt;    // BCSIM_WGT: per-workgroup k_link timing [NT][8] (debug)
+  unsigned long long* wgs;    // BCSIM_WGT: per-workgroup k_scan phase timing [NT][8] (debug)
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   long long *node_tnext, *node_onext;
   long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks
@@ -932,18 +933,27 @@ struct ScanShared {
   uint32_t sub, nops, tn, npp, last_vc;
   uint64_t draws;
   int32_t block_num, leader;
-  uint32_t tkey[kQuorumTab];
+  uint32_t tkey[kQuorumTab];   // (phase, sequence) keys, a contiguous prefix (0 = empty)
   uint32_t tcnt[kQuorumTab];
+  uint16_t wsc[kMaxWaves][kQuorumTab];  // per-wave counts, then per-wave bases (< 2^16: T + cap_arr)
   uint32_t pp_r[64];
   int32_t pp_idx[64], pp_val[64];
   unsigned long long deliv[BCSIM_MSG_TYPES];
   unsigned long long wrong;
   long long tmax;
   uint32_t ocnt[kOpRing];  // reply-slot ops written, by due cell - cell
+  unsigned long long ph[8];  // BCSIM_WGT phase clock (debug)
 };
+#define SPH(k)                                                         \
+  do {                                                                 \
+    if (p.wgs && threadIdx.x == 0) S.ph[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
+__device__ inline int64_t prop_of_slot(const KP& p, uint32_t q) {
+  return p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, q, p.E);
+}
 __device__ inline uint64_t arr_key(const KP& p, const Rec& r, uint32_t q) {
-  const uint32_t dt = static_cast<uint32_t>(AT(p.prop_in, q, p.E) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
+  const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
   return (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~dt);
 }
 
@@ -954,23 +964,29 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
                                  uint64_t* akey, uint32_t* asec, Rec* arec, bool store) {
   const uint32_t tid = threadIdx.x;
   uint32_t n = 0;
-  for (uint32_t base = 0; base < deg; base += blockDim.x) {
-    const uint32_t k = base + tid;
-    Rec r{};
-    bool v = false;
-    if (k < deg) {
-      r = ld_rec(slots + k);
+  for (uint32_t base = 0; base < deg; base += 4 * blockDim.x) {
+    Rec rr[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {  // all loads in flight before the first rank
+      const uint32_t k = base + j * blockDim.x + tid;
+      rr[j] = k < deg ? ld_rec(slots + k) : Rec{};
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      if (base + j * blockDim.x >= deg) break;  // block-uniform
+      const uint32_t k = base + j * blockDim.x + tid;
+      const Rec r = rr[j];
       const long long t = cs + r.t_off;
-      v = (r.flags & RF_VALID) && t >= wa && t < wb;
+      const bool v = k < deg && (r.flags & RF_VALID) && t >= wa && t < wb;
+      uint32_t tot;
+      const uint32_t pos = n + block_rank(v, S.wcnt, tot);
+      if (store && v && pos < p.cap_arr) {
+        arec[pos] = r;
+        asec[pos] = (k << kRidxBits) | pos;
+        akey[pos] = arr_key(p, r, e0 + k);
+      }
+      n += tot;
     }
-    uint32_t tot;
-    const uint32_t pos = n + block_rank(v, S.wcnt, tot);
-    if (store && v && pos < p.cap_arr) {
-      arec[pos] = r;
-      asec[pos] = (k << kRidxBits) | pos;
-      akey[pos] = arr_key(p, r, e0 + k);
-    }
-    n += tot;
   }
   const uint32_t n_main = n;
   for (uint32_t base = 0; base < xn; base += blockDim.x) {
@@ -1037,6 +1053,22 @@ __device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t*
   }
 }
 
+// Table slot of a (phase, sequence) key: linear probing from 0 with a CAS
+// insert, so used slots stay a contiguous prefix.
+__device__ inline uint32_t quorum_slot(const KP& p, ScanShared& S, uint32_t key, bool insert) {
+  for (uint32_t k = 0; k < static_cast<uint32_t>(kQuorumTab); ++k) {
+    const uint32_t t = __hip_atomic_load(&S.tkey[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (t == key) return k;
+    if (t == 0u) {
+      if (!insert) break;
+      const uint32_t old = atomicCAS(&S.tkey[k], 0u, key);
+      if (old == 0u || old == key) return k;
+    }
+  }
+  set_err(p, BCSIM_E_OVERFLOW);
+  return kQuorumTab - 1;
+}
+
 // ---- PBFT, data parallel (pbft-node.cc:166-291) ----------------------------
 // One window of sorted arrivals.  Sequential semantics restated as prefixes:
 //   PRE_PREPARE   tx[n].val = val; bcast PREPARE          sub += deg
@@ -1099,52 +1131,68 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
     acls[r] = w;
   }
   __syncthreads();
-  // ---- B: quorum ranks (wave 0) ----
-  if (tid < 64) {
-    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
-      const uint32_t r = b0 + lane;
-      const uint32_t w = r < n ? acls[r] : 0u;
-      unsigned long long rem = __ballot(w != 0);
-      while (rem) {
-        const int ld = __ffsll(static_cast<long long>(rem)) - 1;
-        const uint32_t wl = __shfl(w, ld, 64);
-        const bool mine = (w == wl);
-        const unsigned long long same = __ballot(mine);
-        uint32_t cnt = 0;
-        if (lane == static_cast<uint32_t>(ld)) {
-          int e = -1;
-          for (uint32_t k = 0; k < S.tn; ++k)
-            if (S.tkey[k] == wl) {
-              e = static_cast<int>(k);
-              break;
-            }
-          if (e < 0) {
-            if (S.tn >= static_cast<uint32_t>(kQuorumTab)) {
-              set_err(p, BCSIM_E_OVERFLOW);
-              e = kQuorumTab - 1;
-            } else {
-              e = static_cast<int>(S.tn++);
-              S.tkey[e] = wl;
-              const uint32_t idx = wl & kIdxMask;
-              S.tcnt[e] = static_cast<uint32_t>((wl >> 30) == 1u ? AT(p.tx_pv, base + idx, p.cap_txn)
-                                                                  : AT(p.tx_cv, base + idx, p.cap_txn));
+  SPH(3);
+  // ---- B: quorum ranks over all waves: each wave counts its contiguous
+  // range per (phase, sequence) key; a cross-wave prefix (seeded with the
+  // stored vote counters) gives every wave its bases; a second pass ranks
+  // each arrival within its key group ----
+  {
+    const uint32_t nwv = blockDim.x >> 6, wv = tid >> 6;
+    for (uint32_t k = tid; k < static_cast<uint32_t>(kQuorumTab); k += blockDim.x) S.tkey[k] = 0;
+    for (uint32_t k = tid; k < static_cast<uint32_t>(kMaxWaves * kQuorumTab); k += blockDim.x) (&S.wsc[0][0])[k] = 0;
+    __syncthreads();
+    const uint32_t per_w = (n + nwv - 1) / nwv;
+    const uint32_t rb = min(n, wv * per_w), re = min(n, rb + per_w);
+    for (int pass = 0; pass < 2; ++pass) {
+      for (uint32_t b0 = rb; b0 < re; b0 += 64) {  // wave-uniform bounds
+        const uint32_t r = b0 + lane;
+        const uint32_t w = r < re ? acls[r] : 0u;
+        unsigned long long rem = __ballot(w != 0);
+        while (rem) {
+          const int ld = __ffsll(static_cast<long long>(rem)) - 1;
+          const uint32_t wl = __shfl(w, ld, 64);
+          const bool mine = (w == wl);
+          const unsigned long long same = __ballot(mine);
+          uint32_t cnt = 0;
+          if (lane == static_cast<uint32_t>(ld)) {
+            const uint32_t k = quorum_slot(p, S, wl, pass == 0);
+            cnt = S.wsc[wv][k];
+            S.wsc[wv][k] = static_cast<uint16_t>(cnt + static_cast<uint32_t>(__popcll(same)));
+          }
+          if (pass == 1) {
+            cnt = __shfl(cnt, ld, 64);
+            if (mine) {
+              const uint32_t v = cnt + static_cast<uint32_t>(__popcll(same & ((1ull << lane) - 1ull))) + 1u;
+              const bool cross = (w >> 30) == 1u ? (v % T1 == 0) : (v % T2 == 0);
+              if (cross) acls[r] = w | kCross;
             }
           }
-          cnt = S.tcnt[e];
-          S.tcnt[e] = cnt + static_cast<uint32_t>(__popcll(same));
+          rem &= ~same;
         }
-        cnt = __shfl(cnt, ld, 64);
-        if (mine) {
-          const uint32_t v = cnt + static_cast<uint32_t>(__popcll(same & ((1ull << lane) - 1ull))) + 1u;
-          const bool cross = (w >> 30) == 1u ? (v % T1 == 0) : (v % T2 == 0);
-          if (cross) acls[r] = w | kCross;
+      }
+      __syncthreads();
+      if (pass == 0) {
+        for (uint32_t k = tid; k < static_cast<uint32_t>(kQuorumTab); k += blockDim.x) {
+          const uint32_t wl = S.tkey[k];
+          if (!wl) continue;
+          const uint32_t idx = wl & kIdxMask;
+          uint32_t run = static_cast<uint32_t>((wl >> 30) == 1u ? AT(p.tx_pv, base + idx, p.cap_txn)
+                                                                : AT(p.tx_cv, base + idx, p.cap_txn));
+          for (uint32_t w2 = 0; w2 < nwv; ++w2) {
+            const uint32_t c = S.wsc[w2][k];
+            S.wsc[w2][k] = static_cast<uint16_t>(run);
+            run += c;
+          }
+          S.tcnt[k] = run;
         }
-        rem &= ~same;
+        __syncthreads();
       }
     }
     // write back the vote counters (tx[idx].prepare_vote / commit_vote)
-    for (uint32_t k = lane; k < S.tn; k += 64) {
-      const uint32_t wl = S.tkey[k], idx = wl & kIdxMask;
+    for (uint32_t k = tid; k < static_cast<uint32_t>(kQuorumTab); k += blockDim.x) {
+      const uint32_t wl = S.tkey[k];
+      if (!wl) continue;
+      const uint32_t idx = wl & kIdxMask;
       if ((wl >> 30) == 1u)
         AT(p.tx_pv, base + idx, p.cap_txn) = static_cast<int32_t>(S.tcnt[k] % T1);
       else
@@ -1152,6 +1200,7 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
     }
   }
   __syncthreads();
+  SPH(4);
   // ---- C: per-arrival increments over contiguous runs, block scan ----
   const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
   const uint32_t r0 = min(n, tid * per), r1 = min(n, r0 + per);
@@ -1159,6 +1208,22 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   const bool slots = p.eslot != nullptr;
   uint4 loc = make_uint4(0, 0, 0, 0);  // sub, draws, commits, ops
   uint32_t rslot = 0;                   // bit j: reply of arrival r0 + j goes to its edge slot
+  int64_t occ[4];                       // reply-slot occupancy of the first 4 arrivals (t of the op there)
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    occ[j] = LLONG_MAX;
+    const uint32_t r = r0 + j;
+    if (r < r1 && slots && fixed) {
+      const uint32_t sec = asec[r];
+      const Rec rec = arec[sec & kRidxMask];
+      if (rec.type == PB_PREPARE && (sec & kRidxMask) < n_main) {
+        const int64_t tr = cs + rec.t_off + p.app_delay;
+        const long long dc = tr / p.L - cell;
+        if (dc >= 0 && dc < static_cast<long long>(kOpRing))
+          occ[j] = eslot_at(p, static_cast<uint32_t>((tr / p.L) % kOpRing), rep, e0 + (sec >> kRidxBits))->t;
+      }
+    }
+  }
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
     const Rec rec = arec[sec & kRidxMask];
@@ -1175,7 +1240,9 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
       si = 1;
       di = fixed ? 0u : 1u;
       const uint32_t q = e0 + (sec >> kRidxBits);
-      if (main_slot && fixed && r - r0 < 32 && reply_slot_free(p, cell, t_lo, cs + rec.t_off + p.app_delay, rep, q))
+      const bool fr = r - r0 < 4 ? occ[r - r0] < t_lo
+                                 : reply_slot_free(p, cell, t_lo, cs + rec.t_off + p.app_delay, rep, q);
+      if (main_slot && fixed && r - r0 < 32 && fr)
         rslot |= 1u << (r - r0);
       else
         oi += 1;
@@ -1193,6 +1260,7 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   }
   uint4 tot;
   const uint4 ex = block_scan4(loc, S.wsum, tot);
+  SPH(5);
   // ---- D: outputs ----
   const uint32_t sub0 = S.sub, nops0 = S.nops;
   const uint64_t draws0 = S.draws;
@@ -1214,8 +1282,9 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
     const bool cross = (w & kCross) != 0;
     const Msg m = rec_msg(rec);
     const int64_t t = cs + rec.t_off;
-    const uint32_t dt = static_cast<uint32_t>(AT(p.prop_in, q, p.E) + p.tx_last[m.big]);
-    const uint32_t origin = AT(p.col, q, p.E);
+    const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[m.big]);
+    const uint32_t le = q - e0;
+    const uint32_t origin = p.mesh ? (le < i ? le : le + 1) : AT(p.col, q, p.E);
     const Key key{t, t - static_cast<int64_t>(dt), origin, rec.sub};
     if (t == ((t / p.pbft_period) * p.pbft_period) && key.ts <= t - p.pbft_period)
       set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
@@ -1295,6 +1364,7 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   for (uint32_t k = 0; k < kOpRing; ++k)
     if (n_slot[k]) atomicAdd(&S.ocnt[k], n_slot[k]);
   __syncthreads();
+  SPH(6);
   // ---- E: tx[n].val of the window's PRE_PREPAREs (last one per index wins) ----
   for (uint32_t k = tid; k < min(S.npp, 64u); k += blockDim.x) {
     bool last = true;
@@ -1351,6 +1421,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     tm[tid] = AT(p.timers, static_cast<size_t>(g) * p.cap_timers + tid, static_cast<uint64_t>(p.NT) * p.cap_timers);
 
   // ---- node state ----
+  SPH(0);
   if (tid == 0) {
     S.sub = AT(p.sub, g, p.NT);
     S.draws = AT(p.draws, g, p.NT);
@@ -1435,7 +1506,9 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
       n = stage_window(p, S, slots, e0, deg, xs, xn, cs, wa, wb, akey, asec, arec, true);
     }
     const uint32_t n_main = S.n_main;
+    SPH(1);
     sort_window(S, n, akey, asec);
+    SPH(2);
 
     if (PROTO == BCSIM_PBFT) {
       pbft_window(p, S, g, rep, i, e0, deg, n, n_main, cell, cs, t_lo, akey, asec, arec, acls);
@@ -1581,6 +1654,10 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   // ---- write back ----
   unsigned long long* cnt = &AT(p.counters, static_cast<size_t>(rep) * CNT_N, static_cast<uint64_t>(p.R) * CNT_N);
   if (tid != 0) return;
+  if (p.wgs) {
+    SPH(7);
+    for (int k = 0; k < 8; ++k) p.wgs[8ull * g + k] = S.ph[k];
+  }
   const uint32_t nops_in = AT(p.n_ops, g, p.NT);
   AT(p.sub, g, p.NT) = S.sub;
   AT(p.draws, g, p.NT) = S.draws;
