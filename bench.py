@@ -31,9 +31,9 @@ METRIC = "delivered consensus msgs/sec (whole node), PBFT n=4096; committed roun
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def make_cfg(n_nodes, rounds, device):
+def make_cfg(n_nodes, rounds, device, workload="pbft"):
     import bcsim
-    c = bcsim.preset("c4_pbft4096")
+    c = bcsim.preset("c4_pbft4096" if workload == "pbft" else "c5_gossip65536")
     c.n_nodes = n_nodes
     c.pbft_rounds = rounds
     c.device = device
@@ -41,11 +41,19 @@ def make_cfg(n_nodes, rounds, device):
     return c
 
 
-def pmc_traffic(n_nodes, kernel="bcsim::k_link"):
+def make_topology(n_nodes, workload):
+    """None = the reference's full mesh; gossip: random 8-regular graph, seed 1."""
+    if workload == "pbft":
+        return None
+    import bcsim
+    return bcsim.random_regular(n_nodes, 8, 1)
+
+
+def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (tools/pmc_summary.py over tests/gpu_prof.sh: FETCH_SIZE x2 gfx950
     correction + WRITE_SIZE), for the same workload; None if absent."""
-    path = os.path.join(REPO, "profiles", f"r01_pmc_pbft{n_nodes}.json")
+    path = os.path.join(REPO, "profiles", f"r01_pmc_{workload}{n_nodes}.json")
     try:
         with open(path) as f:
             return json.load(f)["kernels"][kernel]["hbm_bytes_per_launch"]
@@ -53,12 +61,15 @@ def pmc_traffic(n_nodes, kernel="bcsim::k_link"):
         return None
 
 
-def cpu_baseline(n_nodes, budget_s):
+def cpu_baseline(n_nodes, budget_s, workload="pbft"):
     """Serial oracle DES (same semantics) on the host: a bounded time slice of
     the same workload, run from t=0 in 1 ms slices until budget_s of CPU."""
     import oracle
-    cfg = make_cfg(n_nodes, 100, 0)
+    cfg = make_cfg(n_nodes, 100, 0, workload)
     o = oracle.OracleSim(cfg)
+    topo = make_topology(n_nodes, workload)
+    if topo is not None:
+        o.set_topology(*topo)
     t0 = time.process_time()
     w0 = time.time()
     t = 0
@@ -72,7 +83,7 @@ def cpu_baseline(n_nodes, budget_s):
     cnt = o.counters()
     o.close()
     return dict(value=cnt["delivered_total"] / max(cpu, 1e-9), unit="msgs/s", cores=1, kind="port",
-                sample=f"oracle DES, PBFT n={n_nodes} full mesh, first {t / 1e6:.0f} ms simulated "
+                sample=f"oracle DES, {workload} n={n_nodes}, first {t / 1e6:.0f} ms simulated "
                        f"({cnt['delivered_total']} msgs, {cpu:.1f} s CPU, {wall:.1f} s wall)")
 
 
@@ -94,12 +105,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=6)
-    ap.add_argument("--nodes", type=int, default=4096)
+    ap.add_argument("--workload", choices=("pbft", "gossip"), default="pbft",
+                    help="pbft: BASELINE configs[3] (the metric); gossip: configs[4], random 8-regular graph")
+    ap.add_argument("--nodes", type=int, default=0, help="default 4096 (pbft) / 65536 (gossip)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("pdes", "replicas"), default="pdes",
                     help="multi-GPU mode (N>1): node-partitioned PDES or independent replicas")
     args = ap.parse_args()
+    if args.nodes <= 0:
+        args.nodes = 4096 if args.workload == "pbft" else 65536
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,8 +128,15 @@ def main():
 
     import bcsim
     period = 50_000_001  # Seconds(0.05f) in ns (round mode)
-    cfg = make_cfg(args.nodes, args.warmup + args.steps + 4, local)
-    sim = bcsim.Simulator(cfg)
+    cfg = make_cfg(args.nodes, args.warmup + args.steps + 4, local, args.workload)
+    topo = make_topology(args.nodes, args.workload)
+
+    def new_sim():
+        sm = bcsim.Simulator(cfg)
+        if topo is not None:
+            sm.set_topology(*topo)
+        return sm
+    sim = new_sim()
     mode = "single"
     if dist is not None:
         mode = args.mode
@@ -130,7 +152,7 @@ def main():
                 print(f"[bench] rank {rank}: RCCL partition unavailable ({err or 'peer failed'}); "
                       f"falling back to replicas", file=sys.stderr, flush=True)
                 sim.close()
-                sim = bcsim.Simulator(cfg)
+                sim = new_sim()
                 mode = "replicas"
 
     def barrier():
@@ -170,7 +192,14 @@ def main():
         dom = max(("scan", "link", "group", "aux"), key=lambda k: ks[k]["us"])
         lk = ks["link"]
         ach = (lk["bytes"] / 1e9) / (lk["us"] / 1e6) if lk["us"] > 0 else 0.0
-        traffic = pmc_traffic(args.nodes)
+        traffic = pmc_traffic(args.nodes, workload=args.workload)
+        if args.workload == "pbft":
+            data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, fixed 3 ms app delay)" % args.nodes
+            wl = f"PBFT n={args.nodes} full O(n^2) prepare/commit (BASELINE configs[3])"
+        else:
+            data = ("synthetic (PBFT-style gossip, n=%d random 8-regular graph seed 1, 3Mbps/3ms links, "
+                    "1000 B blocks, fixed 3 ms app delay)" % args.nodes)
+            wl = f"PBFT-style gossip n={args.nodes} random 8-regular (BASELINE configs[4])"
         lk_launch_bytes = lk["bytes"] / max(1, lk["launches"])
         out = {
             "metric": METRIC,
@@ -184,8 +213,8 @@ def main():
             "scaling": "strong" if mode == "pdes" else "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, fixed 3 ms app delay)" % args.nodes,
-            "config": {"workload": f"PBFT n={args.nodes} full O(n^2) prepare/commit (BASELINE configs[3])",
+            "data": data,
+            "config": {"workload": wl,
                        "nodes": args.nodes, "step": "one 50 ms block interval",
                        "parallelism": f"{mode}{world}" if world > 1 else "single"},
             "committed_rounds_per_s": rounds / dt,
@@ -199,7 +228,7 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.nodes, args.cpu_budget)
+                out["cpu_baseline"] = cpu_baseline(args.nodes, args.cpu_budget, args.workload)
             except Exception as e:  # never let the baseline leg kill the GPU number
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)

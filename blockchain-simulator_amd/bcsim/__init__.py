@@ -11,7 +11,7 @@ import subprocess
 
 from . import _abi, partition
 from ._abi import (  # noqa: F401
-    PBFT, RAFT, PAXOS, DELAY_FIXED, DELAY_RANDOM, RNG_GLIBC, RNG_COUNTER,
+    PBFT, RAFT, PAXOS, GOSSIP, DELAY_FIXED, DELAY_RANDOM, RNG_GLIBC, RNG_COUNTER,
     TIME_ROUND, TIME_TRUNC, ENC_EXTENDED, ENC_COMPAT, TR, INT64_MAX,
     Config, TraceRec, Counters, Status, EngineError, default_config,
 )
@@ -45,6 +45,9 @@ def lib():
         _LIB.bcsim_read_kernel_stats.restype = C.c_int
         _LIB.bcsim_reset_kernel_stats.argtypes = [C.c_void_p]
         _LIB.bcsim_reset_kernel_stats.restype = C.c_int
+        _LIB.bcsim_topology_random_regular.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64,
+                                                       C.c_void_p, C.c_void_p]
+        _LIB.bcsim_topology_random_regular.restype = C.c_int
         partition.declare(_LIB)
     return _LIB
 
@@ -108,6 +111,18 @@ def full_mesh(n):
     return row, col
 
 
+def random_regular(n, d=8, seed=1):
+    """CSR (row_ptr, col_idx) of a simple random d-regular graph, rows ascending
+    (bcsim_topology_random_regular, host-only)."""
+    import numpy as np
+    row = np.zeros(n + 1, dtype=np.uint32)
+    col = np.zeros(n * d, dtype=np.uint32)
+    rc = lib().bcsim_topology_random_regular(n, d, seed, row.ctypes.data, col.ctypes.data)
+    if rc:
+        raise EngineError(rc, "bcsim_topology_random_regular")
+    return row, col
+
+
 def preset(name):
     """Named configs from BASELINE.json (synthetic inputs of SURVEY.md §8d)."""
     if name == "c1_pbft16":       # PBFT n=16, fixed 3 ms links, 100 client requests
@@ -132,5 +147,13 @@ def preset(name):
         c.delay_mode = DELAY_FIXED
         c.app_delay_ns = 3_000_000
         c.pbft_rounds = 100
+        return c
+    if name == "c5_gossip65536":  # PBFT-style gossip, random 8-regular graph (random_regular(n, 8, 1))
+        c = default_config(GOSSIP, 65536)
+        c.delay_mode = DELAY_FIXED
+        c.app_delay_ns = 3_000_000
+        c.pbft_rounds = 100
+        c.pbft_block_bytes = 1000
+        c.stop_ns = -1
         return c
     raise KeyError(name)

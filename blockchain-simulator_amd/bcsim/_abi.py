@@ -7,7 +7,7 @@ import ctypes as C
 
 ABI_VERSION = 1
 
-PBFT, RAFT, PAXOS = 0, 1, 2
+PBFT, RAFT, PAXOS, GOSSIP = 0, 1, 2, 3
 DELAY_FIXED, DELAY_RANDOM = 0, 1
 RNG_GLIBC, RNG_COUNTER = 0, 1
 TIME_ROUND, TIME_TRUNC = 0, 1
@@ -24,6 +24,7 @@ TR = dict(
     PBFT_COMMIT=1, PBFT_BLOCK=2, PBFT_STOP=3, PBFT_VIEW=4,
     RAFT_ELECTION=10, RAFT_LEADER=11, RAFT_BLOCK=12, RAFT_DONE=13,
     RAFT_PROPOSAL=14, RAFT_STOP=15, PAXOS_COMMIT=20, PAXOS_TICKET=21,
+    GOSSIP_BLOCK=30, GOSSIP_DELIVER=31,
 )
 
 MSG_TYPES = 16

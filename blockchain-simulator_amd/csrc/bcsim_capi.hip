@@ -42,6 +42,7 @@ struct Sim {
   std::vector<uint32_t> row, col, rev;
   std::vector<int64_t> prop;
   bool started = false;
+  bool topo_ready = false;  // CSR set by bcsim_set_topology_csr, else the full mesh at first run
   int32_t err = 0;
   int64_t L = 0;
   int64_t t_done = 0;
@@ -150,7 +151,7 @@ static int ev_collect(Sim& s) {
 
 static int validate(const bcsim_config& c) {
   if (c.abi_version != BCSIM_ABI_VERSION) return BCSIM_E_INVAL;
-  if (c.protocol > BCSIM_PAXOS || c.n_nodes < 2 || c.link_rate_bps == 0) return BCSIM_E_INVAL;
+  if (c.protocol > BCSIM_GOSSIP || c.n_nodes < 2 || c.link_rate_bps == 0) return BCSIM_E_INVAL;
   if (c.mtu < 68) return BCSIM_E_INVAL;
   if (c.delay_mode == BCSIM_DELAY_RANDOM && c.rng_mode == BCSIM_RNG_GLIBC) {
     // the global glibc stream is consumed at every send in event order; only
@@ -161,6 +162,10 @@ static int validate(const bcsim_config& c) {
 }
 
 static int build_mesh(Sim& s) {
+  if (static_cast<uint64_t>(s.N) * (s.N - 1) >= 0xFFFFFFFFull) {
+    g_detail = "full mesh over 2^32 directed edges: pass a topology (bcsim_set_topology_csr)";
+    return BCSIM_E_UNSUPPORTED;
+  }
   s.row.assign(s.N + 1, 0);
   s.col.clear();
   s.col.reserve(static_cast<size_t>(s.N) * (s.N - 1));
@@ -246,6 +251,9 @@ static int setup_device(Sim& s) {
       const int num = static_cast<int>(2000 / (1000 / (hb * 1000)));
       big = static_cast<uint32_t>(200 * num);
     }
+  } else if (c.protocol == BCSIM_GOSSIP) {  // every gossip message carries the block
+    big = c.pbft_block_bytes ? c.pbft_block_bytes : 50000;
+    small = big;
   }
   const MsgTx ms = message_tx(small, c.mtu, c.link_rate_bps, tr);
   const MsgTx mb = message_tx(big, c.mtu, c.link_rate_bps, tr);
@@ -272,7 +280,7 @@ static int setup_device(Sim& s) {
     g_detail = "lookahead out of range";
     return BCSIM_E_UNSUPPORTED;
   }
-  if (c.protocol == BCSIM_PBFT && p.pbft_period <= 0) return BCSIM_E_INVAL;
+  if ((c.protocol == BCSIM_PBFT || c.protocol == BCSIM_GOSSIP) && p.pbft_period <= 0) return BCSIM_E_INVAL;
   p.L = s.L;
   // delay tables (float seconds -> ns), pbft-node.cc:68, raft-node.cc:65,71, paxos-node.cc:399
   std::vector<int64_t> dpb(3), drf(3), del(150), dpx(50);
@@ -295,7 +303,7 @@ static int setup_device(Sim& s) {
   p.raft_delay = tables + 4;
   p.raft_elec = tables + 8;
   p.paxos_delay = tables + 160;
-  p.jit_delay = c.protocol == BCSIM_PBFT ? p.pbft_delay : c.protocol == BCSIM_RAFT ? p.raft_delay : p.paxos_delay;
+  p.jit_delay = (c.protocol == BCSIM_PBFT || c.protocol == BCSIM_GOSSIP) ? p.pbft_delay : c.protocol == BCSIM_RAFT ? p.raft_delay : p.paxos_delay;
   p.jit_mod = c.protocol == BCSIM_PAXOS ? 50 : 3;
 
   // topology
@@ -392,12 +400,14 @@ static int setup_device(Sim& s) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_GOSSIP>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_link),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(link_lds_bytes(p))));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_pbft_tick),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(s.N)));
   }
-  if (s.N > 60 * 1024) return BCSIM_E_UNSUPPORTED;  // k_pbft_tick keeps one flag per node in LDS
+  if (c.protocol == BCSIM_PBFT && s.N > 60 * 1024) return BCSIM_E_UNSUPPORTED;  // k_pbft_tick: one LDS flag per node
 
   // node partition: rank prank owns [nlo, nlo + nloc) of every replica
   if (s.P > 1) {
@@ -446,6 +456,9 @@ static int setup_device(Sim& s) {
       (rc = dalloc(s, &p.g_n, s.R)) || (rc = dalloc(s, &p.g_nround, s.R)))
     return rc;
   const size_t txn = c.protocol == BCSIM_PBFT ? NT * p.pbft_seq_cap : 1;
+  const size_t gsn = c.protocol == BCSIM_GOSSIP ? NT * p.pbft_seq_cap : 1;
+  if ((rc = dalloc(s, &p.gseen, gsn))) return rc;
+  HIPCHK(hipMemset(p.gseen, 0, gsn));
   p.cap_txn = txn;
   if ((rc = dalloc(s, &p.tx_val, txn)) || (rc = dalloc(s, &p.tx_pv, txn)) || (rc = dalloc(s, &p.tx_cv, txn)))
     return rc;
@@ -657,6 +670,8 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     rc = launch(s, KS_SCAN, k_scan<BCSIM_PBFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   else if (s.cfg.protocol == BCSIM_RAFT)
     rc = launch(s, KS_SCAN, k_scan<BCSIM_RAFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
+  else if (s.cfg.protocol == BCSIM_GOSSIP)
+    rc = launch(s, KS_SCAN, k_scan<BCSIM_GOSSIP>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   else
     rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
   if (rc) return rc;
@@ -872,10 +887,23 @@ static int sync_leaders(Sim& s) {
   return BCSIM_OK;
 }
 
+// the reference's full mesh (blockchain-simulator.cc:34-51) unless a CSR was given; built
+// lazily so that large sparse configs never materialise N*(N-1) edges
+static int ensure_topology(Sim& s) {
+  if (s.topo_ready) return BCSIM_OK;
+  int rc;
+  if ((rc = build_mesh(s)) || (rc = build_rev(s))) return rc;
+  s.E = s.row[s.N];
+  s.deg_max = 0;
+  for (uint32_t i = 0; i < s.N; ++i) s.deg_max = std::max(s.deg_max, s.row[i + 1] - s.row[i]);
+  s.topo_ready = true;
+  return BCSIM_OK;
+}
+
 static int run(Sim& s, int64_t t_until) {
   int rc;
   if (!s.started) {
-    if ((rc = setup_device(s))) return rc;
+    if ((rc = ensure_topology(s)) || (rc = setup_device(s))) return rc;
     s.started = true;
   }
   HIPCHK(hipSetDevice(s.dev));
@@ -1074,7 +1102,7 @@ struct bcsim_sim {
 extern "C" {
 
 int bcsim_config_default(bcsim_config* c, uint32_t protocol, uint32_t n_nodes) {
-  if (!c || protocol > BCSIM_PAXOS) return BCSIM_E_INVAL;
+  if (!c || protocol > BCSIM_GOSSIP) return BCSIM_E_INVAL;
   std::memset(c, 0, sizeof *c);
   c->abi_version = BCSIM_ABI_VERSION;
   c->protocol = protocol;
@@ -1123,14 +1151,6 @@ int bcsim_create(const bcsim_config* cfg, bcsim_sim** out) {
   }
   s->NT = s->N * s->R;
   s->nloc = s->N;
-  bcsim::build_mesh(*s);
-  if ((rc = bcsim::build_rev(*s))) {
-    delete s;
-    return rc;
-  }
-  s->E = s->row[s->N];
-  s->deg_max = 0;
-  for (uint32_t i = 0; i < s->N; ++i) s->deg_max = std::max(s->deg_max, s->row[i + 1] - s->row[i]);
   bcsim_sim* h = new (std::nothrow) bcsim_sim{s};
   if (!h) {
     delete s;
@@ -1159,6 +1179,7 @@ int bcsim_set_topology_csr(bcsim_sim* h, uint32_t n, const uint32_t* row_ptr, co
   s.E = E;
   s.deg_max = 0;
   for (uint32_t i = 0; i < n; ++i) s.deg_max = std::max(s.deg_max, s.row[i + 1] - s.row[i]);
+  s.topo_ready = true;
   return BCSIM_OK;
 }
 

@@ -84,7 +84,8 @@ enum : uint8_t {
   TM_RAFT_ELECTION = 1,
   TM_RAFT_HEARTBEAT = 2,
   TM_RAFT_PROPOSAL = 3,
-  TM_PAXOS_TICKET = 4
+  TM_PAXOS_TICKET = 4,
+  TM_GOSSIP_BLOCK = 5
 };
 
 struct __attribute__((aligned(8))) TimerEnt {

@@ -76,6 +76,8 @@ struct KP {
   int32_t *is_leader, *has_voted, *m_value, *vote_s, *vote_f, *acv, *blockNum, *round;
   uint32_t *next_election, *next_heartbeat;
   int32_t *t_max, *command, *t_store, *ticket, *is_commit, *proposal;
+  // Gossip (BCSIM_GOSSIP): first-receipt flag per (gnode, sequence); origin tick count in round[]
+  uint8_t* gseen;
   // timers / ops
   TimerEnt* timers;
   uint32_t cap_timers;
@@ -1382,6 +1384,45 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   __syncthreads();
 }
 
+// ---------------------------------------------------------------------------
+// Gossip (BCSIM_GOSSIP, build extension for BASELINE configs[4], include/bcsim.h):
+// PBFT-style block flooding.  GS_BLOCK carries f0 = sequence, f1 = hop count.
+// Same order of schedule calls as oracle/bcsim_oracle.c gossip_tick/gossip_recv.
+enum { GS_BLOCK = 1 };
+
+__device__ bool gossip_mark(Ctx& c, int32_t seq) {  // false: already seen (or bad index)
+  const KP& p = *c.p;
+  if (seq < 0 || static_cast<uint32_t>(seq) >= p.pbft_seq_cap) {
+    set_err(p, BCSIM_E_INDEX);
+    return false;
+  }
+  uint8_t& f = AT(p.gseen, static_cast<size_t>(c.g) * p.pbft_seq_cap + seq,
+                  static_cast<uint64_t>(p.NT) * p.pbft_seq_cap);
+  if (f) return false;
+  f = 1;
+  return true;
+}
+
+// origin tick: SendBlock shape (pbft-node.cc:371-411) without the globals
+__device__ void gossip_tick(Ctx& c, int32_t& round) {
+  const KP& p = *c.p;
+  const int32_t seq = round++;
+  if (!gossip_mark(c, seq)) return;
+  ctx_trace(c, BCSIM_TR_GOSSIP_BLOCK, seq, 0, 0);
+  ctx_bcast(c, mkmsg(GS_BLOCK, seq, 0, 0, 1), false);
+  if (round < static_cast<int32_t>(p.pbft_rounds)) (void)ctx_timer(c, TM_GOSSIP_BLOCK, p.pbft_period);
+}
+
+__device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender) {
+  if (m.type != GS_BLOCK) {
+    ++c.wrong;
+    return;
+  }
+  if (!gossip_mark(c, m.f[0])) return;
+  ctx_trace(c, BCSIM_TR_GOSSIP_DELIVER, m.f[0], m.f[1] + 1, static_cast<int32_t>(sender));
+  ctx_bcast(c, mkmsg(GS_BLOCK, m.f[0], m.f[1] + 1, 0, 1), false);
+}
+
 template <int PROTO>
 __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                long long t_hi, long long cs, int final_win, int x_active) {
@@ -1436,6 +1477,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   Ctx c;
   RaftState rs{};
   PaxosState xs_{};
+  int32_t gs_round = 0;
   unsigned long long events = 0;
   bool start_pending = has_start, stop_pending = has_stop;
   if (PROTO != BCSIM_PBFT && tid == 0) {
@@ -1460,6 +1502,8 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
       rs.round = AT(p.round, g, p.NT);
       rs.next_election = AT(p.next_election, g, p.NT);
       rs.next_heartbeat = AT(p.next_heartbeat, g, p.NT);
+    } else if (PROTO == BCSIM_GOSSIP) {
+      gs_round = AT(p.round, g, p.NT);
     } else {
       xs_.t_max = AT(p.t_max, g, p.NT);
       xs_.command = AT(p.command, g, p.NT);
@@ -1576,6 +1620,8 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
           }
           if (PROTO == BCSIM_RAFT)
             raft_recv(c, rs, msg, q);
+          else if (PROTO == BCSIM_GOSSIP)
+            gossip_recv(c, msg, best.origin);
           else
             paxos_recv(c, xs_, msg, q);
         } else if (which == 1) {
@@ -1592,6 +1638,8 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
             } else if (te.kind == TM_RAFT_PROPOSAL) {  // setProposal :432-435
               rs.acv = 1;
             }
+          } else if (PROTO == BCSIM_GOSSIP) {
+            if (te.kind == TM_GOSSIP_BLOCK) gossip_tick(c, gs_round);
           } else {
             if (te.kind == TM_PAXOS_TICKET) paxos_ticket(c, xs_);
           }
@@ -1612,6 +1660,9 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
               const int32_t r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + i, p.cap_glibc);
               rs.next_election = ctx_timer(c, TM_RAFT_ELECTION, AT(p.raft_elec, r % 150, 150));
             }
+          } else if (PROTO == BCSIM_GOSSIP) {
+            gs_round = 0;
+            if (i == 0) (void)ctx_timer(c, TM_GOSSIP_BLOCK, p.pbft_period);
           } else {  // paxos-node.cc:58-139
             xs_.t_max = 0;
             xs_.command = 'e';
@@ -1697,6 +1748,8 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
       AT(p.round, g, p.NT) = rs.round;
       AT(p.next_election, g, p.NT) = rs.next_election;
       AT(p.next_heartbeat, g, p.NT) = rs.next_heartbeat;
+    } else if (PROTO == BCSIM_GOSSIP) {
+      AT(p.round, g, p.NT) = gs_round;
     } else {
       AT(p.t_max, g, p.NT) = xs_.t_max;
       AT(p.command, g, p.NT) = xs_.command;

@@ -34,7 +34,14 @@ extern "C" {
 
 /* ---- enums ---------------------------------------------------------------- */
 /* protocol: replaces the compile-time edit of network-helper.cc:11,17,28 */
-enum { BCSIM_PBFT = 0, BCSIM_RAFT = 1, BCSIM_PAXOS = 2 };
+enum { BCSIM_PBFT = 0, BCSIM_RAFT = 1, BCSIM_PAXOS = 2,
+       /* build extension for BASELINE configs[4] (the reference has no gossip):
+        * PBFT-style block flooding over an arbitrary CSR graph.  Node 0 (the
+        * initial PBFT leader, pbft-node.cc:103) ticks every pbft_timeout_s
+        * like SendBlock (pbft-node.cc:371-411) for pbft_rounds blocks and
+        * broadcasts each block (pbft-node.cc:349-368); every node relays a
+        * block to all its peers the first time it receives it. */
+       BCSIM_GOSSIP = 3 };
 /* app-level send delay model: getRandomDelay() pbft-node.cc:66-69,
  * raft-node.cc:63-66, paxos-node.cc:397-400 */
 enum { BCSIM_DELAY_FIXED = 0, BCSIM_DELAY_RANDOM = 1 };
@@ -123,7 +130,9 @@ enum {
   BCSIM_TR_RAFT_PROPOSAL = 14,/* raft-node.cc:342  a=round */
   BCSIM_TR_RAFT_STOP = 15,    /* raft-node.cc:122-123 a=blockNum b=round */
   BCSIM_TR_PAXOS_COMMIT = 20, /* paxos-node.cc:339 a=ticket */
-  BCSIM_TR_PAXOS_TICKET = 21  /* paxos-node.cc:518 a=ticket */
+  BCSIM_TR_PAXOS_TICKET = 21, /* paxos-node.cc:518 a=ticket */
+  BCSIM_TR_GOSSIP_BLOCK = 30, /* gossip origin tick  a=seq */
+  BCSIM_TR_GOSSIP_DELIVER = 31/* first receipt       a=seq b=hops c=sender */
 };
 
 typedef struct bcsim_trace_rec {
@@ -182,6 +191,16 @@ int bcsim_create(const bcsim_config* cfg, bcsim_sim** out);
 int bcsim_set_topology_csr(bcsim_sim* s, uint32_t n_nodes,
                            const uint32_t* row_ptr, const uint32_t* col_idx,
                            const int64_t* prop_ns);
+
+/* Topology builder (the reference hard-codes the full
+ * mesh of blockchain-simulator.cc:34-51): a simple, symmetric random
+ * d-regular graph on n nodes (configuration model paired by a seeded
+ * splitmix64 Fisher-Yates shuffle, self-loops and multi-edges removed by
+ * random double-edge swaps), rows sorted ascending like the reference's peer
+ * lists.  row_ptr has n+1 entries, col_idx n*d.  Host-only, deterministic in
+ * (n, d, seed).  Needs n*d even and d < n. */
+int bcsim_topology_random_regular(uint32_t n, uint32_t d, uint64_t seed,
+                                  uint32_t* row_ptr, uint32_t* col_idx);
 
 /* Replaces Simulator::Run (blockchain-simulator.cc:57): process every event
  * with t < t_until_ns (INT64_MAX: until quiescence or cfg->t_end_ns). */

@@ -180,7 +180,8 @@ enum {
   TM_RAFT_ELECTION = 1,
   TM_RAFT_HEARTBEAT = 2,
   TM_RAFT_PROPOSAL = 3,
-  TM_PAXOS_TICKET = 4
+  TM_PAXOS_TICKET = 4,
+  TM_GOSSIP_BLOCK = 5
 };
 
 typedef struct {
@@ -231,6 +232,7 @@ struct bcsim_oracle {
   uint32_t cur_rep;
   onode* nodes;          /* N, for the replica being run */
   int32_t *tx_val, *tx_pv, *tx_cv; /* N * seq_cap */
+  uint8_t* gseen;        /* GOSSIP: N * seq_cap first-receipt flags */
   int64_t* busy;         /* per edge */
   oheap heap;
   glibc_rng grng;
@@ -423,6 +425,8 @@ static int64_t app_delay(bcsim_oracle* o, uint32_t node) {
       return o->pbft_delay[r % 3];
     case BCSIM_RAFT:
       return o->raft_delay[r % 3];
+    case BCSIM_GOSSIP: /* PBFT-style: getRandomDelay pbft-node.cc:66-69 */
+      return o->pbft_delay[r % 3];
     default:
       return o->paxos_delay[r % 50];
   }
@@ -840,6 +844,53 @@ static void paxos_recv(bcsim_oracle* o, const oev* e, uint32_t i) {
 }
 
 /* ------------------------------------------------------------------------ */
+/* GOSSIP (BCSIM_GOSSIP, build extension for BASELINE configs[4]; see
+ * include/bcsim.h).  Message GS_BLOCK: f[0] = sequence, f[1] = hop count
+ * (raw integers, no intToChar), block-sized payload. */
+enum { GS_BLOCK = 1 };
+
+static int gossip_seq_ok(bcsim_oracle* o, int32_t seq) {
+  if (seq < 0 || (uint32_t)seq >= o->cfg.pbft_seq_cap) {
+    set_err(o, BCSIM_E_INDEX);
+    return 0;
+  }
+  return 1;
+}
+
+static void gossip_start(bcsim_oracle* o, uint32_t i) {
+  o->nodes[i].round = 0;
+  if (i == 0) sched_timer(o, i, TM_GOSSIP_BLOCK, o->pbft_period); /* like :155 */
+}
+
+/* origin tick: SendBlock shape (pbft-node.cc:371-411) without globals */
+static void gossip_tick(bcsim_oracle* o, const oev* e, uint32_t i) {
+  onode* nd = &o->nodes[i];
+  int32_t seq = nd->round++;
+  if (!gossip_seq_ok(o, seq)) return;
+  o->gseen[(size_t)i * o->cfg.pbft_seq_cap + seq] = 1;
+  emit(o, e, i, BCSIM_TR_GOSSIP_BLOCK, seq, 0, 0);
+  omsg m = mk(GS_BLOCK, seq, 0, 0, 1);
+  bcast(o, i, &m);
+  if (nd->round < (int32_t)o->cfg.pbft_rounds) sched_timer(o, i, TM_GOSSIP_BLOCK, o->pbft_period);
+}
+
+static void gossip_recv(bcsim_oracle* o, const oev* e, uint32_t i) {
+  const omsg* m = &e->m;
+  if (m->type != GS_BLOCK) {
+    o->cnt.wrong_msgs++;
+    return;
+  }
+  int32_t seq = m->f[0];
+  if (!gossip_seq_ok(o, seq)) return;
+  uint8_t* seen = &o->gseen[(size_t)i * o->cfg.pbft_seq_cap + seq];
+  if (*seen) return;
+  *seen = 1;
+  emit(o, e, i, BCSIM_TR_GOSSIP_DELIVER, seq, m->f[1] + 1, (int32_t)e->origin);
+  omsg r = mk(GS_BLOCK, seq, m->f[1] + 1, 0, 1);
+  bcast(o, i, &r);
+}
+
+/* ------------------------------------------------------------------------ */
 /* driver */
 static void exec_event(bcsim_oracle* o, const oev* e) {
   uint32_t i = e->target;
@@ -851,6 +902,8 @@ static void exec_event(bcsim_oracle* o, const oev* e) {
         pbft_start(o, i);
       else if (o->cfg.protocol == BCSIM_RAFT)
         raft_start(o, i);
+      else if (o->cfg.protocol == BCSIM_GOSSIP)
+        gossip_start(o, i);
       else
         paxos_start(o, i);
       break;
@@ -877,6 +930,9 @@ static void exec_event(bcsim_oracle* o, const oev* e) {
           break;
         case TM_PAXOS_TICKET:
           paxos_require_ticket(o, e, i);
+          break;
+        case TM_GOSSIP_BLOCK:
+          gossip_tick(o, e, i);
           break;
       }
       break;
@@ -915,6 +971,8 @@ static void exec_event(bcsim_oracle* o, const oev* e) {
         pbft_recv(o, e, i);
       else if (o->cfg.protocol == BCSIM_RAFT)
         raft_recv(o, e, i);
+      else if (o->cfg.protocol == BCSIM_GOSSIP)
+        gossip_recv(o, e, i);
       else
         paxos_recv(o, e, i);
       break;
@@ -1009,7 +1067,7 @@ int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
 
 int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
   if (!cfg || !out) return BCSIM_E_INVAL;
-  if (cfg->n_nodes < 2 || cfg->protocol > BCSIM_PAXOS || cfg->link_rate_bps == 0)
+  if (cfg->n_nodes < 2 || cfg->protocol > BCSIM_GOSSIP || cfg->link_rate_bps == 0)
     return BCSIM_E_INVAL;
   bcsim_oracle* o = (bcsim_oracle*)calloc(1, sizeof(bcsim_oracle));
   if (!o) return BCSIM_E_NOMEM;
@@ -1039,6 +1097,10 @@ int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
       pb = (uint32_t)(200 * num);
     }
     o->big_bytes = pb;
+  } else if (o->cfg.protocol == BCSIM_GOSSIP) { /* every message is a block */
+    uint32_t bb = o->cfg.pbft_block_bytes ? o->cfg.pbft_block_bytes : 50000;
+    o->small_bytes = bb;
+    o->big_bytes = bb;
   } else {
     o->small_bytes = 3;
     o->big_bytes = 3;
@@ -1071,12 +1133,15 @@ int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
       return BCSIM_E_NOMEM;
     }
   }
-  o->rep_now = (int64_t*)calloc(o->R, sizeof(int64_t));
-  int rc = build_full_mesh(o);
-  if (rc) {
-    bcsim_oracle_destroy(o);
-    return rc;
+  if (o->cfg.protocol == BCSIM_GOSSIP) {
+    o->gseen = (uint8_t*)calloc((size_t)o->N * o->cfg.pbft_seq_cap, 1);
+    if (!o->gseen) {
+      bcsim_oracle_destroy(o);
+      return BCSIM_E_NOMEM;
+    }
   }
+  o->rep_now = (int64_t*)calloc(o->R, sizeof(int64_t));
+  /* the full mesh is built at the first run unless a topology was set */
   *out = o;
   return BCSIM_OK;
 }
@@ -1094,6 +1159,7 @@ static void reset_replica(bcsim_oracle* o, uint32_t rep) {
     memset(o->tx_pv, 0, sz);
     memset(o->tx_cv, 0, sz);
   }
+  if (o->gseen) memset(o->gseen, 0, (size_t)o->N * o->cfg.pbft_seq_cap);
   memset(o->busy, 0, (size_t)o->row[o->N] * sizeof(int64_t));
   o->heap.n = 0;
   glibc_seed(&o->grng, (uint32_t)(o->cfg.seed + rep));
@@ -1130,6 +1196,13 @@ int bcsim_oracle_run(bcsim_oracle* o, int64_t t_until_ns) {
   int64_t lim = t_until_ns;
   if (o->cfg.t_end_ns > 0 && o->cfg.t_end_ns < lim) lim = o->cfg.t_end_ns;
   if (!o->started) {
+    if (!o->topo_set) {
+      int rc = (uint64_t)o->N * (o->N - 1) >= 0xFFFFFFFFull ? BCSIM_E_UNSUPPORTED : build_full_mesh(o);
+      if (rc) {
+        set_err(o, rc);
+        return rc;
+      }
+    }
     o->started = 1;
     reset_replica(o, 0);
   }
@@ -1207,6 +1280,7 @@ int bcsim_oracle_destroy(bcsim_oracle* o) {
   free(o->tx_val);
   free(o->tx_pv);
   free(o->tx_cv);
+  free(o->gseen);
   free(o->row);
   free(o->col);
   free(o->rev);

@@ -19,7 +19,7 @@ def _cfg(proto, n, **kw):
 
 
 def cases():
-    P, R, X = _abi.PBFT, _abi.RAFT, _abi.PAXOS
+    P, R, X, GS = _abi.PBFT, _abi.RAFT, _abi.PAXOS, _abi.GOSSIP
     F, J = _abi.DELAY_FIXED, _abi.DELAY_RANDOM
     G, K = _abi.RNG_GLIBC, _abi.RNG_COUNTER
     return {
@@ -49,7 +49,38 @@ def cases():
         "paxos16_jitter_rep4": _cfg(X, 16, delay_mode=J, rng_mode=K, seed=5, n_replicas=4),
         "pbft8_rep3_ctr": _cfg(P, 8, delay_mode=F, app_delay_ns=3_000_000, rng_mode=K, n_replicas=3,
                                pbft_rounds=20, pbft_block_bytes=2000),
+        # C5 shape (BASELINE configs[4]): PBFT-style gossip on random regular graphs (TOPOLOGY below)
+        "gossip64_d4_fixed": _cfg(GS, 64, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=6,
+                                  pbft_block_bytes=1000, stop_ns=-1),
+        "gossip200_d8_jitter_ctr": _cfg(GS, 200, delay_mode=J, rng_mode=K, seed=9, pbft_rounds=5,
+                                        pbft_block_bytes=1000, stop_ns=-1),
+        "gossip512_d8_blocks": _cfg(GS, 512, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=4,
+                                    stop_ns=-1, n_replicas=2),
+        "gossip24_mesh": _cfg(GS, 24, delay_mode=F, app_delay_ns=0, pbft_rounds=3, pbft_block_bytes=600,
+                              stop_ns=-1),
+        # the reference protocols on a non-mesh graph (CSR path without the mesh transpose)
+        "pbft32_d6_ctr": _cfg(P, 32, delay_mode=J, rng_mode=K, seed=4, pbft_rounds=6, pbft_block_bytes=1500),
+        "raft48_d6_ctr": _cfg(R, 48, delay_mode=J, rng_mode=K, seed=2, t_end_ns=3_000_000_000),
     }
+
+
+# non-mesh cases: name -> (n, degree, seed) of bcsim.random_regular
+TOPOLOGY = {
+    "gossip64_d4_fixed": (64, 4, 1),
+    "gossip200_d8_jitter_ctr": (200, 8, 5),
+    "gossip512_d8_blocks": (512, 8, 1),
+    "pbft32_d6_ctr": (32, 6, 3),
+    "raft48_d6_ctr": (48, 6, 8),
+}
+
+
+def topology(name):
+    """CSR (row_ptr, col_idx, None) of a case, or None for the full mesh."""
+    if name not in TOPOLOGY:
+        return None
+    import bcsim
+    row, col = bcsim.random_regular(*TOPOLOGY[name])
+    return row, col, None
 
 
 def compare(a, b):

@@ -1,14 +1,14 @@
 import sys, time, traceback
 import os; R=os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path[:0]=[R, os.path.join(R,'tests'), os.path.join(R,'blockchain-simulator_amd')]
 import oracle, bcsim
-from parity_cases import cases, compare
+from parity_cases import cases, compare, topology
 ok = 0
 sel = sys.argv[1:]
 for name, cfg in sorted(cases().items()):
     if sel and name not in sel: continue
     try:
-        t0 = time.time(); ref = oracle.run(cfg); t1 = time.time()
-        got = bcsim.run(cfg); t2 = time.time()
+        t0 = time.time(); topo = topology(name); ref = oracle.run(cfg, topology=topo); t1 = time.time()
+        got = bcsim.run(cfg, topology=topo); t2 = time.time()
         d = compare(ref, got)
         print(f"{name:24s} {'OK ' if d is None else 'BAD'} ntr={len(ref[0])}/{len(got[0])} deliv={ref[1]['delivered_total']}/{got[1]['delivered_total']} cpu={t1-t0:.2f}s gpu={t2-t1:.2f}s {d or ''}", flush=True)
         ok += d is None

@@ -25,7 +25,7 @@ def _worker(rank, world, port, names, transport, q):
     sys.path[:0] = [REPO, os.path.join(REPO, "tests"), os.path.join(REPO, "blockchain-simulator_amd")]
     import torch.distributed as dist
     import bcsim
-    from parity_cases import cases
+    from parity_cases import cases, topology
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -34,6 +34,9 @@ def _worker(rank, world, port, names, transport, q):
             cfg = allc[name]
             try:
                 with bcsim.Simulator(cfg) as s:
+                    topo = topology(name)
+                    if topo is not None:
+                        s.set_topology(*topo)
                     s.set_partition(dist, transport=transport)
                     s.run()
                     q.put((name, rank, s.trace(), s.counters(), None))
@@ -103,7 +106,7 @@ if __name__ == "__main__":
             print(f"{name:24s} EXC {err}", flush=True)
             bad += 1
             continue
-        ref = oracle.run(cases()[name])
+        ref = oracle.run(cases()[name], topology=topology(name))
         d = compare(ref, merged)
         print(f"{name:24s} {'OK ' if d is None else 'BAD'} world={world} deliv={ref[1]['delivered_total']}/"
               f"{merged[1]['delivered_total']} {d or ''}", flush=True)

@@ -3,7 +3,7 @@ counter-RNG jitter configs).  The oracle is the checker only."""
 import pytest
 
 import oracle
-from parity_cases import cases, compare
+from parity_cases import cases, compare, topology
 
 pytestmark = pytest.mark.gpu
 
@@ -14,8 +14,9 @@ CASES = cases()
 def test_engine_matches_oracle(name, engine_lib):
     import bcsim
     cfg = CASES[name]
-    ref = oracle.run(cfg)
-    got = bcsim.run(cfg)
+    topo = topology(name)
+    ref = oracle.run(cfg, topology=topo)
+    got = bcsim.run(cfg, topology=topo)
     assert ref[2]["error"] == 0
     diff = compare(ref, got)
     assert diff is None, f"{name}: {diff}"

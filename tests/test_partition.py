@@ -15,7 +15,7 @@ import pytest
 import torch.multiprocessing as mp
 
 import oracle
-from parity_cases import cases, compare
+from parity_cases import cases, compare, topology
 
 
 def _free_port():
@@ -95,7 +95,8 @@ def test_merge_matches_single_process_shape():
 # cases whose RNG is per node (counter) or absent: the glibc global stream of
 # Raft is a single-GPU configuration (bcsim_run returns E_UNSUPPORTED)
 PART_CASES = ["pbft16_fixed_100", "pbft5_odd", "pbft12_jitter_ctr", "pbft8_rep3_ctr", "pbft8_compat",
-              "raft16_jitter_ctr", "paxos8_fixed", "paxos32_jitter_ctr", "paxos16_jitter_rep4"]
+              "raft16_jitter_ctr", "paxos8_fixed", "paxos32_jitter_ctr", "paxos16_jitter_rep4",
+              "gossip64_d4_fixed", "gossip200_d8_jitter_ctr", "gossip24_mesh", "pbft32_d6_ctr"]
 
 
 @pytest.mark.gpu
@@ -108,7 +109,7 @@ def test_partitioned_matches_oracle(world, engine_lib):
     for name in PART_CASES:
         merged, err = res[name]
         assert err is None, f"{name} world={world}: {err}"
-        ref = oracle.run(allc[name])
+        ref = oracle.run(allc[name], topology=topology(name))
         d = compare(ref, merged)
         assert d is None, f"{name} world={world}: {d}"
 
