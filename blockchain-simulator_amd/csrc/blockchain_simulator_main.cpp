@@ -65,14 +65,14 @@ int main(int argc, char* argv[]) {
     if (a == "--nodes") N = std::atoi(val().c_str());
     else if (a == "--protocol") {
       std::string p = val();
-      protocol = p == "raft" ? BCSIM_RAFT : p == "paxos" ? BCSIM_PAXOS : BCSIM_PBFT;
+      protocol = p == "raft" ? BCSIM_RAFT : p == "paxos" ? BCSIM_PAXOS : p == "gossip" ? BCSIM_GOSSIP : BCSIM_PBFT;
     } else if (a == "--rate") rate = val();
     else if (a == "--delay") delay = val();
     else if (a == "--fixed-app-delay-ns") { fixed = true; app_delay = std::atoll(val().c_str()); }
     else if (a == "--rounds") rounds = std::atoi(val().c_str());
     else if (a == "--quiet") quiet = true;
     else {
-      std::fprintf(stderr, "usage: %s [--nodes N] [--protocol pbft|raft|paxos] [--rate 3Mbps] [--delay 3ms]\n"
+      std::fprintf(stderr, "usage: %s [--nodes N] [--protocol pbft|raft|paxos|gossip] [--rate 3Mbps] [--delay 3ms]\n"
                            "          [--fixed-app-delay-ns NS] [--rounds R] [--quiet]\n", argv[0]);
       return 2;
     }

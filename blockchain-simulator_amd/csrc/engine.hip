@@ -2397,37 +2397,43 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint8_t* lead = reinterpret_cast<uint8_t*>(smem);  // N flags
   __shared__ int32_t v_cur, nround0, n_alive, n_ticked;
-  __shared__ long long vk_t, vk_ts;
-  __shared__ uint32_t vk_o, vk_s, vk_tg;
+  __shared__ unsigned long long lmask[64];  // leader flags of the current 4096-node chunk, one bit per node
   const uint32_t rep = blockIdx.x, tid = threadIdx.x;
   const uint32_t N = p.N;
   const long long ts_tick = tk - p.pbft_period;
-  // v = latest v-log write before this tick in canonical order
-  if (tid == 0) {
-    v_cur = 1;
-    vk_t = LLONG_MIN;
-    vk_ts = LLONG_MIN;
-    vk_o = 0;
-    vk_s = 0;
-    vk_tg = 0;
+  // v = latest v-log write before this tick in canonical order: every thread
+  // keeps the latest of a strided share of the log (each VIEW_CHANGE delivery
+  // writes one entry, N-1 per view change), then a block tree-reduction
+  __shared__ uint32_t vbest[1024];
+  {
+    auto later = [](const VLog& a, const VLog& b) {  // key(a) > key(b)
+      if (a.t != b.t) return a.t > b.t;
+      if (a.ts != b.ts) return a.ts > b.ts;
+      if (a.origin != b.origin) return a.origin > b.origin;
+      if (a.sub != b.sub) return a.sub > b.sub;
+      return a.target > b.target;
+    };
     const uint32_t nv = min(*p.vlog_cnt, p.cap_vlog);
-    for (uint32_t k = 0; k < nv; ++k) {
+    uint32_t mine = UINT32_MAX;
+    for (uint32_t k = tid; k < nv; k += blockDim.x) {
       const VLog& e = AT(p.vlog, k, p.cap_vlog);
       if (e.rep != rep) continue;
-      // before the tick key (tk, ts_tick, 0, 0, 0)?
-      bool before = e.t < tk || (e.t == tk && e.ts < ts_tick);
-      if (!before) continue;
-      bool later = e.t > vk_t || (e.t == vk_t && (e.ts > vk_ts || (e.ts == vk_ts && (e.origin > vk_o ||
-                   (e.origin == vk_o && (e.sub > vk_s || (e.sub == vk_s && e.target > vk_tg)))))));
-      if (later) {
-        vk_t = e.t;
-        vk_ts = e.ts;
-        vk_o = e.origin;
-        vk_s = e.sub;
-        vk_tg = e.target;
-        v_cur = e.v;
-      }
+      if (!(e.t < tk || (e.t == tk && e.ts < ts_tick))) continue;  // before the tick key (tk, ts_tick, ...)
+      if (mine == UINT32_MAX || later(e, AT(p.vlog, mine, p.cap_vlog))) mine = k;
     }
+    vbest[tid] = mine;
+    __syncthreads();
+    for (uint32_t off = blockDim.x >> 1; off > 0; off >>= 1) {
+      if (tid < off) {
+        const uint32_t a = vbest[tid], b = vbest[tid + off];
+        if (b != UINT32_MAX && (a == UINT32_MAX || later(AT(p.vlog, b, p.cap_vlog), AT(p.vlog, a, p.cap_vlog))))
+          vbest[tid] = b;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    v_cur = vbest[0] == UINT32_MAX ? 1 : AT(p.vlog, vbest[0], p.cap_vlog).v;
     nround0 = AT(p.g_nround, rep, p.R);
     n_alive = 0;
     n_ticked = 0;
@@ -2441,75 +2447,85 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
       lead[i] = (AT(p.tick_alive, g, p.NT) && AT(p.leader, g, p.NT) == static_cast<int32_t>(i)) ? 1 : 0;
   }
   __syncthreads();
-  // leaders, serially in node order (rare: normally exactly one)
-  if (tid == 0) {
-    int32_t nround = nround0;
-    for (uint32_t i = 0; i < N; ++i) {
-      if (!lead[i]) continue;
-      const uint32_t g = rep * N + i;
-      if (i < p.nlo || i >= p.nlo + p.nloc) {
-        // another rank's leader: advance the replicated file-scope globals
-        // (n_round, n, glibc stream position, v) exactly as its owner does
-        ++nround;
-        AT(p.g_n, rep, p.R) = AT(p.g_n, rep, p.R) + 1;
-        if (p.pbft_view_change && p.rng_mode == BCSIM_RNG_GLIBC) {
-          const uint32_t pos = AT(p.glibc_pos, rep, p.R)++;
-          const int32_t r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + (pos % p.glibc_len), p.cap_glibc);
-          if (r % 100 == 5) v_cur += 1;
-        }
-        continue;
-      }
-      uint32_t sub = AT(p.sub, g, p.NT);
-      const uint32_t deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
-      const int32_t n_seq = AT(p.g_n, rep, p.R);
-      const Key tkey{tk, ts_tick, i, AT(p.tick_sub, g, p.NT)};
-      emit_trace(p, tkey, rep, i, BCSIM_TR_PBFT_BLOCK, n_seq, v_cur, 0);  // :387 leader log
-      // block = generateTX header '1', v, n, n (:79-95)
-      Msg blk = mkmsg(PB_PRE_PREPARE, enc_raw(p, v_cur), enc_raw(p, n_seq), enc_raw(p, n_seq), 1);
-      uint32_t nops = AT(p.n_ops, g, p.NT);
-      Op* ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
-      uint64_t draws = AT(p.draws, g, p.NT);
-      auto push_bcast = [&](const Msg& m) {
-        if (nops >= p.cap_ops) {
-          set_err(p, BCSIM_E_OVERFLOW);
-          return;
-        }
-        if (p.delay_mode == BCSIM_DELAY_FIXED) {
-          AT(ops, nops++, p.cap_ops) = mk_op(p, tk + p.app_delay, static_cast<uint32_t>(p.app_delay), i, sub, 0, m,
-                                             OP_BCAST, 0);
-        } else {
-          AT(ops, nops++, p.cap_ops) = mk_op(p, tk, 0, i, sub, static_cast<uint32_t>(draws), m, OP_BCAST_J, 0);
-          draws += deg;
-        }
-        sub += deg;
-      };
-      push_bcast(blk);
-      ++nround;
-      AT(p.g_n, rep, p.R) = n_seq + 1;
-      if (p.pbft_view_change) {  // rand() % 100 == 5 -> viewChange() :401-403
-        int32_t r;
-        if (p.rng_mode == BCSIM_RNG_GLIBC) {
-          const uint32_t pos = AT(p.glibc_pos, rep, p.R)++;
-          if (pos >= p.glibc_len) set_err(p, BCSIM_E_OVERFLOW);
-          r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + (pos % p.glibc_len), p.cap_glibc);
-        } else {
-          r = ctr_rand(p.seed, rep, i, draws++);
-        }
-        if (r % 100 == 5) {  // viewChange :293-303
-          const int32_t nl = (AT(p.leader, g, p.NT) + 1) % static_cast<int32_t>(N);
-          AT(p.leader, g, p.NT) = nl;
-          v_cur += 1;
-          emit_vlog(p, tkey, rep, i, v_cur);
-          push_bcast(mkmsg(PB_VIEW_CHANGE, enc_raw(p, v_cur), enc_raw(p, nl), 0, 0));
-        }
-      }
-      AT(p.sub, g, p.NT) = sub;
-      AT(p.n_ops, g, p.NT) = nops;
-      AT(p.draws, g, p.NT) = draws;
-      AT(p.node_onext, g, p.NT) = LLONG_MIN;
+  // leaders, serially in node order (rare: normally exactly one); a wave
+  // ballot packs 64 flags per word so thread 0 visits set bits only
+  int32_t nround = nround0;
+  for (uint32_t cb = 0; cb < N; cb += 4096) {
+    for (uint32_t j = tid; j < 4096; j += blockDim.x) {
+      const unsigned long long m = __ballot(cb + j < N && lead[cb + j]);
+      if ((j & 63) == 0) lmask[j >> 6] = m;
     }
-    AT(p.g_nround, rep, p.R) = nround;
+    __syncthreads();
+    if (tid == 0) {
+      for (uint32_t w = 0; w < 64; ++w)
+        for (unsigned long long mw = lmask[w]; mw; mw &= mw - 1) {
+          const uint32_t i = cb + 64 * w + static_cast<uint32_t>(__builtin_ctzll(mw));
+          const uint32_t g = rep * N + i;
+          if (i < p.nlo || i >= p.nlo + p.nloc) {
+            // another rank's leader: advance the replicated file-scope globals
+            // (n_round, n, glibc stream position, v) exactly as its owner does
+            ++nround;
+            AT(p.g_n, rep, p.R) = AT(p.g_n, rep, p.R) + 1;
+            if (p.pbft_view_change && p.rng_mode == BCSIM_RNG_GLIBC) {
+              const uint32_t pos = AT(p.glibc_pos, rep, p.R)++;
+              const int32_t r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + (pos % p.glibc_len), p.cap_glibc);
+              if (r % 100 == 5) v_cur += 1;
+            }
+            continue;
+          }
+          uint32_t sub = AT(p.sub, g, p.NT);
+          const uint32_t deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
+          const int32_t n_seq = AT(p.g_n, rep, p.R);
+          const Key tkey{tk, ts_tick, i, AT(p.tick_sub, g, p.NT)};
+          emit_trace(p, tkey, rep, i, BCSIM_TR_PBFT_BLOCK, n_seq, v_cur, 0);  // :387 leader log
+          // block = generateTX header '1', v, n, n (:79-95)
+          Msg blk = mkmsg(PB_PRE_PREPARE, enc_raw(p, v_cur), enc_raw(p, n_seq), enc_raw(p, n_seq), 1);
+          uint32_t nops = AT(p.n_ops, g, p.NT);
+          Op* ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
+          uint64_t draws = AT(p.draws, g, p.NT);
+          auto push_bcast = [&](const Msg& m) {
+            if (nops >= p.cap_ops) {
+              set_err(p, BCSIM_E_OVERFLOW);
+              return;
+            }
+            if (p.delay_mode == BCSIM_DELAY_FIXED) {
+              AT(ops, nops++, p.cap_ops) = mk_op(p, tk + p.app_delay, static_cast<uint32_t>(p.app_delay), i, sub, 0, m,
+                                                 OP_BCAST, 0);
+            } else {
+              AT(ops, nops++, p.cap_ops) = mk_op(p, tk, 0, i, sub, static_cast<uint32_t>(draws), m, OP_BCAST_J, 0);
+              draws += deg;
+            }
+            sub += deg;
+          };
+          push_bcast(blk);
+          ++nround;
+          AT(p.g_n, rep, p.R) = n_seq + 1;
+          if (p.pbft_view_change) {  // rand() % 100 == 5 -> viewChange() :401-403
+            int32_t r;
+            if (p.rng_mode == BCSIM_RNG_GLIBC) {
+              const uint32_t pos = AT(p.glibc_pos, rep, p.R)++;
+              if (pos >= p.glibc_len) set_err(p, BCSIM_E_OVERFLOW);
+              r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + (pos % p.glibc_len), p.cap_glibc);
+            } else {
+              r = ctr_rand(p.seed, rep, i, draws++);
+            }
+            if (r % 100 == 5) {  // viewChange :293-303
+              const int32_t nl = (AT(p.leader, g, p.NT) + 1) % static_cast<int32_t>(N);
+              AT(p.leader, g, p.NT) = nl;
+              v_cur += 1;
+              emit_vlog(p, tkey, rep, i, v_cur);
+              push_bcast(mkmsg(PB_VIEW_CHANGE, enc_raw(p, v_cur), enc_raw(p, nl), 0, 0));
+            }
+          }
+          AT(p.sub, g, p.NT) = sub;
+          AT(p.n_ops, g, p.NT) = nops;
+          AT(p.draws, g, p.NT) = draws;
+          AT(p.node_onext, g, p.NT) = LLONG_MIN;
+        }
+    }
+    __syncthreads();
   }
+  if (tid == 0) AT(p.g_nround, rep, p.R) = nround;
   __syncthreads();
   // every alive node: n_round seen = n_round0 + #leaders with id <= i
   // (prefix over the leader flags), reschedule, stop check.

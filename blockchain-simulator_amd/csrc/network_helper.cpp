@@ -184,6 +184,13 @@ std::string FormatTraceLine(const bcsim_trace_rec& r) {
     case BCSIM_TR_PAXOS_TICKET:
       std::snprintf(buf, sizeof buf, "node%u require_ticket %d at %.9fs", r.node, r.a, t);
       break;
+    case BCSIM_TR_GOSSIP_BLOCK:
+      std::snprintf(buf, sizeof buf, "node%u gossips block %d at %.9fs", r.node, r.a, t);
+      break;
+    case BCSIM_TR_GOSSIP_DELIVER:
+      std::snprintf(buf, sizeof buf, "node%u received block %d from node%d after %d hops at %.9fs", r.node, r.a, r.c,
+                    r.b, t);
+      break;
     default:
       std::snprintf(buf, sizeof buf, "kind %u node %u t=%.9f a=%d b=%d c=%d", r.kind, r.node, t, r.a, r.b, r.c);
   }
