@@ -355,6 +355,14 @@ static int setup_device(Sim& s) {
   }
   s.bs_scan = static_cast<uint32_t>(std::min<uint64_t>(1024, std::max<uint64_t>(64, next_pow2(s.deg_max + 1))));
   s.bs_link = s.bs_scan;
+  // workgroup size caps (powers of two >= 64; tuning knobs, results do not depend on them)
+  auto bs_cap = [](const char* name, uint32_t bs) {
+    const char* v = std::getenv(name);
+    const uint32_t cap = v ? static_cast<uint32_t>(std::atoi(v)) : 0;
+    return (cap >= 64 && cap <= 1024 && (cap & (cap - 1)) == 0) ? std::min(bs, cap) : bs;
+  };
+  s.bs_scan = bs_cap("BCSIM_BS_SCAN", s.bs_scan);
+  s.bs_link = bs_cap("BCSIM_BS_LINK", s.bs_link);
   // inbox ring: one 16-byte slot per (bucket, replica, edge); as many buckets
   // as ~8 GiB allows, 8..64
   // full mesh (blockchain-simulator.cc:34-51): records are staged sender-major
