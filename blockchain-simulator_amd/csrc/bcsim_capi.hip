@@ -522,7 +522,10 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.trace, p.cap_trace)) || (rc = dalloc(s, &p.vlog, p.cap_vlog)) ||
       (rc = dalloc(s, &p.dreq, p.cap_dreq)))
     return rc;
-  if ((rc = dalloc(s, &p.counters, static_cast<size_t>(s.R) * CNT_N)) || (rc = dalloc(s, &p.kstat, 8)))
+  p.cnt_stripes = 64;  // per-workgroup counter stripes (engine.hip cnt_stripe), <= 32 MiB in total
+  while (p.cnt_stripes > 1 && static_cast<uint64_t>(p.cnt_stripes) * s.R * CNT_N * 8 > (32ull << 20)) p.cnt_stripes >>= 1;
+  if ((rc = dalloc(s, &p.counters, static_cast<size_t>(p.cnt_stripes) * s.R * CNT_N)) ||
+      (rc = dalloc(s, &p.kstat, 8 * kKstStripes)))
     return rc;
   if ((rc = dalloc(s, &p.node_tnext, NT)) || (rc = dalloc(s, &p.node_onext, NT))) return rc;
   // control block: Ctl + bucket counts + extras counts, contiguous for one read-back
@@ -593,8 +596,8 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemset(p.seg_cnt, 0, NT * 4));
   HIPCHK(hipMemset(p.seg_off, 0, (NT + 1) * 4));
   HIPCHK(hipMemset(p.cursor, 0, NT * 4));
-  HIPCHK(hipMemset(p.counters, 0, static_cast<size_t>(s.R) * CNT_N * 8));
-  HIPCHK(hipMemset(p.kstat, 0, 64));
+  HIPCHK(hipMemset(p.counters, 0, static_cast<size_t>(p.cnt_stripes) * s.R * CNT_N * 8));
+  HIPCHK(hipMemset(p.kstat, 0, 64 * kKstStripes));
 #ifdef BCSIM_CHECKED
   {
     const char* tv = std::getenv("BCSIM_TRAIL");
@@ -1064,8 +1067,18 @@ static int fetch_trace(Sim& s) {
 static int read_counters(Sim& s, bcsim_counters* out) {
   std::memset(out, 0, sizeof *out);
   if (!s.started) return BCSIM_OK;
-  std::vector<unsigned long long> c(static_cast<size_t>(s.R) * CNT_N);
-  HIPCHK(hipMemcpy(c.data(), s.kp.counters, c.size() * 8, hipMemcpyDeviceToHost));
+  const size_t per = static_cast<size_t>(s.R) * CNT_N;
+  std::vector<unsigned long long> cs(per * s.kp.cnt_stripes), c(per, 0);
+  HIPCHK(hipMemcpy(cs.data(), s.kp.counters, cs.size() * 8, hipMemcpyDeviceToHost));
+  for (uint32_t st = 0; st < s.kp.cnt_stripes; ++st)
+    for (size_t k = 0; k < per; ++k) {
+      const unsigned long long v = cs[st * per + k];
+      if (k % CNT_N == CNT_TLAST)
+        c[k] = st == 0 ? v : static_cast<unsigned long long>(std::max<long long>(static_cast<long long>(c[k]),
+                                                                                  static_cast<long long>(v)));
+      else
+        c[k] += v;
+    }
   Ctl ctl;
   HIPCHK(hipMemcpy(&ctl, s.ctl_d, sizeof ctl, hipMemcpyDeviceToHost));
   for (uint32_t r = 0; r < s.R; ++r) {
@@ -1270,8 +1283,11 @@ int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, u
   Sim& s = *h->s;
   unsigned long long ks[8] = {0};
   if (s.started) {
-    hipError_t e = hipMemcpy(ks, s.kp.kstat, sizeof ks, hipMemcpyDeviceToHost);
+    unsigned long long kss[8 * bcsim::kKstStripes];
+    hipError_t e = hipMemcpy(kss, s.kp.kstat, sizeof kss, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return BCSIM_E_HIP;
+    for (uint32_t st = 0; st < bcsim::kKstStripes; ++st)
+      for (int k = 0; k < 8; ++k) ks[k] += kss[8 * st + k];
   }
   for (int k = 0; k < 4; ++k) {
     if (us_out4) us_out4[k] = s.us[k];
@@ -1356,7 +1372,7 @@ int bcsim_reset_kernel_stats(bcsim_sim* h) {
     s.us[k] = 0;
     s.launches[k] = 0;
   }
-  if (s.started && hipMemset(s.kp.kstat, 0, 64) != hipSuccess) return BCSIM_E_HIP;
+  if (s.started && hipMemset(s.kp.kstat, 0, 64 * bcsim::kKstStripes) != hipSuccess) return BCSIM_E_HIP;
   return BCSIM_OK;
 }
 

@@ -45,6 +45,7 @@ namespace bcsim {
 
 // ---------------------------------------------------------------------------
 // kernel parameter block (device-resident, one per simulation)
+constexpr uint32_t kKstStripes = 64;  // kstat[kKstStripes][8]: per-workgroup stripes, summed on the host
 struct KP {
   uint32_t N, R, NT, E;
   uint32_t protocol, delay_mode, rng_mode, encoding, echo;
@@ -105,7 +106,7 @@ struct KP {
   uint8_t* tdirty;       // [B][R][nt][nt] outbox tile holds records (full mesh only)
   uint32_t mesh, n_tiles;  // full-mesh topology: records go through the tiled transpose
   uint8_t* iflag;        // [B][NT] node has records in the bucket
-  uint32_t* bucket_cnt;  // [B] records in the bucket (slots + extras)
+  uint32_t* bucket_cnt;  // [B] nonzero = the bucket holds records (slots + extras); see mark_busy
   uint32_t* x_cnt;       // [B] extras in the bucket
   uint32_t n_buckets;
   XRec* xbuf;            // [B][cap_x]
@@ -133,6 +134,7 @@ struct KP {
   uint32_t glibc_len;
   uint32_t* glibc_pos;  // per replica
   unsigned long long* counters;  // R * CNT_N
+  uint32_t cnt_stripes;  // counters[cnt_stripes][R][CNT_N]: workgroup b adds to stripe b % cnt_stripes
   unsigned long long* kstat;     // link / scan algorithmic counters (KST_*)
   int32_t* err;
   int32_t* dbg;  // first error's source line
@@ -307,6 +309,19 @@ __device__ inline Op mk_op(const KP& p, int64_t t, uint32_t dt, uint32_t origin,
   o.type = static_cast<uint8_t>(m.type);
   o.kind_flags = static_cast<uint8_t>(kind | ((flags | (m.big ? OPF_BIG : 0)) << 2));
   return o;
+}
+
+// Contended device atomics on one word serialise in L2: every workgroup of a
+// launch adds its block-reduced counters to its own stripe instead, summed on the host.
+__device__ inline unsigned long long* cnt_stripe(const KP& p, uint32_t rep) {
+  const size_t stripe = blockIdx.x & (p.cnt_stripes - 1);
+  return &AT(p.counters, (stripe * p.R + rep) * CNT_N, static_cast<uint64_t>(p.cnt_stripes) * p.R * CNT_N);
+}
+__device__ inline unsigned long long* kst_stripe(const KP& p) { return p.kstat + 8 * (blockIdx.x & (kKstStripes - 1)); }
+// bucket_cnt is only tested for nonzero: workgroups set it once instead of all adding to it
+__device__ inline void mark_busy(uint32_t* w) {
+  if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    __hip_atomic_store(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ inline void emit_trace(const KP& p, const Key& k, uint32_t rep, uint32_t node, uint32_t kind,
@@ -582,7 +597,7 @@ __global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) 
       AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
     }
     AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(p.n_buckets) * p.NT) = 1;
-    atomicAdd(&p.bucket_cnt[b], 1u);
+    mark_busy(&p.bucket_cnt[b]);
     o.cell = -1;
   } else {
     atomicMin(&p.scal[1], o.cell);
@@ -1413,14 +1428,47 @@ __device__ void gossip_tick(Ctx& c, int32_t& round) {
   if (round < static_cast<int32_t>(p.pbft_rounds)) (void)ctx_timer(c, TM_GOSSIP_BLOCK, p.pbft_period);
 }
 
-__device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender) {
+// `first`: this arrival is the node's first receipt of the block (computed for the whole
+// window by gossip_first_flags, which also marks the blocks seen)
+__device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender, bool first) {
+  const KP& p = *c.p;
   if (m.type != GS_BLOCK) {
     ++c.wrong;
     return;
   }
-  if (!gossip_mark(c, m.f[0])) return;
+  if (m.f[0] < 0 || static_cast<uint32_t>(m.f[0]) >= p.pbft_seq_cap) {
+    set_err(p, BCSIM_E_INDEX);
+    return;
+  }
+  if (!first) return;
   ctx_trace(c, BCSIM_TR_GOSSIP_DELIVER, m.f[0], m.f[1] + 1, static_cast<int32_t>(sender));
   ctx_bcast(c, mkmsg(GS_BLOCK, m.f[0], m.f[1] + 1, 0, 1), false);
+}
+
+// Data-parallel part of the gossip handler: lane r decides whether staged arrival r (key
+// order) is its node's first receipt of that block -- not seen in an earlier window, and no
+// earlier arrival of this window carries the same sequence -- writes the flag to acls[r], and
+// the first receipts are marked seen.  The lane-0 event loop then reads the flags from LDS.
+__device__ void gossip_first_flags(const KP& p, uint32_t g, uint32_t n, const uint32_t* asec, const Rec* arec,
+                                   uint32_t* acls) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t r = tid; r < n; r += blockDim.x) {
+    const Rec& rc = arec[asec[r] & kRidxMask];
+    const int32_t seq = rc.f0;
+    bool first = rc.type == GS_BLOCK && seq >= 0 && static_cast<uint32_t>(seq) < p.pbft_seq_cap &&
+                 AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + seq,
+                    static_cast<uint64_t>(p.NT) * p.pbft_seq_cap) == 0;
+    for (uint32_t r2 = 0; first && r2 < r; ++r2) {
+      const Rec& o = arec[asec[r2] & kRidxMask];
+      if (o.type == GS_BLOCK && o.f0 == seq) first = false;
+    }
+    acls[r] = first ? 1u : 0u;
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += blockDim.x)
+    if (acls[r])
+      AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + arec[asec[r] & kRidxMask].f0,
+         static_cast<uint64_t>(p.NT) * p.pbft_seq_cap) = 1;
 }
 
 template <int PROTO>
@@ -1554,6 +1602,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     sort_window(S, n, akey, asec);
     SPH(2);
 
+    if (PROTO == BCSIM_GOSSIP) gossip_first_flags(p, g, n, asec, arec, acls);
     if (PROTO == BCSIM_PBFT) {
       pbft_window(p, S, g, rep, i, e0, deg, n, n_main, cell, cs, t_lo, akey, asec, arec, acls);
       events += (tid == 0) ? n : 0;
@@ -1572,7 +1621,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
           const uint32_t sec = asec[ai];
           rec = arec[sec & kRidxMask];
           q = e0 + (sec >> kRidxBits);
-          const uint32_t dt = static_cast<uint32_t>(AT(p.prop_in, q, p.E) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
+          const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
           best.t = cs + rec.t_off;
           best.ts = best.t - dt;
           best.origin = AT(p.col, q, p.E);
@@ -1611,7 +1660,14 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
         if (which == 0) {
           ++ai;
           const Msg msg = rec_msg(rec);
-          if (rec.type < BCSIM_MSG_TYPES) ++c.deliv[rec.type];
+          // gossip keeps the per-type counts in LDS so that Ctx has no dynamically indexed
+          // member and stays in registers (Raft/Paxos: see DESIGN.md §8 on the miscompile)
+          if (rec.type < BCSIM_MSG_TYPES) {
+            if (PROTO == BCSIM_GOSSIP)
+              ++S.deliv[rec.type];
+            else
+              ++c.deliv[rec.type];
+          }
           if (p.echo) {  // socket->SendTo(packet, 0, from): reverse-link occupancy
             const Op eo = mk_op(p, best.t, static_cast<uint32_t>(best.t - best.ts), best.origin, rec.sub, q, msg,
                                 OP_ECHO, 0);
@@ -1621,7 +1677,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
           if (PROTO == BCSIM_RAFT)
             raft_recv(c, rs, msg, q);
           else if (PROTO == BCSIM_GOSSIP)
-            gossip_recv(c, msg, best.origin);
+            gossip_recv(c, msg, best.origin, acls[ai - 1] != 0);
           else
             paxos_recv(c, xs_, msg, q);
         } else if (which == 1) {
@@ -1698,12 +1754,12 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   // slot ops make their cells busy (bucket counts) and flag this node for k_link
   if (tid < kOpRing && S.ocnt[tid]) {
     const long long dc = cell + tid;
-    atomicAdd(&p.bucket_cnt[dc % p.n_buckets], S.ocnt[tid]);
+    mark_busy(&p.bucket_cnt[dc % p.n_buckets]);
     AT(p.sflag, (dc % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 1;
   }
 
   // ---- write back ----
-  unsigned long long* cnt = &AT(p.counters, static_cast<size_t>(rep) * CNT_N, static_cast<uint64_t>(p.R) * CNT_N);
+  unsigned long long* cnt = cnt_stripe(p, rep);
   if (tid != 0) return;
   if (p.wgs) {
     SPH(7);
@@ -1726,7 +1782,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     if (tot) {
       atomicAdd(&cnt[CNT_DELIV_TOTAL], tot);
       if (p.echo) atomicAdd(&cnt[CNT_ECHOES], tot);
-      atomicAdd(&p.kstat[KST_DELIV], tot);
+      atomicAdd(&kst_stripe(p)[KST_DELIV], tot);
     }
     if (S.wrong) atomicAdd(&cnt[CNT_WRONG], S.wrong);
     if (events) atomicAdd(&cnt[CNT_EVENTS], events);
@@ -1761,13 +1817,14 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
       AT(p.vote_f, g, p.NT) = xs_.vf;
     }
     for (int k = 0; k < BCSIM_MSG_TYPES; ++k)
-      if (c.deliv[k]) {
-        atomicAdd(&cnt[CNT_DELIV + k], c.deliv[k]);
-        tot += c.deliv[k];
+      if (PROTO == BCSIM_GOSSIP ? S.deliv[k] : c.deliv[k]) {
+        const unsigned long long dk = PROTO == BCSIM_GOSSIP ? S.deliv[k] : c.deliv[k];
+        atomicAdd(&cnt[CNT_DELIV + k], dk);
+        tot += dk;
       }
     if (tot) {
       atomicAdd(&cnt[CNT_DELIV_TOTAL], tot);
-      atomicAdd(&p.kstat[KST_DELIV], tot);
+      atomicAdd(&kst_stripe(p)[KST_DELIV], tot);
     }
     if (c.echoes) atomicAdd(&cnt[CNT_ECHOES], c.echoes);
     if (c.wrong) atomicAdd(&cnt[CNT_WRONG], c.wrong);
@@ -1874,7 +1931,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   int64_t* busy = p.busy + eb0;
   int64_t* lastc = p.lastc + eb0;
   const int64_t* prop = p.prop + e0;
-  unsigned long long* cnt = &AT(p.counters, static_cast<size_t>(rep) * CNT_N, static_cast<uint64_t>(p.R) * CNT_N);
+  unsigned long long* cnt = cnt_stripe(p, rep);
   const uint32_t B = p.n_buckets;
 
   // ---- 0. expand jitter broadcasts into per-edge SEND ops ----
@@ -2245,14 +2302,14 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   if (tid == 0) {
     if (t1.x) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(t1.x));
     if (t1.y) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(t1.y));
-    if (t1.z) atomicAdd(&p.kstat[KST_REC], static_cast<unsigned long long>(t1.z));
-    if (t1.w) atomicAdd(&p.kstat[KST_OPS], static_cast<unsigned long long>(t1.w));
-    if (t2.x) atomicAdd(&p.kstat[KST_EDGES], static_cast<unsigned long long>(t2.x));
-    if (t2.y) atomicAdd(&p.kstat[KST_ECHO], static_cast<unsigned long long>(t2.y));
+    if (t1.z) atomicAdd(&kst_stripe(p)[KST_REC], static_cast<unsigned long long>(t1.z));
+    if (t1.w) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(t1.w));
+    if (t2.x) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(t2.x));
+    if (t2.y) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(t2.y));
   }
   __syncthreads();
   for (uint32_t k = tid; k < B; k += blockDim.x)
-    if (L.lcnt[k]) atomicAdd(&p.bucket_cnt[k], L.lcnt[k]);
+    if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
   if (p.wgt && tid == 0) {
     p.wgt[8ull * g] = wg_t0;
     p.wgt[8ull * g + 1] = __builtin_amdgcn_s_memrealtime();
@@ -2268,7 +2325,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     if (rx && final_win) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
     AT(p.n_ops, g, p.NT) = L.n_keep;
     AT(p.node_onext, g, p.NT) = L.omin;
-    atomicAdd(&p.kstat[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
+    atomicAdd(&kst_stripe(p)[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
   }
 }
 
@@ -2325,7 +2382,7 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
   }
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < B; q += blockDim.x)
-    if (lb[q]) atomicAdd(&p.bucket_cnt[q], lb[q]);
+    if (lb[q]) mark_busy(&p.bucket_cnt[q]);
   if (threadIdx.x == 0 && ovmin != LLONG_MAX) atomicMin(&p.scal[1], ovmin);
 }
 
@@ -2568,7 +2625,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
   if (tid == 0) {
     atomicAdd(reinterpret_cast<unsigned long long*>(&p.scal[2]), static_cast<unsigned long long>(n_alive));
     if (n_ticked > 0) {
-      unsigned long long* cnt = &AT(p.counters, static_cast<size_t>(rep) * CNT_N, static_cast<uint64_t>(p.R) * CNT_N);
+      unsigned long long* cnt = cnt_stripe(p, rep);
       atomicAdd(&cnt[CNT_EVENTS], static_cast<unsigned long long>(n_ticked));
       atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), tk);
     }
