@@ -324,9 +324,9 @@ __device__ inline void mark_busy(uint32_t* w) {
     __hip_atomic_store(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ inline void emit_trace(const KP& p, const Key& k, uint32_t rep, uint32_t node, uint32_t kind,
-                                  int32_t a, int32_t b, int32_t c) {
-  const uint32_t pos = atomicAdd(p.trace_cnt, 1u);
+// trace record at a reserved position (emit_trace reserves one; gossip reserves a window's worth)
+__device__ inline void put_trace(const KP& p, uint32_t pos, const Key& k, uint32_t rep, uint32_t node, uint32_t kind,
+                                 int32_t a, int32_t b, int32_t c) {
   if (pos >= p.cap_trace) {
     set_err(p, BCSIM_E_OVERFLOW);
     return;
@@ -343,6 +343,11 @@ __device__ inline void emit_trace(const KP& p, const Key& k, uint32_t rep, uint3
   r.b = b;
   r.c = c;
   AT(p.trace, pos, p.cap_trace) = r;
+}
+
+__device__ inline void emit_trace(const KP& p, const Key& k, uint32_t rep, uint32_t node, uint32_t kind,
+                                  int32_t a, int32_t b, int32_t c) {
+  put_trace(p, atomicAdd(p.trace_cnt, 1u), k, rep, node, kind, a, b, c);
 }
 
 __device__ inline void emit_vlog(const KP& p, const Key& k, uint32_t rep, uint32_t node, int32_t v) {
@@ -959,6 +964,7 @@ struct ScanShared {
   unsigned long long wrong;
   long long tmax;
   uint32_t ocnt[kOpRing];  // reply-slot ops written, by due cell - cell
+  uint32_t tr_n, tr_pos;   // gossip: first receipts of the window, next reserved trace position
   unsigned long long ph[8];  // BCSIM_WGT phase clock (debug)
 };
 #define SPH(k)                                                         \
@@ -1430,7 +1436,7 @@ __device__ void gossip_tick(Ctx& c, int32_t& round) {
 
 // `first`: this arrival is the node's first receipt of the block (computed for the whole
 // window by gossip_first_flags, which also marks the blocks seen)
-__device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender, bool first) {
+__device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender, bool first, uint32_t& tr_pos) {
   const KP& p = *c.p;
   if (m.type != GS_BLOCK) {
     ++c.wrong;
@@ -1441,7 +1447,8 @@ __device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender, bool first) {
     return;
   }
   if (!first) return;
-  ctx_trace(c, BCSIM_TR_GOSSIP_DELIVER, m.f[0], m.f[1] + 1, static_cast<int32_t>(sender));
+  TRAIL(c);
+  put_trace(p, tr_pos++, c.cur, c.rep, c.i, BCSIM_TR_GOSSIP_DELIVER, m.f[0], m.f[1] + 1, static_cast<int32_t>(sender));
   ctx_bcast(c, mkmsg(GS_BLOCK, m.f[0], m.f[1] + 1, 0, 1), false);
 }
 
@@ -1449,9 +1456,11 @@ __device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender, bool first) {
 // order) is its node's first receipt of that block -- not seen in an earlier window, and no
 // earlier arrival of this window carries the same sequence -- writes the flag to acls[r], and
 // the first receipts are marked seen.  The lane-0 event loop then reads the flags from LDS.
-__device__ void gossip_first_flags(const KP& p, uint32_t g, uint32_t n, const uint32_t* asec, const Rec* arec,
-                                   uint32_t* acls) {
+__device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint32_t n, const uint32_t* asec,
+                                   const Rec* arec, uint32_t* acls) {
   const uint32_t tid = threadIdx.x;
+  if (tid == 0) S.tr_n = 0;
+  __syncthreads();
   for (uint32_t r = tid; r < n; r += blockDim.x) {
     const Rec& rc = arec[asec[r] & kRidxMask];
     const int32_t seq = rc.f0;
@@ -1463,8 +1472,11 @@ __device__ void gossip_first_flags(const KP& p, uint32_t g, uint32_t n, const ui
       if (o.type == GS_BLOCK && o.f0 == seq) first = false;
     }
     acls[r] = first ? 1u : 0u;
+    if (first) atomicAdd(&S.tr_n, 1u);
   }
   __syncthreads();
+  // one trace reservation per window for all its first receipts (no per-record global atomic)
+  if (tid == 0) S.tr_pos = S.tr_n ? atomicAdd(p.trace_cnt, S.tr_n) : 0u;
   for (uint32_t r = tid; r < n; r += blockDim.x)
     if (acls[r])
       AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + arec[asec[r] & kRidxMask].f0,
@@ -1602,7 +1614,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     sort_window(S, n, akey, asec);
     SPH(2);
 
-    if (PROTO == BCSIM_GOSSIP) gossip_first_flags(p, g, n, asec, arec, acls);
+    if (PROTO == BCSIM_GOSSIP) gossip_first_flags(p, S, g, n, asec, arec, acls);
     if (PROTO == BCSIM_PBFT) {
       pbft_window(p, S, g, rep, i, e0, deg, n, n_main, cell, cs, t_lo, akey, asec, arec, acls);
       events += (tid == 0) ? n : 0;
@@ -1677,7 +1689,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
           if (PROTO == BCSIM_RAFT)
             raft_recv(c, rs, msg, q);
           else if (PROTO == BCSIM_GOSSIP)
-            gossip_recv(c, msg, best.origin, acls[ai - 1] != 0);
+            gossip_recv(c, msg, best.origin, acls[ai - 1] != 0, S.tr_pos);
           else
             paxos_recv(c, xs_, msg, q);
         } else if (which == 1) {
