@@ -1866,6 +1866,7 @@ __device__ inline bool op_key_less(const Op& a, uint32_t sa, const Op& b, uint32
 struct LinkShared {
   uint32_t n_bc, n_keep;
   uint32_t bc[kBcastCap];
+  Op bco[kBcastCap];         // the due broadcasts in key order (LDS copies: every lane reads them per edge)
   uint32_t lcnt[kMaxBuckets];
   uint4 wsum[kMaxWaves];
   uint32_t wcnt[kMaxWaves];
@@ -2037,6 +2038,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       }
       L.bc[b2] = x;
     }
+    for (uint32_t a = 0; a < L.n_bc; ++a) L.bco[a] = ops[L.bc[a]];
   }
   for (uint32_t k = tid; k < n; k += blockDim.x) {
     const Op& o = ops[k];
@@ -2059,6 +2061,14 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     const uint32_t e = e0 + le;
     // full mesh: peers ascending without self (validated on the host)
     const uint32_t s = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e, p.E);
+    // link state of an edge that is certainly used: issued before the inbox / reply-slot
+    // loads below so that the three HBM reads overlap instead of forming a chain
+    const bool pre = n_bc != 0 || ee > eb;
+    int64_t bu = 0, lc = 0;
+    if (pre) {
+      bu = busy[le];
+      lc = lastc[le];
+    }
     // implicit echo: this node's main inbox record of in-slot le, delivered in
     // [t_lo, t_hi), goes back out on out-edge le (the same peer); release the slot
     bool he = false;
@@ -2104,8 +2114,10 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       eidx[b2] = x;
     }
     ++st_edges;
-    int64_t bu = busy[le];
-    int64_t lc = lastc[le];
+    if (!pre) {
+      bu = busy[le];
+      lc = lastc[le];
+    }
     const int64_t pr = p.prop_const >= 0 ? p.prop_const : prop[le];
     // in-slot of this edge in the receiver's row (full mesh: arithmetic)
     const uint32_t slot = p.mesh ? s * (p.N - 1) + (i < s ? i : i - 1) : AT(p.rev, e, p.E);
@@ -2113,14 +2125,14 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     uint32_t a = eb, bi = 0;
     for (;;) {
       // next broadcast that targets this edge (Paxos broadcasts skip peers[0])
-      while (bi < n_bc && (op_flags(ops[L.bc[bi]]) & OPF_PAXOS) && le == 0) ++bi;
+      while (bi < n_bc && (op_flags(L.bco[bi]) & OPF_PAXOS) && le == 0) ++bi;
       // four sorted sources, each applied in canonical key order: broadcasts
       // (1), this edge's listed ops (0), the reply slot (2), the implicit echo (3)
       int src = -1;
       Op o;
       uint32_t sub = 0;
       if (bi < n_bc) {
-        o = ops[L.bc[bi]];
+        o = L.bco[bi];
         sub = o.sub + ((op_flags(o) & OPF_PAXOS) ? le - 1 : le);
         src = 1;
       }
