@@ -541,6 +541,8 @@ static int setup_device(Sim& s) {
   p.dreq_cnt = &cd->dreq_cnt;
   p.ov_cnt = &cd->ov_cnt;
   p.scal = cd->scal;
+  if ((rc = dalloc(s, &p.nxt_part, kNextBlocks)) || (rc = dalloc(s, &p.nxt_done, 1))) return rc;
+  HIPCHK(hipMemset(p.nxt_done, 0, 4));
   p.bucket_cnt = reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl));
   p.x_cnt = p.bucket_cnt + s.B;
   p.send_cnt = p.x_cnt + s.B;
@@ -976,7 +978,8 @@ static int run(Sim& s, int64_t t_until) {
     if (s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC) {
       if ((rc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp_dev, 0u))) return rc;
     }
-    if ((rc = launch(s, KS_AUX, k_next, dim3(1), dim3(1024), 0, s.kp_dev))) return rc;
+    const uint32_t nbn = static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
+    if ((rc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev))) return rc;
     if (hi == ce) {
       // cell finished: its bucket is free again
       HIPCHK(hipMemsetAsync(s.kp.bucket_cnt + (c % s.B), 0, 4, s.stream));

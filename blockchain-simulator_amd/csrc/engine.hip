@@ -45,7 +45,8 @@ namespace bcsim {
 
 // ---------------------------------------------------------------------------
 // kernel parameter block (device-resident, one per simulation)
-constexpr uint32_t kKstStripes = 64;  // kstat[kKstStripes][8]: per-workgroup stripes, summed on the host
+constexpr uint32_t kKstStripes = 64;
+constexpr uint32_t kNextBlocks = 64;  // k_next workgroups at most  // kstat[kKstStripes][8]: per-workgroup stripes, summed on the host
 struct KP {
   uint32_t N, R, NT, E;
   uint32_t protocol, delay_mode, rng_mode, encoding, echo;
@@ -144,6 +145,8 @@ struct KP {
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   long long *node_tnext, *node_onext;
   long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks
+  long long* nxt_part;  // [kNextBlocks] k_next per-workgroup minima
+  uint32_t* nxt_done;   // k_next workgroups finished (the last one reduces and resets it)
   // node partition (multi-GPU PDES): this rank owns nodes
   // [nlo, nlo + nloc) of every replica; records for other ranks' receivers
   // are staged in sendbuf and exchanged once per cell
@@ -2703,12 +2706,15 @@ __global__ void k_draws(const KP* __restrict__ pk, uint32_t) {
 }
 
 // global min over node_tnext / node_onext
+// next event time over all nodes: every workgroup reduces a strided share, the last one to
+// finish (threadfence reduction) combines the partial minima
 __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ long long red[1024];
   long long m = LLONG_MAX;
-  for (uint32_t k = threadIdx.x; k < p.NT; k += blockDim.x) {
+  const uint32_t nb = gridDim.x;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < p.NT; k += nb * blockDim.x) {
     const long long a = AT(p.node_tnext, k, p.NT), b = AT(p.node_onext, k, p.NT);
     m = min(m, min(a, b));
   }
@@ -2718,7 +2724,20 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk) {
     if (threadIdx.x < s) red[threadIdx.x] = min(red[threadIdx.x], red[threadIdx.x + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) p.scal[0] = red[0];
+  if (threadIdx.x != 0) return;
+  if (nb == 1) {
+    p.scal[0] = red[0];
+    return;
+  }
+  __hip_atomic_store(&p.nxt_part[blockIdx.x], red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence();
+  if (atomicAdd(p.nxt_done, 1u) != nb - 1) return;
+  __threadfence();
+  long long mm = LLONG_MAX;
+  for (uint32_t b = 0; b < nb; ++b)
+    mm = min(mm, __hip_atomic_load(&p.nxt_part[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  p.scal[0] = mm;
+  __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace bcsim

@@ -120,11 +120,14 @@ def _rccl1_worker(port, names, q):
     sys.path[:0] = [repo, os.path.join(repo, "tests"), os.path.join(repo, "blockchain-simulator_amd")]
     import torch.distributed as dist
     import bcsim
-    from parity_cases import cases
+    from parity_cases import cases, topology
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=0, world_size=1)
     for name in names:
         with bcsim.Simulator(cases()[name]) as s:
+            topo = topology(name)
+            if topo is not None:
+                s.set_topology(*topo)
             s.set_partition(dist, transport="rccl")
             s.run()
             q.put((name, s.trace(), s.counters()))
@@ -133,7 +136,7 @@ def _rccl1_worker(port, names, q):
 
 @pytest.mark.gpu
 def test_rccl_transport_world1(engine_lib):
-    names = ["pbft16_fixed_100", "raft16_jitter_ctr", "paxos16_jitter_rep4"]
+    names = ["pbft16_fixed_100", "raft16_jitter_ctr", "paxos16_jitter_rep4", "gossip200_d8_jitter_ctr"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_rccl1_worker, args=(_free_port(), names, q))
@@ -146,5 +149,5 @@ def test_rccl_transport_world1(engine_lib):
     assert p.exitcode == 0
     allc = cases()
     for name in names:
-        d = compare(oracle.run(allc[name]), got[name])
+        d = compare(oracle.run(allc[name], topology=topology(name)), got[name])
         assert d is None, f"{name}: {d}"
