@@ -31,10 +31,11 @@ METRIC = "delivered consensus msgs/sec (whole node), PBFT n=4096; committed roun
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def make_cfg(n_nodes, rounds, device, workload="pbft"):
+def make_cfg(n_nodes, rounds, device, workload="pbft", replicas=1):
     import bcsim
-    c = bcsim.preset("c4_pbft4096" if workload == "pbft" else "c5_gossip65536")
+    c = bcsim.preset({"pbft": "c4_pbft4096", "gossip": "c5_gossip65536", "paxos": "c3_paxos"}[workload])
     c.n_nodes = n_nodes
+    c.n_replicas = replicas
     c.pbft_rounds = rounds
     c.device = device
     c.stop_ns = -1
@@ -43,7 +44,7 @@ def make_cfg(n_nodes, rounds, device, workload="pbft"):
 
 def make_topology(n_nodes, workload):
     """None = the reference's full mesh; gossip: random 8-regular graph, seed 1."""
-    if workload == "pbft":
+    if workload != "gossip":
         return None
     import bcsim
     return bcsim.random_regular(n_nodes, 8, 1)
@@ -65,7 +66,7 @@ def cpu_baseline(n_nodes, budget_s, workload="pbft"):
     """Serial oracle DES (same semantics) on the host: a bounded time slice of
     the same workload, run from t=0 in 1 ms slices until budget_s of CPU."""
     import oracle
-    cfg = make_cfg(n_nodes, 100, 0, workload)
+    cfg = make_cfg(n_nodes, 100, 0, workload)  # one replica (the oracle runs replicas serially)
     o = oracle.OracleSim(cfg)
     topo = make_topology(n_nodes, workload)
     if topo is not None:
@@ -105,16 +106,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=6)
-    ap.add_argument("--workload", choices=("pbft", "gossip"), default="pbft",
-                    help="pbft: BASELINE configs[3] (the metric); gossip: configs[4], random 8-regular graph")
-    ap.add_argument("--nodes", type=int, default=0, help="default 4096 (pbft) / 65536 (gossip)")
+    ap.add_argument("--workload", choices=("pbft", "gossip", "paxos"), default="pbft",
+                    help="pbft: BASELINE configs[3] (the metric); gossip: configs[4], random 8-regular graph; "
+                         "paxos: configs[2] shape (jittered links, batched Monte Carlo replicas)")
+    ap.add_argument("--nodes", type=int, default=0, help="default 4096 (pbft, paxos) / 65536 (gossip)")
+    ap.add_argument("--replicas", type=int, default=0, help="paxos: replicas in one launch (default 16)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("pdes", "replicas"), default="pdes",
                     help="multi-GPU mode (N>1): node-partitioned PDES or independent replicas")
     args = ap.parse_args()
     if args.nodes <= 0:
-        args.nodes = 4096 if args.workload == "pbft" else 65536
+        args.nodes = 65536 if args.workload == "gossip" else 4096
+    if args.replicas <= 0:
+        args.replicas = 16 if args.workload == "paxos" else 1
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,7 +133,7 @@ def main():
 
     import bcsim
     period = 50_000_001  # Seconds(0.05f) in ns (round mode)
-    cfg = make_cfg(args.nodes, args.warmup + args.steps + 4, local, args.workload)
+    cfg = make_cfg(args.nodes, args.warmup + args.steps + 4, local, args.workload, args.replicas)
     topo = make_topology(args.nodes, args.workload)
 
     def new_sim():
@@ -196,6 +201,10 @@ def main():
         if args.workload == "pbft":
             data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, fixed 3 ms app delay)" % args.nodes
             wl = f"PBFT n={args.nodes} full O(n^2) prepare/commit (BASELINE configs[3])"
+        elif args.workload == "paxos":
+            data = ("synthetic (Paxos n=%d full mesh, 3Mbps/3ms links, app delay U{0..49} ms, counter RNG, "
+                    "%d replicas, seeds by replica)" % (args.nodes, args.replicas))
+            wl = f"Paxos n={args.nodes} jittered links, {args.replicas} batched Monte Carlo replicas (BASELINE configs[2] shape)"
         else:
             data = ("synthetic (PBFT-style gossip, n=%d random 8-regular graph seed 1, 3Mbps/3ms links, "
                     "1000 B blocks, fixed 3 ms app delay)" % args.nodes)

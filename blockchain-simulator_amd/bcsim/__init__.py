@@ -136,6 +136,7 @@ def preset(name):
         c.delay_mode = DELAY_FIXED
         c.app_delay_ns = 1_000_000
         c.t_end_ns = 4_000_000_000
+        c.cap_ops_per_node = 16384  # the leader holds ~2 waves of N-1 pending reply/echo ops
         return c
     if name == "c3_paxos":        # Paxos, jittered app delay U{0..49} ms, replicas
         c = default_config(PAXOS, 4096)

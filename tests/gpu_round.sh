@@ -25,6 +25,7 @@ for st in $steps; do
     bench)   run bench 400 python bench.py ;;
     gprof)   run gprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/gprof -o g -- python3 bench.py --workload gossip --no-cpu-baseline --steps 2 --warmup 4 ;;
     mc)      run mc 300 python -u -m pytest tests/test_montecarlo.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    paxos)   run paxos 400 python bench.py --workload paxos --cpu-budget 10 ;;
     gossip)  run gossip 400 python bench.py --workload gossip --cpu-budget 10 ;;
     newcases) run newcases 300 env BCSIM_LIB="$PWD/blockchain-simulator_amd/libbcsim_checked.so" BCSIM_SYNC_EACH=1 python tests/parity_run.py gossip64_d4_fixed gossip200_d8_jitter_ctr gossip512_d8_blocks gossip24_mesh pbft32_d6_ctr raft48_d6_ctr ;;
     prof)    run prof 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python bench.py --no-cpu-baseline ;;

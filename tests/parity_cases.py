@@ -43,6 +43,17 @@ def cases():
         "raft8_fixed": _cfg(R, 8, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=5_000_000_000),
         "raft8_fixed0": _cfg(R, 8, delay_mode=F, app_delay_ns=0, t_end_ns=4_000_000_000),
         "raft64_fixed": _cfg(R, 64, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=4_000_000_000),
+        # C2 exactly (BASELINE configs[1]): Raft n=1024, fixed-delay mesh, glibc seed 1
+        "raft1024_fixed_c2": _cfg(R, 1024, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=4_000_000_000,
+                                   cap_ops_per_node=16384),  # leader: ~2 reply waves of pending ops
+        "raft256_fixed": _cfg(R, 256, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=2_000_000_000,
+                              cap_ops_per_node=8192),
+        "raft512_fixed": _cfg(R, 512, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=2_000_000_000,
+                              cap_ops_per_node=8192),
+        "raft1024_ctr": _cfg(R, 1024, delay_mode=F, app_delay_ns=1_000_000, rng_mode=K, seed=1,
+                             t_end_ns=2_000_000_000, cap_ops_per_node=16384),
+        # C3 shape (BASELINE configs[2]) at a size the oracle runs in seconds: jitter U{0..49} ms, replicas
+        "paxos256_jitter_rep8": _cfg(X, 256, delay_mode=J, rng_mode=K, seed=21, n_replicas=8),
         "raft16_jitter_ctr": _cfg(R, 16, delay_mode=J, rng_mode=K, seed=3, t_end_ns=4_000_000_000),
         # Paxos: single decree, proposers 0,1,2
         "paxos8_fixed": _cfg(X, 8, delay_mode=F, app_delay_ns=2_000_000),
