@@ -619,6 +619,8 @@ static int setup_device(Sim& s) {
     HIPCHK(hipMemset(p.wgt, 0, NT * 64));
     HIPCHK(hipMemset(p.wgs, 0, NT * 64));
   }
+  p.dbg_tmax = LLONG_MIN;
+  if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p.node_onext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));

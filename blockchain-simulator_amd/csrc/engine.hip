@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -157,6 +158,9 @@ struct KP {
   uint32_t cap_send;
   const uint8_t* lead_all;  // [R][N] PBFT leader flags gathered from all ranks
   uint8_t* lead_loc;        // [R][N] this rank's leader flags (k_lead)
+  // debug (BCSIM_DBG_EVENTS=<t_max ns>): Raft/Paxos/gossip serial handlers emit one
+  // trace record of kind 90 + event class per handled event with t < dbg_tmax
+  long long dbg_tmax;
 };
 
 constexpr int kMaxRanks = 16;
@@ -404,6 +408,40 @@ __device__ inline void st_op(Op* q, const Op& o) {
   v[0] = a;
   v[1] = b;
 }
+
+// An Op as its two raw dwordx4 words: a = {t lo, t hi, dt, origin}, b = {sub, edge,
+// f0 | f1 << 16, f2 | type << 16 | kind_flags << 24} (the Op layout above).
+struct RawOp {
+  uint4 a, b;
+};
+__device__ inline RawOp raw_zero() { return RawOp{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)}; }
+__device__ inline RawOp ld_raw(const Op* q) {
+  const uint4* v = reinterpret_cast<const uint4*>(q);
+  return RawOp{v[0], v[1]};
+}
+__device__ inline int64_t raw_t(const RawOp& o) {
+  return static_cast<int64_t>((static_cast<uint64_t>(o.a.y) << 32) | o.a.x);
+}
+__device__ inline uint32_t raw_dt(const RawOp& o) { return o.a.z; }
+__device__ inline uint32_t raw_origin(const RawOp& o) { return o.a.w; }
+__device__ inline uint32_t raw_sub(const RawOp& o) { return o.b.x; }
+__device__ inline uint32_t raw_kind(const RawOp& o) { return (o.b.w >> 24) & 3u; }
+__device__ inline uint32_t raw_flags(const RawOp& o) { return o.b.w >> 26; }
+__device__ inline RawOp raw_make(int64_t t, uint32_t dt, uint32_t origin, uint32_t sub, uint8_t kind_flags) {
+  const uint64_t ut = static_cast<uint64_t>(t);
+  return RawOp{make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), dt, origin),
+               make_uint4(sub, 0, 0, static_cast<uint32_t>(kind_flags) << 24)};
+}
+// canonical key order of two ops (t, t - dt, origin, sub): see op_key_less
+__device__ inline bool raw_key_less(const RawOp& a, uint32_t sa, const RawOp& b, uint32_t sb) {
+  const int64_t ta = raw_t(a), tb = raw_t(b);
+  if (ta != tb) return ta < tb;
+  const int64_t tsa = ta - raw_dt(a), tsb = tb - raw_dt(b);
+  if (tsa != tsb) return tsa < tsb;
+  if (raw_origin(a) != raw_origin(b)) return raw_origin(a) < raw_origin(b);
+  return sa < sb;
+}
+static_assert(offsetof(Op, sub) == 16 && offsetof(Op, f0) == 24 && offsetof(Op, kind_flags) == 31, "RawOp layout");
 
 // per-edge op slots
 constexpr uint32_t kOpRing = 4;
@@ -1749,6 +1787,10 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
           stop_pending = false;
           if (PROTO == BCSIM_RAFT && rs.is_leader == 1) ctx_trace(c, BCSIM_TR_RAFT_STOP, rs.blockNum, rs.round, 0);
         }
+        if (best.t < p.dbg_tmax)  // debug event log (BCSIM_DBG_EVENTS)
+          emit_trace(p, best, rep, i, 90 + which, which == 0 ? rec.type * 256 + (rec.f0 & 255) : which == 1 ? tm[tsel].kind : 0,
+                     PROTO == BCSIM_RAFT ? rs.vs * 65536 + rs.vf : xs_.vs * 65536 + xs_.vf,
+                     PROTO == BCSIM_RAFT ? rs.has_voted + 2 * rs.is_leader : xs_.ticket);
       }
       S.sub = c.sub;
       S.draws = c.draws;
@@ -2072,10 +2114,14 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       bu = busy[le];
       lc = lastc[le];
     }
+    // The four op sources of this edge are merged as raw 32-byte words (RawOp): selecting
+    // whole Op structs with int16 members between sources was miscompiled on gfx950 /
+    // ROCm 7.2 (a record took f0 from a broadcast and the rest from a listed op; the Raft
+    // N>=300 parity gap).  Integer word selects are what the compiler sees.
     // implicit echo: this node's main inbox record of in-slot le, delivered in
     // [t_lo, t_hi), goes back out on out-edge le (the same peer); release the slot
     bool he = false;
-    Op eo;
+    RawOp eo = raw_zero();
     if (rx) {
       Rec* ir = const_cast<Rec*>(in_row) + e;
       const Rec r0 = ld_rec(ir);
@@ -2085,11 +2131,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         if (p.echo) {
           const int bg = (r0.flags & RF_BIG) ? 1 : 0;
           const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
-          eo.t = ta0;
-          eo.dt = static_cast<uint32_t>(pin + p.tx_last[bg]);
-          eo.origin = s;
-          eo.sub = r0.sub;
-          eo.kind_flags = static_cast<uint8_t>(OP_ECHO | (bg ? (OPF_BIG << 2) : 0));
+          eo = raw_make(ta0, static_cast<uint32_t>(pin + p.tx_last[bg]), s, r0.sub,
+                        static_cast<uint8_t>(OP_ECHO | (bg ? (OPF_BIG << 2) : 0)));
           he = true;
           ++st_echo;
         }
@@ -2097,10 +2140,10 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     }
     // this edge's reply-slot op due in [t_lo, t_hi)
     bool hr = false;
-    Op ro;
+    RawOp ro = raw_zero();
     if (sl) {
-      ro = ld_op(eslot_at(p, ob, rep, e));
-      hr = ro.t >= t_lo && ro.t < t_hi;
+      ro = ld_raw(eslot_at(p, ob, rep, e));
+      hr = raw_t(ro) >= t_lo && raw_t(ro) < t_hi;
       if (hr) ++st_ops;
     }
     if (ee == eb && n_bc == 0 && !he && !hr) continue;
@@ -2132,29 +2175,29 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       // four sorted sources, each applied in canonical key order: broadcasts
       // (1), this edge's listed ops (0), the reply slot (2), the implicit echo (3)
       int src = -1;
-      Op o;
+      RawOp o = raw_zero();
       uint32_t sub = 0;
       if (bi < n_bc) {
-        o = L.bco[bi];
-        sub = o.sub + ((op_flags(o) & OPF_PAXOS) ? le - 1 : le);
+        o = ld_raw(&L.bco[bi]);
+        sub = raw_sub(o) + ((raw_flags(o) & OPF_PAXOS) ? le - 1 : le);
         src = 1;
       }
       if (a < ee) {
-        const Op oa = ops[eidx[a]];
-        if (src < 0 || op_key_less(oa, oa.sub, o, sub)) {
+        const RawOp oa = ld_raw(&ops[eidx[a]]);
+        if (src < 0 || raw_key_less(oa, raw_sub(oa), o, sub)) {
           o = oa;
-          sub = oa.sub;
+          sub = raw_sub(oa);
           src = 0;
         }
       }
-      if (hr && (src < 0 || op_key_less(ro, ro.sub, o, sub))) {
+      if (hr && (src < 0 || raw_key_less(ro, raw_sub(ro), o, sub))) {
         o = ro;
-        sub = ro.sub;
+        sub = raw_sub(ro);
         src = 2;
       }
-      if (he && (src < 0 || op_key_less(eo, eo.sub, o, sub))) {
+      if (he && (src < 0 || raw_key_less(eo, raw_sub(eo), o, sub))) {
         o = eo;
-        sub = eo.sub;
+        sub = raw_sub(eo);
         src = 3;
       }
       if (src < 0) break;
@@ -2166,10 +2209,11 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         hr = false;
       else
         he = false;
-      if (src == 2 && op_kind(o) == OP_SEND) ++sends;
-      const bool is_echo = src != 1 && op_kind(o) == OP_ECHO;
-      const int big = (op_flags(o) & OPF_BIG) ? 1 : 0;
-      const int64_t start = bu > o.t ? bu : o.t;
+      if (src == 2 && raw_kind(o) == OP_SEND) ++sends;
+      const bool is_echo = src != 1 && raw_kind(o) == OP_ECHO;
+      const int big = (raw_flags(o) & OPF_BIG) ? 1 : 0;
+      const int64_t ot = raw_t(o);
+      const int64_t start = bu > ot ? bu : ot;
       const int64_t end = start + p.tx_tot[big];
       bu = end;
       if (is_echo) continue;
@@ -2181,14 +2225,14 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         continue;
       }
       ++n_rec;
+      // the record: t_off | sub | payload word (f0, f1) | (f2, type, flags) -- raw words only
+      const uint32_t tof = static_cast<uint32_t>(ta - ca * p.L);
+      const uint32_t w3 = (o.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
       Rec r;
-      r.t_off = static_cast<uint32_t>(ta - ca * p.L);
-      r.sub = sub;
-      r.f0 = o.f0;
-      r.f1 = o.f1;
-      r.f2 = o.f2;
-      r.type = o.type;
-      r.flags = static_cast<uint8_t>(RF_VALID | (big ? RF_BIG : 0));
+      {
+        const uint4 rv = make_uint4(tof, sub, o.b.z, w3);
+        __builtin_memcpy(&r, &rv, sizeof r);
+      }
       const bool owner = lc != ca;
       lc = ca;
       if (p.nranks > 1) {

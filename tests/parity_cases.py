@@ -48,6 +48,10 @@ def cases():
                                    cap_ops_per_node=16384),  # leader: ~2 reply waves of pending ops
         "raft256_fixed": _cfg(R, 256, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=2_000_000_000,
                               cap_ops_per_node=8192),
+        # N=300: a candidate's VOTE_RES and its own VOTE_REQ broadcast share an edge and an
+        # arrival cell (the k_link merge that was miscompiled)
+        "raft300_fixed": _cfg(R, 300, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=2_000_000_000,
+                              cap_ops_per_node=8192),
         "raft512_fixed": _cfg(R, 512, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=2_000_000_000,
                               cap_ops_per_node=8192),
         "raft1024_ctr": _cfg(R, 1024, delay_mode=F, app_delay_ns=1_000_000, rng_mode=K, seed=1,

@@ -142,6 +142,11 @@ inline std::common_type_t<A, B> max(A a, B b) { return a < b ? b : a; }
 #define __HIP_MEMORY_SCOPE_SYSTEM 0
 template <typename T, typename U>
 inline void __hip_atomic_store(T* p, U v, int, int) { __atomic_store_n(p, static_cast<T>(v), __ATOMIC_RELAXED); }
+template <typename T>
+inline T __hip_atomic_load(T* p, int, int) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+#define __HIP_MEMORY_SCOPE_AGENT 1
+#define __HIP_MEMORY_SCOPE_WORKGROUP 2
+inline void __threadfence() { std::atomic_thread_fence(std::memory_order_seq_cst); }
 
 // ---- runtime API subset ----
 typedef int hipError_t;
