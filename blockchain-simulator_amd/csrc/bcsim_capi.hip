@@ -372,7 +372,7 @@ static int setup_device(Sim& s) {
   if (const char* nm = std::getenv("BCSIM_NO_MESH"); nm && *nm == '1') mesh = false;  // debugging aid
   p.mesh = mesh ? 1u : 0u;
   p.n_tiles = (s.N + kTile - 1) / kTile;
-  const uint64_t per_bucket = static_cast<uint64_t>(s.R) * s.E * sizeof(Rec) * (mesh ? 2 : 1);
+  const uint64_t per_bucket = static_cast<uint64_t>(s.R) * s.E * sizeof(Rec);
   s.B = c.n_buckets ? c.n_buckets : 0;
   if (s.B == 0) {
     const uint64_t nb = per_bucket ? (8ull << 30) / per_bucket : kMaxBuckets;
@@ -506,11 +506,9 @@ static int setup_device(Sim& s) {
     HIPCHK(hipMemset(p.sflag, 0, static_cast<size_t>(kOpRing) * NT));
     if (!on) p.eslot = nullptr;
   }
-  if ((rc = dalloc(s, &p.busy, static_cast<size_t>(s.R) * s.E)) ||
-      (rc = dalloc(s, &p.lastc, static_cast<size_t>(s.R) * s.E)))
-    return rc;
-  const size_t n_dirty = p.mesh ? static_cast<size_t>(s.B) * s.R * p.n_tiles * p.n_tiles : 1;
-  if ((rc = dalloc(s, &p.outbox, p.mesh ? p.cap_inbox : 1)) || (rc = dalloc(s, &p.tdirty, n_dirty))) return rc;
+  if ((rc = dalloc(s, &p.link, static_cast<size_t>(s.R) * s.E))) return rc;
+  const size_t n_rtile = p.mesh ? static_cast<size_t>(s.B) * s.R * p.n_tiles : 1;
+  if ((rc = dalloc(s, &p.rtile, n_rtile))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
       (rc = dalloc(s, &p.xbuf, p.cap_xbuf)) || (rc = dalloc(s, &p.xgrp, p.cap_x)) ||
       (rc = dalloc(s, &p.xstage, NT * p.cap_stage)) || (rc = dalloc(s, &p.xmeta, NT * p.cap_stage)) ||
@@ -589,11 +587,12 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemset(p.next_heartbeat, 0, NT * 4));
   HIPCHK(hipMemset(p.timers, 0, NT * p.cap_timers * sizeof(TimerEnt)));
   HIPCHK(hipMemset(p.n_ops, 0, NT * 4));
-  HIPCHK(hipMemset(p.busy, 0, static_cast<size_t>(s.R) * s.E * 8));
-  HIPCHK(hipMemset(p.lastc, 0xFF, static_cast<size_t>(s.R) * s.E * 8));  // -1: no record yet
+  {  // busy_until 0, no record yet (cell tag 0xFFFF)
+    std::vector<uint64_t> l0(static_cast<size_t>(s.R) * s.E, 0xFFFFull);
+    HIPCHK(hipMemcpy(p.link, l0.data(), l0.size() * 8, hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMemset(p.inbox, 0, p.cap_inbox * sizeof(Rec)));
-  if (p.mesh) HIPCHK(hipMemset(p.outbox, 0, p.cap_inbox * sizeof(Rec)));
-  HIPCHK(hipMemset(p.tdirty, 0, n_dirty));
+  HIPCHK(hipMemset(p.rtile, 0, n_rtile));
   HIPCHK(hipMemset(p.iflag, 0, static_cast<size_t>(s.B) * NT));
   HIPCHK(hipMemset(p.seg_cnt, 0, NT * 4));
   HIPCHK(hipMemset(p.seg_off, 0, (NT + 1) * 4));
@@ -782,11 +781,6 @@ static int group_cell(Sim& s, long long cell) {
     return BCSIM_E_OVERFLOW;
   }
   s.x_active = 0;
-  if (s.kp.mesh) {  // sender-major outbox -> receiver rows of this cell's bucket
-    const uint32_t nt = s.kp.n_tiles;
-    int rc = launch(s, KS_GROUP, k_transpose, dim3(s.R * nt * nt), dim3(256), 0, s.kp_dev, b);
-    if (rc) return rc;
-  }
   if (nx) {
     HIPCHK(hipMemsetAsync(s.kp.seg_cnt, 0, s.NT * 4ull, s.stream));
     HIPCHK(hipMemsetAsync(s.kp.cursor, 0, s.NT * 4ull, s.stream));
@@ -986,6 +980,9 @@ static int run(Sim& s, int64_t t_until) {
       // cell finished: its bucket is free again
       HIPCHK(hipMemsetAsync(s.kp.bucket_cnt + (c % s.B), 0, 4, s.stream));
       HIPCHK(hipMemsetAsync(s.kp.x_cnt + (c % s.B), 0, 4, s.stream));
+      if (s.kp.mesh)  // receiver-tile flags of the bucket (every node of the cell has run)
+        HIPCHK(hipMemsetAsync(s.kp.rtile + static_cast<size_t>(c % s.B) * s.R * s.kp.n_tiles, 0,
+                              static_cast<size_t>(s.R) * s.kp.n_tiles, s.stream));
     }
     if ((rc = readback(s))) return rc;
     if (tick) {

@@ -100,13 +100,12 @@ struct KP {
   uint32_t impl;
   int64_t prop_const;    // propagation delay of every edge, or -1 (per-edge array)
   // links
-  int64_t* busy;
-  int64_t* lastc;  // cell of the last record emitted on the edge (-1: none)
+  uint64_t* link;  // per edge: busy_until << 16 | (arrival cell of the last record & 0xFFFF)
   // inbox
   Rec* inbox;            // [B][R][E]  receiver-major (in-slot order)
-  Rec* outbox;           // [B][R][E]  sender-major staging (full mesh only)
-  uint8_t* tdirty;       // [B][R][nt][nt] outbox tile holds records (full mesh only)
-  uint32_t mesh, n_tiles;  // full-mesh topology: records go through the tiled transpose
+  uint8_t* rtile;        // [B][R][n_tiles] full mesh: a record for a receiver of this 64-node
+                         // tile sits in the bucket (senders set one byte per tile, not one per node)
+  uint32_t mesh, n_tiles;  // full-mesh topology (arithmetic peers / in-slots)
   uint8_t* iflag;        // [B][NT] node has records in the bucket
   uint32_t* bucket_cnt;  // [B] nonzero = the bucket holds records (slots + extras); see mark_busy
   uint32_t* x_cnt;       // [B] extras in the bucket
@@ -217,6 +216,18 @@ __device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int l
 __device__ inline uint32_t xcd_map(uint32_t b, uint32_t n) {
   const uint32_t x = b & 7u, k = b >> 3, per = n >> 3, rem = n & 7u;
   return x * per + min(x, rem) + k;
+}
+
+// does gnode g (node i of replica rep) have arrivals in bucket b?  (own flag, or its
+// receiver tile's flag in the full mesh)
+__device__ inline bool node_flagged(const KP& p, uint32_t b, uint32_t g, uint32_t rep, uint32_t i) {
+  if (AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT)) return true;
+  return p.mesh && AT(p.rtile, (static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6),
+                      static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles) != 0;
+}
+// set-once byte flag (many writers of the same byte: read first, store only if clear)
+__device__ inline void set_flag_once(uint8_t* f) {
+  if (*reinterpret_cast<volatile uint8_t*>(f) == 0) *f = 1;
 }
 
 // blockIdx -> gnode of this rank's partition (XCD-contiguous ranges)
@@ -1546,10 +1557,10 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
   const size_t fidx = static_cast<size_t>(b) * p.NT + g;
-  const bool flag = AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) != 0;
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const bool flag = node_flagged(p, b, g, rep, i);
   if (!flag && AT(p.node_tnext, g, p.NT) >= t_hi && !has_start && !has_stop) return;
 
-  const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
   const Rec* slots = p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0;
   uint32_t xn = 0;
@@ -1897,7 +1908,8 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
 // cell (a second record of the same edge and cell goes to the extras list,
 // a cell beyond the ring to the overflow list).
 constexpr int kBcastCap = 64;  // due broadcasts per node per cell
-constexpr int kMaxTiles = 1024;  // 64-node tiles of the full-mesh transpose (N <= 65536)
+constexpr int kTile = 64;        // receiver tile of the full-mesh tile flags (rtile)
+constexpr int kMaxTiles = 1024;  // 64-node tiles (N <= 65536)
 constexpr int kMaxBuckets = 64;
 
 __device__ inline bool op_key_less(const Op& a, uint32_t sa, const Op& b, uint32_t sb) {
@@ -1973,21 +1985,20 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   const bool sl = p.eslot && AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT);
   const uint32_t ib = static_cast<uint32_t>(cell % p.n_buckets);
   const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
-  const bool rx = p.impl && AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT);
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const bool rx = p.impl && node_flagged(p, ib, g, rep, i);
   if (n == 0 && !sl && !rx) return;
   const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
   unsigned long long ph[4] = {0, 0, 0, 0};
   const uint32_t n_in = n;
   const uint32_t tid = threadIdx.x;
-  const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
   Op* ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
   uint32_t* ecnt = reinterpret_cast<uint32_t*>(smem);   // deg+1
   uint32_t* efill = ecnt + (p.deg_max + 1);              // deg
   uint32_t* eidx = efill + p.deg_max;                    // cap_ops
   const size_t eb0 = static_cast<size_t>(rep) * p.E + e0;
-  int64_t* busy = p.busy + eb0;
-  int64_t* lastc = p.lastc + eb0;
+  uint64_t* lnk = p.link + eb0;
   const int64_t* prop = p.prop + e0;
   unsigned long long* cnt = cnt_stripe(p, rep);
   const uint32_t B = p.n_buckets;
@@ -2109,11 +2120,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     // link state of an edge that is certainly used: issued before the inbox / reply-slot
     // loads below so that the three HBM reads overlap instead of forming a chain
     const bool pre = n_bc != 0 || ee > eb;
-    int64_t bu = 0, lc = 0;
-    if (pre) {
-      bu = busy[le];
-      lc = lastc[le];
-    }
+    uint64_t lw = 0;
+    if (pre) lw = lnk[le];
     // The four op sources of this edge are merged as raw 32-byte words (RawOp): selecting
     // whole Op structs with int16 members between sources was miscompiled on gfx950 /
     // ROCm 7.2 (a record took f0 from a broadcast and the rest from a listed op; the Raft
@@ -2160,10 +2168,12 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       eidx[b2] = x;
     }
     ++st_edges;
-    if (!pre) {
-      bu = busy[le];
-      lc = lastc[le];
-    }
+    if (!pre) lw = lnk[le];
+    // link word: FIFO busy_until (ns, < 2^48) and the 16 low bits of the arrival cell of the
+    // edge's last record (slot ownership; a false "not owner" after 2^16 cells only routes a
+    // record through the extras list, which delivers it identically)
+    int64_t bu = static_cast<int64_t>(lw >> 16);
+    uint32_t lc = static_cast<uint32_t>(lw & 0xFFFFu);
     const int64_t pr = p.prop_const >= 0 ? p.prop_const : prop[le];
     // in-slot of this edge in the receiver's row (full mesh: arithmetic)
     const uint32_t slot = p.mesh ? s * (p.N - 1) + (i < s ? i : i - 1) : AT(p.rev, e, p.E);
@@ -2233,8 +2243,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         const uint4 rv = make_uint4(tof, sub, o.b.z, w3);
         __builtin_memcpy(&r, &rv, sizeof r);
       }
-      const bool owner = lc != ca;
-      lc = ca;
+      const bool owner = lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
+      lc = static_cast<uint32_t>(ca) & 0xFFFFu;
       if (p.nranks > 1) {
         const uint32_t orank = p.owner[s];
         if (orank != p.rank) {  // receiver on another GPU: ship the record (k_import places it)
@@ -2252,10 +2262,12 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         const uint32_t bk = static_cast<uint32_t>(ca % B);
         bool flag_rx = true;
         if (owner) {
-          if (p.mesh) {  // sender-major staging, moved to the receiver by k_transpose
-            st_rec(&AT(p.outbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + e, p.cap_inbox), r);
-            // tile flag: one LDS byte per receiver tile, flushed once per workgroup
-            // (k_transpose then sets the receivers' iflag once per tile)
+          // the receiver's in-slot of this bucket, written directly: a receiver-major 16-byte
+          // scatter from XCD-contiguous senders merges in L2 and costs ~2x a coalesced row
+          // write, a third of staging sender-major and transposing (tools/microbench/scatter.hip)
+          st_rec(&AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox), r);
+          if (p.mesh) {
+            // receiver-tile flag: one LDS byte per 64-node tile, flushed once per workgroup
             uint32_t tb = kInvalid;
             if (tmap) {  // the first bucket seen owns the LDS map; others flag directly
               tb = L.tbk;
@@ -2264,15 +2276,12 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
                 tb = old == kInvalid ? bk : old;
               }
             }
-            if (tb == bk) {
+            if (tb == bk)
               L.tflag[s >> 6] = 1;
-            } else {
-              AT(p.tdirty, ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (i >> 6)) * p.n_tiles + (s >> 6),
-                 static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
-            }
+            else
+              set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
+                                static_cast<uint64_t>(B) * p.R * p.n_tiles));
             flag_rx = false;
-          } else {
-            st_rec(&AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox), r);
           }
         } else {
           XRec x;
@@ -2300,16 +2309,16 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         if (ca < ovmin) ovmin = ca;
       }
     }
-    busy[le] = bu;
-    lastc[le] = lc;
+    if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+    lnk[le] = (static_cast<uint64_t>(bu) << 16) | lc;
   }
   if (cbn) atomicAdd(&L.lcnt[cb], cbn);
   __syncthreads();
-  // flush the tile flags of this sender's full-mesh records
+  // flush the receiver-tile flags of this sender's full-mesh records
   if (tmap && L.tbk != kInvalid) {
-    const size_t tb = (static_cast<size_t>(L.tbk) * p.R + rep) * p.n_tiles + (i >> 6);
+    const size_t tb = (static_cast<size_t>(L.tbk) * p.R + rep) * p.n_tiles;
     for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x)
-      if (L.tflag[k]) AT(p.tdirty, tb * p.n_tiles + k, static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
+      if (L.tflag[k]) set_flag_once(&AT(p.rtile, tb + k, static_cast<uint64_t>(B) * p.R * p.n_tiles));
   }
 
   if (p.wgt && tid == 0) ph[2] = __builtin_amdgcn_s_memrealtime();
@@ -2418,21 +2427,13 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) {
     XRec x = rx[k];
-    const uint32_t rep = x.g / p.N, s = x.g % p.N;
+    const uint32_t rep = x.g / p.N;
     if (x.cell < g_cur + static_cast<long long>(B)) {
       const uint32_t b = static_cast<uint32_t>(x.cell % B);
       const bool owner = (x.r.flags & RF_OWNER) != 0;
       x.r.flags = static_cast<uint8_t>(x.r.flags & ~RF_OWNER);
       if (owner) {
-        if (p.mesh) {
-          const uint32_t i = AT(p.col, x.slot, p.E);  // the sender: slot = edge s -> i
-          const uint32_t e = AT(p.rev, x.slot, p.E);
-          st_rec(&AT(p.outbox, (static_cast<size_t>(b) * p.R + rep) * p.E + e, p.cap_inbox), x.r);
-          AT(p.tdirty, ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6)) * p.n_tiles + (s >> 6),
-             static_cast<uint64_t>(B) * p.R * p.n_tiles * p.n_tiles) = 1;
-        } else {
-          st_rec(&AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox), x.r);
-        }
+        st_rec(&AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox), x.r);
       } else {
         const uint32_t pos = atomicAdd(&p.x_cnt[b], 1u);
         if (pos < p.cap_x)
@@ -2440,7 +2441,7 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
         else
           set_err(p, BCSIM_E_OVERFLOW);
       }
-      AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(B) * p.NT) = 1;
+      set_flag_once(&AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(B) * p.NT));
       atomicAdd(&lb[b], 1u);
     } else {
       const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
@@ -2465,54 +2466,6 @@ __global__ __launch_bounds__(1024) void k_lead(const KP* __restrict__ pk) {
     const uint32_t i = p.nlo + k, g = rep * p.N + i;
     p.lead_loc[g] = (p.tick_alive[g] && p.leader[g] == static_cast<int32_t>(i)) ? 1 : 0;
   }
-}
-
-// ---------------------------------------------------------------------------
-// k_transpose (full mesh): move the records of bucket b from the sender-major
-// outbox (coalesced k_link writes) to the receivers' inbox rows (coalesced
-// k_scan reads) through a 64 x 64 LDS tile — the all-to-all transpose of the
-// O(N^2) message matrix.  Edge i->s sits at i*(N-1) + s - (s > i) in the
-// outbox and at s*(N-1) + i - (i > s) in the inbox.  Clean tiles exit.
-constexpr int kTile = 64;
-
-__global__ __launch_bounds__(256) void k_transpose(const KP* __restrict__ pk, uint32_t b) {
-  const KP& p = *pk;
-  BAIL_IF_ERR();
-  __shared__ Rec tile[kTile][kTile];  // column index XOR row: column reads spread over banks
-  const uint32_t nt = p.n_tiles;
-  const uint32_t tj = blockIdx.x % nt, ti = (blockIdx.x / nt) % nt, rep = blockIdx.x / (nt * nt);
-  const size_t didx = ((static_cast<size_t>(b) * p.R + rep) * nt + ti) * nt + tj;
-  uint8_t& dirty = AT(p.tdirty, didx, static_cast<uint64_t>(p.n_buckets) * p.R * nt * nt);
-  if (!dirty) return;
-  const uint32_t N = p.N, lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const size_t base = (static_cast<size_t>(b) * p.R + rep) * p.E;
-  Rec* ob = p.outbox + base;
-  Rec* ib = p.inbox + base;
-  const uint32_t i0 = ti * kTile, s0 = tj * kTile;
-  // rows of the outbox: sender i, receivers s0 + lane
-  for (uint32_t r = w; r < kTile; r += nw) {
-    const uint32_t i = i0 + r, s = s0 + lane;
-    Rec v{};
-    if (i < N && s < N && s != i) {
-      const size_t e = static_cast<size_t>(i) * (N - 1) + s - (s > i ? 1 : 0);
-      v = ld_rec(&AT(ob, e, p.E));
-      if (v.flags) clr_rec(&AT(ob, e, p.E));
-    }
-    tile[r][lane ^ r] = v;
-  }
-  __syncthreads();
-  // rows of the inbox: receiver s, senders i0 + lane
-  for (uint32_t c = w; c < kTile; c += nw) {
-    const uint32_t s = s0 + c, i = i0 + lane;
-    const bool ok = i < N && s < N && s != i;
-    const Rec v = tile[lane][c ^ lane];
-    const bool has = ok && v.flags != 0;
-    if (has) st_rec(&AT(ib, static_cast<size_t>(s) * (N - 1) + i - (i > s ? 1 : 0), p.E), v);
-    // receiver s has arrivals in this bucket (k_link leaves the flag to us)
-    if (__ballot(has) && lane == 0)
-      AT(p.iflag, static_cast<size_t>(b) * p.NT + rep * N + s, static_cast<uint64_t>(p.n_buckets) * p.NT) = 1;
-  }
-  if (threadIdx.x == 0) dirty = 0;
 }
 
 // ---------------------------------------------------------------------------
