@@ -50,16 +50,40 @@ def make_topology(n_nodes, workload):
     return bcsim.random_regular(n_nodes, 8, 1)
 
 
+PMC_ROUND = "r02"
+
+
 def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (tools/pmc_summary.py over tests/gpu_prof.sh: FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE), for the same workload; None if absent."""
-    path = os.path.join(REPO, "profiles", f"r01_pmc_{workload}{n_nodes}.json")
+    """HBM bytes per launch of `kernel` from this round's committed rocprofv3 PMC
+    summary (tools/pmc_summary.py over tests/gpu_prof.sh: FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE, separate passes), same workload; None if absent."""
+    path = os.path.join(REPO, "profiles", f"{PMC_ROUND}_pmc_{workload}{n_nodes}.json")
     try:
         with open(path) as f:
             return json.load(f)["kernels"][kernel]["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
+
+
+def host_cpu():
+    """CPU model and logical core count of this host (for the cpu_baseline line)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def commit_records(sim, workload):
+    """Commit-kind trace records so far (PBFT commit lines, gossip first receipts)."""
+    import bcsim
+    kind = {"pbft": bcsim.TR["PBFT_COMMIT"], "gossip": bcsim.TR["GOSSIP_DELIVER"], "paxos": bcsim.TR["PAXOS_COMMIT"]}[workload]
+    return sum(1 for r in sim.trace() if r[6] == kind)
 
 
 def cpu_baseline(n_nodes, budget_s, workload="pbft"):
@@ -83,9 +107,12 @@ def cpu_baseline(n_nodes, budget_s, workload="pbft"):
     wall = time.time() - w0
     cnt = o.counters()
     o.close()
+    model, nproc = host_cpu()
     return dict(value=cnt["delivered_total"] / max(cpu, 1e-9), unit="msgs/s", cores=1, kind="port",
-                sample=f"oracle DES, {workload} n={n_nodes}, first {t / 1e6:.0f} ms simulated "
-                       f"({cnt['delivered_total']} msgs, {cpu:.1f} s CPU, {wall:.1f} s wall)")
+                cpu_model=model, nproc=nproc,
+                sample=f"oracle DES (serial, one core of {nproc}: {model}), {workload} n={n_nodes}, "
+                       f"first {t / 1e6:.0f} ms simulated ({cnt['delivered_total']} msgs, {cpu:.1f} s CPU, "
+                       f"{wall:.1f} s wall)")
 
 
 def aggregate(dist, device, dt, msgs, trace_delta):
@@ -175,7 +202,7 @@ def main():
             print(f"[bench] warmup {k}: {time.perf_counter() - w:.2f}s msgs={sim.counters()['delivered_total']}",
                   file=sys.stderr, flush=True)
     c0 = sim.counters()
-    tr0 = c0["trace_records"]
+    cm0 = commit_records(sim, args.workload)
     sim.reset_kernel_stats()
     barrier()
     w0 = time.perf_counter()
@@ -187,17 +214,21 @@ def main():
     c1 = sim.counters()
     ks = sim.kernel_stats()
     msgs = c1["delivered_total"] - c0["delivered_total"]
-    trace_delta = c1["trace_records"] - tr0
-    dt, msgs, trace_delta = aggregate(dist, f"cuda:{local}", dt, msgs, trace_delta)
+    commits = commit_records(sim, args.workload) - cm0
+    dt, msgs, commits = aggregate(dist, f"cuda:{local}", dt, msgs, commits)
     sim.close()
 
     if rank == 0:
-        # committed rounds: commit records / N (every node commits each block)
-        rounds = trace_delta / args.nodes
+        # committed rounds: commit-kind records / N (every node commits each block;
+        # block / stop / view records are not counted)
+        rounds = commits / args.nodes
         dom = max(("scan", "link", "group", "aux"), key=lambda k: ks[k]["us"])
         lk = ks["link"]
+        # roofline of the scatter (k_link): SURVEY.md §8(d) algorithmic bytes = 48 B per record
+        # emitted by the timed k_link launches, over their HIP-event time on the engine stream
         ach = (lk["bytes"] / 1e9) / (lk["us"] / 1e6) if lk["us"] > 0 else 0.0
         traffic = pmc_traffic(args.nodes, workload=args.workload)
+        all_us = sum(v["us"] for v in ks.values())
         if args.workload == "pbft":
             data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, fixed 3 ms app delay)" % args.nodes
             wl = f"PBFT n={args.nodes} full O(n^2) prepare/commit (BASELINE configs[3])"
@@ -210,6 +241,7 @@ def main():
                     "1000 B blocks, fixed 3 ms app delay)" % args.nodes)
             wl = f"PBFT-style gossip n={args.nodes} random 8-regular (BASELINE configs[4])"
         lk_launch_bytes = lk["bytes"] / max(1, lk["launches"])
+        impl_launch_bytes = ks["aux"]["bytes"] / max(1, lk["launches"])
         out = {
             "metric": METRIC,
             "value": msgs / dt,
@@ -230,7 +262,11 @@ def main():
             "roofline": {"kernel": "k_link (inbox scatter)", "bound": "hbm", "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": lk_launch_bytes,
+                         "bytes_per_record": 48, "records": lk["bytes"] / 48.0,
+                         "implementation_bytes_per_launch": impl_launch_bytes,
                          "avg_launch_us": lk["us"] / max(1, lk["launches"]),
+                         "launches": lk["launches"],
+                         "pipeline_frac": (48.0 * msgs / 1e9) / (all_us / 1e6) / HBM_PEAK_GBS if all_us else 0.0,
                          "dominant_kernel_class": dom},
             "kernel_us": {k: v["us"] for k, v in ks.items()},
             "kernel_launches": {k: v["launches"] for k, v in ks.items()},

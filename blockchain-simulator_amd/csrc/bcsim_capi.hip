@@ -1296,16 +1296,16 @@ int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, u
     if (launches_out4) launches_out4[k] = s.launches[k];
   }
   if (bytes_out4) {
-    // algorithmic bytes.  k_link: 32 B per due op read, 16 B
-    // per record scattered, 32 B per touched edge (busy_until + last_cell
-    // read + write), 32 B per op kept (compaction write).  k_scan: 16 B per
-    // record read + 16 B slot release, 32 B per op written (echo + reply).
-    bytes_out4[bcsim::KS_LINK] = 32.0 * ks[bcsim::KST_OPS] + 16.0 * ks[bcsim::KST_REC] +
-                                 32.0 * ks[bcsim::KST_EDGES] + 32.0 * ks[bcsim::KST_KEPT] +
-                                 32.0 * ks[bcsim::KST_ECHO];
+    // [link]: algorithmic bytes of the inbox scatter, SURVEY.md §8(d): 48 B per record
+    // emitted (16 B record write + 16 B read by the receiver + 16 B busy_until read+write).
+    // [scan]: 16 B per delivered record read.  [aux]: device-counted implementation bytes
+    // of k_link (32 B per due op read, 16 B per record, 8 B per touched edge's link word
+    // read+write, 32 B per kept op, 32 B per implicit echo read+clear).
+    bytes_out4[bcsim::KS_LINK] = 48.0 * ks[bcsim::KST_REC];
     bytes_out4[bcsim::KS_SCAN] = 16.0 * ks[bcsim::KST_DELIV];
     bytes_out4[bcsim::KS_GROUP] = 0;
-    bytes_out4[bcsim::KS_AUX] = static_cast<double>(ks[bcsim::KST_REC]);  // records emitted
+    bytes_out4[bcsim::KS_AUX] = 32.0 * ks[bcsim::KST_OPS] + 16.0 * ks[bcsim::KST_REC] + 16.0 * ks[bcsim::KST_EDGES] +
+                                32.0 * ks[bcsim::KST_KEPT] + 32.0 * ks[bcsim::KST_ECHO];
   }
   return BCSIM_OK;
 }

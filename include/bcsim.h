@@ -248,10 +248,12 @@ int bcsim_rccl_unique_id(void* out, uint64_t cap, uint64_t* n_out);
 int bcsim_set_partition_rccl(bcsim_sim* s, uint32_t rank, uint32_t nranks, const void* unique_id,
                              uint64_t id_bytes);
 
-/* Device timing of the last bcsim_run: per-kernel-class accumulated
- * microseconds measured with hipEvents on the engine stream.  kinds:
- * 0 scan, 1 link (fan-out scatter), 2 group, 3 tick/aux.  Also the
- * algorithmic bytes moved by each class. */
+/* Device timing since the last reset: per-kernel-class accumulated
+ * microseconds measured with hipEvents on the engine stream and launch
+ * counts.  kinds: 0 scan, 1 link (fan-out scatter), 2 group, 3 tick/aux.
+ * bytes_out4: [1] algorithmic bytes of the scatter (48 B per
+ * record emitted), [0] 16 B per delivered record read, [2] 0, [3] k_link's
+ * device-counted implementation bytes. */
 int bcsim_reset_kernel_stats(bcsim_sim* s);
 int bcsim_read_kernel_stats(bcsim_sim* s, double* us_out4, double* bytes_out4,
                             uint64_t* launches_out4);
