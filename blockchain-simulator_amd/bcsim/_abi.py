@@ -17,7 +17,7 @@ OK = 0
 ERRORS = {
     -1: "E_INVAL", -2: "E_NOMEM", -3: "E_HIP", -4: "E_OVERFLOW",
     -5: "E_UNSUPPORTED", -6: "E_ENCODING", -7: "E_TIE", -8: "E_NODEVICE",
-    -9: "E_STATE", -10: "E_INDEX",
+    -9: "E_STATE", -10: "E_INDEX", -11: "E_PEER",
 }
 
 TR = dict(

@@ -17,6 +17,7 @@ import ctypes as C
 
 from . import _abi
 
+PEER_ERR = 1 << 62  # send count of a failed rank (include/bcsim.h bcsim_transport)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_uint32, C.c_int32)
 ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p,
                            C.c_uint64, C.POINTER(C.c_uint64))
@@ -72,6 +73,10 @@ class TorchTransport:
             rows = [torch.empty(P, dtype=torch.int64) for _ in range(P)]
             self.dist.all_gather(rows, sz, group=self.group)
             mat = torch.stack(rows)
+            if bool((mat >= PEER_ERR).any()):  # a rank failed: counts only, no payload
+                for r in range(P):
+                    recv_bytes[r] = int(mat[r, self.rank])
+                return 0
             width = max(1, int(mat.sum(dim=1).max()))
             buf = torch.zeros(width, dtype=torch.uint8)
             tot = sum(sb)

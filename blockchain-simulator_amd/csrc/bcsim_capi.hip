@@ -63,6 +63,7 @@ struct Sim {
   std::vector<uint32_t> xcnt;  // extras counts (host view)
   int x_active = 0;            // extras of the grouped cell are in xgrp
   uint32_t bs_scan = 64, bs_link = 64;
+  long long dbg_fail_cell = -1;  // test hook (BCSIM_DBG_FAIL_CELL): this rank fails at that cell
   long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
   long long n_alive = 0;
   uint64_t cells = 0;
@@ -619,6 +620,7 @@ static int setup_device(Sim& s) {
     HIPCHK(hipMemset(p.wgs, 0, NT * 64));
   }
   p.dbg_tmax = LLONG_MIN;
+  if (const char* fv = std::getenv("BCSIM_DBG_FAIL_CELL"); fv && *fv) s.dbg_fail_cell = std::atoll(fv);
   if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -817,19 +819,27 @@ static int readback(Sim& s) {
 // ---- multi-GPU steps (all ranks call them in the same order) -------------
 // Records for other ranks' receivers, staged by k_link during the cell, go
 // out in one all-to-all; k_import places what came in.
-static int exchange(Sim& s, long long cell) {
+// `lrc` is this rank's status of the cell so far: a failed rank sends the kPeerErr
+// count to everyone instead of data, so every rank leaves together (no rank is left
+// waiting in a collective the failed one never joins).
+static int exchange(Sim& s, long long cell, int lrc) {
   std::vector<uint64_t> sb(s.P), rb(s.P);
-  for (uint32_t r = 0; r < s.P; ++r) {
+  for (uint32_t r = 0; r < s.P && !lrc; ++r)
     if (s.scnt_h[r] > s.kp.cap_send) {
       g_detail = "multi-GPU send list overflowed";
-      return BCSIM_E_OVERFLOW;
+      lrc = BCSIM_E_OVERFLOW;
     }
-    sb[r] = static_cast<uint64_t>(s.scnt_h[r]) * sizeof(XRec);
-  }
+  for (uint32_t r = 0; r < s.P; ++r) sb[r] = lrc ? kPeerErr : static_cast<uint64_t>(s.scnt_h[r]) * sizeof(XRec);
   int rc = s.xp->alltoallv_dev(s.stream, reinterpret_cast<const char*>(s.kp.sendbuf),
                                static_cast<uint64_t>(s.kp.cap_send) * sizeof(XRec), sb.data(),
                                reinterpret_cast<char*>(s.recvbuf), s.cap_recv * sizeof(XRec), rb.data());
   if (rc) return rc;
+  if (lrc) return lrc;
+  for (uint32_t r = 0; r < s.P; ++r)
+    if (rb[r] == kPeerErr) {
+      g_detail = "rank " + std::to_string(r) + " of the partition failed";
+      return BCSIM_E_PEER;
+    }
   HIPCHK(hipMemsetAsync(s.kp.send_cnt, 0, 4ull * kMaxRanks, s.stream));
   uint64_t n = 0;
   for (uint32_t r = 0; r < s.P; ++r) n += rb[r] / sizeof(XRec);
@@ -843,7 +853,12 @@ static int exchange(Sim& s, long long cell) {
 
 // Share the v-log entries written since the last sync (PBFT file-scope `v`,
 // pbft-node.cc:26, written by VIEW_CHANGE receipts on every node).
-static int sync_vlog(Sim& s) {
+static int sync_vlog(Sim& s, int lrc = 0) {
+  if (lrc) {  // tell the other ranks (their SUM goes negative), then leave
+    int64_t bad = -(1ll << 40);
+    int rc = s.xp->allreduce_i64(s.stream, &bad, 1, 1);
+    return rc ? rc : lrc;
+  }
   uint32_t cnt = 0;
   HIPCHK(hipMemcpyAsync(&cnt, s.kp.vlog_cnt, 4, hipMemcpyDeviceToHost, s.stream));
   HIPCHK(hipStreamSynchronize(s.stream));
@@ -859,6 +874,10 @@ static int sync_vlog(Sim& s) {
   int64_t tot = mine;
   int rc = s.xp->allreduce_i64(s.stream, &tot, 1, 1);
   if (rc) return rc;
+  if (tot < 0) {
+    g_detail = "another rank of the partition failed";
+    return BCSIM_E_PEER;
+  }
   std::vector<char> rcv(static_cast<size_t>(tot) * sizeof(VLog) + 16);
   rc = s.xp->alltoallv_host(s.stream, snd.data(), sb.data(), rcv.data(), rcv.size(), rb.data());
   if (rc) return rc;
@@ -920,6 +939,20 @@ static int run(Sim& s, int64_t t_until) {
   if (s.cfg.t_end_ns > 0 && s.cfg.t_end_ns < lim) lim = s.cfg.t_end_ns;
   s.trace_valid = false;
   const long long L = s.L;
+  // multi-GPU: a rank-local failure is never returned on its own between two
+  // collectives; it rides the next one (next-cell MIN, the exchange counts, the v-log
+  // SUM) so that every rank returns together (BCSIM_E_PEER on the others)
+  int lerr = 0;
+#define LOCAL(x)                                  \
+  do {                                            \
+    if (!lrc) {                                   \
+      hipError_t e_ = (x);                        \
+      if (e_ != hipSuccess) {                     \
+        g_detail = std::string(#x) + ": " + hipGetErrorString(e_); \
+        lrc = BCSIM_E_HIP;                        \
+      }                                           \
+    }                                             \
+  } while (0)
   for (;;) {
     // earliest cell with work
     long long c = LLONG_MAX;
@@ -936,10 +969,17 @@ static int run(Sim& s, int64_t t_until) {
     if (s.ov_min != LLONG_MAX) c = std::min(c, s.ov_min);
     if (s.n_alive > 0 && s.next_tick != INT64_MAX) c = std::min(c, s.next_tick / L);
     if (s.stop_pending && s.cfg.stop_ns >= 0 && s.cfg.stop_ns >= s.t_done) c = std::min(c, s.cfg.stop_ns / L);
-    if (s.xp) {  // the next cell of the whole system
-      int64_t cv = c;
-      if ((rc = s.xp->allreduce_i64(s.stream, &cv, 1, 0))) return rc;
-      c = cv;
+    if (s.xp) {  // the next cell of the whole system, and every rank's status
+      int64_t cv[2] = {c, lerr};
+      if ((rc = s.xp->allreduce_i64(s.stream, cv, 2, 0))) return rc;
+      if (cv[1] < 0) {
+        if (lerr) return lerr;
+        g_detail = "another rank of the partition failed";
+        return BCSIM_E_PEER;
+      }
+      c = cv[0];
+    } else if (lerr) {
+      return lerr;
     }
     if (c == LLONG_MAX || c * L >= lim) {
       if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
@@ -952,47 +992,51 @@ static int run(Sim& s, int64_t t_until) {
       if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
       break;
     }
-    if (s.grouped_cell != c) {
-      if ((rc = group_cell(s, c))) return rc;
-    }
+    int lrc = 0;  // this rank's status of the cell
+    if (s.grouped_cell != c) lrc = group_cell(s, c);
     const bool tick = s.cfg.protocol == BCSIM_PBFT && s.n_alive > 0 && s.next_tick >= lo && s.next_tick < hi;
     if (tick) {
       const long long tk = s.next_tick;
-      if (tk > lo) {
-        if ((rc = do_scan(s, c, lo, tk, cs, false))) return rc;
-      }
+      if (!lrc && tk > lo) lrc = do_scan(s, c, lo, tk, cs, false);
       if (s.xp) {
-        if ((rc = sync_vlog(s)) || (rc = sync_leaders(s))) return rc;
+        if ((rc = sync_vlog(s, lrc)) || (rc = sync_leaders(s))) return rc;
+      } else if (lrc) {
+        return lrc;
       }
-      HIPCHK(hipMemsetAsync(s.kp.scal + 2, 0, 8, s.stream));
-      if ((rc = launch(s, KS_AUX, k_pbft_tick, dim3(s.R), dim3(1024), static_cast<size_t>(s.N), s.kp_dev, tk)))
-        return rc;
-      if ((rc = do_scan(s, c, tk, hi, cs, hi == ce))) return rc;
-    } else {
-      if ((rc = do_scan(s, c, lo, hi, cs, hi == ce))) return rc;
+      LOCAL(hipMemsetAsync(s.kp.scal + 2, 0, 8, s.stream));
+      if (!lrc)
+        lrc = launch(s, KS_AUX, k_pbft_tick, dim3(s.R), dim3(1024), static_cast<size_t>(s.N), s.kp_dev, tk);
+      if (!lrc) lrc = do_scan(s, c, tk, hi, cs, hi == ce);
+    } else if (!lrc) {
+      lrc = do_scan(s, c, lo, hi, cs, hi == ce);
     }
-    if (s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC) {
-      if ((rc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp_dev, 0u))) return rc;
-    }
+    if (!lrc && s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC)
+      lrc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp_dev, 0u);
     const uint32_t nbn = static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
-    if ((rc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev))) return rc;
+    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev);
     if (hi == ce) {
       // cell finished: its bucket is free again
-      HIPCHK(hipMemsetAsync(s.kp.bucket_cnt + (c % s.B), 0, 4, s.stream));
-      HIPCHK(hipMemsetAsync(s.kp.x_cnt + (c % s.B), 0, 4, s.stream));
+      LOCAL(hipMemsetAsync(s.kp.bucket_cnt + (c % s.B), 0, 4, s.stream));
+      LOCAL(hipMemsetAsync(s.kp.x_cnt + (c % s.B), 0, 4, s.stream));
       if (s.kp.mesh)  // receiver-tile flags of the bucket (every node of the cell has run)
-        HIPCHK(hipMemsetAsync(s.kp.rtile + static_cast<size_t>(c % s.B) * s.R * s.kp.n_tiles, 0,
-                              static_cast<size_t>(s.R) * s.kp.n_tiles, s.stream));
+        LOCAL(hipMemsetAsync(s.kp.rtile + static_cast<size_t>(c % s.B) * s.R * s.kp.n_tiles, 0,
+                             static_cast<size_t>(s.R) * s.kp.n_tiles, s.stream));
     }
-    if ((rc = readback(s))) return rc;
+    if (!lrc) lrc = readback(s);
+    if (!lrc && s.dbg_fail_cell >= 0 && static_cast<long long>(s.cells) >= s.dbg_fail_cell) {
+      g_detail = "injected failure (BCSIM_DBG_FAIL_CELL)";  // test hook: one rank fails alone
+      lrc = BCSIM_E_OVERFLOW;
+    }
+    if (!s.xp && lrc) return lrc;
+    if (s.xp) {  // ship records for other ranks' nodes, place the received ones
+      if ((rc = exchange(s, c, lrc))) return rc;
+      lerr = readback(s);  // a failure here rides the next cell's MIN
+    }
     if (tick) {
-      int64_t na = s.ctl_h->scal[2];
+      int64_t na = lerr ? 0 : s.ctl_h->scal[2];
       if (s.xp && (rc = s.xp->allreduce_i64(s.stream, &na, 1, 1))) return rc;
       s.n_alive = na;
       s.next_tick += s.kp.pbft_period;
-    }
-    if (s.xp) {  // ship records for other ranks' nodes, place the received ones
-      if ((rc = exchange(s, c)) || (rc = readback(s))) return rc;
     }
     s.start_pending = false;
     if (s.cfg.stop_ns >= 0 && s.cfg.stop_ns < hi) s.stop_pending = false;
@@ -1005,6 +1049,7 @@ static int run(Sim& s, int64_t t_until) {
       s.x_active = 0;
     }
   }
+#undef LOCAL
   if (s.xp && s.cfg.protocol == BCSIM_PBFT && (rc = sync_vlog(s))) return rc;
   return BCSIM_OK;
 }
@@ -1274,6 +1319,7 @@ const char* bcsim_strerror(int code) {
     case BCSIM_E_NODEVICE: return "no HIP device";
     case BCSIM_E_STATE: return "call out of order";
     case BCSIM_E_INDEX: return "PBFT tx[] index out of range";
+    case BCSIM_E_PEER: return "another rank of the partition failed";
     default: return "unknown error";
   }
 }

@@ -13,6 +13,10 @@
 
 namespace bcsim {
 
+// byte count a failed rank sends in place of a segment size: a
+// transport that sees it in any count of an exchange moves no data and returns OK
+constexpr uint64_t kPeerErr = 1ull << 62;
+
 struct Xport {
   uint32_t rank = 0, nranks = 1;
   virtual ~Xport() = default;
@@ -73,7 +77,12 @@ struct RcclXport : Xport {
     HIPCHK(hipMemcpyAsync(recv_bytes, d_cnt + nranks, nranks * 8ull, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     uint64_t tot = 0;
-    for (uint32_t r = 0; r < nranks; ++r) tot += recv_bytes[r];
+    bool peer_err = false;
+    for (uint32_t r = 0; r < nranks; ++r) {
+      tot += recv_bytes[r];
+      peer_err = peer_err || recv_bytes[r] == kPeerErr || send_bytes[r] == kPeerErr;
+    }
+    if (peer_err) return BCSIM_OK;  // the caller reports it (every rank saw the count)
     if (tot > recv_cap) {
       g_detail = "multi-GPU receive buffer too small";
       return BCSIM_E_OVERFLOW;
@@ -139,7 +148,15 @@ struct CbXport : Xport {
   int alltoallv_dev(hipStream_t st, const char* send_dev, uint64_t stride, const uint64_t* send_bytes,
                     char* recv_dev, uint64_t recv_cap, uint64_t* recv_bytes) override {
     uint64_t tot = 0;
-    for (uint32_t r = 0; r < nranks; ++r) tot += send_bytes[r];
+    bool err = false;
+    for (uint32_t r = 0; r < nranks; ++r) {
+      err = err || send_bytes[r] == kPeerErr;
+      tot += err ? 0 : send_bytes[r];
+    }
+    if (err) {  // no payload: the callback still runs the count exchange
+      int rc = alltoallv_host(st, nullptr, send_bytes, nullptr, 0, recv_bytes);
+      return rc;
+    }
     hs.resize(std::max<uint64_t>(tot, 1));
     hr.resize(std::max<uint64_t>(recv_cap, 1));
     uint64_t off = 0;
@@ -151,7 +168,10 @@ struct CbXport : Xport {
     int rc = alltoallv_host(st, hs.data(), send_bytes, hr.data(), recv_cap, recv_bytes);
     if (rc) return rc;
     uint64_t rt = 0;
-    for (uint32_t r = 0; r < nranks; ++r) rt += recv_bytes[r];
+    for (uint32_t r = 0; r < nranks; ++r) {
+      if (recv_bytes[r] == kPeerErr) return BCSIM_OK;  // a peer failed: the caller reports it
+      rt += recv_bytes[r];
+    }
     if (rt > recv_cap) {
       g_detail = "multi-GPU receive buffer too small";
       return BCSIM_E_OVERFLOW;

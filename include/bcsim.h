@@ -67,7 +67,8 @@ enum {
   BCSIM_E_TIE = -7,          /* a tie-order precondition of the engine failed */
   BCSIM_E_NODEVICE = -8,     /* no HIP device */
   BCSIM_E_STATE = -9,        /* call out of order */
-  BCSIM_E_INDEX = -10        /* PBFT tx[] index out of range (reference UB) */
+  BCSIM_E_INDEX = -10,       /* PBFT tx[] index out of range (reference UB) */
+  BCSIM_E_PEER = -11         /* multi-GPU: another rank of the partition failed */
 };
 
 /* ---- configuration -------------------------------------------------------- */
@@ -234,7 +235,11 @@ typedef struct bcsim_transport {
   int (*allreduce_i64)(void* ctx, int64_t* v, uint32_t n, int32_t op);
   /* all-to-all-v of host bytes: send holds nranks consecutive segments of
    * send_bytes[r] bytes (segment r goes to rank r); recv gets the segments
-   * from ranks 0..nranks-1 back to back, recv_bytes[r] each (<= recv_cap) */
+   * from ranks 0..nranks-1 back to back, recv_bytes[r] each (<= recv_cap).
+   * A failed rank passes send_bytes[r] = 2^62 for every r and send = NULL:
+   * if any rank's count is 2^62, no payload moves, recv_bytes[r] is the count
+   * rank r sent (2^62 for the failed one) and the call returns 0, so every
+   * rank leaves the run together (BCSIM_E_PEER on the healthy ones). */
   int (*alltoallv)(void* ctx, const void* send, const uint64_t* send_bytes, void* recv, uint64_t recv_cap,
                    uint64_t* recv_bytes);
 } bcsim_transport;

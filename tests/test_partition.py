@@ -55,7 +55,15 @@ def _transport_worker(rank, world, port, q):
     # a receive buffer that is too small is an error, not a truncation
     small = (C.c_uint8 * 1)()
     rc_small = tr.struct.alltoallv(None, C.cast(sbuf, C.c_void_p), sb, C.cast(small, C.c_void_p), 1, rb)
-    q.put((rank, mn, sm, list(rb), got, rc_small))
+    # a failed rank (the last one) sends the PEER_ERR count and no payload: every rank's call
+    # returns 0 with the counts only, so all of them leave the engine run together
+    from bcsim.partition import PEER_ERR
+    fail = rank == world - 1
+    sb2 = (C.c_uint64 * world)(*([PEER_ERR] * world if fail else [len(x) for x in segs]))
+    rb2 = (C.c_uint64 * world)()
+    rc_peer = tr.struct.alltoallv(None, None if fail else C.cast(sbuf, C.c_void_p), sb2,
+                                  C.cast(recv, C.c_void_p), cap, rb2)
+    q.put((rank, mn, sm, list(rb), got, rc_small, rc_peer, list(rb2)))
     dist.destroy_process_group()
 
 
@@ -71,13 +79,14 @@ def test_torch_transport_gloo_world2():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, mn, sm, rb, got, rc_small in res:
+    for rank, mn, sm, rb, got, rc_small, rc_peer, rb2 in res:
         assert mn == [10, -1, 1 << 40]
         assert sm == [21, -1, 2 << 40]
         want = [(r + 1) * (rank + 1) for r in range(world)]
         assert rb == want
         assert got == b"".join(bytes([16 * r + rank]) * want[r] for r in range(world))
         assert rc_small != 0
+        assert rc_peer == 0 and rb2[world - 1] == 1 << 62
 
 
 def test_merge_matches_single_process_shape():
@@ -151,3 +160,45 @@ def test_rccl_transport_world1(engine_lib):
     for name in names:
         d = compare(oracle.run(allc[name], topology=topology(name)), got[name])
         assert d is None, f"{name}: {d}"
+
+
+def _fail_worker(rank, world, port, fail_rank, q):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "tests"), os.path.join(repo, "blockchain-simulator_amd")]
+    if rank == fail_rank:
+        os.environ["BCSIM_DBG_FAIL_CELL"] = "3"  # this rank alone fails at its 4th cell
+    import torch.distributed as dist
+    import bcsim
+    from parity_cases import cases
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    code = 0
+    try:
+        with bcsim.Simulator(cases()["pbft16_fixed_100"]) as s:
+            s.set_partition(dist, transport="host")
+            s.run()
+    except bcsim.EngineError as e:
+        code = e.code
+    q.put((rank, code))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_one_rank_failure_stops_every_rank(engine_lib):
+    """A rank-local failure (here injected) must end the run on every rank -- the failed
+    one with its own error, the others with E_PEER -- instead of leaving them blocked in
+    the next collective (include/bcsim.h bcsim_transport)."""
+    world, fail_rank = 2, 1
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_fail_worker, args=(r, world, port, fail_rank, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res[fail_rank] == -4  # BCSIM_E_OVERFLOW (injected)
+    assert res[1 - fail_rank] == -11  # BCSIM_E_PEER
