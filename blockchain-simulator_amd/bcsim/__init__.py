@@ -48,8 +48,26 @@ def lib():
         _LIB.bcsim_topology_random_regular.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64,
                                                        C.c_void_p, C.c_void_p]
         _LIB.bcsim_topology_random_regular.restype = C.c_int
+        _LIB.bcsim_format_trace_line.argtypes = [C.POINTER(TraceRec), C.c_void_p, C.c_char_p, C.c_uint64,
+                                                 C.POINTER(C.c_uint64)]
+        _LIB.bcsim_format_trace_line.restype = C.c_int
         partition.declare(_LIB)
     return _LIB
+
+
+def format_trace_line(rec, cfg=None):
+    """The reference's NS_LOG_INFO text of one trace record (tuple as returned by
+    trace()), byte for byte -- bcsim_format_trace_line (host code, no GPU)."""
+    r = TraceRec(t_ns=rec[1], key_ts=rec[2], key_origin=rec[3], key_sub=rec[4], replica=rec[0],
+                 node=rec[5], kind=rec[6], a=rec[7], b=rec[8], c=rec[9])
+    n = C.c_uint64(0)
+    cp = C.byref(cfg) if cfg is not None else None
+    lib().bcsim_format_trace_line(C.byref(r), cp, None, 0, C.byref(n))
+    buf = C.create_string_buffer(n.value + 1)
+    rc = lib().bcsim_format_trace_line(C.byref(r), cp, buf, n.value + 1, C.byref(n))
+    if rc:
+        raise EngineError(rc, "bcsim_format_trace_line")
+    return buf.raw[:n.value].decode("utf-8", errors="surrogateescape")
 
 
 def c_default_config(protocol=PBFT, n_nodes=8):

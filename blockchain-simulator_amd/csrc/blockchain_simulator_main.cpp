@@ -12,15 +12,19 @@
 using namespace bcsim;
 
 static int startSimulator(int N, uint32_t protocol, const std::string& rate, const std::string& delay,
-                          int64_t app_delay_ns, bool fixed, int rounds, bool quiet) {
+                          int64_t app_delay_ns, bool fixed, int rounds, bool quiet, int spread_us) {
   NodeContainer nodes;
   nodes.Create(N);
   NetworkHelper networkHelper(N, protocol);
   PointToPointHelper pointToPoint;
   pointToPoint.SetDeviceAttribute("DataRate", rate);   // :23
   pointToPoint.SetChannelAttribute("Delay", delay);    // :24
+  const int64_t base_ns = ParseTimeNs(delay);
   for (int i = 0; i < N; i++) {                         // :34-51 (j < i pairs)
     for (int j = 0; j < N && j != i; j++) {
+      if (spread_us > 0)  // heterogeneous links: the helper's Delay attribute changed per link
+        pointToPoint.SetChannelAttribute(
+            "Delay", std::to_string(base_ns + 1000ll * ((i * 7 + j * 3) % (spread_us + 1))) + "ns");
       pointToPoint.Install(i, j);
       networkHelper.m_nodesConnectionsIps[i].push_back(j);
       networkHelper.m_nodesConnectionsIps[j].push_back(i);
@@ -43,7 +47,8 @@ static int startSimulator(int N, uint32_t protocol, const std::string& rate, con
     return 1;
   }
   if (!quiet)
-    for (const auto& r : Simulator::Current()->Trace()) std::printf("%s\n", FormatTraceLine(r).c_str());
+    for (const auto& r : Simulator::Current()->Trace())  // NS_LOG_INFO(msg) prints msg + newline
+      std::printf("%s\n", FormatTraceLine(r, &cfg).c_str());
   bcsim_counters c = Simulator::Current()->Counters();
   std::printf("delivered=%llu echoes=%llu sends=%llu t_last_ns=%lld\n",
               static_cast<unsigned long long>(c.delivered_total), static_cast<unsigned long long>(c.echoes),
@@ -58,7 +63,7 @@ int main(int argc, char* argv[]) {
   std::string rate = "3Mbps", delay = "3ms";
   int64_t app_delay = 3000000;
   bool fixed = false, quiet = false;
-  int rounds = 0;
+  int rounds = 0, spread_us = 0;
   for (int k = 1; k < argc; ++k) {
     std::string a = argv[k];
     auto val = [&]() { return k + 1 < argc ? std::string(argv[++k]) : std::string(); };
@@ -71,11 +76,12 @@ int main(int argc, char* argv[]) {
     else if (a == "--fixed-app-delay-ns") { fixed = true; app_delay = std::atoll(val().c_str()); }
     else if (a == "--rounds") rounds = std::atoi(val().c_str());
     else if (a == "--quiet") quiet = true;
+    else if (a == "--delay-spread-us") spread_us = std::atoi(val().c_str());
     else {
       std::fprintf(stderr, "usage: %s [--nodes N] [--protocol pbft|raft|paxos|gossip] [--rate 3Mbps] [--delay 3ms]\n"
-                           "          [--fixed-app-delay-ns NS] [--rounds R] [--quiet]\n", argv[0]);
+                           "          [--fixed-app-delay-ns NS] [--rounds R] [--quiet] [--delay-spread-us K]\n", argv[0]);
       return 2;
     }
   }
-  return startSimulator(N, protocol, rate, delay, app_delay, fixed, rounds, quiet);
+  return startSimulator(N, protocol, rate, delay, app_delay, fixed, rounds, quiet, spread_us);
 }

@@ -1,9 +1,12 @@
 // network_helper.cpp — see include/network_helper.hpp.
 #include "../../include/network_helper.hpp"
 
+#include <algorithm>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <sstream>
 #include <stdexcept>
 
 namespace bcsim {
@@ -144,57 +147,95 @@ void Simulator::SetCurrent(Simulation* s) { g_current = s; }
 int Simulator::Run() { return g_current ? g_current->Run(INT64_MAX) : BCSIM_E_STATE; }
 void Simulator::Destroy() { g_current = nullptr; }
 
-std::string FormatTraceLine(const bcsim_trace_rec& r) {
-  char buf[256];
-  const double t = static_cast<double>(r.t_ns) / 1e9;
+// Simulator::Now().GetSeconds() streamed with the default ostream format (6 significant
+// digits, trailing zeros dropped), as every NS_LOG_INFO line of the reference prints it
+static std::string secs(int64_t t_ns) {
+  std::ostringstream o;
+  o << static_cast<double>(t_ns) / 1e9;
+  return o.str();
+}
+// a uint8_t data[3] payload streamed as a C string (raft-node.cc:399, paxos-node.cc:518):
+// data[0], intToChar(x), then the uninitialised data[2], read as NUL
+static std::string payload2(int c0, int32_t x, uint32_t encoding) {
+  std::string d(1, static_cast<char>(c0));
+  int32_t c1 = x + '0';
+  if (encoding == BCSIM_ENC_COMPAT) c1 = static_cast<int8_t>(static_cast<uint8_t>(c1));
+  const char b = static_cast<char>(static_cast<uint8_t>(c1 & 0xFF));
+  if (b != 0) d.push_back(b);
+  return d;
+}
+
+std::string FormatTraceLine(const bcsim_trace_rec& r, const bcsim_config* cfg) {
+  std::ostringstream o;
+  const std::string t = secs(r.t_ns);
+  const uint32_t enc = cfg ? cfg->encoding : BCSIM_ENC_EXTENDED;
   switch (r.kind) {
-    case BCSIM_TR_PBFT_COMMIT:
-      std::snprintf(buf, sizeof buf, "node %u in view %d committed #%d at %.9fs, value is %d", r.node, r.a, r.b, t, r.c);
+    case BCSIM_TR_PBFT_COMMIT:  // pbft-node.cc:259
+      o << "node " << r.node << " 在视图 " << r.a << " 中完成了第 " << r.b << " 次提交, 时间为 " << t
+        << "s, value is " << r.c << "\n";
       break;
-    case BCSIM_TR_PBFT_BLOCK:
-      std::snprintf(buf, sizeof buf, "leader node%u broadcasts block n=%d at %.9fs", r.node, r.a, t);
+    case BCSIM_TR_PBFT_BLOCK:  // pbft-node.cc:387
+      o << "主节点 node" << r.node << "开始广播区块, 时间为" << t << "s\n";
       break;
-    case BCSIM_TR_PBFT_STOP:
-      std::snprintf(buf, sizeof buf, " sent block %d at time: %.9fs (node %u stops)", r.a, t, r.node);
+    case BCSIM_TR_PBFT_STOP:  // pbft-node.cc:408
+      o << " 已经发送了第 " << r.a << "个区块 at time: " << t << "s";
       break;
-    case BCSIM_TR_PBFT_VIEW:
-      std::snprintf(buf, sizeof buf, "view-change done, leader is %d view is %d", r.b, r.a);
+    case BCSIM_TR_PBFT_VIEW:  // pbft-node.cc:278 (a = v, b = leader)
+      o << "view-change完成, 当前主节点为 " << r.b << "视图为 " << r.a;
       break;
-    case BCSIM_TR_RAFT_ELECTION:
-      std::snprintf(buf, sizeof buf, "node%u start election at time: %.9fs", r.node, t);
+    case BCSIM_TR_RAFT_ELECTION:  // raft-node.cc:399
+      o << "node" << r.node << " start election: " << payload2('2', static_cast<int32_t>(r.node), enc)
+        << " at time: " << t << "s";
       break;
-    case BCSIM_TR_RAFT_LEADER:
-      std::snprintf(buf, sizeof buf, "Node %u become leader! at time %.9fs", r.node, t);
+    case BCSIM_TR_RAFT_LEADER:  // raft-node.cc:212
+      o << "Node " << r.node << " become leader! at time " << t << "s";
       break;
-    case BCSIM_TR_RAFT_BLOCK:
-      std::snprintf(buf, sizeof buf, "At time %.9f leader finished block %d", t, r.a);
+    case BCSIM_TR_RAFT_BLOCK:  // raft-node.cc:246 (a = blockNum before the increment)
+      o << "At time " << t << " leader处理完一个区块 " << r.a;
       break;
-    case BCSIM_TR_RAFT_DONE:
-      std::snprintf(buf, sizeof buf, "node%u finished %d blocks at time: %.9fs", r.node, r.a, t);
+    case BCSIM_TR_RAFT_DONE:  // raft-node.cc:249
+      o << "node" << r.node << " 已经处理完 " << r.a << "个区块 at time: " << t << "s";
       break;
-    case BCSIM_TR_RAFT_PROPOSAL:
-      std::snprintf(buf, sizeof buf, "broadcast block: %d, time: %.9f s", r.a, t);
+    case BCSIM_TR_RAFT_PROPOSAL: {  // raft-node.cc:342, and :362 once round reaches the limit
+      o << "广播区块: " << r.a << ", time: " << t << " s";
+      const int32_t lim = cfg ? static_cast<int32_t>(cfg->raft_proposal_rounds) : 50;
+      if (r.a + 1 == lim) o << "\n" << "node" << r.node << " 已经发送了 " << lim << "个区块 at time: " << t << "s";
       break;
-    case BCSIM_TR_RAFT_STOP:
-      std::snprintf(buf, sizeof buf, "Blocks:%d Rounds:%d / At time %.9f Stop", r.a, r.b, t);
+    }
+    case BCSIM_TR_RAFT_STOP:  // raft-node.cc:122-123 (two NS_LOG_INFO lines)
+      o << "Blocks:" << r.a << " Rounds:" << r.b << "\n" << "At time " << t << " Stop";
       break;
-    case BCSIM_TR_PAXOS_COMMIT:
-      std::snprintf(buf, sizeof buf, "CLIENT COMMIT SUCCESS ##clinet ticket##: %d id: %u at time: %.9fs", r.a, r.node, t);
+    case BCSIM_TR_PAXOS_COMMIT:  // paxos-node.cc:339
+      o << "CLIENT COMMIT SUCCESS\n   ##clinet ticket##: " << r.a << " id: " << r.node << " at time: " << t << "s";
       break;
-    case BCSIM_TR_PAXOS_TICKET:
-      std::snprintf(buf, sizeof buf, "node%u require_ticket %d at %.9fs", r.node, r.a, t);
+    case BCSIM_TR_PAXOS_TICKET:  // paxos-node.cc:518
+      o << "node" << r.node << " require_data: " << payload2('0', r.a, enc);
       break;
-    case BCSIM_TR_GOSSIP_BLOCK:
-      std::snprintf(buf, sizeof buf, "node%u gossips block %d at %.9fs", r.node, r.a, t);
+    case BCSIM_TR_GOSSIP_BLOCK:  // build extension (no reference line)
+      o << "node" << r.node << " gossips block " << r.a << " at time: " << t << "s";
       break;
     case BCSIM_TR_GOSSIP_DELIVER:
-      std::snprintf(buf, sizeof buf, "node%u received block %d from node%d after %d hops at %.9fs", r.node, r.a, r.c,
-                    r.b, t);
+      o << "node" << r.node << " received block " << r.a << " from node" << r.c << " after " << r.b
+        << " hops at time: " << t << "s";
       break;
     default:
-      std::snprintf(buf, sizeof buf, "kind %u node %u t=%.9f a=%d b=%d c=%d", r.kind, r.node, t, r.a, r.b, r.c);
+      o << "kind " << r.kind << " node " << r.node << " at time: " << t << "s a=" << r.a << " b=" << r.b
+        << " c=" << r.c;
   }
-  return buf;
+  return o.str();
 }
 
 }  // namespace bcsim
+
+extern "C" int bcsim_format_trace_line(const bcsim_trace_rec* r, const bcsim_config* cfg, char* buf, uint64_t cap,
+                                       uint64_t* n_out) {
+  if (!r) return BCSIM_E_INVAL;
+  const std::string line = bcsim::FormatTraceLine(*r, cfg);
+  if (n_out) *n_out = line.size();
+  if (buf && cap) {
+    const size_t n = std::min<size_t>(line.size(), cap - 1);
+    std::memcpy(buf, line.data(), n);
+    buf[n] = 0;
+  }
+  return BCSIM_OK;
+}

@@ -216,6 +216,15 @@ int bcsim_read_status(bcsim_sim* s, bcsim_status* out);
 /* Replaces Simulator::Destroy (blockchain-simulator.cc:58). */
 int bcsim_destroy(bcsim_sim* s);
 
+/* Trace writer: the reference's NS_LOG_INFO message for
+ * one trace record -- original strings (pbft-node.cc:259,278,387,408;
+ * raft-node.cc:122-123,212,246,249,342,362,399; paxos-node.cc:339,518),
+ * GetSeconds() at default ostream precision, embedded newlines kept (NS_LOG
+ * appends the final one).  cfg may be NULL.  Host-only; writes at most cap-1
+ * bytes + NUL, *n_out = full length. */
+int bcsim_format_trace_line(const bcsim_trace_rec* r, const bcsim_config* cfg, char* buf, uint64_t cap,
+                            uint64_t* n_out);
+
 const char* bcsim_strerror(int code);
 /* Last HIP/engine diagnostic text (thread-unsafe, for logs). */
 const char* bcsim_last_error_detail(void);

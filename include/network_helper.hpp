@@ -124,8 +124,11 @@ struct Simulator {
   static void SetCurrent(Simulation* s);
 };
 
-// Format one trace record like the reference's NS_LOG_INFO line
-// (pbft-node.cc:259, raft-node.cc:212,246, paxos-node.cc:339, ...).
-std::string FormatTraceLine(const bcsim_trace_rec& r);
+// The reference's NS_LOG_INFO text of one trace record, byte for byte (pbft-node.cc:259,
+// 278,387,408; raft-node.cc:122-123,212,246,249,342,362,399; paxos-node.cc:339,518): the
+// original strings, GetSeconds() at the default ostream precision, embedded "\n" kept;
+// NS_LOG adds the final newline.  cfg (may be NULL) supplies the encoding and the Raft
+// proposal limit.  Same as bcsim_format_trace_line.
+std::string FormatTraceLine(const bcsim_trace_rec& r, const bcsim_config* cfg = nullptr);
 
 }  // namespace bcsim

@@ -75,6 +75,11 @@ def cases():
                                     stop_ns=-1, n_replicas=2),
         "gossip24_mesh": _cfg(GS, 24, delay_mode=F, app_delay_ns=0, pbft_rounds=3, pbft_block_bytes=600,
                               stop_ns=-1),
+        # heterogeneous per-edge propagation delays (prop_ns array, TOPOLOGY_PROP below)
+        "pbft12_hetero_prop": _cfg(P, 12, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=15),
+        "raft24_hetero_prop": _cfg(R, 24, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=3_000_000_000),
+        "gossip96_d6_hetero_prop": _cfg(GS, 96, delay_mode=F, app_delay_ns=2_000_000, pbft_rounds=4,
+                                        pbft_block_bytes=1200, stop_ns=-1),
         # the reference protocols on a non-mesh graph (CSR path without the mesh transpose)
         "pbft32_d6_ctr": _cfg(P, 32, delay_mode=J, rng_mode=K, seed=4, pbft_rounds=6, pbft_block_bytes=1500),
         "raft48_d6_ctr": _cfg(R, 48, delay_mode=J, rng_mode=K, seed=2, t_end_ns=3_000_000_000),
@@ -91,13 +96,38 @@ TOPOLOGY = {
 }
 
 
+# per-edge propagation delays: name -> (base ns, spread ns); symmetric per link
+TOPOLOGY_PROP = {
+    "pbft12_hetero_prop": (3_000_000, 700_000),
+    "raft24_hetero_prop": (2_500_000, 1_500_000),
+    "gossip96_d6_hetero_prop": (3_000_000, 2_000_000),
+}
+TOPOLOGY["gossip96_d6_hetero_prop"] = (96, 6, 11)
+
+
+def hetero_prop(row, col, base, spread):
+    """prop[e] for edge i -> col[e]: base + a hash of the unordered pair (same both ways)."""
+    import numpy as np
+    n = len(row) - 1
+    src = np.repeat(np.arange(n, dtype=np.int64), np.diff(np.asarray(row, dtype=np.int64)))
+    dst = np.asarray(col, dtype=np.int64)
+    lo, hi = np.minimum(src, dst), np.maximum(src, dst)
+    h = (lo * 2654435761 + hi * 40503) % 1000003
+    return (base + h * spread // 1000003).astype(np.int64)
+
+
 def topology(name):
-    """CSR (row_ptr, col_idx, None) of a case, or None for the full mesh."""
-    if name not in TOPOLOGY:
+    """CSR (row_ptr, col_idx, prop_ns or None) of a case, or None for the uniform full mesh."""
+    if name not in TOPOLOGY and name not in TOPOLOGY_PROP:
         return None
     import bcsim
-    row, col = bcsim.random_regular(*TOPOLOGY[name])
-    return row, col, None
+    if name in TOPOLOGY:
+        row, col = bcsim.random_regular(*TOPOLOGY[name])
+    else:
+        n = cases()[name].n_nodes
+        row, col = bcsim.full_mesh(n)
+    prop = hetero_prop(row, col, *TOPOLOGY_PROP[name]) if name in TOPOLOGY_PROP else None
+    return row, col, prop
 
 
 def compare(a, b):
