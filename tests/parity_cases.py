@@ -32,6 +32,8 @@ def cases():
                                     pbft_block_bytes=1000),
         # degree 99 > a 64-lane workgroup: strided per-edge loops (BCSIM_BS_LINK/BCSIM_BS_SCAN=64)
         "pbft100_fixed": _cfg(P, 100, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=6, pbft_block_bytes=3000),
+        # P=2 partition at n >= 512 (tests/test_partition.py)
+        "pbft512_small": _cfg(P, 512, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=3, pbft_block_bytes=1000),
         "pbft5_odd": _cfg(P, 5, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=20),
         "pbft12_jitter_ctr": _cfg(P, 12, delay_mode=J, rng_mode=K, seed=7, pbft_rounds=25),
         "pbft8_trunc": _cfg(P, 8, delay_mode=F, app_delay_ns=5_000_000, time_round=_abi.TIME_TRUNC,

@@ -123,6 +123,18 @@ def test_partitioned_matches_oracle(world, engine_lib):
         assert d is None, f"{name} world={world}: {d}"
 
 
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_partitioned_n512_matches_oracle(engine_lib):
+    """SURVEY.md §8e at a size where each rank owns 256 nodes x 511 in-edges."""
+    import partition_run
+    name = "pbft512_small"
+    merged, err = partition_run.run(2, [name], transport="host", timeout=240)[name]
+    assert err is None, err
+    d = compare(oracle.run(cases()[name]), merged)
+    assert d is None, d
+
+
 def _rccl1_worker(port, names, q):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
