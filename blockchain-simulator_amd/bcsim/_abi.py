@@ -12,6 +12,7 @@ DELAY_FIXED, DELAY_RANDOM = 0, 1
 RNG_GLIBC, RNG_COUNTER = 0, 1
 TIME_ROUND, TIME_TRUNC = 0, 1
 ENC_EXTENDED, ENC_COMPAT = 0, 1
+QUEUE_INFINITE, QUEUE_DROPTAIL = 0, 1
 
 OK = 0
 ERRORS = {
@@ -66,7 +67,11 @@ class Config(C.Structure):
         ("n_buckets", C.c_uint32),
         ("cap_timers_per_node", C.c_uint32),
         ("max_events", C.c_uint64),
-        ("reserved", C.c_uint32 * 8),
+        ("queue_model", C.c_uint32),
+        ("queue_dev_pkts", C.c_uint32),
+        ("queue_disc_pkts", C.c_uint32),
+        ("cap_queue_msgs", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
     ]
 
 
@@ -96,7 +101,9 @@ class Counters(C.Structure):
         ("events", C.c_uint64),
         ("t_last_ns", C.c_int64),
         ("trace_records", C.c_uint64),
-        ("reserved", C.c_uint64 * 7),
+        ("frames_dropped", C.c_uint64),
+        ("msgs_lost", C.c_uint64),
+        ("reserved", C.c_uint64 * 5),
     ]
 
 
@@ -142,6 +149,9 @@ def default_config(protocol=PBFT, n_nodes=8):
     c.raft_proposal_rounds = 50
     c.raft_proposal_delay_ns = 1_000_000_000
     c.paxos_proposers = 3
+    c.queue_model = QUEUE_INFINITE
+    c.queue_dev_pkts = 100               # DropTailQueue "100p" (PointToPointNetDevice)
+    c.queue_disc_pkts = 1000             # pfifo_fast "1000p"
     return c
 
 

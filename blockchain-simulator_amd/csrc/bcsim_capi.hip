@@ -154,6 +154,8 @@ static int validate(const bcsim_config& c) {
   if (c.abi_version != BCSIM_ABI_VERSION) return BCSIM_E_INVAL;
   if (c.protocol > BCSIM_GOSSIP || c.n_nodes < 2 || c.link_rate_bps == 0) return BCSIM_E_INVAL;
   if (c.mtu < 68) return BCSIM_E_INVAL;
+  if (c.queue_model > BCSIM_QUEUE_DROPTAIL) return BCSIM_E_INVAL;
+  if (c.queue_model == BCSIM_QUEUE_DROPTAIL && c.queue_dev_pkts + c.queue_disc_pkts == 0) return BCSIM_E_INVAL;
   if (c.delay_mode == BCSIM_DELAY_RANDOM && c.rng_mode == BCSIM_RNG_GLIBC) {
     // the global glibc stream is consumed at every send in event order; only
     // the oracle replays that serially
@@ -262,6 +264,14 @@ static int setup_device(Sim& s) {
   p.tx_last[0] = ms.last;
   p.tx_tot[1] = mb.total;
   p.tx_last[1] = mb.last;
+  const MsgTx* mt[2] = {&ms, &mb};
+  for (int k = 0; k < 2; ++k) {  // DROPTAIL frame model: F frames, full fragments of equal time
+    p.nfr[k] = mt[k]->frames;
+    p.tx_full[k] = mt[k]->frames > 1 ? (mt[k]->total - mt[k]->last) / (mt[k]->frames - 1) : mt[k]->total;
+  }
+  p.qmodel = c.queue_model == BCSIM_QUEUE_DROPTAIL ? 1u : 0u;
+  p.qcap_frames = c.queue_dev_pkts + c.queue_disc_pkts;
+  p.cap_q = c.cap_queue_msgs ? c.cap_queue_msgs : 256;
   p.pbft_period = fsec_to_ns(c.pbft_timeout_s, tr);
   p.raft_hb = fsec_to_ns(c.raft_heartbeat_s, tr);
   p.raft_prop_delay = c.raft_proposal_delay_ns;
@@ -508,6 +518,15 @@ static int setup_device(Sim& s) {
     if (!on) p.eslot = nullptr;
   }
   if ((rc = dalloc(s, &p.link, static_cast<size_t>(s.R) * s.E))) return rc;
+  {  // DROPTAIL link queues: ring of cap_q message entries per edge
+    const size_t ne = p.qmodel ? static_cast<size_t>(s.R) * s.E : 1;
+    if (p.cap_q > 65535) {
+      g_detail = "cap_queue_msgs must be < 65536";
+      return BCSIM_E_INVAL;
+    }
+    if ((rc = dalloc(s, &p.qmeta, ne)) || (rc = dalloc(s, &p.qring, ne * (p.qmodel ? p.cap_q : 1)))) return rc;
+    HIPCHK(hipMemset(p.qmeta, 0, ne * 8));
+  }
   const size_t n_rtile = p.mesh ? static_cast<size_t>(s.B) * s.R * p.n_tiles : 1;
   if ((rc = dalloc(s, &p.rtile, n_rtile))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
@@ -1138,6 +1157,8 @@ static int read_counters(Sim& s, bcsim_counters* out) {
     out->wrong_msgs += x[CNT_WRONG];
     out->events += x[CNT_EVENTS];
     out->t_last_ns = std::max<int64_t>(out->t_last_ns, static_cast<int64_t>(x[CNT_TLAST]));
+    out->frames_dropped += x[CNT_FDROP];
+    out->msgs_lost += x[CNT_LOST];
   }
   out->trace_records = std::min(ctl.trace_cnt, s.kp.cap_trace);
   return BCSIM_OK;
@@ -1199,6 +1220,9 @@ int bcsim_config_default(bcsim_config* c, uint32_t protocol, uint32_t n_nodes) {
   c->raft_proposal_rounds = 50;     // :361
   c->raft_proposal_delay_ns = 1000000000ll;  // :216 Seconds(1)
   c->paxos_proposers = 3;           // paxos-node.cc:136
+  c->queue_model = BCSIM_QUEUE_INFINITE;
+  c->queue_dev_pkts = 100;          // PointToPointNetDevice TxQueue DropTail "100p"
+  c->queue_disc_pkts = 1000;        // pfifo_fast "1000p" (default root queue disc)
   return BCSIM_OK;
 }
 

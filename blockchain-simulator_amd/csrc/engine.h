@@ -128,6 +128,8 @@ enum {
   CNT_WRONG,
   CNT_EVENTS,
   CNT_TLAST,            // max event time (atomicMax)
+  CNT_FDROP,            // DROPTAIL: frames refused by a full link queue
+  CNT_LOST,             // DROPTAIL: messages with a dropped fragment
   CNT_N
 };
 

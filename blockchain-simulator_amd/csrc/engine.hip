@@ -101,6 +101,13 @@ struct KP {
   int64_t prop_const;    // propagation delay of every edge, or -1 (per-edge array)
   // links
   uint64_t* link;  // per edge: busy_until << 16 | (arrival cell of the last record & 0xFFFF)
+  // DROPTAIL link queues: per edge a ring of the messages of its busy
+  // period, entry = start << 17 | big << 16 | accepted frames; meta = head | n << 16 |
+  // frames << 32
+  uint32_t qmodel, qcap_frames, cap_q;
+  uint32_t nfr[2];
+  int64_t tx_full[2];
+  uint64_t *qring, *qmeta;
   // inbox
   Rec* inbox;            // [B][R][E]  receiver-major (in-slot order)
   uint8_t* rtile;        // [B][R][n_tiles] full mesh: a record for a receiver of this 64-node
@@ -1920,6 +1927,49 @@ __device__ inline bool op_key_less(const Op& a, uint32_t sa, const Op& b, uint32
   return sa < sb;
 }
 
+// ---- DROPTAIL link queue (oracle/bcsim_oracle.c q_admit restated) ----------
+// frames of a queue entry that started transmission by time t
+__device__ inline uint32_t q_started(const KP& p, uint64_t ent, int64_t t) {
+  const int64_t s = static_cast<int64_t>(ent >> 17);
+  const uint32_t big = static_cast<uint32_t>(ent >> 16) & 1u, k = static_cast<uint32_t>(ent & 0xFFFFu);
+  if (t < s) return 0;
+  if (p.nfr[big] == 1) return k;
+  const int64_t j = (t - s) / p.tx_full[big] + 1;
+  return j < static_cast<int64_t>(k) ? static_cast<uint32_t>(j) : k;
+}
+// admit a message of class `big` enqueued at t that would start at `start`: pops the
+// entries whose frames all started, counts the waiting frames, accepts a prefix of the
+// message while fewer than qcap_frames frames wait; returns the accepted frame count
+__device__ inline uint32_t q_admit(const KP& p, uint64_t* ring, uint64_t& meta, int64_t t, int big, int64_t start) {
+  uint32_t head = static_cast<uint32_t>(meta & 0xFFFFu), n = static_cast<uint32_t>((meta >> 16) & 0xFFFFu);
+  uint32_t frames = static_cast<uint32_t>(meta >> 32);
+  while (n) {
+    const uint64_t e = ring[head];
+    const uint32_t k = static_cast<uint32_t>(e & 0xFFFFu);
+    if (q_started(p, e, t) != k) break;
+    frames -= k;
+    head = head + 1 == p.cap_q ? 0u : head + 1;
+    --n;
+  }
+  const uint32_t waiting = n ? frames - q_started(p, ring[head], t) : 0u;
+  const uint32_t F = p.nfr[big];
+  const uint32_t room = waiting >= p.qcap_frames ? 0u : p.qcap_frames - waiting;
+  const uint32_t k = room < F ? room : F;
+  if (k) {
+    if (n == p.cap_q) {
+      set_err(p, BCSIM_E_OVERFLOW);  // more queued messages on one link than cap_queue_msgs
+    } else {
+      uint32_t tail = head + n;
+      if (tail >= p.cap_q) tail -= p.cap_q;
+      ring[tail] = (static_cast<uint64_t>(start) << 17) | (static_cast<uint64_t>(big) << 16) | k;
+      ++n;
+      frames += k;
+    }
+  }
+  meta = head | (static_cast<uint64_t>(n) << 16) | (static_cast<uint64_t>(frames) << 32);
+  return k;
+}
+
 struct LinkShared {
   uint32_t n_bc, n_keep;
   uint32_t bc[kBcastCap];
@@ -2108,7 +2158,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
 
   if (p.wgt && tid == 0) ph[1] = __builtin_amdgcn_s_memrealtime();
   // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO, emit ----
-  unsigned long long n_rec = 0, st_edges = 0, st_echo = 0;
+  unsigned long long n_rec = 0, st_edges = 0, st_echo = 0, fdrop = 0, lost = 0;
   long long ovmin = LLONG_MAX;
   const long long cs = cell * p.L;
   const Rec* in_row = p.inbox + (static_cast<size_t>(ib) * p.R + rep) * p.E;
@@ -2174,6 +2224,12 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     // record through the extras list, which delivers it identically)
     int64_t bu = static_cast<int64_t>(lw >> 16);
     uint32_t lc = static_cast<uint32_t>(lw & 0xFFFFu);
+    uint64_t qm = 0;
+    uint64_t* qr = nullptr;
+    if (p.qmodel) {
+      qm = p.qmeta[eb0 + le];
+      qr = p.qring + (eb0 + le) * p.cap_q;
+    }
     const int64_t pr = p.prop_const >= 0 ? p.prop_const : prop[le];
     // in-slot of this edge in the receiver's row (full mesh: arithmetic)
     const uint32_t slot = p.mesh ? s * (p.N - 1) + (i < s ? i : i - 1) : AT(p.rev, e, p.E);
@@ -2224,6 +2280,16 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       const int big = (raw_flags(o) & OPF_BIG) ? 1 : 0;
       const int64_t ot = raw_t(o);
       const int64_t start = bu > ot ? bu : ot;
+      if (p.qmodel) {  // DROPTAIL: a refused fragment loses the message (its accepted prefix still occupies the link)
+        const uint32_t F = p.nfr[big];
+        const uint32_t k = q_admit(p, qr, qm, ot, big, start);
+        if (k < F) {
+          fdrop += F - k;
+          if (k) bu = start + static_cast<int64_t>(k) * p.tx_full[big];
+          if (!is_echo) ++lost;
+          continue;
+        }
+      }
       const int64_t end = start + p.tx_tot[big];
       bu = end;
       if (is_echo) continue;
@@ -2311,6 +2377,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     }
     if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
     lnk[le] = (static_cast<uint64_t>(bu) << 16) | lc;
+    if (p.qmodel) p.qmeta[eb0 + le] = qm;
   }
   if (cbn) atomicAdd(&L.lcnt[cb], cbn);
   __syncthreads();
@@ -2378,7 +2445,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   uint4 t1, t2;
   (void)block_scan4(make_uint4(static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends),
                                static_cast<uint32_t>(n_rec), static_cast<uint32_t>(st_ops)), L.wsum, t1);
-  (void)block_scan4(make_uint4(static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo), 0, 0), L.wsum, t2);
+  (void)block_scan4(make_uint4(static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo),
+                               static_cast<uint32_t>(fdrop), static_cast<uint32_t>(lost)), L.wsum, t2);
   if (tid == 0) {
     if (t1.x) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(t1.x));
     if (t1.y) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(t1.y));
@@ -2386,6 +2454,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     if (t1.w) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(t1.w));
     if (t2.x) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(t2.x));
     if (t2.y) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(t2.y));
+    if (t2.z) atomicAdd(&cnt[CNT_FDROP], static_cast<unsigned long long>(t2.z));
+    if (t2.w) atomicAdd(&cnt[CNT_LOST], static_cast<unsigned long long>(t2.w));
   }
   __syncthreads();
   for (uint32_t k = tid; k < B; k += blockDim.x)

@@ -54,6 +54,9 @@ enum { BCSIM_TIME_ROUND = 0, BCSIM_TIME_TRUNC = 1 };
 /* wire field encoding: COMPAT = intToChar/charToInt through signed char
  * (pbft-node.cc:57-63), EXTENDED = same +48 offset without the 8-bit wrap */
 enum { BCSIM_ENC_EXTENDED = 0, BCSIM_ENC_COMPAT = 1 };
+/* Link queue model: INFINITE = unbounded FIFO; DROPTAIL = at most queue_dev_pkts +
+ * queue_disc_pkts frames waiting per link, later frames dropped (fragment loss) */
+enum { BCSIM_QUEUE_INFINITE = 0, BCSIM_QUEUE_DROPTAIL = 1 };
 
 /* ---- status codes --------------------------------------------------------- */
 enum {
@@ -114,7 +117,15 @@ typedef struct bcsim_config {
   uint32_t n_buckets;          /* time-bucket ring length */
   uint32_t cap_timers_per_node;
   uint64_t max_events;         /* oracle guard (0 = unlimited) */
-  uint32_t reserved[8];
+  /* link queues: the PointToPointNetDevice
+   * DropTail TX queue ("100p", blockchain-simulator.cc:20-24) behind the root
+   * queue disc that address.Assign installs (:41-42; pfifo_fast "1000p" here,
+   * the ns-3 default is version dependent).  DESIGN.md §2.2. */
+  uint32_t queue_model;        /* BCSIM_QUEUE_INFINITE (default) / _DROPTAIL */
+  uint32_t queue_dev_pkts;     /* device queue limit, packets (100) */
+  uint32_t queue_disc_pkts;    /* queue-disc limit, packets (1000; 0 = none) */
+  uint32_t cap_queue_msgs;     /* GPU engine: queued messages per link (0 = 256) */
+  uint32_t reserved[4];
 } bcsim_config;
 
 /* ---- outputs -------------------------------------------------------------- */
@@ -158,7 +169,9 @@ typedef struct bcsim_counters {
   uint64_t events;                     /* protocol events processed */
   int64_t  t_last_ns;                  /* latest processed event time */
   uint64_t trace_records;
-  uint64_t reserved[7];
+  uint64_t frames_dropped;             /* DROPTAIL: frames refused by a full link queue */
+  uint64_t msgs_lost;                  /* DROPTAIL: messages with a dropped fragment (never delivered) */
+  uint64_t reserved[5];
 } bcsim_counters;
 
 typedef struct bcsim_status {

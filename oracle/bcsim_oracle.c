@@ -220,6 +220,18 @@ typedef struct {
   size_t n, cap;
 } oheap;
 
+/* DROPTAIL link queue: the messages of the link's current busy
+ * period, back to back in FIFO order; k = frames accepted (a prefix of the message) */
+typedef struct {
+  int64_t start;
+  uint32_t k, big;
+} qent;
+typedef struct {
+  qent* a;
+  uint32_t head, n, cap;
+  uint64_t frames; /* frames of the entries in the deque */
+} oqueue;
+
 struct bcsim_oracle {
   bcsim_config cfg;
   uint32_t N;
@@ -234,6 +246,9 @@ struct bcsim_oracle {
   int32_t *tx_val, *tx_pv, *tx_cv; /* N * seq_cap */
   uint8_t* gseen;        /* GOSSIP: N * seq_cap first-receipt flags */
   int64_t* busy;         /* per edge */
+  oqueue* q;             /* per edge (DROPTAIL only) */
+  uint32_t nfr[2];       /* frames per message class (small, big) */
+  int64_t tx_full[2];    /* time of a full (non-last) fragment frame */
   oheap heap;
   glibc_rng grng;
   int32_t g_v, g_n, g_nround; /* PBFT file-scope globals pbft-node.cc:24-30 */
@@ -467,10 +482,69 @@ static omsg mk(int32_t type, int32_t f0, int32_t f1, int32_t f2, int32_t big) {
   return m;
 }
 
-/* link FIFO: returns arrival, sets *ts_last */
+/* DROPTAIL: frames of queue entry e that started transmission by time t (frame j
+ * of a message starting at s starts at s + j * tx_full; a frame starting at t is
+ * no longer waiting) */
+static uint32_t q_started(const bcsim_oracle* o, const qent* e, int64_t t) {
+  if (t < e->start) return 0;
+  if (o->nfr[e->big] == 1) return e->k;
+  int64_t j = (t - e->start) / o->tx_full[e->big] + 1;
+  return j < (int64_t)e->k ? (uint32_t)j : e->k;
+}
+
+/* DROPTAIL admission at o->now of a message of class big that would start at
+ * `start`: frames are accepted while fewer than queue_dev_pkts + queue_disc_pkts
+ * frames wait on the link (pfifo_fast in front of the device queue, flow control;
+ * the frame in transmission does not count).  Returns the accepted prefix. */
+static uint32_t q_admit(bcsim_oracle* o, uint32_t edge, int big, int64_t start) {
+  oqueue* q = &o->q[edge];
+  while (q->n && q_started(o, &q->a[q->head], o->now) == q->a[q->head].k) {
+    q->frames -= q->a[q->head].k;
+    q->head = (q->head + 1) % q->cap;
+    --q->n;
+  }
+  uint64_t waiting = q->n ? q->frames - q_started(o, &q->a[q->head], o->now) : 0;
+  uint64_t cap = (uint64_t)o->cfg.queue_dev_pkts + o->cfg.queue_disc_pkts;
+  uint32_t F = o->nfr[big];
+  uint32_t k = waiting >= cap ? 0 : (uint32_t)((cap - waiting) < F ? (cap - waiting) : F);
+  if (!k) return 0;
+  if (q->n == q->cap) { /* grow the ring */
+    uint32_t nc = q->cap ? 2 * q->cap : 16;
+    qent* na = (qent*)malloc(nc * sizeof(qent));
+    if (!na) {
+      set_err(o, BCSIM_E_NOMEM);
+      return 0;
+    }
+    for (uint32_t i = 0; i < q->n; ++i) na[i] = q->a[(q->head + i) % q->cap];
+    free(q->a);
+    q->a = na;
+    q->head = 0;
+    q->cap = nc;
+  }
+  qent* e = &q->a[(q->head + q->n) % q->cap];
+  e->start = start;
+  e->k = k;
+  e->big = (uint32_t)big;
+  ++q->n;
+  q->frames += k;
+  return k;
+}
+
+/* link FIFO (+ DROPTAIL): returns the arrival time and sets *ts_last, or returns
+ * -1 if a fragment was dropped (the message is lost; its accepted frames still
+ * occupy the link) */
 static int64_t link_xmit(bcsim_oracle* o, uint32_t edge, int big,
                          int64_t* ts_last) {
   int64_t start = o->busy[edge] > o->now ? o->busy[edge] : o->now;
+  if (o->cfg.queue_model == BCSIM_QUEUE_DROPTAIL) {
+    uint32_t F = o->nfr[big];
+    uint32_t k = q_admit(o, edge, big, start);
+    if (k < F) {
+      o->cnt.frames_dropped += F - k;
+      if (k) o->busy[edge] = start + (int64_t)k * o->tx_full[big];
+      return -1;
+    }
+  }
   int64_t end = start + o->tx_tot[big];
   o->busy[edge] = end;
   *ts_last = end - o->tx_last[big];
@@ -944,8 +1018,12 @@ static void exec_event(bcsim_oracle* o, const oev* e) {
       }
       oev r;
       memset(&r, 0, sizeof r);
-      int64_t tsl;
+      int64_t tsl = 0;
       r.t = link_xmit(o, e->aux, e->m.big, &tsl);
+      if (r.t < 0) { /* fragment dropped by a full link queue: never delivered */
+        o->cnt.msgs_lost++;
+        break;
+      }
       r.ts = tsl;
       r.origin = i;
       r.sub = e->sub;
@@ -1014,6 +1092,13 @@ static int etrip_cmp(const void* x, const void* y) {
   return 0;
 }
 
+static void free_queues(bcsim_oracle* o) {
+  if (o->q && o->row)
+    for (uint32_t e = 0; e < o->row[o->N]; ++e) free(o->q[e].a);
+  free(o->q);
+  o->q = NULL;
+}
+
 int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
                                   const uint32_t* row_ptr,
                                   const uint32_t* col_idx,
@@ -1021,6 +1106,7 @@ int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
   if (!o || n != o->N || !row_ptr || !col_idx) return BCSIM_E_INVAL;
   if (o->started) return BCSIM_E_STATE;
   uint32_t E = row_ptr[n];
+  free_queues(o);
   free(o->row);
   free(o->col);
   free(o->rev);
@@ -1031,7 +1117,8 @@ int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
   o->rev = (uint32_t*)malloc((E ? E : 1) * sizeof(uint32_t));
   o->prop = (int64_t*)malloc((E ? E : 1) * sizeof(int64_t));
   o->busy = (int64_t*)calloc(E ? E : 1, sizeof(int64_t));
-  if (!o->row || !o->col || !o->rev || !o->prop || !o->busy) return BCSIM_E_NOMEM;
+  o->q = (oqueue*)calloc(E ? E : 1, sizeof(oqueue));
+  if (!o->row || !o->col || !o->rev || !o->prop || !o->busy || !o->q) return BCSIM_E_NOMEM;
   memcpy(o->row, row_ptr, (n + 1) * sizeof(uint32_t));
   memcpy(o->col, col_idx, E * sizeof(uint32_t));
   for (uint32_t e = 0; e < E; ++e)
@@ -1106,9 +1193,11 @@ int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
     o->big_bytes = 3;
   }
   oracle_msg_tx(o->small_bytes, o->cfg.mtu, o->cfg.link_rate_bps, mode,
-                &o->tx_tot[0], &o->tx_last[0], NULL, NULL);
+                &o->tx_tot[0], &o->tx_last[0], &o->nfr[0], NULL);
   oracle_msg_tx(o->big_bytes, o->cfg.mtu, o->cfg.link_rate_bps, mode,
-                &o->tx_tot[1], &o->tx_last[1], NULL, NULL);
+                &o->tx_tot[1], &o->tx_last[1], &o->nfr[1], NULL);
+  for (int k = 0; k < 2; ++k) /* full fragment frame: (mtu - 20) & ~7 IP payload + 22 */
+    o->tx_full[k] = o->nfr[k] > 1 ? (o->tx_tot[k] - o->tx_last[k]) / (o->nfr[k] - 1) : o->tx_tot[k];
   o->pbft_period = fsec_ns(o->cfg.pbft_timeout_s, mode);
   o->raft_hb = fsec_ns(o->cfg.raft_heartbeat_s, mode);
   for (int k = 0; k < 3; ++k) {
@@ -1161,6 +1250,11 @@ static void reset_replica(bcsim_oracle* o, uint32_t rep) {
   }
   if (o->gseen) memset(o->gseen, 0, (size_t)o->N * o->cfg.pbft_seq_cap);
   memset(o->busy, 0, (size_t)o->row[o->N] * sizeof(int64_t));
+  for (uint32_t e = 0; e < o->row[o->N]; ++e) {
+    o->q[e].head = 0;
+    o->q[e].n = 0;
+    o->q[e].frames = 0;
+  }
   o->heap.n = 0;
   glibc_seed(&o->grng, (uint32_t)(o->cfg.seed + rep));
   o->g_v = 1;
@@ -1281,6 +1375,7 @@ int bcsim_oracle_destroy(bcsim_oracle* o) {
   free(o->tx_pv);
   free(o->tx_cv);
   free(o->gseen);
+  free_queues(o);
   free(o->row);
   free(o->col);
   free(o->rev);

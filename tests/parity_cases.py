@@ -77,6 +77,16 @@ def cases():
                                     stop_ns=-1, n_replicas=2),
         "gossip24_mesh": _cfg(GS, 24, delay_mode=F, app_delay_ns=0, pbft_rounds=3, pbft_block_bytes=600,
                               stop_ns=-1),
+        # link queues (DROPTAIL): C1 with the device DropTail 100p + pfifo_fast
+        # 1000p (the saturated 50 KB leader links start dropping after ~2.7 s), the device
+        # queue alone, and a gossip graph with a 20-packet queue
+        "pbft16_droptail_100": _cfg(P, 16, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=100,
+                                    queue_model=_abi.QUEUE_DROPTAIL, t_end_ns=9_000_000_000),
+        "pbft16_devq_only": _cfg(P, 16, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=100,
+                                 queue_model=_abi.QUEUE_DROPTAIL, queue_disc_pkts=0, t_end_ns=5_000_000_000),
+        "gossip64_d4_droptail": _cfg(GS, 64, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=30, stop_ns=-1,
+                                     pbft_block_bytes=20000, queue_model=_abi.QUEUE_DROPTAIL, queue_dev_pkts=20,
+                                     queue_disc_pkts=0),
         # heterogeneous per-edge propagation delays (prop_ns array, TOPOLOGY_PROP below)
         "pbft12_hetero_prop": _cfg(P, 12, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=15),
         "raft24_hetero_prop": _cfg(R, 24, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=3_000_000_000),
@@ -94,6 +104,7 @@ TOPOLOGY = {
     "gossip200_d8_jitter_ctr": (200, 8, 5),
     "gossip512_d8_blocks": (512, 8, 1),
     "pbft32_d6_ctr": (32, 6, 3),
+    "gossip64_d4_droptail": (64, 4, 1),
     "raft48_d6_ctr": (48, 6, 8),
 }
 
@@ -144,7 +155,7 @@ def compare(a, b):
             msgs.append(f"first trace diff at {k}: {x} != {y}")
             break
     for key in ("delivered", "delivered_total", "echoes", "sends", "dropped", "wrong_msgs", "events",
-                "t_last_ns", "trace_records"):
+                "t_last_ns", "trace_records", "frames_dropped", "msgs_lost"):
         if ca[key] != cb[key]:
             msgs.append(f"counter {key}: {ca[key]} != {cb[key]}")
     return "; ".join(msgs) if msgs else None
