@@ -138,7 +138,9 @@ def test_oracle_trace_fixture(name):
         setattr(c, k, v)
     tr, cnt, st = oracle.run(c)
     assert [list(r) for r in tr] == gold["trace"]
-    assert cnt == gold["counters"]
+    # counters added after the fixture was made (link-queue drops) are zero there
+    assert {k: cnt[k] for k in gold["counters"]} == gold["counters"]
+    assert all(cnt[k] == 0 for k in cnt if k not in gold["counters"])
 
 
 def test_paxos_offbyone_broadcast():
