@@ -71,7 +71,8 @@ class Config(C.Structure):
         ("queue_dev_pkts", C.c_uint32),
         ("queue_disc_pkts", C.c_uint32),
         ("cap_queue_msgs", C.c_uint32),
-        ("reserved", C.c_uint32 * 4),
+        ("paxos_decrees", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 

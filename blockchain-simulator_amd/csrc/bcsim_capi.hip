@@ -492,12 +492,15 @@ static int setup_device(Sim& s) {
   p.acv = ibuf + 5 * NT;
   p.blockNum = ibuf + 6 * NT;
   p.round = ibuf + 7 * NT;
-  p.t_max = ibuf + 8 * NT;
-  p.command = ibuf + 9 * NT;
-  p.t_store = ibuf + 10 * NT;
+  p.decree = ibuf + 8 * NT;
   p.ticket = ibuf + 11 * NT;
-  p.is_commit = ibuf + 12 * NT;
   p.proposal = ibuf + 13 * NT;
+  p.K = c.paxos_decrees ? c.paxos_decrees : 1;
+  {  // Paxos acceptor state per decree (START initialises it)
+    const size_t npx = c.protocol == BCSIM_PAXOS ? static_cast<size_t>(NT) * p.K * 4 : 4;
+    if ((rc = dalloc(s, &p.px, npx))) return rc;
+    HIPCHK(hipMemset(p.px, 0, npx * 4));
+  }
   if ((rc = dalloc(s, &p.next_election, NT)) || (rc = dalloc(s, &p.next_heartbeat, NT))) return rc;
   if ((rc = dalloc(s, &p.timers, NT * p.cap_timers)) || (rc = dalloc(s, &p.ops, NT * p.cap_ops)) ||
       (rc = dalloc(s, &p.n_ops, NT)))

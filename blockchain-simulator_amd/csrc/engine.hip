@@ -78,7 +78,9 @@ struct KP {
   // Raft / Paxos
   int32_t *is_leader, *has_voted, *m_value, *vote_s, *vote_f, *acv, *blockNum, *round;
   uint32_t *next_election, *next_heartbeat;
-  int32_t *t_max, *command, *t_store, *ticket, *is_commit, *proposal;
+  int32_t *ticket, *proposal, *decree;
+  int32_t* px;   // Paxos acceptor state [NT][K][4]: t_max, command, t_store, isCommit (per decree)
+  uint32_t K;    // Paxos decrees (>= 1)
   // Gossip (BCSIM_GOSSIP): first-receipt flag per (gnode, sequence); origin tick count in round[]
   uint8_t* gseen;
   // timers / ops
@@ -902,14 +904,25 @@ enum {
 };
 
 struct PaxosState {
-  int32_t t_max, command, t_store, ticket, is_commit, proposal, vs, vf;
+  int32_t ticket, proposal, vs, vf, decree;
 };
+
+// acceptor state of this node for decree d (carried in data[3] = f2 by every Paxos
+// message: outside the reference's 3-byte packet, 0 for the single decree)
+__device__ inline int32_t* px_of(Ctx& c, int32_t d) {
+  const KP& p = *c.p;
+  if (d < 0 || static_cast<uint32_t>(d) >= p.K) {
+    set_err(p, BCSIM_E_INDEX);
+    d = 0;
+  }
+  return &AT(p.px, (static_cast<size_t>(c.g) * p.K + static_cast<uint32_t>(d)) * 4, static_cast<uint64_t>(p.NT) * p.K * 4);
+}
 
 __device__ void paxos_ticket(Ctx& c, PaxosState& s) {  // requireTicket :510-522
   const KP& p = *c.p;
   ++s.ticket;
-  ctx_bcast(c, mkmsg(PX_REQ_TICKET, enc_raw(p, s.ticket), 0, 0, 0), true);
-  ctx_trace(c, BCSIM_TR_PAXOS_TICKET, s.ticket, 0, 0);
+  ctx_bcast(c, mkmsg(PX_REQ_TICKET, enc_raw(p, s.ticket), 0, s.decree, 0), true);
+  ctx_trace(c, BCSIM_TR_PAXOS_TICKET, s.ticket, s.decree, 0);
 }
 
 __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t back_edge) {
@@ -919,41 +932,45 @@ __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t back_ed
   switch (ty) {
     case PX_REQ_TICKET: {  // :177-198
       const int32_t t = c2i(mch(m, 1));
+      int32_t* a = px_of(c, m.f[2]);
       Msg r;
-      if (t > s.t_max) {
-        s.t_max = t;
-        r = mkmsg(PX_RES_TICKET, enc_raw(p, 0), s.command, 0, 0);
+      if (t > a[0]) {
+        a[0] = t;
+        r = mkmsg(PX_RES_TICKET, enc_raw(p, 0), a[1], m.f[2], 0);
       } else {
-        r = mkmsg(PX_RES_TICKET, enc_raw(p, 1), 0, 0, 0);
+        r = mkmsg(PX_RES_TICKET, enc_raw(p, 1), 0, m.f[2], 0);
       }
       ctx_unicast(c, back_edge, r);
       break;
     }
     case PX_REQ_PROPOSE: {  // :199-221
       const int32_t t = c2i(mch(m, 1));
+      int32_t* a = px_of(c, m.f[2]);
       int32_t st = 1;
-      if (t == s.t_max) {
-        s.command = mch(m, 2);
-        s.t_store = t;
+      if (t == a[0]) {
+        a[1] = mch(m, 2);
+        a[2] = t;
         st = 0;
       }
-      ctx_unicast(c, back_edge, mkmsg(PX_RES_PROPOSE, enc_raw(p, st), 0, 0, 0));
+      ctx_unicast(c, back_edge, mkmsg(PX_RES_PROPOSE, enc_raw(p, st), 0, m.f[2], 0));
       break;
     }
     case PX_REQ_COMMIT: {  // :222-247
       const int32_t t = c2i(mch(m, 1));
       const int32_t cc = mch(m, 2);
+      int32_t* a = px_of(c, m.f[2]);
       int32_t st = 1;
-      if (t == s.t_store && cc == s.command) {
-        s.is_commit = 1;
+      if (t == a[2] && cc == a[1]) {
+        a[3] = 1;
         st = 0;
       }
-      ctx_unicast(c, back_edge, mkmsg(PX_RES_COMMIT, enc_raw(p, st), 0, 0, 0));
+      ctx_unicast(c, back_edge, mkmsg(PX_RES_COMMIT, enc_raw(p, st), 0, m.f[2], 0));
       break;
     }
     case PX_RES_TICKET:
     case PX_RES_PROPOSE:
     case PX_RES_COMMIT: {  // :248-353
+      if (m.f[2] != s.decree) break;  // a response of a finished decree: not counted
       if (c2i(mch(m, 1)) == 0)
         ++s.vs;
       else
@@ -964,11 +981,17 @@ __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t back_ed
           s.vf = 0;
           if (ty == PX_RES_TICKET) {
             if (mch(m, 2) != 'e') s.proposal = mch(m, 2);
-            ctx_bcast(c, mkmsg(PX_REQ_PROPOSE, enc_raw(p, s.ticket), s.proposal, 0, 0), true);
+            ctx_bcast(c, mkmsg(PX_REQ_PROPOSE, enc_raw(p, s.ticket), s.proposal, s.decree, 0), true);
           } else if (ty == PX_RES_PROPOSE) {
-            ctx_bcast(c, mkmsg(PX_REQ_COMMIT, enc_raw(p, s.ticket), s.proposal, 0, 0), true);
+            ctx_bcast(c, mkmsg(PX_REQ_COMMIT, enc_raw(p, s.ticket), s.proposal, s.decree, 0), true);
           } else {
-            ctx_trace(c, BCSIM_TR_PAXOS_COMMIT, s.ticket, 0, 0);
+            ctx_trace(c, BCSIM_TR_PAXOS_COMMIT, s.ticket, s.decree, 0);
+            if (static_cast<uint32_t>(s.decree) + 1 < p.K) {  // next decree: fresh ticket and proposal
+              s.decree += 1;
+              s.ticket = 0;
+              s.proposal = enc_raw(p, static_cast<int32_t>(c.i));
+              paxos_ticket(c, s);
+            }
           }
         } else {
           s.vs = 0;
@@ -1624,12 +1647,9 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     } else if (PROTO == BCSIM_GOSSIP) {
       gs_round = AT(p.round, g, p.NT);
     } else {
-      xs_.t_max = AT(p.t_max, g, p.NT);
-      xs_.command = AT(p.command, g, p.NT);
-      xs_.t_store = AT(p.t_store, g, p.NT);
       xs_.ticket = AT(p.ticket, g, p.NT);
-      xs_.is_commit = AT(p.is_commit, g, p.NT);
       xs_.proposal = AT(p.proposal, g, p.NT);
+      xs_.decree = AT(p.decree, g, p.NT);
       xs_.vs = AT(p.vote_s, g, p.NT);
       xs_.vf = AT(p.vote_f, g, p.NT);
     }
@@ -1791,11 +1811,15 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
             gs_round = 0;
             if (i == 0) (void)ctx_timer(c, TM_GOSSIP_BLOCK, p.pbft_period);
           } else {  // paxos-node.cc:58-139
-            xs_.t_max = 0;
-            xs_.command = 'e';
-            xs_.t_store = 0;
+            for (uint32_t d = 0; d < p.K; ++d) {
+              int32_t* a = px_of(c, static_cast<int32_t>(d));
+              a[0] = 0;    // t_max
+              a[1] = 'e';  // command
+              a[2] = 0;    // t_store
+              a[3] = 0;    // isCommit
+            }
             xs_.ticket = 0;
-            xs_.is_commit = 0;
+            xs_.decree = 0;
             xs_.proposal = enc_raw(p, static_cast<int32_t>(i));
             xs_.vs = 0;
             xs_.vf = 0;
@@ -1882,12 +1906,9 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     } else if (PROTO == BCSIM_GOSSIP) {
       AT(p.round, g, p.NT) = gs_round;
     } else {
-      AT(p.t_max, g, p.NT) = xs_.t_max;
-      AT(p.command, g, p.NT) = xs_.command;
-      AT(p.t_store, g, p.NT) = xs_.t_store;
       AT(p.ticket, g, p.NT) = xs_.ticket;
-      AT(p.is_commit, g, p.NT) = xs_.is_commit;
       AT(p.proposal, g, p.NT) = xs_.proposal;
+      AT(p.decree, g, p.NT) = xs_.decree;
       AT(p.vote_s, g, p.NT) = xs_.vs;
       AT(p.vote_f, g, p.NT) = xs_.vf;
     }

@@ -125,7 +125,11 @@ typedef struct bcsim_config {
   uint32_t queue_dev_pkts;     /* device queue limit, packets (100) */
   uint32_t queue_disc_pkts;    /* queue-disc limit, packets (1000; 0 = none) */
   uint32_t cap_queue_msgs;     /* GPU engine: queued messages per link (0 = 256) */
-  uint32_t reserved[4];
+  /* Paxos decrees (build extension for BASELINE configs[2]): each
+   * proposer runs instances 0..paxos_decrees-1 one after another; 0/1 = the
+   * reference's single decree (paxos-node.cc:510-522, :323-361) */
+  uint32_t paxos_decrees;
+  uint32_t reserved[3];
 } bcsim_config;
 
 /* ---- outputs -------------------------------------------------------------- */

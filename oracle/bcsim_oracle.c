@@ -208,8 +208,8 @@ typedef struct {
   int32_t is_leader, has_voted, m_value, vote_success, vote_failed;
   int32_t add_change_value, blockNum, round;
   uint32_t next_election, next_heartbeat;
-  /* Paxos (paxos-node.h:40-52) */
-  int32_t t_max, command, t_store, ticket, isCommit, proposal;
+  /* Paxos (paxos-node.h:40-52); acceptor fields per decree in o->px */
+  int32_t ticket, proposal, decree;
   /* cancelled timer ids (ns-3 Simulator::Cancel) */
   uint32_t* cancelled;
   uint32_t n_cancelled, cap_cancelled;
@@ -245,6 +245,8 @@ struct bcsim_oracle {
   onode* nodes;          /* N, for the replica being run */
   int32_t *tx_val, *tx_pv, *tx_cv; /* N * seq_cap */
   uint8_t* gseen;        /* GOSSIP: N * seq_cap first-receipt flags */
+  int32_t* px;           /* PAXOS: [N][decrees][4] t_max, command, t_store, isCommit */
+  uint32_t K;            /* Paxos decrees (>= 1) */
   int64_t* busy;         /* per edge */
   oqueue* q;             /* per edge (DROPTAIL only) */
   uint32_t nfr[2];       /* frames per message class (small, big) */
@@ -810,21 +812,36 @@ enum {
   X_RES_PROPOSE = 4, X_RES_COMMIT = 5, X_CLIENT_PROPOSE = 6
 };
 
+/* acceptor state of node i for decree d: t_max, command, t_store, isCommit */
+static int32_t* px_of(bcsim_oracle* o, uint32_t i, int32_t d) {
+  if (d < 0 || (uint32_t)d >= o->K) {
+    set_err(o, BCSIM_E_INDEX);
+    d = 0;
+  }
+  return &o->px[((size_t)i * o->K + (uint32_t)d) * 4];
+}
+
+/* every Paxos message carries its decree in data[3] (f[2]): outside the
+ * reference's 3-byte packet, so 0 for the single decree */
 static void paxos_require_ticket(bcsim_oracle* o, const oev* e, uint32_t i) {
   onode* nd = &o->nodes[i]; /* :510-522 */
   nd->ticket += 1;
-  omsg m = mk(X_REQ_TICKET, enc(o, nd->ticket), 0, 0, 0);
+  omsg m = mk(X_REQ_TICKET, enc(o, nd->ticket), 0, nd->decree, 0);
   bcast_paxos(o, i, &m);
-  emit(o, e, i, BCSIM_TR_PAXOS_TICKET, nd->ticket, 0, 0);
+  emit(o, e, i, BCSIM_TR_PAXOS_TICKET, nd->ticket, nd->decree, 0);
 }
 
 static void paxos_start(bcsim_oracle* o, uint32_t i) { /* :58-139 */
   onode* nd = &o->nodes[i];
-  nd->t_max = 0;
-  nd->command = 'e';
-  nd->t_store = 0;
+  for (uint32_t d = 0; d < o->K; ++d) {
+    int32_t* a = px_of(o, i, (int32_t)d);
+    a[0] = 0;   /* t_max */
+    a[1] = 'e'; /* command */
+    a[2] = 0;   /* t_store */
+    a[3] = 0;   /* isCommit */
+  }
   nd->ticket = 0;
-  nd->isCommit = 0;
+  nd->decree = 0;
   nd->proposal = as_char(o, (int32_t)i + '0');
   nd->vote_success = 0;
   nd->vote_failed = 0;
@@ -839,41 +856,44 @@ static void paxos_recv(bcsim_oracle* o, const oev* e, uint32_t i) {
   switch (dec(mchar(m, 0))) {
     case X_REQ_TICKET: { /* :177-198 */
       int32_t t = dec(mchar(m, 1));
+      int32_t* a = px_of(o, i, m->f[2]);
       omsg r;
-      if (t > nd->t_max) {
-        nd->t_max = t;
-        r = mk(X_RES_TICKET, enc(o, 0), nd->command, 0, 0);
+      if (t > a[0]) {
+        a[0] = t;
+        r = mk(X_RES_TICKET, enc(o, 0), a[1], m->f[2], 0);
       } else {
-        r = mk(X_RES_TICKET, enc(o, 1), 0, 0, 0);
+        r = mk(X_RES_TICKET, enc(o, 1), 0, m->f[2], 0);
       }
       unicast(o, i, e->aux, &r);
       break;
     }
     case X_REQ_PROPOSE: { /* :199-221 */
       int32_t t = dec(mchar(m, 1));
+      int32_t* a = px_of(o, i, m->f[2]);
       int32_t st;
-      if (t == nd->t_max) {
-        nd->command = mchar(m, 2);
-        nd->t_store = t;
+      if (t == a[0]) {
+        a[1] = mchar(m, 2);
+        a[2] = t;
         st = 0;
       } else {
         st = 1;
       }
-      omsg r = mk(X_RES_PROPOSE, enc(o, st), 0, 0, 0);
+      omsg r = mk(X_RES_PROPOSE, enc(o, st), 0, m->f[2], 0);
       unicast(o, i, e->aux, &r);
       break;
     }
     case X_REQ_COMMIT: { /* :222-247 */
       int32_t t = dec(mchar(m, 1));
       int32_t c = mchar(m, 2);
+      int32_t* a = px_of(o, i, m->f[2]);
       int32_t st;
-      if (t == nd->t_store && c == nd->command) {
-        nd->isCommit = 1;
+      if (t == a[2] && c == a[1]) {
+        a[3] = 1;
         st = 0;
       } else {
         st = 1;
       }
-      omsg r = mk(X_RES_COMMIT, enc(o, st), 0, 0, 0);
+      omsg r = mk(X_RES_COMMIT, enc(o, st), 0, m->f[2], 0);
       unicast(o, i, e->aux, &r);
       break;
     }
@@ -882,6 +902,7 @@ static void paxos_recv(bcsim_oracle* o, const oev* e, uint32_t i) {
     case X_RES_COMMIT: { /* :248-353 */
       int32_t ty = dec(mchar(m, 0));
       int32_t st = dec(mchar(m, 1));
+      if (m->f[2] != nd->decree) break; /* a response of a finished decree: not counted */
       if (st == 0)
         nd->vote_success += 1;
       else
@@ -892,13 +913,19 @@ static void paxos_recv(bcsim_oracle* o, const oev* e, uint32_t i) {
           nd->vote_failed = 0;
           if (ty == X_RES_TICKET) {
             if (mchar(m, 2) != 'e') nd->proposal = mchar(m, 2);
-            omsg r = mk(X_REQ_PROPOSE, enc(o, nd->ticket), nd->proposal, 0, 0);
+            omsg r = mk(X_REQ_PROPOSE, enc(o, nd->ticket), nd->proposal, nd->decree, 0);
             bcast_paxos(o, i, &r);
           } else if (ty == X_RES_PROPOSE) {
-            omsg r = mk(X_REQ_COMMIT, enc(o, nd->ticket), nd->proposal, 0, 0);
+            omsg r = mk(X_REQ_COMMIT, enc(o, nd->ticket), nd->proposal, nd->decree, 0);
             bcast_paxos(o, i, &r);
           } else {
-            emit(o, e, i, BCSIM_TR_PAXOS_COMMIT, nd->ticket, 0, 0);
+            emit(o, e, i, BCSIM_TR_PAXOS_COMMIT, nd->ticket, nd->decree, 0);
+            if ((uint32_t)nd->decree + 1 < o->K) { /* next decree: fresh ticket and proposal */
+              nd->decree += 1;
+              nd->ticket = 0;
+              nd->proposal = as_char(o, (int32_t)i + '0');
+              paxos_require_ticket(o, e, i);
+            }
           }
         } else {
           nd->vote_success = 0;
@@ -1222,6 +1249,12 @@ int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
       return BCSIM_E_NOMEM;
     }
   }
+  o->K = o->cfg.paxos_decrees ? o->cfg.paxos_decrees : 1;
+  o->px = (int32_t*)calloc((size_t)o->N * (o->cfg.protocol == BCSIM_PAXOS ? o->K : 1) * 4, sizeof(int32_t));
+  if (!o->px) {
+    bcsim_oracle_destroy(o);
+    return BCSIM_E_NOMEM;
+  }
   if (o->cfg.protocol == BCSIM_GOSSIP) {
     o->gseen = (uint8_t*)calloc((size_t)o->N * o->cfg.pbft_seq_cap, 1);
     if (!o->gseen) {
@@ -1375,6 +1408,7 @@ int bcsim_oracle_destroy(bcsim_oracle* o) {
   free(o->tx_pv);
   free(o->tx_cv);
   free(o->gseen);
+  free(o->px);
   free_queues(o);
   free(o->row);
   free(o->col);

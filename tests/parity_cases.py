@@ -66,6 +66,10 @@ def cases():
         "paxos8_fixed0": _cfg(X, 8, delay_mode=F, app_delay_ns=0),
         "paxos32_jitter_ctr": _cfg(X, 32, delay_mode=J, rng_mode=K, seed=11),
         "paxos16_jitter_rep4": _cfg(X, 16, delay_mode=J, rng_mode=K, seed=5, n_replicas=4),
+        # multi-decree Paxos (build extension for configs[2])
+        "paxos8_fixed_k3": _cfg(X, 8, delay_mode=F, app_delay_ns=2_000_000, paxos_decrees=3),
+        "paxos32_jitter_k4": _cfg(X, 32, delay_mode=J, rng_mode=K, seed=13, paxos_decrees=4),
+        "paxos128_jitter_rep6_k3": _cfg(X, 128, delay_mode=J, rng_mode=K, seed=17, n_replicas=6, paxos_decrees=3),
         "pbft8_rep3_ctr": _cfg(P, 8, delay_mode=F, app_delay_ns=3_000_000, rng_mode=K, n_replicas=3,
                                pbft_rounds=20, pbft_block_bytes=2000),
         # C5 shape (BASELINE configs[4]): PBFT-style gossip on random regular graphs (TOPOLOGY below)

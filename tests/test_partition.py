@@ -106,7 +106,7 @@ def test_merge_matches_single_process_shape():
 PART_CASES = ["pbft16_fixed_100", "pbft5_odd", "pbft12_jitter_ctr", "pbft8_rep3_ctr", "pbft8_compat",
               "raft16_jitter_ctr", "paxos8_fixed", "paxos32_jitter_ctr", "paxos16_jitter_rep4",
               "gossip64_d4_fixed", "gossip200_d8_jitter_ctr", "gossip24_mesh", "pbft32_d6_ctr",
-              "pbft16_droptail_100", "gossip64_d4_droptail", "pbft12_hetero_prop"]
+              "pbft16_droptail_100", "gossip64_d4_droptail", "pbft12_hetero_prop", "paxos32_jitter_k4"]
 
 
 @pytest.mark.gpu
