@@ -13,6 +13,7 @@ RNG_GLIBC, RNG_COUNTER = 0, 1
 TIME_ROUND, TIME_TRUNC = 0, 1
 ENC_EXTENDED, ENC_COMPAT = 0, 1
 QUEUE_INFINITE, QUEUE_DROPTAIL = 0, 1
+ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE = 0, 1, 2
 
 OK = 0
 ERRORS = {
@@ -72,7 +73,8 @@ class Config(C.Structure):
         ("queue_disc_pkts", C.c_uint32),
         ("cap_queue_msgs", C.c_uint32),
         ("paxos_decrees", C.c_uint32),
-        ("reserved", C.c_uint32 * 3),
+        ("engine_mode", C.c_uint32),
+        ("reserved", C.c_uint32 * 2),
     ]
 
 

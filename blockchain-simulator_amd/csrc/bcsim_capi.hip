@@ -64,6 +64,9 @@ struct Sim {
   int x_active = 0;            // extras of the grouped cell are in xgrp
   uint32_t bs_scan = 64, bs_link = 64;
   long long dbg_fail_cell = -1;  // test hook (BCSIM_DBG_FAIL_CELL): this rank fails at that cell
+  bool sparse = false;
+  uint32_t act_grid = 0;         // sparse mode: workgroups of k_scan / k_link (grid-stride over the active list)
+  uint32_t* seg_part = nullptr;  // multi-block segment scan partials
   long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
   long long n_alive = 0;
   uint64_t cells = 0;
@@ -316,6 +319,7 @@ static int setup_device(Sim& s) {
   p.paxos_delay = tables + 160;
   p.jit_delay = (c.protocol == BCSIM_PBFT || c.protocol == BCSIM_GOSSIP) ? p.pbft_delay : c.protocol == BCSIM_RAFT ? p.raft_delay : p.paxos_delay;
   p.jit_mod = c.protocol == BCSIM_PAXOS ? 50 : 3;
+  const int64_t* tab_jit = tab.data() + (p.jit_delay - tables);
 
   // topology
   uint32_t *row, *col, *rev;
@@ -360,6 +364,15 @@ static int setup_device(Sim& s) {
   if (p.cap_timers > 64) p.cap_timers = 64;
   p.cap_ops = c.cap_ops_per_node ? c.cap_ops_per_node
                                  : static_cast<uint32_t>(std::max<uint64_t>(1024, 4ull * s.deg_max + 256));
+  // engine layout: the dense per-edge state of every replica (8 buckets
+  // of inbox slots, link word, reply slots) or the sparse list-only layout
+  {
+    const double dense_bytes = static_cast<double>(s.R) * s.E * (8.0 * sizeof(Rec) + 8.0 + kOpRing * sizeof(Op));
+    s.sparse = c.engine_mode == BCSIM_ENGINE_SPARSE || (c.engine_mode == BCSIM_ENGINE_AUTO && dense_bytes > 96e9);
+  }
+  p.sparse = s.sparse ? 1u : 0u;
+  p.n_heavy = s.N;
+  p.cap_ops_light = p.cap_ops;
   if (link_lds_bytes(p) > 150 * 1024) {
     g_detail = "node degree / op capacity exceed the LDS budget of k_link";
     return BCSIM_E_UNSUPPORTED;
@@ -383,8 +396,17 @@ static int setup_device(Sim& s) {
   if (const char* nm = std::getenv("BCSIM_NO_MESH"); nm && *nm == '1') mesh = false;  // debugging aid
   p.mesh = mesh ? 1u : 0u;
   p.n_tiles = (s.N + kTile - 1) / kTile;
-  const uint64_t per_bucket = static_cast<uint64_t>(s.R) * s.E * sizeof(Rec);
+  const uint64_t per_bucket = s.sparse ? 0 : static_cast<uint64_t>(s.R) * s.E * sizeof(Rec);
   s.B = c.n_buckets ? c.n_buckets : 0;
+  if (s.B == 0 && s.sparse) {  // list-only buckets: enough cells for the longest send-to-arrival delay
+    int64_t dmax = c.delay_mode == BCSIM_DELAY_FIXED ? c.app_delay_ns : 0;
+    for (uint32_t k = 0; k < p.jit_mod && c.delay_mode != BCSIM_DELAY_FIXED; ++k)
+      dmax = std::max<int64_t>(dmax, tab_jit[k]);
+    int64_t pmax = 0;
+    for (int64_t v : s.prop) pmax = std::max(pmax, v);
+    const uint64_t cells = static_cast<uint64_t>((dmax + std::max(p.tx_tot[0], p.tx_tot[1]) + pmax) / s.L) + 3;
+    s.B = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(kMaxBuckets, cells)));
+  }
   if (s.B == 0) {
     const uint64_t nb = per_bucket ? (8ull << 30) / per_bucket : kMaxBuckets;
     s.B = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(kMaxBuckets, nb)));
@@ -395,15 +417,35 @@ static int setup_device(Sim& s) {
   }
   p.n_buckets = s.B;
   uint64_t cap_x = c.cap_bucket_records;
-  if (cap_x == 0) cap_x = std::max<uint64_t>(65536, NT * 8);
+  if (cap_x == 0) cap_x = s.sparse ? std::min<uint64_t>(1ull << 25, std::max<uint64_t>({65536, NT * 2, static_cast<uint64_t>(s.R) * s.E}))
+                                   : std::max<uint64_t>(65536, NT * 8);
   p.cap_x = static_cast<uint32_t>(std::min<uint64_t>(cap_x, 1ull << 26));
-  p.cap_stage = static_cast<uint32_t>(2ull * s.deg_max + 256);  // k_link staging per node
+  p.cap_stage = static_cast<uint32_t>(2ull * s.deg_max + 256);  // k_link staging per workgroup
+  if (s.sparse) {
+    // hub-compact link state: Paxos on the full mesh (only proposers broadcast; every
+    // reply and echo travels a proposer edge)
+    const bool mesh_topo = s.E == static_cast<uint64_t>(s.N) * (s.N - 1);
+    p.hubs = (c.protocol == BCSIM_PAXOS && mesh_topo && c.queue_model == BCSIM_QUEUE_INFINITE)
+                 ? std::min<uint32_t>(c.paxos_proposers, s.N) : 0u;
+    if (p.hubs) {  // proposers hold broadcast expansions and reply waves; acceptors a few ops
+      p.n_heavy = p.hubs;
+      p.cap_ops_light = std::min<uint32_t>(p.cap_ops, c.cap_ops_per_node ? p.cap_ops : 32);
+      if (!c.cap_timers_per_node) p.cap_timers = 4;  // Paxos: the t=0 ticket timer only
+    }
+    s.act_grid = static_cast<uint32_t>(std::min<uint64_t>(NT, 4096));
+    // small workgroups over many nodes: k_scan windows of <= 512 arrivals (split by
+    // time), 256 lanes; k_link_sparse has no per-edge LDS arrays
+    if (c.delay_mode == BCSIM_DELAY_RANDOM) p.cap_arr = std::min<uint32_t>(p.cap_arr, 512);  // spread arrivals
+    s.bs_scan = std::min<uint32_t>(s.bs_scan, 256);
+    s.bs_link = 256;
+  }
   p.cap_ov = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(1ull << 20, NT * 256), 1ull << 26));
   p.cap_trace = static_cast<uint32_t>(std::min<uint64_t>(1ull << 26, std::max<uint64_t>(1u << 20, NT * 256)));
   p.cap_vlog = 1u << 20;
-  p.cap_dreq = static_cast<uint32_t>(std::max<uint64_t>(4096, 4 * NT));
+  const bool glibc_draws = c.protocol == BCSIM_RAFT && c.rng_mode == BCSIM_RNG_GLIBC;
+  p.cap_dreq = glibc_draws ? static_cast<uint32_t>(std::max<uint64_t>(4096, 4 * NT)) : 1;
   p.cap_E = static_cast<uint64_t>(s.R) * s.E;
-  p.cap_inbox = static_cast<uint64_t>(s.B) * s.R * s.E;
+  p.cap_inbox = s.sparse ? 1 : static_cast<uint64_t>(s.B) * s.R * s.E;
   p.cap_xbuf = static_cast<uint64_t>(s.B) * p.cap_x;
 
   // dynamic LDS above the 64 KiB default needs an explicit opt-in (160 KiB per CU on gfx950)
@@ -502,7 +544,9 @@ static int setup_device(Sim& s) {
     HIPCHK(hipMemset(p.px, 0, npx * 4));
   }
   if ((rc = dalloc(s, &p.next_election, NT)) || (rc = dalloc(s, &p.next_heartbeat, NT))) return rc;
-  if ((rc = dalloc(s, &p.timers, NT * p.cap_timers)) || (rc = dalloc(s, &p.ops, NT * p.cap_ops)) ||
+  const size_t n_ops_total = static_cast<size_t>(s.R) * (static_cast<size_t>(p.n_heavy) * p.cap_ops +
+                                                         static_cast<size_t>(s.N - p.n_heavy) * p.cap_ops_light);
+  if ((rc = dalloc(s, &p.timers, NT * p.cap_timers)) || (rc = dalloc(s, &p.ops, n_ops_total)) ||
       (rc = dalloc(s, &p.n_ops, NT)))
     return rc;
   // per-edge reply slots of main-slot arrivals (kOpRing cells) and implicit
@@ -511,8 +555,8 @@ static int setup_device(Sim& s) {
     const uint64_t ne = static_cast<uint64_t>(kOpRing) * s.R * s.E;
     const char* ns = std::getenv("BCSIM_NO_SLOTS");
     const bool off = ns && *ns == '1';
-    p.impl = off ? 0u : 1u;
-    const bool on = ne * sizeof(Op) <= (16ull << 30) && !off;
+    p.impl = (off || s.sparse) ? 0u : 1u;  // sparse: no slots, echoes listed by k_scan
+    const bool on = ne * sizeof(Op) <= (16ull << 30) && !off && !s.sparse;
     p.cap_eslot = on ? ne : 1;
     if ((rc = dalloc(s, &p.eslot, p.cap_eslot)) || (rc = dalloc(s, &p.sflag, static_cast<size_t>(kOpRing) * NT)))
       return rc;
@@ -520,7 +564,10 @@ static int setup_device(Sim& s) {
     HIPCHK(hipMemset(p.sflag, 0, static_cast<size_t>(kOpRing) * NT));
     if (!on) p.eslot = nullptr;
   }
-  if ((rc = dalloc(s, &p.link, static_cast<size_t>(s.R) * s.E))) return rc;
+  const size_t n_link = p.hubs ? static_cast<size_t>(s.R) * (static_cast<size_t>(p.hubs) * (s.N - 1) +
+                                                              static_cast<size_t>(s.N - p.hubs) * p.hubs)
+                               : static_cast<size_t>(s.R) * s.E;
+  if ((rc = dalloc(s, &p.link, n_link))) return rc;
   {  // DROPTAIL link queues: ring of cap_q message entries per edge
     const size_t ne = p.qmodel ? static_cast<size_t>(s.R) * s.E : 1;
     if (p.cap_q > 65535) {
@@ -534,9 +581,14 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.rtile, n_rtile))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
       (rc = dalloc(s, &p.xbuf, p.cap_xbuf)) || (rc = dalloc(s, &p.xgrp, p.cap_x)) ||
-      (rc = dalloc(s, &p.xstage, NT * p.cap_stage)) || (rc = dalloc(s, &p.xmeta, NT * p.cap_stage)) ||
+      (rc = dalloc(s, &p.xstage, static_cast<size_t>(s.sparse ? s.act_grid : NT) * p.cap_stage)) ||
+      (rc = dalloc(s, &p.xmeta, static_cast<size_t>(s.sparse ? s.act_grid : NT) * p.cap_stage)) ||
       (rc = dalloc(s, &p.ov, p.cap_ov)))
     return rc;
+  if (s.sparse) {  // active lists of k_scan / k_link
+    if ((rc = dalloc(s, &p.act, 2 * NT)) || (rc = dalloc(s, &p.act_n, 2))) return rc;
+  }
+  if ((rc = dalloc(s, &s.seg_part, (NT + kSegChunk - 1) / kSegChunk + 1))) return rc;
   if ((rc = dalloc(s, &p.seg_cnt, NT)) || (rc = dalloc(s, &p.seg_off, NT + 1)) ||
       (rc = dalloc(s, &p.cursor, NT)))
     return rc;
@@ -611,7 +663,7 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemset(p.timers, 0, NT * p.cap_timers * sizeof(TimerEnt)));
   HIPCHK(hipMemset(p.n_ops, 0, NT * 4));
   {  // busy_until 0, no record yet (cell tag 0xFFFF)
-    std::vector<uint64_t> l0(static_cast<size_t>(s.R) * s.E, 0xFFFFull);
+    std::vector<uint64_t> l0(n_link, 0xFFFFull);
     HIPCHK(hipMemcpy(p.link, l0.data(), l0.size() * 8, hipMemcpyHostToDevice));
   }
   HIPCHK(hipMemset(p.inbox, 0, p.cap_inbox * sizeof(Rec)));
@@ -702,6 +754,14 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
   dim3 grid(s.R * s.nloc), block(s.bs_scan);
+  if (s.sparse) {  // compact lists of the window's active gnodes; fixed grids stride over them
+    HIPCHK(hipMemsetAsync(s.kp.act_n, 0, 8, s.stream));
+    const uint32_t nb = static_cast<uint32_t>(std::min<uint64_t>(8192, (static_cast<uint64_t>(s.R) * s.nloc + 255) / 256));
+    int rc = launch(s, KS_AUX, k_active, dim3(nb), dim3(256), 0, s.kp_dev, lo, hi,
+                    static_cast<uint32_t>(cell % s.B));
+    if (rc) return rc;
+    grid = dim3(s.act_grid);
+  }
   const int fw = final_win ? 1 : 0, xa = s.x_active;
   int rc;
   if (s.cfg.protocol == BCSIM_PBFT)
@@ -742,7 +802,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
                    acc[3] / nw / 100, acc[4] / nw / 100, acc[5] / nw / 100, acc[6] / nw / 100, acc[7] / nw / 100);
     }
   }
-  rc = launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw);
+  if (s.sparse)
+    rc = launch(s, KS_LINK, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw);
+  else
+    rc = launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw);
   if (rc || !s.kp.wgt) return rc;
   // debug (BCSIM_WGT=1): report the slowest k_link workgroups of this launch
   std::vector<unsigned long long> w(8ull * s.NT);
@@ -810,7 +873,15 @@ static int group_cell(Sim& s, long long cell) {
     HIPCHK(hipMemsetAsync(s.kp.cursor, 0, s.NT * 4ull, s.stream));
     int rc;
     if ((rc = launch(s, KS_GROUP, k_xcount, dim3((nx + 255) / 256), dim3(256), 0, s.kp_dev, b, nx))) return rc;
-    if ((rc = launch(s, KS_GROUP, k_offsets, dim3(1), dim3(1024), 0, s.kp_dev))) return rc;
+    if (s.NT <= (1u << 20)) {
+      if ((rc = launch(s, KS_GROUP, k_offsets, dim3(1), dim3(1024), 0, s.kp_dev))) return rc;
+    } else {  // multi-block scan
+      const uint32_t np = static_cast<uint32_t>((s.NT + kSegChunk - 1) / kSegChunk);
+      if ((rc = launch(s, KS_GROUP, k_seg_sums, dim3(np), dim3(1024), 0, s.kp_dev, s.seg_part)) ||
+          (rc = launch(s, KS_GROUP, k_seg_top, dim3(1), dim3(1024), 0, s.seg_part, np)) ||
+          (rc = launch(s, KS_GROUP, k_seg_apply, dim3(np), dim3(1024), 0, s.kp_dev, s.seg_part)))
+        return rc;
+    }
     if ((rc = launch(s, KS_GROUP, k_xplace, dim3((nx + 255) / 256), dim3(256), 0, s.kp_dev, b, nx))) return rc;
     s.x_active = 1;
   }

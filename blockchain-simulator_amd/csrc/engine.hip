@@ -166,6 +166,13 @@ struct KP {
   uint32_t cap_send;
   const uint8_t* lead_all;  // [R][N] PBFT leader flags gathered from all ranks
   uint8_t* lead_loc;        // [R][N] this rank's leader flags (k_lead)
+  // sparse mode: no per-edge inbox slots (every record goes through
+  // the bucket lists), launches over compact lists of active gnodes, hub-compact link
+  // state (hubs > 0: only edges with an endpoint < hubs carry traffic)
+  uint32_t sparse, hubs;
+  uint32_t cap_ops_light, n_heavy;  // nodes < n_heavy hold cap_ops pending ops, others cap_ops_light
+  uint32_t* act;    // [2][NT] gnodes of the window for k_scan / k_link (sparse mode)
+  uint32_t* act_n;  // [2]
   // debug (BCSIM_DBG_EVENTS=<t_max ns>): Raft/Paxos/gossip serial handlers emit one
   // trace record of kind 90 + event class per handled event with t < dbg_tmax
   long long dbg_tmax;
@@ -243,6 +250,32 @@ __device__ inline void set_flag_once(uint8_t* f) {
 __device__ inline uint32_t local_gnode(const KP& p, uint32_t b) {
   const uint32_t j = xcd_map(b, p.R * p.nloc);
   return (j / p.nloc) * p.N + p.nlo + j % p.nloc;
+}
+
+// pending-op list of gnode g: nodes < n_heavy of every replica have cap_ops entries,
+// the others cap_ops_light (n_heavy = N: uniform)
+__device__ inline size_t op_base(const KP& p, uint32_t g) {
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const size_t per = static_cast<size_t>(p.n_heavy) * p.cap_ops + static_cast<size_t>(p.N - p.n_heavy) * p.cap_ops_light;
+  return rep * per + (i < p.n_heavy ? static_cast<size_t>(i) * p.cap_ops
+                                    : static_cast<size_t>(p.n_heavy) * p.cap_ops +
+                                          static_cast<size_t>(i - p.n_heavy) * p.cap_ops_light);
+}
+__device__ inline uint32_t op_cap(const KP& p, uint32_t g) { return (g % p.N) < p.n_heavy ? p.cap_ops : p.cap_ops_light; }
+
+// link-state word of out-edge le of node i (replica rep).  Hub-compact (sparse mode,
+// full mesh): rows of the hub nodes in full, then (node, hub) pairs; an edge between
+// two non-hubs has no state (BCSIM_E_UNSUPPORTED if it ever carries traffic).
+__device__ inline size_t link_index(const KP& p, uint32_t rep, uint32_t i, uint32_t e0, uint32_t le) {
+  if (!p.hubs) return static_cast<size_t>(rep) * p.E + e0 + le;
+  const size_t per = static_cast<size_t>(p.hubs) * (p.N - 1) + static_cast<size_t>(p.N - p.hubs) * p.hubs;
+  if (i < p.hubs) return rep * per + static_cast<size_t>(i) * (p.N - 1) + le;
+  const uint32_t j = le < i ? le : le + 1;  // full mesh peer
+  if (j >= p.hubs) {
+    set_err(p, BCSIM_E_UNSUPPORTED);
+    return rep * per;
+  }
+  return rep * per + static_cast<size_t>(p.hubs) * (p.N - 1) + static_cast<size_t>(i - p.hubs) * p.hubs + j;
 }
 
 struct Key {
@@ -628,6 +661,86 @@ __global__ __launch_bounds__(1024) void k_offsets(const KP* __restrict__ pk) {
   if (tid == 0) AT(p.seg_off, p.NT, p.NT + 1) = carry;
 }
 
+// multi-block exclusive scan of seg_cnt[0..NT) -> seg_off[0..NT] (large NT: sparse mode)
+constexpr uint32_t kSegChunk = 8192;  // 1024 threads x 8 entries per block
+__global__ __launch_bounds__(1024) void k_seg_sums(const KP* __restrict__ pk, uint32_t* part) {
+  const KP& p = *pk;
+  __shared__ uint32_t red[1024];
+  const size_t b0 = static_cast<size_t>(blockIdx.x) * kSegChunk;
+  uint32_t acc = 0;
+  for (uint32_t k = threadIdx.x; k < kSegChunk; k += blockDim.x)
+    if (b0 + k < p.NT) acc += p.seg_cnt[b0 + k];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t o = blockDim.x / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ __launch_bounds__(1024) void k_seg_top(uint32_t* part, uint32_t nparts) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nparts; base += 1024) {
+    const uint32_t idx = base + tid;
+    const uint32_t v = idx < nparts ? part[idx] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64);
+      if (lane >= static_cast<uint32_t>(off)) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t a = 0;
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t t = wsum[k];
+        wsum[k] = a;
+        a += t;
+      }
+    }
+    __syncthreads();
+    const uint32_t excl = carry + wsum[w] + x - v;
+    if (idx < nparts) part[idx] = excl;
+    __syncthreads();
+    if (tid == 1023) carry = excl + v;
+    __syncthreads();
+  }
+}
+__global__ __launch_bounds__(1024) void k_seg_apply(const KP* __restrict__ pk, const uint32_t* part) {
+  const KP& p = *pk;
+  __shared__ uint32_t wsum[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const size_t b0 = static_cast<size_t>(blockIdx.x) * kSegChunk + static_cast<size_t>(tid) * 8;
+  uint32_t v[8], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[k] = b0 + k < p.NT ? p.seg_cnt[b0 + k] : 0u;
+    sum += v[k];
+  }
+  uint32_t x = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= static_cast<uint32_t>(off)) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t wb = 0;
+  for (uint32_t k = 0; k < w; ++k) wb += wsum[k];
+  uint32_t acc = part[blockIdx.x] + wb + x - sum;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (b0 + k < p.NT) p.seg_off[b0 + k] = acc;
+    acc += v[k];
+  }
+  if (b0 < p.NT && b0 + 8 >= p.NT) p.seg_off[p.NT] = acc;  // the thread holding the last entry
+}
+
 __global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   const KP& p = *pk;
   BAIL_IF_ERR();
@@ -679,7 +792,7 @@ struct Ctx {
   uint32_t sub;
   uint64_t draws;
   Op* ops;
-  uint32_t nops;
+  uint32_t nops, cap_ops;
   TimerEnt* tm;  // LDS copy of the node's timers
   uint32_t cap_t;
   unsigned long long deliv[BCSIM_MSG_TYPES];
@@ -694,11 +807,11 @@ __device__ inline void ctx_trace(Ctx& c, uint32_t kind, int32_t a, int32_t b, in
 __device__ inline void ctx_op(Ctx& c, const Op& o) {
   const KP& p = *c.p;
   TRAIL(c);
-  if (c.nops >= p.cap_ops) {
+  if (c.nops >= c.cap_ops) {
     set_err(p, BCSIM_E_OVERFLOW);
     return;
   }
-  AT(c.ops, c.nops++, p.cap_ops) = o;
+  AT(c.ops, c.nops++, c.cap_ops) = o;
 }
 
 __device__ inline int32_t ctx_draw(Ctx& c) {
@@ -1370,11 +1483,11 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   const uint32_t sub0 = S.sub, nops0 = S.nops;
   const uint64_t draws0 = S.draws;
   const int32_t bn0 = S.block_num;
-  if (nops0 + tot.w > p.cap_ops) {
+  if (nops0 + tot.w > op_cap(p, g)) {
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
     return;
   }
-  Op* ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
+  Op* ops = p.ops + op_base(p, g);
   uint32_t sp = sub0 + ex.x, op = nops0 + ex.w, cp = ex.z;
   uint64_t dp = draws0 + ex.y;
   unsigned long long wrong = 0;
@@ -1566,10 +1679,9 @@ __device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint3
 }
 
 template <int PROTO>
-__global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                               long long t_hi, long long cs, int final_win, int x_active) {
+__device__ void scan_node(const KP* __restrict__ pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
+                          long long cs, int final_win, int x_active) {
   const KP& p = *pk;
-  BAIL_IF_ERR();
   // LDS: akey[cap] u64 | asec[cap] u32 | arec[cap] Rec | acls[cap] u32 | timers
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ ScanShared S;
@@ -1580,8 +1692,6 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   uint32_t* acls = reinterpret_cast<uint32_t*>(arec + cap);
   TimerEnt* tm = reinterpret_cast<TimerEnt*>(acls + cap);
 
-  if (blockIdx.x >= p.R * p.nloc) return;
-  const uint32_t g = local_gnode(p, blockIdx.x);
   const uint32_t tid = threadIdx.x;
   const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
@@ -1592,7 +1702,9 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   if (!flag && AT(p.node_tnext, g, p.NT) >= t_hi && !has_start && !has_stop) return;
 
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
-  const Rec* slots = p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0;
+  // sparse mode: no inbox slots, the node's arrivals are all in the cell's grouped lists
+  const Rec* slots = p.sparse ? nullptr : p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0;
+  const uint32_t deg_in = p.sparse ? 0u : deg;
   uint32_t xn = 0;
   const XRec* xs = p.xgrp;
   if (x_active) {
@@ -1628,7 +1740,8 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
     c.rep = rep;
     c.i = i;
     c.deg = deg;
-    c.ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
+    c.ops = p.ops + op_base(p, g);
+    c.cap_ops = op_cap(p, g);
     c.tm = tm;
     c.cap_t = p.cap_timers;
     for (int k = 0; k < BCSIM_MSG_TYPES; ++k) c.deliv[k] = 0;
@@ -1671,12 +1784,12 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   long long wa = t_lo;
   for (;;) {
     long long wb = t_hi;
-    uint32_t n = flag ? stage_window(p, S, slots, e0, deg, xs, xn, cs, wa, wb, akey, asec, arec, true) : 0u;
+    uint32_t n = flag ? stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, wb, akey, asec, arec, true) : 0u;
     if (n > cap) {  // more than cap arrivals: shrink the window (rare)
       long long lo = wa, hi = t_hi;  // count(lo) <= cap < count(hi)
       while (hi - lo > 1) {
         const long long mid = lo + (hi - lo) / 2;
-        if (stage_window(p, S, slots, e0, deg, xs, xn, cs, wa, mid, akey, asec, arec, false) <= cap)
+        if (stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, mid, akey, asec, arec, false) <= cap)
           lo = mid;
         else
           hi = mid;
@@ -1686,7 +1799,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
         if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
         return;
       }
-      n = stage_window(p, S, slots, e0, deg, xs, xn, cs, wa, wb, akey, asec, arec, true);
+      n = stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, wb, akey, asec, arec, true);
     }
     const uint32_t n_main = S.n_main;
     SPH(1);
@@ -1929,6 +2042,25 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   if (S.tmax > LLONG_MIN) atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), S.tmax);
 }
 
+// dense mode: one workgroup per gnode of this rank; sparse mode: a fixed grid strides
+// over the window's active list (k_active)
+template <int PROTO>
+__global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                               long long t_hi, long long cs, int final_win, int x_active) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  if (!p.sparse) {
+    if (blockIdx.x >= p.R * p.nloc) return;
+    scan_node<PROTO>(pk, local_gnode(p, blockIdx.x), cell, t_lo, t_hi, cs, final_win, x_active);
+    return;
+  }
+  const uint32_t na = *p.act_n;
+  for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
+    scan_node<PROTO>(pk, p.act[k], cell, t_lo, t_hi, cs, final_win, x_active);
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_link: per-node link stage.  Ops due in [.., t_hi) are applied to their
 // out-edge's FIFO in canonical key order; every non-echo op produces one
@@ -2013,7 +2145,7 @@ __device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32
   const uint32_t spos = atomicAdd(&L.nst, 1u);
   if (spos < p.cap_stage) {
     const uint32_t rank = atomicAdd(&L.lst[list], 1u);
-    const size_t k = static_cast<size_t>(g) * p.cap_stage + spos;
+    const size_t k = static_cast<size_t>(blockIdx.x) * p.cap_stage + spos;  // per workgroup (sequential nodes)
     p.xstage[k] = x;
     p.xmeta[k] = (list << 24) | rank;
     return;
@@ -2043,14 +2175,11 @@ __device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32
   }
 }
 
-__global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                              long long t_hi, int final_win) {
+__device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
+                          int final_win) {
   const KP& p = *pk;
-  BAIL_IF_ERR();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ LinkShared L;
-  if (blockIdx.x >= p.R * p.nloc) return;
-  const uint32_t g = local_gnode(p, blockIdx.x);
   uint32_t n = AT(p.n_ops, g, p.NT);
   const uint32_t ob = static_cast<uint32_t>(cell % kOpRing);
   const bool sl = p.eslot && AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT);
@@ -2064,12 +2193,12 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   const uint32_t n_in = n;
   const uint32_t tid = threadIdx.x;
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
-  Op* ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
+  Op* ops = p.ops + op_base(p, g);
+  const uint32_t ocap = op_cap(p, g);
   uint32_t* ecnt = reinterpret_cast<uint32_t*>(smem);   // deg+1
   uint32_t* efill = ecnt + (p.deg_max + 1);              // deg
   uint32_t* eidx = efill + p.deg_max;                    // cap_ops
   const size_t eb0 = static_cast<size_t>(rep) * p.E + e0;
-  uint64_t* lnk = p.link + eb0;
   const int64_t* prop = p.prop + e0;
   unsigned long long* cnt = cnt_stripe(p, rep);
   const uint32_t B = p.n_buckets;
@@ -2077,9 +2206,9 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   // ---- 0. expand jitter broadcasts into per-edge SEND ops ----
   if (p.delay_mode != BCSIM_DELAY_FIXED) {
     for (uint32_t k = 0; k < n; ++k) {  // uniform loop over the (few) ops
-      Op o = AT(ops, k, p.cap_ops);
+      Op o = AT(ops, k, ocap);
       if (op_kind(o) != OP_BCAST_J || (op_flags(o) & OPF_DONE)) continue;
-      if (n + deg > p.cap_ops) {
+      if (n + deg > ocap) {
         if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
         return;
       }
@@ -2094,10 +2223,10 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         s.sub = o.sub + it;
         s.edge = paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it;
         s.kind_flags = static_cast<uint8_t>(OP_SEND | ((op_flags(o) & OPF_BIG) << 2));
-        AT(ops, n + it, p.cap_ops) = s;
+        AT(ops, n + it, ocap) = s;
       }
       __syncthreads();
-      if (tid == 0) AT(ops, k, p.cap_ops).kind_flags = static_cast<uint8_t>(OP_BCAST_J | (OPF_DONE << 2));
+      if (tid == 0) AT(ops, k, ocap).kind_flags = static_cast<uint8_t>(OP_BCAST_J | (OPF_DONE << 2));
       n += deg;
       __syncthreads();
     }
@@ -2148,7 +2277,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   }
   if (p.wgt && tid == 0) ph[0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t n_due = block_scan_array(ecnt, deg + 1, L.wsum);
-  if (n_due > p.cap_ops) {  // unreachable: n_due <= n <= cap_ops
+  if (n_due > ocap) {  // unreachable: n_due <= n <= cap_ops
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
     return;
   }
@@ -2191,8 +2320,12 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     // link state of an edge that is certainly used: issued before the inbox / reply-slot
     // loads below so that the three HBM reads overlap instead of forming a chain
     const bool pre = n_bc != 0 || ee > eb;
+    uint64_t* lwp = nullptr;
     uint64_t lw = 0;
-    if (pre) lw = lnk[le];
+    if (pre) {
+      lwp = p.link + link_index(p, rep, i, e0, le);
+      lw = *lwp;
+    }
     // The four op sources of this edge are merged as raw 32-byte words (RawOp): selecting
     // whole Op structs with int16 members between sources was miscompiled on gfx950 /
     // ROCm 7.2 (a record took f0 from a broadcast and the rest from a listed op; the Raft
@@ -2239,7 +2372,10 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       eidx[b2] = x;
     }
     ++st_edges;
-    if (!pre) lw = lnk[le];
+    if (!pre) {
+      lwp = p.link + link_index(p, rep, i, e0, le);
+      lw = *lwp;
+    }
     // link word: FIFO busy_until (ns, < 2^48) and the 16 low bits of the arrival cell of the
     // edge's last record (slot ownership; a false "not owner" after 2^16 cells only routes a
     // record through the extras list, which delivers it identically)
@@ -2330,7 +2466,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
         const uint4 rv = make_uint4(tof, sub, o.b.z, w3);
         __builtin_memcpy(&r, &rv, sizeof r);
       }
-      const bool owner = lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
+      // sparse mode has no slots: every record is a list record
+      const bool owner = !p.sparse && lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
       lc = static_cast<uint32_t>(ca) & 0xFFFFu;
       if (p.nranks > 1) {
         const uint32_t orank = p.owner[s];
@@ -2397,7 +2534,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
       }
     }
     if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
-    lnk[le] = (static_cast<uint64_t>(bu) << 16) | lc;
+    *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
     if (p.qmodel) p.qmeta[eb0 + le] = qm;
   }
   if (cbn) atomicAdd(&L.lcnt[cb], cbn);
@@ -2451,7 +2588,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   __syncthreads();
   const uint32_t nst = min(L.nst, p.cap_stage);
   for (uint32_t k = tid; k < nst; k += blockDim.x) {
-    const size_t sidx = static_cast<size_t>(g) * p.cap_stage + k;
+    const size_t sidx = static_cast<size_t>(blockIdx.x) * p.cap_stage + k;
     const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
     const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
     if (list > B) {
@@ -2497,6 +2634,393 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
     AT(p.n_ops, g, p.NT) = L.n_keep;
     AT(p.node_onext, g, p.NT) = L.omin;
     atomicAdd(&kst_stripe(p)[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                              long long t_hi, int final_win) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  if (blockIdx.x >= p.R * p.nloc) return;
+  link_node(pk, local_gnode(p, blockIdx.x), cell, t_lo, t_hi, final_win);
+}
+
+// ---------------------------------------------------------------------------
+// k_link_sparse (sparse mode): the link stage of the window's active
+// nodes, a fixed grid striding over the list.  No per-edge arrays in LDS: broadcasts
+// are expanded into per-edge SEND ops, the due ops are sorted by (edge, list position)
+// in LDS in edge-range batches of at most kDueCap, and one lane walks each edge's run
+// in canonical key order (FIFO busy_until, DROPTAIL admission) and stages its records
+// for the cell's lists.  Same semantics as link_node (the parity suite runs both).
+constexpr uint32_t kDueCap = 1024;
+
+__device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long long t_lo, long long t_hi,
+                                 int final_win) {
+  __shared__ LinkShared L;
+  __shared__ uint32_t dkey[kDueCap], didx[kDueCap], rst[kDueCap + 1];
+  __shared__ uint32_t s_cnt;
+  uint32_t n = AT(p.n_ops, g, p.NT);
+  if (n == 0) return;
+  const uint32_t tid = threadIdx.x, bs = blockDim.x;
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
+  Op* ops = p.ops + op_base(p, g);
+  const uint32_t ocap = op_cap(p, g);
+  unsigned long long* cnt = cnt_stripe(p, rep);
+  const uint32_t B = p.n_buckets;
+  const long long cs = cell * p.L;
+  // ---- 0. broadcasts -> per-edge SEND ops (jitter: per-edge draws; fixed: when due) ----
+  const uint32_t n_in = n;
+  for (uint32_t k = 0; k < n_in; ++k) {  // uniform loop over the node's (few) ops
+    const Op o = AT(ops, k, ocap);
+    const uint8_t kind = op_kind(o);
+    const bool jit = kind == OP_BCAST_J && !(op_flags(o) & OPF_DONE);
+    const bool fix = kind == OP_BCAST && o.t < t_hi;
+    if (!jit && !fix) continue;
+    if (n + deg > ocap) {
+      if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
+      return;
+    }
+    const bool paxos = (op_flags(o) & OPF_PAXOS) != 0;
+    for (uint32_t it = tid; it < deg; it += bs) {
+      int64_t d = 0;
+      if (jit) d = delay_from_draw(p, ctr_rand(p.seed, rep, i, static_cast<uint64_t>(o.edge) + it));
+      Op sop = o;
+      sop.t = o.t + d;
+      sop.dt = jit ? static_cast<uint32_t>(d) : o.dt;
+      sop.sub = o.sub + it;  // Paxos: edge it + 1 (peers[0] skipped), the last one *end()
+      sop.edge = paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it;
+      sop.kind_flags = static_cast<uint8_t>(OP_SEND | ((op_flags(o) & OPF_BIG) << 2));
+      AT(ops, n + it, ocap) = sop;
+    }
+    __syncthreads();
+    if (tid == 0) AT(ops, k, ocap).kind_flags = static_cast<uint8_t>(OP_BCAST_J | (OPF_DONE << 2));  // consumed
+    n += deg;
+    __syncthreads();
+  }
+  const uint32_t n_lists = B + 1 + (p.nranks > 1 ? p.nranks : 0);
+  for (uint32_t k = tid; k < B; k += bs) L.lcnt[k] = 0;
+  for (uint32_t k = tid; k < n_lists; k += bs) L.lst[k] = 0;
+  if (tid == 0) {
+    L.nst = 0;
+    L.omin = LLONG_MAX;
+    L.ovmin = LLONG_MAX;
+  }
+  __syncthreads();
+  unsigned long long dropped = 0, sends = 0, n_rec = 0, st_ops = 0, st_edges = 0, st_echo = 0, fdrop = 0, lost = 0;
+  long long ovmin = LLONG_MAX;
+  // due ops with no route (Paxos *end()): dropped at SendPacket
+  for (uint32_t k = tid; k < n; k += bs) {
+    const Op& o = ops[k];
+    const uint8_t kind = op_kind(o);
+    if ((kind == OP_SEND || kind == OP_ECHO) && o.t < t_hi && o.edge == kInvalid) {
+      ++dropped;
+      ++sends;
+      ++st_ops;
+    }
+  }
+  // ---- 1. due ops in edge-range batches of at most kDueCap ----
+  uint32_t lo_e = 0;
+  while (lo_e < deg) {  // block-uniform
+    uint32_t hi_e = deg;
+    for (;;) {  // the widest range [lo_e, hi_e) whose due ops fit the batch
+      if (tid == 0) s_cnt = 0;
+      __syncthreads();
+      uint32_t c = 0;
+      for (uint32_t k = tid; k < n; k += bs) {
+        const Op& o = ops[k];
+        const uint8_t kind = op_kind(o);
+        if ((kind == OP_SEND || kind == OP_ECHO) && o.t < t_hi && o.edge != kInvalid) {
+          const uint32_t le = o.edge - e0;
+          c += (le >= lo_e && le < hi_e) ? 1u : 0u;
+        }
+      }
+      if (c) atomicAdd(&s_cnt, c);
+      __syncthreads();
+      const uint32_t tot = s_cnt;
+      __syncthreads();
+      if (tot <= kDueCap) break;
+      if (hi_e - lo_e <= 1) {  // more due ops on one edge than a batch holds
+        if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
+        return;
+      }
+      hi_e = lo_e + (hi_e - lo_e) / 2;
+    }
+    // keys: (edge in range) << 13 | list rank, in op-list order (stable)
+    uint32_t nd = 0;
+    for (uint32_t k0 = 0; k0 < n; k0 += bs) {
+      const uint32_t k = k0 + tid;
+      bool due = false;
+      uint32_t le = 0;
+      if (k < n) {
+        const Op& o = ops[k];
+        const uint8_t kind = op_kind(o);
+        if ((kind == OP_SEND || kind == OP_ECHO) && o.t < t_hi && o.edge != kInvalid) {
+          le = o.edge - e0;
+          due = le >= lo_e && le < hi_e;
+        }
+      }
+      uint32_t tot;
+      const uint32_t pos = nd + block_rank(due, L.wcnt, tot);
+      if (due) {
+        dkey[pos] = ((le - lo_e) << 13) | pos;
+        didx[pos] = k;
+      }
+      nd += tot;
+    }
+    // bitonic sort of the keys (ranks < 2^13 since nd <= kDueCap)
+    uint32_t P2 = 1;
+    while (P2 < nd) P2 <<= 1;
+    for (uint32_t k = nd + tid; k < P2; k += bs) dkey[k] = ~0u;
+    __syncthreads();
+    for (uint32_t k2 = 2; k2 <= P2; k2 <<= 1)
+      for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+        for (uint32_t t = tid; t < P2 / 2; t += bs) {
+          const uint32_t lo = 2 * t - (t & (j - 1)), hi = lo + j;
+          const bool up = (lo & k2) == 0;
+          const uint32_t a = dkey[lo], b2 = dkey[hi];
+          if (up == (b2 < a)) {
+            dkey[lo] = b2;
+            dkey[hi] = a;
+          }
+        }
+        __syncthreads();
+      }
+    // runs of equal edge
+    uint32_t nr = 0;
+    for (uint32_t k0 = 0; k0 < nd; k0 += bs) {
+      const uint32_t k = k0 + tid;
+      const bool st = k < nd && (k == 0 || (dkey[k] >> 13) != (dkey[k - 1] >> 13));
+      uint32_t tot;
+      const uint32_t pos = nr + block_rank(st, L.wcnt, tot);
+      if (st) rst[pos] = k;
+      nr += tot;
+    }
+    if (tid == 0) rst[nr] = nd;
+    __syncthreads();
+    // ---- 2. one lane per edge run: key order, FIFO, records ----
+    for (uint32_t r = tid; r < nr; r += bs) {
+      const uint32_t j0 = rst[r], j1 = rst[r + 1];
+      const uint32_t le = lo_e + (dkey[j0] >> 13);
+      for (uint32_t a = j0 + 1; a < j1; ++a) {  // insertion sort by the canonical key (short runs)
+        const uint32_t ka = dkey[a];
+        const RawOp ox = ld_raw(&ops[didx[ka & 0x1FFFu]]);
+        uint32_t b2 = a;
+        while (b2 > j0) {
+          const uint32_t kb = dkey[b2 - 1];
+          const RawOp oy = ld_raw(&ops[didx[kb & 0x1FFFu]]);
+          if (!raw_key_less(ox, raw_sub(ox), oy, raw_sub(oy))) break;
+          dkey[b2] = kb;
+          --b2;
+        }
+        dkey[b2] = ka;
+      }
+      const uint32_t e = e0 + le;
+      const uint32_t sn = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e, p.E);
+      uint64_t* lwp = p.link + link_index(p, rep, i, e0, le);
+      const uint64_t lw = *lwp;
+      int64_t bu = static_cast<int64_t>(lw >> 16);
+      uint32_t lc = static_cast<uint32_t>(lw & 0xFFFFu);
+      uint64_t qm = 0;
+      uint64_t* qr = nullptr;
+      const size_t qe = static_cast<size_t>(rep) * p.E + e;
+      if (p.qmodel) {
+        qm = p.qmeta[qe];
+        qr = p.qring + qe * p.cap_q;
+      }
+      const int64_t pr = p.prop_const >= 0 ? p.prop_const : AT(p.prop, e, p.E);
+      const uint32_t slot = p.mesh ? sn * (p.N - 1) + (i < sn ? i : i - 1) : AT(p.rev, e, p.E);
+      const uint32_t dg = rep * p.N + sn;
+      ++st_edges;
+      for (uint32_t j = j0; j < j1; ++j) {
+        const RawOp o = ld_raw(&ops[didx[dkey[j] & 0x1FFFu]]);
+        ++st_ops;
+        const uint32_t kind = raw_kind(o);
+        if (kind == OP_SEND) ++sends;
+        const bool is_echo = kind == OP_ECHO;
+        const int big = (raw_flags(o) & OPF_BIG) ? 1 : 0;
+        const int64_t ot = raw_t(o);
+        const int64_t start = bu > ot ? bu : ot;
+        if (p.qmodel) {
+          const uint32_t F = p.nfr[big];
+          const uint32_t k = q_admit(p, qr, qm, ot, big, start);
+          if (k < F) {
+            fdrop += F - k;
+            if (k) bu = start + static_cast<int64_t>(k) * p.tx_full[big];
+            if (!is_echo) ++lost;
+            continue;
+          }
+        }
+        const int64_t end = start + p.tx_tot[big];
+        bu = end;
+        if (is_echo) {
+          ++st_echo;
+          continue;
+        }
+        const int64_t ta = end + pr;
+        const long long ca = ta / p.L;
+        const long long rel = ca - cell;
+        if (rel < 1) {
+          set_err(p, BCSIM_E_TIE);  // lookahead violated
+          continue;
+        }
+        ++n_rec;
+        lc = static_cast<uint32_t>(ca) & 0xFFFFu;
+        XRec x;
+        {
+          const uint32_t w3 = (o.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+          const uint4 rv = make_uint4(static_cast<uint32_t>(ta - ca * p.L), raw_sub(o), o.b.z, w3);
+          __builtin_memcpy(&x.r, &rv, sizeof x.r);
+        }
+        x.cell = ca;
+        x.slot = slot;
+        x.g = dg;
+        uint32_t orank = p.rank;
+        if (p.nranks > 1) orank = p.owner[sn];
+        if (orank != p.rank) {
+          link_stage(p, L, g, B + 1 + orank, x);  // receiver on another GPU (k_import places it)
+        } else if (rel < static_cast<long long>(B)) {
+          const uint32_t bk = static_cast<uint32_t>(ca % B);
+          link_stage(p, L, g, bk, x);
+          set_flag_once(&AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT));
+          atomicAdd(&L.lcnt[bk], 1u);
+        } else {
+          link_stage(p, L, g, B, x);
+          if (ca < ovmin) ovmin = ca;
+        }
+      }
+      if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+      *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
+      if (p.qmodel) p.qmeta[qe] = qm;
+    }
+    __syncthreads();
+    lo_e = hi_e;
+  }
+  // ---- 3. keep the ops that are not due (in order) ----
+  long long omin = LLONG_MAX;
+  uint32_t kept = 0;
+  for (uint32_t k0 = 0; k0 < n; k0 += bs) {
+    const uint32_t k = k0 + tid;
+    Op o{};
+    bool keep = false;
+    if (k < n) {
+      o = ops[k];
+      const uint8_t kind = op_kind(o);
+      if (kind == OP_BCAST_J)
+        keep = !(op_flags(o) & OPF_DONE);
+      else if (o.t >= t_hi) {
+        keep = true;
+        if (o.t < omin) omin = o.t;
+      }
+    }
+    uint32_t tot;
+    const uint32_t pos = kept + block_rank(keep, L.wcnt, tot);
+    if (keep) ops[pos] = o;
+    kept += tot;
+  }
+  if (tid == 0) L.n_keep = kept;
+  if (omin != LLONG_MAX) atomicMin(&L.omin, omin);
+  if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
+  // ---- 4. flush the staged records: one global atomic per list ----
+  for (uint32_t k = tid; k < n_lists; k += bs) {
+    const uint32_t c = L.lst[k];
+    if (!c) continue;
+    uint32_t* ctr = k < B ? &p.x_cnt[k] : k == B ? p.ov_cnt : &p.send_cnt[k - B - 1];
+    const uint32_t cap = k < B ? p.cap_x : k == B ? p.cap_ov : p.cap_send;
+    const uint32_t base = atomicAdd(ctr, c);
+    if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
+    L.lbase[k] = base;
+  }
+  __syncthreads();
+  const uint32_t nst = min(L.nst, p.cap_stage);
+  for (uint32_t k = tid; k < nst; k += bs) {
+    const size_t sidx = static_cast<size_t>(blockIdx.x) * p.cap_stage + k;
+    const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
+    const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
+    if (list > B) {
+      if (pos < p.cap_send) p.sendbuf[static_cast<size_t>(list - B - 1) * p.cap_send + pos] = p.xstage[sidx];
+    } else if (list == B) {
+      if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
+    } else if (pos < p.cap_x) {
+      p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
+    }
+  }
+  // ---- 5. counters ----
+  uint4 t1, t2;
+  (void)block_scan4(make_uint4(static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends),
+                               static_cast<uint32_t>(n_rec), static_cast<uint32_t>(st_ops)), L.wsum, t1);
+  (void)block_scan4(make_uint4(static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo),
+                               static_cast<uint32_t>(fdrop), static_cast<uint32_t>(lost)), L.wsum, t2);
+  if (tid == 0) {
+    if (t1.x) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(t1.x));
+    if (t1.y) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(t1.y));
+    if (t1.z) atomicAdd(&kst_stripe(p)[KST_REC], static_cast<unsigned long long>(t1.z));
+    if (t1.w) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(t1.w));
+    if (t2.x) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(t2.x));
+    if (t2.y) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(t2.y));
+    if (t2.z) atomicAdd(&cnt[CNT_FDROP], static_cast<unsigned long long>(t2.z));
+    if (t2.w) atomicAdd(&cnt[CNT_LOST], static_cast<unsigned long long>(t2.w));
+  }
+  __syncthreads();
+  for (uint32_t k = tid; k < B; k += bs)
+    if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
+  if (tid == 0) {
+    if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
+    AT(p.n_ops, g, p.NT) = L.n_keep;
+    AT(p.node_onext, g, p.NT) = L.omin;
+    atomicAdd(&kst_stripe(p)[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
+  }
+  (void)final_win;
+  (void)cs;
+}
+
+__global__ __launch_bounds__(256) void k_link_sparse(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                     long long t_hi, int final_win) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  const uint32_t na = p.act_n[1];
+  for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
+    link_node_sparse(p, p.act[p.NT + k], cell, t_lo, t_hi, final_win);
+    __syncthreads();
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// k_active (sparse mode): the gnodes of this rank that have work in [t_lo, t_hi) --
+// k_scan: arrivals in the bucket, a due timer, START / STOP; k_link: those plus the
+// nodes with an op due -- as two compact lists (one returning atomic per wave; the
+// loop bound is wave-uniform, so every ballot runs with the whole wave active)
+__global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long long t_lo, long long t_hi, uint32_t b) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  const bool has_start = (t_lo <= 0 && 0 < t_hi);
+  const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t n_loc = static_cast<uint64_t>(p.R) * p.nloc;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); base < n_loc;
+       base += stride) {
+    const uint64_t k = base + lane;
+    bool sc = false, lk = false;
+    uint32_t g = 0;
+    if (k < n_loc) {
+      g = static_cast<uint32_t>((k / p.nloc) * p.N + p.nlo + k % p.nloc);
+      const uint32_t rep = g / p.N, i = g % p.N;
+      sc = has_start || has_stop || node_flagged(p, b, g, rep, i) || AT(p.node_tnext, g, p.NT) < t_hi;
+      lk = sc || AT(p.node_onext, g, p.NT) < t_hi;
+    }
+    const unsigned long long ms = __ballot(sc), ml = __ballot(lk);
+    uint32_t ps = 0, pl = 0;
+    if (lane == 0) {
+      if (ms) ps = atomicAdd(&p.act_n[0], static_cast<uint32_t>(__popcll(ms)));
+      if (ml) pl = atomicAdd(&p.act_n[1], static_cast<uint32_t>(__popcll(ml)));
+    }
+    ps = __shfl(ps, 0, 64);
+    pl = __shfl(pl, 0, 64);
+    if (sc) p.act[ps + static_cast<uint32_t>(__popcll(ms & lt))] = g;
+    if (lk) p.act[p.NT + pl + static_cast<uint32_t>(__popcll(ml & lt))] = g;
   }
 }
 
@@ -2653,7 +3177,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
           // block = generateTX header '1', v, n, n (:79-95)
           Msg blk = mkmsg(PB_PRE_PREPARE, enc_raw(p, v_cur), enc_raw(p, n_seq), enc_raw(p, n_seq), 1);
           uint32_t nops = AT(p.n_ops, g, p.NT);
-          Op* ops = p.ops + static_cast<size_t>(g) * p.cap_ops;
+          Op* ops = p.ops + op_base(p, g);
           uint64_t draws = AT(p.draws, g, p.NT);
           auto push_bcast = [&](const Msg& m) {
             if (nops >= p.cap_ops) {

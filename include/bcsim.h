@@ -57,6 +57,7 @@ enum { BCSIM_ENC_EXTENDED = 0, BCSIM_ENC_COMPAT = 1 };
 /* Link queue model: INFINITE = unbounded FIFO; DROPTAIL = at most queue_dev_pkts +
  * queue_disc_pkts frames waiting per link, later frames dropped (fragment loss) */
 enum { BCSIM_QUEUE_INFINITE = 0, BCSIM_QUEUE_DROPTAIL = 1 };
+enum { BCSIM_ENGINE_AUTO = 0, BCSIM_ENGINE_DENSE = 1, BCSIM_ENGINE_SPARSE = 2 };
 
 /* ---- status codes --------------------------------------------------------- */
 enum {
@@ -129,7 +130,12 @@ typedef struct bcsim_config {
    * proposer runs instances 0..paxos_decrees-1 one after another; 0/1 = the
    * reference's single decree (paxos-node.cc:510-522, :323-361) */
   uint32_t paxos_decrees;
-  uint32_t reserved[3];
+  /* GPU engine layout: DENSE = a 16-byte inbox slot per edge and
+   * bucket, one workgroup per node per launch; SPARSE = list-only inbox, launches
+   * over the active nodes, hub-compact link state (Paxos on the full mesh); AUTO =
+   * SPARSE when the dense per-edge state of all replicas exceeds ~96 GB */
+  uint32_t engine_mode;        /* BCSIM_ENGINE_AUTO / _DENSE / _SPARSE */
+  uint32_t reserved[2];
 } bcsim_config;
 
 /* ---- outputs -------------------------------------------------------------- */
