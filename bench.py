@@ -137,7 +137,9 @@ def main():
                     help="pbft: BASELINE configs[3] (the metric); gossip: configs[4], random 8-regular graph; "
                          "paxos: configs[2] shape (jittered links, batched Monte Carlo replicas)")
     ap.add_argument("--nodes", type=int, default=0, help="default 4096 (pbft, paxos) / 65536 (gossip)")
-    ap.add_argument("--replicas", type=int, default=0, help="paxos: replicas in one launch (default 16)")
+    ap.add_argument("--replicas", type=int, default=0,
+                    help="paxos: replicas in one engine (default 2048, sparse layout; configs[2] names 10k)")
+    ap.add_argument("--decrees", type=int, default=2, help="paxos: decrees per proposer (multi-decree extension)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("pdes", "replicas"), default="pdes",
@@ -146,7 +148,7 @@ def main():
     if args.nodes <= 0:
         args.nodes = 65536 if args.workload == "gossip" else 4096
     if args.replicas <= 0:
-        args.replicas = 16 if args.workload == "paxos" else 1
+        args.replicas = 2048 if args.workload == "paxos" else 1
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -161,6 +163,8 @@ def main():
     import bcsim
     period = 50_000_001  # Seconds(0.05f) in ns (round mode)
     cfg = make_cfg(args.nodes, args.warmup + args.steps + 4, local, args.workload, args.replicas)
+    if args.workload == "paxos":
+        cfg.paxos_decrees = args.decrees
     topo = make_topology(args.nodes, args.workload)
 
     def new_sim():
@@ -234,8 +238,9 @@ def main():
             wl = f"PBFT n={args.nodes} full O(n^2) prepare/commit (BASELINE configs[3])"
         elif args.workload == "paxos":
             data = ("synthetic (Paxos n=%d full mesh, 3Mbps/3ms links, app delay U{0..49} ms, counter RNG, "
-                    "%d replicas, seeds by replica)" % (args.nodes, args.replicas))
-            wl = f"Paxos n={args.nodes} jittered links, {args.replicas} batched Monte Carlo replicas (BASELINE configs[2] shape)"
+                    "%d replicas, %d decrees, seeds by replica, sparse layout)" % (args.nodes, args.replicas, args.decrees))
+            wl = (f"Paxos n={args.nodes} multi-decree ({args.decrees}), jittered links, {args.replicas} batched "
+                  f"Monte Carlo replicas (BASELINE configs[2])")
         else:
             data = ("synthetic (PBFT-style gossip, n=%d random 8-regular graph seed 1, 3Mbps/3ms links, "
                     "1000 B blocks, fixed 3 ms app delay)" % args.nodes)
