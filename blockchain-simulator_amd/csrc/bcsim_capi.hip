@@ -367,7 +367,7 @@ static int setup_device(Sim& s) {
   // engine layout: the dense per-edge state of every replica (8 buckets
   // of inbox slots, link word, reply slots) or the sparse list-only layout
   {
-    const double dense_bytes = static_cast<double>(s.R) * s.E * (8.0 * sizeof(Rec) + 8.0 + kOpRing * sizeof(Op));
+    const double dense_bytes = static_cast<double>(s.R) * s.E * (8.0 * sizeof(Rec) + 8.0 + kOpRing * 16.0);
     s.sparse = c.engine_mode == BCSIM_ENGINE_SPARSE || (c.engine_mode == BCSIM_ENGINE_AUTO && dense_bytes > 96e9);
   }
   p.sparse = s.sparse ? 1u : 0u;
@@ -455,16 +455,25 @@ static int setup_device(Sim& s) {
       g_detail = "k_scan LDS request too large";
       return BCSIM_E_UNSUPPORTED;
     }
-    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT>),
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
-    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_RAFT>),
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
-    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS>),
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_RAFT, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
-    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_GOSSIP>),
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_RAFT, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
-    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_link),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(link_lds_bytes(p))));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS, false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_GOSSIP, false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_GOSSIP, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    for (const void* f : {reinterpret_cast<const void*>(k_link<false, false>), reinterpret_cast<const void*>(k_link<false, true>),
+                          reinterpret_cast<const void*>(k_link<true, false>), reinterpret_cast<const void*>(k_link<true, true>)})
+      HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(link_lds_bytes(p))));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_pbft_tick),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(s.N)));
   }
@@ -556,11 +565,13 @@ static int setup_device(Sim& s) {
     const char* ns = std::getenv("BCSIM_NO_SLOTS");
     const bool off = ns && *ns == '1';
     p.impl = (off || s.sparse) ? 0u : 1u;  // sparse: no slots, echoes listed by k_scan
-    const bool on = ne * sizeof(Op) <= (16ull << 30) && !off && !s.sparse;
+    // PBFT replies with a fixed app delay < L (due in the arrival cell or the next)
+    const bool on = ne * 16 <= (16ull << 30) && !off && !s.sparse && c.protocol == BCSIM_PBFT &&
+                    c.delay_mode == BCSIM_DELAY_FIXED && c.app_delay_ns < s.L;
     p.cap_eslot = on ? ne : 1;
     if ((rc = dalloc(s, &p.eslot, p.cap_eslot)) || (rc = dalloc(s, &p.sflag, static_cast<size_t>(kOpRing) * NT)))
       return rc;
-    HIPCHK(hipMemset(p.eslot, 0xFF, p.cap_eslot * sizeof(Op)));  // t = -1: no live op
+    HIPCHK(hipMemset(p.eslot, 0xFF, p.cap_eslot * 16));  // due t = -1: no live reply
     HIPCHK(hipMemset(p.sflag, 0, static_cast<size_t>(kOpRing) * NT));
     if (!on) p.eslot = nullptr;
   }
@@ -764,14 +775,18 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   }
   const int fw = final_win ? 1 : 0, xa = s.x_active;
   int rc;
+#define BCSIM_SCAN(P)                                                                                   \
+  (s.sparse ? launch(s, KS_SCAN, k_scan<P, true>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa) \
+            : launch(s, KS_SCAN, k_scan<P, false>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa))
   if (s.cfg.protocol == BCSIM_PBFT)
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_PBFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
+    rc = BCSIM_SCAN(BCSIM_PBFT);
   else if (s.cfg.protocol == BCSIM_RAFT)
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_RAFT>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
+    rc = BCSIM_SCAN(BCSIM_RAFT);
   else if (s.cfg.protocol == BCSIM_GOSSIP)
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_GOSSIP>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
+    rc = BCSIM_SCAN(BCSIM_GOSSIP);
   else
-    rc = launch(s, KS_SCAN, k_scan<BCSIM_PAXOS>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
+    rc = BCSIM_SCAN(BCSIM_PAXOS);
+#undef BCSIM_SCAN
   if (rc) return rc;
   if (s.kp.wgs) {  // debug (BCSIM_WGT=1): mean k_scan phase times of a heavy launch
     std::vector<unsigned long long> w(8ull * s.NT);
@@ -804,8 +819,14 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   }
   if (s.sparse)
     rc = launch(s, KS_LINK, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw);
-  else
-    rc = launch(s, KS_LINK, k_link, grid, dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw);
+  else {
+    const size_t ll = link_lds_bytes(s.kp);
+    const bool qm = s.kp.qmodel != 0, xr = s.kp.nranks > 1;
+    rc = qm ? (xr ? launch(s, KS_LINK, k_link<true, true>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw)
+                  : launch(s, KS_LINK, k_link<true, false>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw))
+            : (xr ? launch(s, KS_LINK, k_link<false, true>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw)
+                  : launch(s, KS_LINK, k_link<false, false>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw));
+  }
   if (rc || !s.kp.wgt) return rc;
   // debug (BCSIM_WGT=1): report the slowest k_link workgroups of this launch
   std::vector<unsigned long long> w(8ull * s.NT);

@@ -93,8 +93,13 @@ struct KP {
   // (replica, edge) for a unicast reply (PBFT PREPARE_RES) of the edge's main
   // inbox record.  A slot op is live while t >= the current window start;
   // nullptr = disabled (replies go to the op lists)
-  Op* eslot;             // [kOpRing][R][E]
-  uint8_t* sflag;        // [kOpRing][NT] node has reply-slot ops in the ring cell
+  // 16-byte reply slots keyed by the ARRIVAL cell (ring index = arrival cell % kOpRing):
+  // a main-slot arrival has at most one reply, so a slot is never occupied when written
+  // (no read-before-write); entry = {due t lo, due t hi, sub, f0 | f1 << 16} of the PBFT
+  // PREPARE_RES (type, f2 = '0', dt = app delay, origin = node are implied).  Only with
+  // fixed app delays < L (due cell <= arrival cell + 1).
+  uint4* eslot;          // [kOpRing][R][E]
+  uint8_t* sflag;        // [kOpRing][NT] bit k: replies of this arrival cell due in arrival cell + k
   uint64_t cap_eslot;
   // implicit echoes: k_link echoes a node's main inbox records itself (the
   // in-slot index is the reverse out-edge) and releases the slots; k_scan
@@ -498,17 +503,16 @@ static_assert(offsetof(Op, sub) == 16 && offsetof(Op, f0) == 24 && offsetof(Op, 
 
 // per-edge op slots
 constexpr uint32_t kOpRing = 4;
-__device__ inline Op* eslot_at(const KP& p, uint32_t ob, uint32_t rep, uint32_t e) {
+__device__ inline uint4* eslot_at(const KP& p, uint32_t ob, uint32_t rep, uint32_t e) {
   return &AT(p.eslot, (static_cast<size_t>(ob) * p.R + rep) * p.E + e, p.cap_eslot);
 }
-// may the reply of a main-slot arrival, due at t_r, sit in its edge's slot 1?
-// (within the ring, and the slot holds no live op: live = t >= t_lo)
-__device__ inline bool reply_slot_free(const KP& p, long long cell, long long t_lo, int64_t t_r, uint32_t rep,
-                                       uint32_t q) {
-  const long long dc = t_r / p.L - cell;
-  if (dc < 0 || dc >= static_cast<long long>(kOpRing)) return false;
-  const uint32_t ob = static_cast<uint32_t>((t_r / p.L) % kOpRing);
-  return eslot_at(p, ob, rep, q)->t < t_lo;
+constexpr uint32_t kPbPrepareRes = 5;  // PBFT PREPARE_RES (pbft-node.h:80-91), the only slot reply
+// the full op of a reply slot: SEND at the stored due time, dt = app delay, origin =
+// this node, payload (v, n, intToChar(0)) of a PREPARE_RES
+__device__ inline RawOp slot_op(const KP& p, const uint4 w, uint32_t i, uint32_t e) {
+  const uint32_t f2 = static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0)));
+  return RawOp{make_uint4(w.x, w.y, static_cast<uint32_t>(p.app_delay), i),
+               make_uint4(w.z, e, w.w, f2 | (kPbPrepareRes << 16) | (static_cast<uint32_t>(OP_SEND) << 24))};
 }
 
 // ---- block-wide primitives (blockDim.x a multiple of 64, <= 1024) ----------
@@ -1184,6 +1188,7 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
   uint32_t n = 0;
   for (uint32_t base = 0; base < deg; base += 4 * blockDim.x) {
     Rec rr[4];
+    bool vv[4];
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {  // all loads in flight before the first rank
       const uint32_t k = base + j * blockDim.x + tid;
@@ -1191,20 +1196,24 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
     }
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
-      if (base + j * blockDim.x >= deg) break;  // block-uniform
       const uint32_t k = base + j * blockDim.x + tid;
-      const Rec r = rr[j];
-      const long long t = cs + r.t_off;
-      const bool v = k < deg && (r.flags & RF_VALID) && t >= wa && t < wb;
-      uint32_t tot;
-      const uint32_t pos = n + block_rank(v, S.wcnt, tot);
-      if (store && v && pos < p.cap_arr) {
-        arec[pos] = r;
-        asec[pos] = (k << kRidxBits) | pos;
-        akey[pos] = arr_key(p, r, e0 + k);
-      }
-      n += tot;
+      const long long t = cs + rr[j].t_off;
+      vv[j] = k < deg && (rr[j].flags & RF_VALID) && t >= wa && t < wb;
     }
+    // one block scan ranks all four chunks: chunk j's records follow chunks < j (slot order)
+    uint4 tot;
+    const uint4 ex = block_scan4(make_uint4(vv[0], vv[1], vv[2], vv[3]), S.wsum, tot);
+    const uint32_t pos4[4] = {n + ex.x, n + tot.x + ex.y, n + tot.x + tot.y + ex.z, n + tot.x + tot.y + tot.z + ex.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t k = base + j * blockDim.x + tid, pos = pos4[j];
+      if (store && vv[j] && pos < p.cap_arr) {
+        arec[pos] = rr[j];
+        asec[pos] = (k << kRidxBits) | pos;
+        akey[pos] = arr_key(p, rr[j], e0 + k);
+      }
+    }
+    n += tot.x + tot.y + tot.z + tot.w;
   }
   const uint32_t n_main = n;
   for (uint32_t base = 0; base < xn; base += blockDim.x) {
@@ -1296,7 +1305,7 @@ __device__ inline uint32_t quorum_slot(const KP& p, ScanShared& S, uint32_t key,
 //   VIEW_CHANGE   leader = msg (last one wins), "Wrong msg"
 // Crossings are ranks within each (phase, sequence) group: wave 0 walks the
 // window 64 arrivals at a time, grouping lanes by ballot.
-__device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep, uint32_t i, uint32_t e0,
+__device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep, uint32_t i, uint32_t e0,
                             uint32_t deg, uint32_t n, uint32_t n_main, long long cell, long long cs, long long t_lo,
                             const uint64_t* akey, const uint32_t* asec, const Rec* arec, uint32_t* acls) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -1426,22 +1435,7 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   const bool slots = p.eslot != nullptr;
   uint4 loc = make_uint4(0, 0, 0, 0);  // sub, draws, commits, ops
   uint32_t rslot = 0;                   // bit j: reply of arrival r0 + j goes to its edge slot
-  int64_t occ[4];                       // reply-slot occupancy of the first 4 arrivals (t of the op there)
-#pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
-    occ[j] = LLONG_MAX;
-    const uint32_t r = r0 + j;
-    if (r < r1 && slots && fixed) {
-      const uint32_t sec = asec[r];
-      const Rec rec = arec[sec & kRidxMask];
-      if (rec.type == PB_PREPARE && (sec & kRidxMask) < n_main) {
-        const int64_t tr = cs + rec.t_off + p.app_delay;
-        const long long dc = tr / p.L - cell;
-        if (dc >= 0 && dc < static_cast<long long>(kOpRing))
-          occ[j] = eslot_at(p, static_cast<uint32_t>((tr / p.L) % kOpRing), rep, e0 + (sec >> kRidxBits))->t;
-      }
-    }
-  }
+#pragma nounroll
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
     const Rec rec = arec[sec & kRidxMask];
@@ -1457,10 +1451,8 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
     } else if (rec.type == PB_PREPARE) {
       si = 1;
       di = fixed ? 0u : 1u;
-      const uint32_t q = e0 + (sec >> kRidxBits);
-      const bool fr = r - r0 < 4 ? occ[r - r0] < t_lo
-                                 : reply_slot_free(p, cell, t_lo, cs + rec.t_off + p.app_delay, rep, q);
-      if (main_slot && fixed && r - r0 < 32 && fr)
+      // the reply of a main-slot arrival owns its edge's slot of this arrival cell
+      if (main_slot && fixed && r - r0 < 32)
         rslot |= 1u << (r - r0);
       else
         oi += 1;
@@ -1491,7 +1483,8 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
   uint32_t sp = sub0 + ex.x, op = nops0 + ex.w, cp = ex.z;
   uint64_t dp = draws0 + ex.y;
   unsigned long long wrong = 0;
-  uint32_t n_slot[kOpRing] = {0, 0, 0, 0};
+  uint32_t n_slot0 = 0, n_slot1 = 0;  // slot replies due in this cell / the next (app delay < L)
+#pragma nounroll
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
     const Rec rec = arec[sec & kRidxMask];
@@ -1524,8 +1517,15 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
         const Op ro = mk_op(p, t + d, static_cast<uint32_t>(d), i, sp++, q, rr, OP_SEND, 0);
         if (rslot & (1u << (r - r0))) {
           const long long dc = ro.t / p.L;
-          st_op(eslot_at(p, static_cast<uint32_t>(dc % kOpRing), rep, q), ro);
-          ++n_slot[dc - cell];
+          const uint64_t ut = static_cast<uint64_t>(ro.t);
+          *eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q) =
+              make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), ro.sub,
+                         (static_cast<uint32_t>(static_cast<uint16_t>(ro.f0))) |
+                             (static_cast<uint32_t>(static_cast<uint16_t>(ro.f1)) << 16));
+          if (dc == cell)
+            ++n_slot0;
+          else
+            ++n_slot1;
         } else {
           ops[op++] = ro;
         }
@@ -1579,8 +1579,8 @@ __device__ void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep
     wave_add_by_key(act && ty < BCSIM_MSG_TYPES, ty, 1u, S.deliv);
   }
   if (wrong) atomicAdd(&S.wrong, wrong);
-  for (uint32_t k = 0; k < kOpRing; ++k)
-    if (n_slot[k]) atomicAdd(&S.ocnt[k], n_slot[k]);
+  if (n_slot0) atomicAdd(&S.ocnt[0], n_slot0);
+  if (n_slot1) atomicAdd(&S.ocnt[1], n_slot1);
   __syncthreads();
   SPH(6);
   // ---- E: tx[n].val of the window's PRE_PREPAREs (last one per index wins) ----
@@ -1678,8 +1678,8 @@ __device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint3
          static_cast<uint64_t>(p.NT) * p.pbft_seq_cap) = 1;
 }
 
-template <int PROTO>
-__device__ void scan_node(const KP* __restrict__ pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
+template <int PROTO, bool SP>
+__device__ __attribute__((always_inline)) inline void scan_node(const KP* __restrict__ pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
                           long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   // LDS: akey[cap] u64 | asec[cap] u32 | arec[cap] Rec | acls[cap] u32 | timers
@@ -1703,8 +1703,8 @@ __device__ void scan_node(const KP* __restrict__ pk, uint32_t g, long long cell,
 
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
   // sparse mode: no inbox slots, the node's arrivals are all in the cell's grouped lists
-  const Rec* slots = p.sparse ? nullptr : p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0;
-  const uint32_t deg_in = p.sparse ? 0u : deg;
+  const Rec* slots = SP ? nullptr : p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0;
+  const uint32_t deg_in = SP ? 0u : deg;
   uint32_t xn = 0;
   const XRec* xs = p.xgrp;
   if (x_active) {
@@ -1964,10 +1964,14 @@ __device__ void scan_node(const KP* __restrict__ pk, uint32_t g, long long cell,
   // (implicit echoes: k_link still reads this cell's slots and clears the flag)
   if (final_win && flag && tid == 0 && !p.impl) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
   // slot ops make their cells busy (bucket counts) and flag this node for k_link
-  if (tid < kOpRing && S.ocnt[tid]) {
-    const long long dc = cell + tid;
-    mark_busy(&p.bucket_cnt[dc % p.n_buckets]);
-    AT(p.sflag, (dc % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 1;
+  if (tid < kOpRing && S.ocnt[tid]) mark_busy(&p.bucket_cnt[(cell + tid) % p.n_buckets]);
+  if (tid == 0) {
+    uint32_t m = 0;
+    for (uint32_t k = 0; k < kOpRing; ++k) m |= S.ocnt[k] ? (1u << k) : 0u;
+    if (m) {
+      uint8_t& f = AT(p.sflag, (cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT);
+      f = static_cast<uint8_t>(f | m);
+    }
   }
 
   // ---- write back ----
@@ -2044,19 +2048,19 @@ __device__ void scan_node(const KP* __restrict__ pk, uint32_t g, long long cell,
 
 // dense mode: one workgroup per gnode of this rank; sparse mode: a fixed grid strides
 // over the window's active list (k_active)
-template <int PROTO>
+template <int PROTO, bool SP>
 __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                long long t_hi, long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  if (!p.sparse) {
+  if (!SP) {
     if (blockIdx.x >= p.R * p.nloc) return;
-    scan_node<PROTO>(pk, local_gnode(p, blockIdx.x), cell, t_lo, t_hi, cs, final_win, x_active);
+    scan_node<PROTO, false>(pk, local_gnode(p, blockIdx.x), cell, t_lo, t_hi, cs, final_win, x_active);
     return;
   }
   const uint32_t na = *p.act_n;
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
-    scan_node<PROTO>(pk, p.act[k], cell, t_lo, t_hi, cs, final_win, x_active);
+    scan_node<PROTO, true>(pk, p.act[k], cell, t_lo, t_hi, cs, final_win, x_active);
     __syncthreads();
   }
 }
@@ -2175,14 +2179,21 @@ __device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32
   }
 }
 
-__device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
+// QM: DROPTAIL queue model; XR: node-partitioned run (records for other ranks).  Both are
+// template flags so the common case (infinite queues, one rank) carries none of their
+// registers through the per-edge loop.
+template <bool QM, bool XR>
+__device__ __attribute__((always_inline)) inline void link_node(const KP* __restrict__ pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
                           int final_win) {
   const KP& p = *pk;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ LinkShared L;
   uint32_t n = AT(p.n_ops, g, p.NT);
-  const uint32_t ob = static_cast<uint32_t>(cell % kOpRing);
-  const bool sl = p.eslot && AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT);
+  // reply slots of this arrival cell (bit 0: due now) and of the previous one (bit 1)
+  const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
+  const bool sl0 = p.eslot && (AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u);
+  const bool sl1 = p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u);
+  const bool sl = sl0 || sl1;
   const uint32_t ib = static_cast<uint32_t>(cell % p.n_buckets);
   const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
   const uint32_t rep = g / p.N, i = g % p.N;
@@ -2350,15 +2361,20 @@ __device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell,
         }
       }
     }
-    // this edge's reply-slot op due in [t_lo, t_hi)
-    bool hr = false;
-    RawOp ro = raw_zero();
-    if (sl) {
-      ro = ld_raw(eslot_at(p, ob, rep, e));
+    // this edge's reply-slot ops due in [t_lo, t_hi): of this arrival cell and the previous one
+    bool hr = false, hr2 = false;
+    RawOp ro = raw_zero(), ro2 = raw_zero();
+    if (sl0) {
+      ro = slot_op(p, *eslot_at(p, ob, rep, e), i, e);
       hr = raw_t(ro) >= t_lo && raw_t(ro) < t_hi;
       if (hr) ++st_ops;
     }
-    if (ee == eb && n_bc == 0 && !he && !hr) continue;
+    if (sl1) {
+      ro2 = slot_op(p, *eslot_at(p, obp, rep, e), i, e);
+      hr2 = raw_t(ro2) >= t_lo && raw_t(ro2) < t_hi;
+      if (hr2) ++st_ops;
+    }
+    if (ee == eb && n_bc == 0 && !he && !hr && !hr2) continue;
     for (uint32_t a = eb + 1; a < ee; ++a) {  // insertion sort of this edge's ops (few)
       const uint32_t x = eidx[a];
       const Op ox = ops[x];
@@ -2383,7 +2399,7 @@ __device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell,
     uint32_t lc = static_cast<uint32_t>(lw & 0xFFFFu);
     uint64_t qm = 0;
     uint64_t* qr = nullptr;
-    if (p.qmodel) {
+    if (QM) {
       qm = p.qmeta[eb0 + le];
       qr = p.qring + (eb0 + le) * p.cap_q;
     }
@@ -2418,6 +2434,11 @@ __device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell,
         sub = raw_sub(ro);
         src = 2;
       }
+      if (hr2 && (src < 0 || raw_key_less(ro2, raw_sub(ro2), o, sub))) {
+        o = ro2;
+        sub = raw_sub(ro2);
+        src = 4;
+      }
       if (he && (src < 0 || raw_key_less(eo, raw_sub(eo), o, sub))) {
         o = eo;
         sub = raw_sub(eo);
@@ -2430,14 +2451,16 @@ __device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell,
         ++bi;
       else if (src == 2)
         hr = false;
+      else if (src == 4)
+        hr2 = false;
       else
         he = false;
-      if (src == 2 && raw_kind(o) == OP_SEND) ++sends;
+      if ((src == 2 || src == 4) && raw_kind(o) == OP_SEND) ++sends;
       const bool is_echo = src != 1 && raw_kind(o) == OP_ECHO;
       const int big = (raw_flags(o) & OPF_BIG) ? 1 : 0;
       const int64_t ot = raw_t(o);
       const int64_t start = bu > ot ? bu : ot;
-      if (p.qmodel) {  // DROPTAIL: a refused fragment loses the message (its accepted prefix still occupies the link)
+      if (QM) {  // DROPTAIL: a refused fragment loses the message (its accepted prefix still occupies the link)
         const uint32_t F = p.nfr[big];
         const uint32_t k = q_admit(p, qr, qm, ot, big, start);
         if (k < F) {
@@ -2469,7 +2492,7 @@ __device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell,
       // sparse mode has no slots: every record is a list record
       const bool owner = !p.sparse && lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
       lc = static_cast<uint32_t>(ca) & 0xFFFFu;
-      if (p.nranks > 1) {
+      if (XR) {
         const uint32_t orank = p.owner[s];
         if (orank != p.rank) {  // receiver on another GPU: ship the record (k_import places it)
           XRec x;
@@ -2535,7 +2558,7 @@ __device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell,
     }
     if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
     *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
-    if (p.qmodel) p.qmeta[eb0 + le] = qm;
+    if (QM) p.qmeta[eb0 + le] = qm;
   }
   if (cbn) atomicAdd(&L.lcnt[cb], cbn);
   __syncthreads();
@@ -2629,7 +2652,8 @@ __device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell,
   }
   if (tid == 0) {
     if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
-    if (sl && final_win) AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 0;
+    // the previous arrival cell's replies are all consumed now
+    if (sl1 && final_win) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 0;
     if (rx && final_win) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
     AT(p.n_ops, g, p.NT) = L.n_keep;
     AT(p.node_onext, g, p.NT) = L.omin;
@@ -2637,12 +2661,13 @@ __device__ void link_node(const KP* __restrict__ pk, uint32_t g, long long cell,
   }
 }
 
+template <bool QM, bool XR>
 __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                               long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (blockIdx.x >= p.R * p.nloc) return;
-  link_node(pk, local_gnode(p, blockIdx.x), cell, t_lo, t_hi, final_win);
+  link_node<QM, XR>(pk, local_gnode(p, blockIdx.x), cell, t_lo, t_hi, final_win);
 }
 
 // ---------------------------------------------------------------------------
