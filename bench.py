@@ -60,9 +60,14 @@ def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):
     path = os.path.join(REPO, "profiles", f"{PMC_ROUND}_pmc_{workload}{n_nodes}.json")
     try:
         with open(path) as f:
-            return json.load(f)["kernels"][kernel]["hbm_bytes_per_launch"]
+            ks = json.load(f)["kernels"]
     except (OSError, KeyError, ValueError):
         return None
+    # templated kernels (k_link<QM, XR>): the instantiation with the most dispatches
+    cands = [v for k, v in ks.items() if k == kernel or k.startswith(kernel + "<")]
+    if not cands:
+        return None
+    return max(cands, key=lambda v: v.get("dispatches", 0))["hbm_bytes_per_launch"]
 
 
 def host_cpu():
@@ -86,11 +91,13 @@ def commit_records(sim, workload):
     return sum(1 for r in sim.trace() if r[6] == kind)
 
 
-def cpu_baseline(n_nodes, budget_s, workload="pbft"):
+def cpu_baseline(n_nodes, budget_s, workload="pbft", tweak=None):
     """Serial oracle DES (same semantics) on the host: a bounded time slice of
     the same workload, run from t=0 in 1 ms slices until budget_s of CPU."""
     import oracle
     cfg = make_cfg(n_nodes, 100, 0, workload)  # one replica (the oracle runs replicas serially)
+    if tweak:
+        tweak(cfg)
     o = oracle.OracleSim(cfg)
     topo = make_topology(n_nodes, workload)
     if topo is not None:
@@ -142,6 +149,11 @@ def main():
     ap.add_argument("--decrees", type=int, default=2, help="paxos: decrees per proposer (multi-decree extension)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--engine", choices=("auto", "dense", "sparse"), default="auto",
+                    help="engine layout (DESIGN.md §4): per-edge inbox slots or sparse bucket lists")
+    ap.add_argument("--jitter", action="store_true",
+                    help="pbft: the reference's default getRandomDelay() app delay (3-5 ms per send, "
+                         "pbft-node.cc:66-69) with the counter RNG, instead of the fixed 3 ms")
     ap.add_argument("--mode", choices=("pdes", "replicas"), default="pdes",
                     help="multi-GPU mode (N>1): node-partitioned PDES or independent replicas")
     args = ap.parse_args()
@@ -165,6 +177,11 @@ def main():
     cfg = make_cfg(args.nodes, args.warmup + args.steps + 4, local, args.workload, args.replicas)
     if args.workload == "paxos":
         cfg.paxos_decrees = args.decrees
+    cfg.engine_mode = {"auto": bcsim.ENGINE_AUTO, "dense": bcsim.ENGINE_DENSE, "sparse": bcsim.ENGINE_SPARSE}[args.engine]
+    if args.jitter and args.workload == "pbft":
+        cfg.delay_mode = bcsim.DELAY_RANDOM
+        cfg.rng_mode = bcsim.RNG_COUNTER
+        cfg.app_delay_ns = 0
     topo = make_topology(args.nodes, args.workload)
 
     def new_sim():
@@ -234,7 +251,8 @@ def main():
         traffic = pmc_traffic(args.nodes, workload=args.workload)
         all_us = sum(v["us"] for v in ks.values())
         if args.workload == "pbft":
-            data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, fixed 3 ms app delay)" % args.nodes
+            data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, %s)" % (
+                args.nodes, "app delay U{3,4,5} ms per send, counter RNG" if args.jitter else "fixed 3 ms app delay")
             wl = f"PBFT n={args.nodes} full O(n^2) prepare/commit (BASELINE configs[3])"
         elif args.workload == "paxos":
             data = ("synthetic (Paxos n=%d full mesh, 3Mbps/3ms links, app delay U{0..49} ms, counter RNG, "
@@ -262,6 +280,7 @@ def main():
             "data": data,
             "config": {"workload": wl,
                        "nodes": args.nodes, "step": "one 50 ms block interval",
+                       "engine": args.engine,
                        "parallelism": f"{mode}{world}" if world > 1 else "single"},
             "committed_rounds_per_s": rounds / dt,
             "roofline": {"kernel": "k_link (inbox scatter)", "bound": "hbm", "achieved": ach,
@@ -278,7 +297,11 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.nodes, args.cpu_budget, args.workload)
+                def tweak(c):
+                    c.delay_mode, c.rng_mode, c.app_delay_ns = cfg.delay_mode, cfg.rng_mode, cfg.app_delay_ns
+                    if args.workload == "paxos":
+                        c.paxos_decrees = args.decrees
+                out["cpu_baseline"] = cpu_baseline(args.nodes, args.cpu_budget, args.workload, tweak)
             except Exception as e:  # never let the baseline leg kill the GPU number
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)

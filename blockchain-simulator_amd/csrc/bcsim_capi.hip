@@ -108,7 +108,10 @@ static std::string trail_dump(const Sim& s) {
 static size_t scan_lds_bytes(const KP& p) {
   return static_cast<size_t>(p.cap_arr) * (8 + 4 + sizeof(Rec) + 4) + p.cap_timers * sizeof(TimerEnt);
 }
-static size_t link_lds_bytes(const KP& p) { return (2ull * (p.deg_max + 1) + p.cap_ops) * 4; }
+// k_link dynamic LDS: ecnt[deg+1] | eidx[cap_eidx]
+static size_t link_lds_bytes(const KP& p) { return (static_cast<size_t>(p.deg_max) + 1 + p.cap_eidx) * 4; }
+// k_link: at most this much dynamic LDS, so that two 512-lane workgroups share a CU
+constexpr size_t kLinkLdsTarget = 72 * 1024;
 
 template <typename T>
 static int dalloc(Sim& s, T** p, size_t count) {
@@ -373,12 +376,18 @@ static int setup_device(Sim& s) {
   p.sparse = s.sparse ? 1u : 0u;
   p.n_heavy = s.N;
   p.cap_ops_light = p.cap_ops;
+  {
+    const size_t room = kLinkLdsTarget / 4 > s.deg_max + 1 + 1024 ? kLinkLdsTarget / 4 - (s.deg_max + 1) : 1024;
+    p.cap_eidx = static_cast<uint32_t>(std::min<size_t>(p.cap_ops, room));
+  }
   if (link_lds_bytes(p) > 150 * 1024) {
     g_detail = "node degree / op capacity exceed the LDS budget of k_link";
     return BCSIM_E_UNSUPPORTED;
   }
   s.bs_scan = static_cast<uint32_t>(std::min<uint64_t>(1024, std::max<uint64_t>(64, next_pow2(s.deg_max + 1))));
-  s.bs_link = s.bs_scan;
+  // k_link: two 512-lane workgroups per CU (LDS <= kLinkLdsTarget each) overlap one
+  // another's barrier phases; one 1024-lane group per CU was 15 % slower at N=4096
+  s.bs_link = std::min<uint32_t>(s.bs_scan, 512);
   // workgroup size caps (powers of two >= 64; tuning knobs, results do not depend on them)
   auto bs_cap = [](const char* name, uint32_t bs) {
     const char* v = std::getenv(name);
@@ -418,7 +427,9 @@ static int setup_device(Sim& s) {
   p.n_buckets = s.B;
   uint64_t cap_x = c.cap_bucket_records;
   if (cap_x == 0) cap_x = s.sparse ? std::min<uint64_t>(1ull << 25, std::max<uint64_t>({65536, NT * 2, static_cast<uint64_t>(s.R) * s.E}))
-                                   : std::max<uint64_t>(65536, NT * 8);
+                                   : std::max<uint64_t>({65536, NT * 8,
+                                                         // jittered sends: several records per edge and cell
+                                                         c.delay_mode == BCSIM_DELAY_RANDOM ? static_cast<uint64_t>(s.R) * s.E / 4 : 0});
   p.cap_x = static_cast<uint32_t>(std::min<uint64_t>(cap_x, 1ull << 26));
   p.cap_stage = static_cast<uint32_t>(2ull * s.deg_max + 256);  // k_link staging per workgroup
   if (s.sparse) {
@@ -558,6 +569,11 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.timers, NT * p.cap_timers)) || (rc = dalloc(s, &p.ops, n_ops_total)) ||
       (rc = dalloc(s, &p.n_ops, NT)))
     return rc;
+  if (!s.sparse && p.cap_eidx < p.cap_ops) {  // k_link index area of nodes with > cap_eidx due ops
+    if ((rc = dalloc(s, &p.eidx_g, static_cast<size_t>(s.R) * s.N * p.cap_ops))) return rc;
+  } else {
+    p.eidx_g = nullptr;
+  }
   // per-edge reply slots of main-slot arrivals (kOpRing cells) and implicit
   // echoes; slots off beyond a 16 GiB budget, both off with BCSIM_NO_SLOTS=1 (A/B aid)
   {
@@ -842,8 +858,19 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       tmax = std::max(tmax, w[8 * g + 1]);
     }
   std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return w[8 * a + 1] - w[8 * a] > w[8 * b + 1] - w[8 * b]; });
-  if (!idx.empty() && tmax - tmin > 100000) {  // > 1 ms (100 MHz clock)
-    std::fprintf(stderr, "[wgt] cell %lld k_link span %.2f ms, %zu WGs:", cell, (tmax - tmin) / 1e5, idx.size());
+  if (!idx.empty() && tmax - tmin > 20000) {  // > 0.2 ms (100 MHz clock)
+    double m[5] = {0, 0, 0, 0, 0};
+    for (uint32_t g : idx) {
+      const unsigned long long* q = &w[8 * g];
+      m[0] += q[1] - q[0];
+      m[1] += q[3] - q[0];
+      m[2] += q[4] - q[3];
+      m[3] += q[5] - q[4];
+      m[4] += q[1] - q[6];
+    }
+    for (double& v : m) v /= 100.0 * idx.size();
+    std::fprintf(stderr, "[wgt] cell %lld k_link span %.2f ms, %zu WGs, mean us: total %.1f classify %.1f scan+place %.1f edges %.1f compact %.1f; slowest:",
+                 cell, (tmax - tmin) / 1e5, idx.size(), m[0], m[1], m[2], m[3], m[4]);
     for (size_t k = 0; k < std::min<size_t>(5, idx.size()); ++k) {
       const uint32_t g = idx[k];
       const unsigned long long* q = &w[8 * g];

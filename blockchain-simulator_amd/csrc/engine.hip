@@ -89,6 +89,8 @@ struct KP {
   Op* ops;
   uint32_t* n_ops;
   uint32_t cap_ops;
+  uint32_t cap_eidx;  // k_link LDS index capacity for listed due ops
+  uint32_t* eidx_g;   // [grid][cap_ops] k_link index area of a node with more (nullptr: cap_eidx == cap_ops)
   // per-edge reply slots: ring of kOpRing cells, one slot per
   // (replica, edge) for a unicast reply (PBFT PREPARE_RES) of the edge's main
   // inbox record.  A slot op is live while t >= the current window start;
@@ -593,6 +595,13 @@ __device__ inline uint32_t block_scan_array(uint32_t* a, uint32_t n, uint4* wsum
   }
   __syncthreads();
   return tot.x;
+}
+
+// Sum of v over the wave (all lanes get it).
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
 }
 
 // Add `inc` to lds[key] once per distinct key of the wave (wave-aggregated
@@ -2128,7 +2137,8 @@ __device__ inline uint32_t q_admit(const KP& p, uint64_t* ring, uint64_t& meta, 
 }
 
 struct LinkShared {
-  uint32_t n_bc, n_keep;
+  uint32_t n_bc, n_keep, n_list;
+  uint32_t csum[8];  // block counters (wave sums, LDS atomics)
   uint32_t bc[kBcastCap];
   Op bco[kBcastCap];         // the due broadcasts in key order (LDS copies: every lane reads them per edge)
   uint32_t lcnt[kMaxBuckets];
@@ -2206,55 +2216,74 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
   Op* ops = p.ops + op_base(p, g);
   const uint32_t ocap = op_cap(p, g);
-  uint32_t* ecnt = reinterpret_cast<uint32_t*>(smem);   // deg+1
-  uint32_t* efill = ecnt + (p.deg_max + 1);              // deg
-  uint32_t* eidx = efill + p.deg_max;                    // cap_ops
+  // LDS: ecnt[deg+1] (per-edge counts -> offsets -> ends) | eidx[cap_eidx] (listed due ops
+  // grouped by edge; a node with more due ops than cap_eidx uses its global area eidx_g)
+  uint32_t* ecnt = reinterpret_cast<uint32_t*>(smem);
   const size_t eb0 = static_cast<size_t>(rep) * p.E + e0;
   const int64_t* prop = p.prop + e0;
   unsigned long long* cnt = cnt_stripe(p, rep);
   const uint32_t B = p.n_buckets;
 
   // ---- 0. expand jitter broadcasts into per-edge SEND ops ----
+  // The unexpanded broadcasts are found by a parallel pass (batches of kBcastCap, in op
+  // order) and expanded one after another by the whole workgroup; the position of an
+  // expanded op in the list does not matter (every edge sorts its ops by key).
   if (p.delay_mode != BCSIM_DELAY_FIXED) {
-    for (uint32_t k = 0; k < n; ++k) {  // uniform loop over the (few) ops
-      Op o = AT(ops, k, ocap);
-      if (op_kind(o) != OP_BCAST_J || (op_flags(o) & OPF_DONE)) continue;
-      if (n + deg > ocap) {
+    for (;;) {
+      if (tid == 0) L.n_bc = 0;
+      __syncthreads();
+      for (uint32_t k = tid; k < n; k += blockDim.x) {
+        const Op& o = ops[k];
+        if (op_kind(o) == OP_BCAST_J && !(op_flags(o) & OPF_DONE)) {
+          const uint32_t pos = atomicAdd(&L.n_bc, 1u);
+          if (pos < kBcastCap) L.bc[pos] = k;
+        }
+      }
+      __syncthreads();
+      const uint32_t nfound = L.n_bc, nb = min(nfound, static_cast<uint32_t>(kBcastCap));
+      if (nb == 0) break;
+      if (n + nb * deg > ocap) {
         if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
         return;
       }
-      const bool paxos = (op_flags(o) & OPF_PAXOS) != 0;
-      const uint64_t dbase = static_cast<uint64_t>(o.edge);
-      for (uint32_t it = tid; it < deg; it += blockDim.x) {
-        const int32_t r = ctr_rand(p.seed, rep, i, dbase + it);
-        const int64_t d = delay_from_draw(p, r);
-        Op s = o;
-        s.t = o.t + d;
-        s.dt = static_cast<uint32_t>(d);
-        s.sub = o.sub + it;
-        s.edge = paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it;
-        s.kind_flags = static_cast<uint8_t>(OP_SEND | ((op_flags(o) & OPF_BIG) << 2));
-        AT(ops, n + it, ocap) = s;
+      for (uint32_t b2 = 0; b2 < nb; ++b2) {
+        const Op o = ops[L.bc[b2]];
+        const bool paxos = (op_flags(o) & OPF_PAXOS) != 0;
+        const uint64_t dbase = static_cast<uint64_t>(o.edge);
+        const uint32_t at = n + b2 * deg;
+        for (uint32_t it = tid; it < deg; it += blockDim.x) {
+          const int32_t r = ctr_rand(p.seed, rep, i, dbase + it);
+          const int64_t d = delay_from_draw(p, r);
+          Op s = o;
+          s.t = o.t + d;
+          s.dt = static_cast<uint32_t>(d);
+          s.sub = o.sub + it;
+          s.edge = paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it;
+          s.kind_flags = static_cast<uint8_t>(OP_SEND | ((op_flags(o) & OPF_BIG) << 2));
+          AT(ops, at + it, ocap) = s;
+        }
       }
       __syncthreads();
-      if (tid == 0) AT(ops, k, ocap).kind_flags = static_cast<uint8_t>(OP_BCAST_J | (OPF_DONE << 2));
-      n += deg;
+      for (uint32_t b2 = tid; b2 < nb; b2 += blockDim.x)
+        AT(ops, L.bc[b2], ocap).kind_flags = static_cast<uint8_t>(OP_BCAST_J | (OPF_DONE << 2));
+      n += nb * deg;
       __syncthreads();
+      if (nfound <= static_cast<uint32_t>(kBcastCap)) break;
     }
   }
 
-  // ---- 1. classify due ops: per-edge counts, broadcast list ----
-  for (uint32_t k = tid; k <= deg; k += blockDim.x) ecnt[k] = 0;
-  for (uint32_t k = tid; k < deg; k += blockDim.x) efill[k] = 0;
+  // ---- 1. classify due ops: broadcast list, listed-op count ----
   for (uint32_t k = tid; k < B; k += blockDim.x) L.lcnt[k] = 0;
-  const uint32_t n_lists = B + 1 + (p.nranks > 1 ? p.nranks : 0);
+  const uint32_t n_lists = B + 1 + (XR ? p.nranks : 0);
   for (uint32_t k = tid; k < n_lists; k += blockDim.x) L.lst[k] = 0;
   const bool tmap = p.mesh && p.n_tiles <= static_cast<uint32_t>(kMaxTiles);
   if (tmap)
     for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x) L.tflag[k] = 0;
+  if (tid < 8) L.csum[tid] = 0;
   if (tid == 0) {
     L.n_bc = 0;
     L.n_keep = 0;
+    L.n_list = 0;
     L.nst = 0;
     L.omin = LLONG_MAX;
     L.ovmin = LLONG_MAX;
@@ -2263,6 +2292,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   __syncthreads();
   unsigned long long dropped = 0, sends = 0, st_ops = 0;
   uint32_t cb = kInvalid, cbn = 0;  // run-length bucket count of this thread's records
+  uint32_t my_list = 0;
   for (uint32_t k = tid; k < n; k += blockDim.x) {
     const Op& o = ops[k];
     const uint8_t kind = op_kind(o);
@@ -2278,44 +2308,57 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       sends += 1;
     } else {
       if (kind == OP_SEND) sends += 1;
-      atomicAdd(&ecnt[o.edge - e0], 1u);
+      ++my_list;
     }
   }
+  {
+    const uint32_t ws = wave_sum(my_list);
+    if ((tid & 63u) == 0 && ws) atomicAdd(&L.n_list, ws);
+  }
   __syncthreads();
-  if (L.n_bc > kBcastCap) {
+  const uint32_t n_bc = L.n_bc, n_list = L.n_list;
+  if (n_bc > kBcastCap) {
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
     return;
   }
   if (p.wgt && tid == 0) ph[0] = __builtin_amdgcn_s_memrealtime();
-  const uint32_t n_due = block_scan_array(ecnt, deg + 1, L.wsum);
-  if (n_due > ocap) {  // unreachable: n_due <= n <= cap_ops
-    if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
-    return;
-  }
-  if (tid == 0) {  // sort the broadcasts by key (insertion sort, few)
-    for (uint32_t a = 1; a < L.n_bc; ++a) {
-      const uint32_t x = L.bc[a];
-      const Op ox = ops[x];
+  // the due broadcasts: parallel copy to LDS, then key order (insertion sort, few)
+  if (tid < n_bc) L.bco[tid] = ld_op(&ops[L.bc[tid]]);
+  __syncthreads();
+  if (tid == 0) {
+    for (uint32_t a = 1; a < n_bc; ++a) {
+      const Op ox = L.bco[a];
       uint32_t b2 = a;
-      while (b2 > 0) {
-        const Op& oy = ops[L.bc[b2 - 1]];
-        if (!op_key_less(ox, ox.sub, oy, oy.sub)) break;
-        L.bc[b2] = L.bc[b2 - 1];
+      while (b2 > 0 && op_key_less(ox, ox.sub, L.bco[b2 - 1], L.bco[b2 - 1].sub)) {
+        st_op(&L.bco[b2], L.bco[b2 - 1]);
         --b2;
       }
-      L.bc[b2] = x;
+      st_op(&L.bco[b2], ox);
     }
-    for (uint32_t a = 0; a < L.n_bc; ++a) L.bco[a] = ops[L.bc[a]];
   }
-  for (uint32_t k = tid; k < n; k += blockDim.x) {
-    const Op& o = ops[k];
-    const uint8_t kind = op_kind(o);
-    if (kind == OP_BCAST_J || kind == OP_BCAST || o.t >= t_hi || o.edge == kInvalid) continue;
-    const uint32_t le = o.edge - e0;
-    eidx[ecnt[le] + atomicAdd(&efill[le], 1u)] = k;
+  // listed due ops (unicast / echo) grouped by edge: counting sort over the out-edges.
+  // After the fill ecnt[le] is the END of edge le's range ([ecnt[le-1], ecnt[le])).
+  uint32_t* eidx = ecnt + (p.deg_max + 1);
+  if (n_list) {
+    if (n_list > p.cap_eidx) eidx = p.eidx_g + static_cast<size_t>(blockIdx.x) * p.cap_ops;
+    for (uint32_t k = tid; k <= deg; k += blockDim.x) ecnt[k] = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < n; k += blockDim.x) {
+      const Op& o = ops[k];
+      const uint8_t kind = op_kind(o);
+      if (kind == OP_BCAST_J || kind == OP_BCAST || o.t >= t_hi || o.edge == kInvalid) continue;
+      atomicAdd(&ecnt[o.edge - e0], 1u);
+    }
+    __syncthreads();
+    (void)block_scan_array(ecnt, deg + 1, L.wsum);
+    for (uint32_t k = tid; k < n; k += blockDim.x) {
+      const Op& o = ops[k];
+      const uint8_t kind = op_kind(o);
+      if (kind == OP_BCAST_J || kind == OP_BCAST || o.t >= t_hi || o.edge == kInvalid) continue;
+      eidx[atomicAdd(&ecnt[o.edge - e0], 1u)] = k;
+    }
   }
   __syncthreads();
-  const uint32_t n_bc = L.n_bc;
 
   if (p.wgt && tid == 0) ph[1] = __builtin_amdgcn_s_memrealtime();
   // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO, emit ----
@@ -2324,7 +2367,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   const long long cs = cell * p.L;
   const Rec* in_row = p.inbox + (static_cast<size_t>(ib) * p.R + rep) * p.E;
   for (uint32_t le = tid; le < deg; le += blockDim.x) {
-    const uint32_t eb = ecnt[le], ee = ecnt[le + 1];
+    const uint32_t eb = n_list && le ? ecnt[le - 1] : 0u, ee = n_list ? ecnt[le] : 0u;
     const uint32_t e = e0 + le;
     // full mesh: peers ascending without self (validated on the host)
     const uint32_t s = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e, p.E);
@@ -2622,23 +2665,28 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
     }
   }
-  // ---- 5. counters: one global atomic per workgroup ----
-  uint4 t1, t2;
-  (void)block_scan4(make_uint4(static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends),
-                               static_cast<uint32_t>(n_rec), static_cast<uint32_t>(st_ops)), L.wsum, t1);
-  (void)block_scan4(make_uint4(static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo),
-                               static_cast<uint32_t>(fdrop), static_cast<uint32_t>(lost)), L.wsum, t2);
-  if (tid == 0) {
-    if (t1.x) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(t1.x));
-    if (t1.y) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(t1.y));
-    if (t1.z) atomicAdd(&kst_stripe(p)[KST_REC], static_cast<unsigned long long>(t1.z));
-    if (t1.w) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(t1.w));
-    if (t2.x) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(t2.x));
-    if (t2.y) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(t2.y));
-    if (t2.z) atomicAdd(&cnt[CNT_FDROP], static_cast<unsigned long long>(t2.z));
-    if (t2.w) atomicAdd(&cnt[CNT_LOST], static_cast<unsigned long long>(t2.w));
+  // ---- 5. counters: wave sums, LDS atomics, one global atomic per workgroup ----
+  {
+    const uint32_t v[8] = {static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends), static_cast<uint32_t>(n_rec),
+                           static_cast<uint32_t>(st_ops), static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo),
+                           static_cast<uint32_t>(fdrop), static_cast<uint32_t>(lost)};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t ws = wave_sum(v[k]);
+      if ((tid & 63u) == 0 && ws) atomicAdd(&L.csum[k], ws);
+    }
   }
   __syncthreads();
+  if (tid == 0) {
+    if (L.csum[0]) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(L.csum[0]));
+    if (L.csum[1]) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(L.csum[1]));
+    if (L.csum[2]) atomicAdd(&kst_stripe(p)[KST_REC], static_cast<unsigned long long>(L.csum[2]));
+    if (L.csum[3]) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(L.csum[3]));
+    if (L.csum[4]) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(L.csum[4]));
+    if (L.csum[5]) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(L.csum[5]));
+    if (L.csum[6]) atomicAdd(&cnt[CNT_FDROP], static_cast<unsigned long long>(L.csum[6]));
+    if (L.csum[7]) atomicAdd(&cnt[CNT_LOST], static_cast<unsigned long long>(L.csum[7]));
+  }
   for (uint32_t k = tid; k < B; k += blockDim.x)
     if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
   if (p.wgt && tid == 0) {
