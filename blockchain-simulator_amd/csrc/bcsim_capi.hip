@@ -56,6 +56,7 @@ struct Sim {
   std::vector<void*> allocs;
   // host mirrors
   Ctl* ctl_h = nullptr;  // pinned
+  uint32_t* act_h = nullptr;  // pinned: the window's active-list lengths (k_scan, k_link)
   uint32_t* bcnt_h = nullptr;
   uint32_t* xcnt_h = nullptr;
   void* ctl_d = nullptr;
@@ -65,7 +66,7 @@ struct Sim {
   uint32_t bs_scan = 64, bs_link = 64;
   long long dbg_fail_cell = -1;  // test hook (BCSIM_DBG_FAIL_CELL): this rank fails at that cell
   bool sparse = false;
-  uint32_t act_grid = 0;         // sparse mode: workgroups of k_scan / k_link (grid-stride over the active list)
+  uint32_t grid_scan = 0, grid_link = 0;  // k_scan / k_link workgroups (walking the active lists)
   uint32_t* seg_part = nullptr;  // multi-block segment scan partials
   long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
   long long n_alive = 0;
@@ -443,7 +444,7 @@ static int setup_device(Sim& s) {
       p.cap_ops_light = std::min<uint32_t>(p.cap_ops, c.cap_ops_per_node ? p.cap_ops : 32);
       if (!c.cap_timers_per_node) p.cap_timers = 4;  // Paxos: the t=0 ticket timer only
     }
-    s.act_grid = static_cast<uint32_t>(std::min<uint64_t>(NT, 4096));
+
     // small workgroups over many nodes: k_scan windows of <= 512 arrivals (split by
     // time), 256 lanes; k_link_sparse has no per-edge LDS arrays
     if (c.delay_mode == BCSIM_DELAY_RANDOM) p.cap_arr = std::min<uint32_t>(p.cap_arr, 512);  // spread arrivals
@@ -604,17 +605,24 @@ static int setup_device(Sim& s) {
     if ((rc = dalloc(s, &p.qmeta, ne)) || (rc = dalloc(s, &p.qring, ne * (p.qmodel ? p.cap_q : 1)))) return rc;
     HIPCHK(hipMemset(p.qmeta, 0, ne * 8));
   }
+  // k_scan / k_link grids (multiples of 8: one list chunk per XCD).  Dense layout: one
+  // workgroup per possible list entry (an inactive node's workgroup exits at once); sparse
+  // layout: a fixed grid strides over lists of up to millions of gnodes
+  {
+    const uint64_t nl = (static_cast<uint64_t>(s.R) * s.nloc + 7) / 8 * 8;
+    s.grid_scan = s.grid_link = static_cast<uint32_t>(s.sparse ? std::min<uint64_t>(nl, 4096) : nl);
+  }
   const size_t n_rtile = p.mesh ? static_cast<size_t>(s.B) * s.R * p.n_tiles : 1;
   if ((rc = dalloc(s, &p.rtile, n_rtile))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
       (rc = dalloc(s, &p.xbuf, p.cap_xbuf)) || (rc = dalloc(s, &p.xgrp, p.cap_x)) ||
-      (rc = dalloc(s, &p.xstage, static_cast<size_t>(s.sparse ? s.act_grid : NT) * p.cap_stage)) ||
-      (rc = dalloc(s, &p.xmeta, static_cast<size_t>(s.sparse ? s.act_grid : NT) * p.cap_stage)) ||
+      (rc = dalloc(s, &p.xstage, static_cast<size_t>(s.grid_link) * p.cap_stage)) ||
+      (rc = dalloc(s, &p.xmeta, static_cast<size_t>(s.grid_link) * p.cap_stage)) ||
       (rc = dalloc(s, &p.ov, p.cap_ov)))
     return rc;
-  if (s.sparse) {  // active lists of k_scan / k_link
-    if ((rc = dalloc(s, &p.act, 2 * NT)) || (rc = dalloc(s, &p.act_n, 2))) return rc;
-  }
+  // active lists of k_scan / k_link (k_active; emptied by k_next / k_pbft_tick)
+  if ((rc = dalloc(s, &p.act, 2 * NT)) || (rc = dalloc(s, &p.act_n, 2))) return rc;
+  HIPCHK(hipMemset(p.act_n, 0, 8));
   if ((rc = dalloc(s, &s.seg_part, (NT + kSegChunk - 1) / kSegChunk + 1))) return rc;
   if ((rc = dalloc(s, &p.seg_cnt, NT)) || (rc = dalloc(s, &p.seg_off, NT + 1)) ||
       (rc = dalloc(s, &p.cursor, NT)))
@@ -647,6 +655,7 @@ static int setup_device(Sim& s) {
   p.x_cnt = p.bucket_cnt + s.B;
   p.send_cnt = p.x_cnt + s.B;
   HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), ctl_bytes));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.act_h), 8));
   s.bcnt_h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.ctl_h) + sizeof(Ctl));
   s.xcnt_h = s.bcnt_h + s.B;
   s.scnt_h = s.xcnt_h + s.B;
@@ -780,21 +789,32 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
 
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
-  dim3 grid(s.R * s.nloc), block(s.bs_scan);
-  if (s.sparse) {  // compact lists of the window's active gnodes; fixed grids stride over them
-    HIPCHK(hipMemsetAsync(s.kp.act_n, 0, 8, s.stream));
+  dim3 grid(s.grid_scan), block(s.bs_scan);
+  uint32_t n_link = 1;
+  {  // compact lists of the window's active gnodes
     const uint32_t nb = static_cast<uint32_t>(std::min<uint64_t>(8192, (static_cast<uint64_t>(s.R) * s.nloc + 255) / 256));
-    int rc = launch(s, KS_AUX, k_active, dim3(nb), dim3(256), 0, s.kp_dev, lo, hi,
-                    static_cast<uint32_t>(cell % s.B));
+    int rc = launch(s, KS_AUX, k_active, dim3(nb), dim3(256), 0, s.kp_dev, lo, hi, static_cast<uint32_t>(cell % s.B),
+                    static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing));
     if (rc) return rc;
-    grid = dim3(s.act_grid);
+    if (!s.sparse) {
+      // dense layout: read the list lengths back and launch exactly one workgroup per entry
+      // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
+      // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
+      // per CU: 4096 of them took ~24 us, the read-back takes ~10.
+      HIPCHK(hipMemcpyAsync(s.act_h, s.kp.act_n, 8, hipMemcpyDeviceToHost, s.stream));
+      HIPCHK(hipStreamSynchronize(s.stream));
+      grid = dim3((s.act_h[0] + 7) / 8 * 8);
+      n_link = s.act_h[1];
+    }
   }
   const int fw = final_win ? 1 : 0, xa = s.x_active;
-  int rc;
+  int rc = BCSIM_OK;
 #define BCSIM_SCAN(P)                                                                                   \
   (s.sparse ? launch(s, KS_SCAN, k_scan<P, true>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa) \
             : launch(s, KS_SCAN, k_scan<P, false>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa))
-  if (s.cfg.protocol == BCSIM_PBFT)
+  if (grid.x == 0)
+    rc = BCSIM_OK;  // no node has work in the window
+  else if (s.cfg.protocol == BCSIM_PBFT)
     rc = BCSIM_SCAN(BCSIM_PBFT);
   else if (s.cfg.protocol == BCSIM_RAFT)
     rc = BCSIM_SCAN(BCSIM_RAFT);
@@ -833,7 +853,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
                    acc[3] / nw / 100, acc[4] / nw / 100, acc[5] / nw / 100, acc[6] / nw / 100, acc[7] / nw / 100);
     }
   }
-  if (s.sparse)
+  grid = dim3(s.sparse ? s.grid_link : (n_link + 7) / 8 * 8);
+  if (grid.x == 0)
+    rc = BCSIM_OK;
+  else if (s.sparse)
     rc = launch(s, KS_LINK, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw);
   else {
     const size_t ll = link_lds_bytes(s.kp);
@@ -1154,15 +1177,9 @@ static int run(Sim& s, int64_t t_until) {
     if (!lrc && s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC)
       lrc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp_dev, 0u);
     const uint32_t nbn = static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
-    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev);
-    if (hi == ce) {
-      // cell finished: its bucket is free again
-      LOCAL(hipMemsetAsync(s.kp.bucket_cnt + (c % s.B), 0, 4, s.stream));
-      LOCAL(hipMemsetAsync(s.kp.x_cnt + (c % s.B), 0, 4, s.stream));
-      if (s.kp.mesh)  // receiver-tile flags of the bucket (every node of the cell has run)
-        LOCAL(hipMemsetAsync(s.kp.rtile + static_cast<size_t>(c % s.B) * s.R * s.kp.n_tiles, 0,
-                             static_cast<size_t>(s.R) * s.kp.n_tiles, s.stream));
-    }
+    // (a finished cell's bucket is free again: k_next clears its counts and tile flags)
+    const uint32_t clr_b = hi == ce ? static_cast<uint32_t>(c % s.B) : 0xFFFFFFFFu;
+    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b);
     if (!lrc) lrc = readback(s);
     if (!lrc && s.dbg_fail_cell >= 0 && static_cast<long long>(s.cells) >= s.dbg_fail_cell) {
       g_detail = "injected failure (BCSIM_DBG_FAIL_CELL)";  // test hook: one rank fails alone

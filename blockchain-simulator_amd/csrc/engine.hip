@@ -259,6 +259,27 @@ __device__ inline uint32_t local_gnode(const KP& p, uint32_t b) {
   return (j / p.nloc) * p.N + p.nlo + j % p.nloc;
 }
 
+// Active-list launches (k_scan, k_link): a fixed grid (a multiple of 8) walks the list of
+// the window's active gnodes built by k_active.  Workgroups are dispatched round-robin
+// over the 8 XCDs, so XCD x = blockIdx & 7 takes the contiguous list chunk x (neighbouring
+// senders share an L2, as with xcd_map) and its workgroups stride through the chunk.
+struct ListRange {
+  uint32_t k, end, step;
+};
+__device__ inline ListRange list_range(uint32_t na) {
+  const uint32_t x = blockIdx.x & 7u, per = (na + 7u) >> 3;
+  const uint32_t lo = min(na, x * per), hi = min(na, lo + per);
+  return ListRange{lo + (blockIdx.x >> 3), hi, gridDim.x >> 3};
+}
+// dense layout: the grid has at least one workgroup per list entry (gridDim >= 8 * ceil(na / 8)),
+// so a workgroup takes one entry or none -- no loop, whose loop-carried state would cost
+// registers in these 128-VGPR kernels
+__device__ inline bool list_one(uint32_t na, uint32_t& k) {
+  const ListRange lr = list_range(na);
+  k = lr.k;
+  return lr.k < lr.end;
+}
+
 // pending-op list of gnode g: nodes < n_heavy of every replica have cap_ops entries,
 // the others cap_ops_light (n_heavy = N: uniform)
 __device__ inline size_t op_base(const KP& p, uint32_t g) {
@@ -2055,21 +2076,19 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* __rest
   if (S.tmax > LLONG_MIN) atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), S.tmax);
 }
 
-// dense mode: one workgroup per gnode of this rank; sparse mode: a fixed grid strides
-// over the window's active list (k_active)
+// a fixed grid over the window's active list (k_active); SP: sparse layout (no inbox slots)
 template <int PROTO, bool SP>
 __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                long long t_hi, long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (!SP) {
-    if (blockIdx.x >= p.R * p.nloc) return;
-    scan_node<PROTO, false>(pk, local_gnode(p, blockIdx.x), cell, t_lo, t_hi, cs, final_win, x_active);
+    uint32_t k;
+    if (list_one(p.act_n[0], k)) scan_node<PROTO, false>(pk, p.act[k], cell, t_lo, t_hi, cs, final_win, x_active);
     return;
   }
-  const uint32_t na = *p.act_n;
-  for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
-    scan_node<PROTO, true>(pk, p.act[k], cell, t_lo, t_hi, cs, final_win, x_active);
+  for (ListRange lr = list_range(p.act_n[0]); lr.k < lr.end; lr.k += lr.step) {
+    scan_node<PROTO, true>(pk, p.act[lr.k], cell, t_lo, t_hi, cs, final_win, x_active);
     __syncthreads();
   }
 }
@@ -2714,8 +2733,8 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
                                               long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  if (blockIdx.x >= p.R * p.nloc) return;
-  link_node<QM, XR>(pk, local_gnode(p, blockIdx.x), cell, t_lo, t_hi, final_win);
+  uint32_t k;
+  if (list_one(p.act_n[1], k)) link_node<QM, XR>(pk, p.act[p.NT + k], cell, t_lo, t_hi, final_win);
 }
 
 // ---------------------------------------------------------------------------
@@ -3051,9 +3070,8 @@ __global__ __launch_bounds__(256) void k_link_sparse(const KP* __restrict__ pk, 
                                                      long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  const uint32_t na = p.act_n[1];
-  for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
-    link_node_sparse(p, p.act[p.NT + k], cell, t_lo, t_hi, final_win);
+  for (ListRange lr = list_range(p.act_n[1]); lr.k < lr.end; lr.k += lr.step) {
+    link_node_sparse(p, p.act[p.NT + lr.k], cell, t_lo, t_hi, final_win);
     __syncthreads();
   }
 }
@@ -3064,7 +3082,8 @@ __global__ __launch_bounds__(256) void k_link_sparse(const KP* __restrict__ pk, 
 // k_scan: arrivals in the bucket, a due timer, START / STOP; k_link: those plus the
 // nodes with an op due -- as two compact lists (one returning atomic per wave; the
 // loop bound is wave-uniform, so every ballot runs with the whole wave active)
-__global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long long t_lo, long long t_hi, uint32_t b) {
+__global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long long t_lo, long long t_hi, uint32_t b,
+                                                uint32_t obp) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
@@ -3082,7 +3101,9 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
       g = static_cast<uint32_t>((k / p.nloc) * p.N + p.nlo + k % p.nloc);
       const uint32_t rep = g / p.N, i = g % p.N;
       sc = has_start || has_stop || node_flagged(p, b, g, rep, i) || AT(p.node_tnext, g, p.NT) < t_hi;
-      lk = sc || AT(p.node_onext, g, p.NT) < t_hi;
+      // k_link also runs nodes with reply-slot ops of the previous arrival cell due
+      lk = sc || AT(p.node_onext, g, p.NT) < t_hi ||
+           (p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u));
     }
     const unsigned long long ms = __ballot(sc), ml = __ballot(lk);
     uint32_t ps = 0, pl = 0;
@@ -3168,6 +3189,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
   __shared__ int32_t v_cur, nround0, n_alive, n_ticked;
   __shared__ unsigned long long lmask[64];  // leader flags of the current 4096-node chunk, one bit per node
   const uint32_t rep = blockIdx.x, tid = threadIdx.x;
+  if (rep == 0 && tid < 2) p.act_n[tid] = 0;  // the second window of the cell builds fresh lists
   const uint32_t N = p.N;
   const long long ts_tick = tk - p.pbft_period;
   // v = latest v-log write before this tick in canonical order: every thread
@@ -3393,9 +3415,23 @@ __global__ void k_draws(const KP* __restrict__ pk, uint32_t) {
 // global min over node_tnext / node_onext
 // next event time over all nodes: every workgroup reduces a strided share, the last one to
 // finish (threadfence reduction) combines the partial minima
-__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk) {
+// k_next also ends the cell: the next window's active lists start empty, and a finished
+// cell's bucket (clr_b < n_buckets) is free again (its counts and receiver-tile flags).
+__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < 2) p.act_n[threadIdx.x] = 0;
+    if (clr_b < p.n_buckets) {
+      if (threadIdx.x == 0) {
+        p.bucket_cnt[clr_b] = 0;
+        p.x_cnt[clr_b] = 0;
+      }
+      if (p.mesh)
+        for (uint32_t k = threadIdx.x; k < p.R * p.n_tiles; k += blockDim.x)
+          p.rtile[static_cast<size_t>(clr_b) * p.R * p.n_tiles + k] = 0;
+    }
+  }
   __shared__ long long red[1024];
   long long m = LLONG_MAX;
   const uint32_t nb = gridDim.x;
