@@ -67,6 +67,8 @@ struct Sim {
   long long dbg_fail_cell = -1;  // test hook (BCSIM_DBG_FAIL_CELL): this rank fails at that cell
   bool sparse = false;
   uint32_t grid_scan = 0, grid_link = 0;  // k_scan / k_link workgroups (walking the active lists)
+  uint32_t gossip_g = 0;  // dense gossip: lanes per node of k_gossip_scan (0 = generic k_scan only)
+  bool gossip_link = false;  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
   uint32_t* seg_part = nullptr;  // multi-block segment scan partials
   long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
   long long n_alive = 0;
@@ -481,9 +483,12 @@ static int setup_device(Sim& s) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_GOSSIP, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_GOSSIP, false, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_GOSSIP, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     for (const void* f : {reinterpret_cast<const void*>(k_link<false, false>), reinterpret_cast<const void*>(k_link<false, true>),
+                          reinterpret_cast<const void*>(k_link<false, false, true>),
                           reinterpret_cast<const void*>(k_link<true, false>), reinterpret_cast<const void*>(k_link<true, true>)})
       HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(link_lds_bytes(p))));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_pbft_tick),
@@ -582,6 +587,12 @@ static int setup_device(Sim& s) {
     const char* ns = std::getenv("BCSIM_NO_SLOTS");
     const bool off = ns && *ns == '1';
     p.impl = (off || s.sparse) ? 0u : 1u;  // sparse: no slots, echoes listed by k_scan
+    // dense gossip of degree <= 64: k_gossip_scan takes the simple nodes (BCSIM_NO_GFAST=1: off)
+    const char* nf = std::getenv("BCSIM_NO_GFAST");
+    s.gossip_g = (c.protocol == BCSIM_GOSSIP && p.impl && s.deg_max <= 64 && !(nf && *nf == '1'))
+                     ? static_cast<uint32_t>(next_pow2(std::max<uint64_t>(1, s.deg_max))) : 0u;
+    s.gossip_link = s.gossip_g && !p.mesh && s.P == 1 && c.delay_mode == BCSIM_DELAY_FIXED &&
+                    c.queue_model == BCSIM_QUEUE_INFINITE;
     // PBFT replies with a fixed app delay < L (due in the arrival cell or the next)
     const bool on = ne * 16 <= (16ull << 30) && !off && !s.sparse && c.protocol == BCSIM_PBFT &&
                     c.delay_mode == BCSIM_DELAY_FIXED && c.app_delay_ns < s.L;
@@ -621,8 +632,8 @@ static int setup_device(Sim& s) {
       (rc = dalloc(s, &p.ov, p.cap_ov)))
     return rc;
   // active lists of k_scan / k_link (k_active; emptied by k_next / k_pbft_tick)
-  if ((rc = dalloc(s, &p.act, 2 * NT)) || (rc = dalloc(s, &p.act_n, 2))) return rc;
-  HIPCHK(hipMemset(p.act_n, 0, 8));
+  if ((rc = dalloc(s, &p.act, 4 * NT)) || (rc = dalloc(s, &p.act_n, 4))) return rc;
+  HIPCHK(hipMemset(p.act_n, 0, 16));
   if ((rc = dalloc(s, &s.seg_part, (NT + kSegChunk - 1) / kSegChunk + 1))) return rc;
   if ((rc = dalloc(s, &p.seg_cnt, NT)) || (rc = dalloc(s, &p.seg_off, NT + 1)) ||
       (rc = dalloc(s, &p.cursor, NT)))
@@ -655,7 +666,7 @@ static int setup_device(Sim& s) {
   p.x_cnt = p.bucket_cnt + s.B;
   p.send_cnt = p.x_cnt + s.B;
   HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), ctl_bytes));
-  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.act_h), 8));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.act_h), 16));
   s.bcnt_h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.ctl_h) + sizeof(Ctl));
   s.xcnt_h = s.bcnt_h + s.B;
   s.scnt_h = s.xcnt_h + s.B;
@@ -790,25 +801,39 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
   dim3 grid(s.grid_scan), block(s.bs_scan);
+  const int fw = final_win ? 1 : 0, xa = s.x_active;
+  int rc = BCSIM_OK;
+  // dense gossip: groups of G lanes walk all gnodes and take the simple ones; small looped
+  // grids the rest (lists 2, 3) -- no k_active and no read-back in the window
+  if (s.gossip_link && s.kp.dbg_tmax <= lo) {
+    const uint32_t per_wg = 256 / s.gossip_g;
+    const dim3 gg(static_cast<uint32_t>((static_cast<uint64_t>(s.R) * s.nloc + per_wg - 1) / per_wg));
+    if ((rc = launch(s, KS_SCAN, k_gossip_scan, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g)) ||
+        (rc = launch(s, KS_SCAN, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), block, lds, s.kp_dev, cell, lo, hi, cs,
+                     fw, xa)) ||
+        (rc = launch(s, KS_LINK, k_gossip_link, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, s.gossip_g)) ||
+        (rc = launch(s, KS_LINK, (k_link<false, false, true>), dim3(256), dim3(s.bs_link), link_lds_bytes(s.kp),
+                     s.kp_dev, cell, lo, hi, fw)))
+      return rc;
+    return BCSIM_OK;
+  }
   uint32_t n_link = 1;
   {  // compact lists of the window's active gnodes
     const uint32_t nb = static_cast<uint32_t>(std::min<uint64_t>(8192, (static_cast<uint64_t>(s.R) * s.nloc + 255) / 256));
-    int rc = launch(s, KS_AUX, k_active, dim3(nb), dim3(256), 0, s.kp_dev, lo, hi, static_cast<uint32_t>(cell % s.B),
-                    static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing));
+    rc = launch(s, KS_AUX, k_active, dim3(nb), dim3(256), 0, s.kp_dev, lo, hi, static_cast<uint32_t>(cell % s.B),
+                static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing));
     if (rc) return rc;
     if (!s.sparse) {
       // dense layout: read the list lengths back and launch exactly one workgroup per entry
       // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
       // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
       // per CU: 4096 of them took ~24 us, the read-back takes ~10.
-      HIPCHK(hipMemcpyAsync(s.act_h, s.kp.act_n, 8, hipMemcpyDeviceToHost, s.stream));
+      HIPCHK(hipMemcpyAsync(s.act_h, s.kp.act_n, 16, hipMemcpyDeviceToHost, s.stream));
       HIPCHK(hipStreamSynchronize(s.stream));
       grid = dim3((s.act_h[0] + 7) / 8 * 8);
       n_link = s.act_h[1];
     }
   }
-  const int fw = final_win ? 1 : 0, xa = s.x_active;
-  int rc = BCSIM_OK;
 #define BCSIM_SCAN(P)                                                                                   \
   (s.sparse ? launch(s, KS_SCAN, k_scan<P, true>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa) \
             : launch(s, KS_SCAN, k_scan<P, false>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa))

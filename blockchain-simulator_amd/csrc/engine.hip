@@ -178,8 +178,9 @@ struct KP {
   // state (hubs > 0: only edges with an endpoint < hubs carry traffic)
   uint32_t sparse, hubs;
   uint32_t cap_ops_light, n_heavy;  // nodes < n_heavy hold cap_ops pending ops, others cap_ops_light
-  uint32_t* act;    // [2][NT] gnodes of the window for k_scan / k_link (sparse mode)
-  uint32_t* act_n;  // [2]
+  uint32_t* act;    // [4][NT] gnodes of the window: k_scan list, k_link list, and (dense gossip)
+                    // the nodes k_gossip_scan / k_gossip_link leave to the generic kernels
+  uint32_t* act_n;  // [4] their lengths
   // debug (BCSIM_DBG_EVENTS=<t_max ns>): Raft/Paxos/gossip serial handlers emit one
   // trace record of kind 90 + event class per handled event with t < dbg_tmax
   long long dbg_tmax;
@@ -2077,11 +2078,19 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* __rest
 }
 
 // a fixed grid over the window's active list (k_active); SP: sparse layout (no inbox slots)
-template <int PROTO, bool SP>
+// LOOP (dense gossip): a small grid walks list 2, the nodes k_gossip_scan left over
+template <int PROTO, bool SP, bool LOOP = false>
 __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                long long t_hi, long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  if (LOOP) {
+    for (ListRange lr = list_range(p.act_n[2]); lr.k < lr.end; lr.k += lr.step) {
+      scan_node<PROTO, false>(pk, p.act[2ull * p.NT + lr.k], cell, t_lo, t_hi, cs, final_win, x_active);
+      __syncthreads();
+    }
+    return;
+  }
   if (!SP) {
     uint32_t k;
     if (list_one(p.act_n[0], k)) scan_node<PROTO, false>(pk, p.act[k], cell, t_lo, t_hi, cs, final_win, x_active);
@@ -2090,6 +2099,168 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   for (ListRange lr = list_range(p.act_n[0]); lr.k < lr.end; lr.k += lr.step) {
     scan_node<PROTO, true>(pk, p.act[lr.k], cell, t_lo, t_hi, cs, final_win, x_active);
     __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_gossip_scan (dense layout, BCSIM_GOSSIP, degree <= 64): the common window of a gossip
+// node -- only main-slot arrivals, no timer, START or STOP due, no extras -- handled by a
+// group of G lanes (lane j = in-slot j) instead of a workgroup with a lane-0 event loop.
+// Same result as scan_node<BCSIM_GOSSIP> (gossip_first_flags + gossip_recv in key order):
+//   rank   = position of the arrival in the canonical key order (t, t - dt, origin)
+//   first  = GS_BLOCK, not seen before the window, no earlier arrival of the window with
+//            the same sequence -> GOSSIP_DELIVER trace + one broadcast (sub += deg each)
+// The kernel walks all of this rank's gnodes (no k_active): a node with work in the window
+// (k_active's rule) that is not simple is appended to list 2 for k_scan<.., LOOP>.
+__global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                     long long t_hi, long long cs, int x_active, uint32_t G) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ uint32_t s_deliv[BCSIM_MSG_TYPES];
+  __shared__ uint32_t s_ev, s_wr, s_nf, s_trbase;
+  __shared__ long long s_tmax;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, j = tid & (G - 1u), gb = lane & ~(G - 1u);
+  const uint32_t per_wg = blockDim.x / G;
+  if (tid < BCSIM_MSG_TYPES) s_deliv[tid] = 0;
+  if (tid == 0) {
+    s_ev = s_wr = s_nf = 0;
+    s_tmax = LLONG_MIN;
+  }
+  __syncthreads();
+  const uint32_t na = p.R * p.nloc;
+  const uint32_t kl = blockIdx.x * per_wg + tid / G;
+  const uint32_t k0 = blockIdx.x * per_wg;
+  const uint32_t g0 = (k0 / p.nloc) * p.N + p.nlo + k0 % p.nloc;
+  const uint32_t g = kl < na ? (kl / p.nloc) * p.N + p.nlo + kl % p.nloc : 0u;
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const uint32_t rep0 = g0 / p.N;  // counters of this replica go through LDS
+  const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
+  const bool has_start = (t_lo <= 0 && 0 < t_hi);
+  const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
+  const bool flagged = kl < na && node_flagged(p, b, g, rep, i);
+  const bool tdue = kl < na && AT(p.node_tnext, g, p.NT) < t_hi;
+  const bool have = kl < na && (has_start || has_stop || flagged || tdue);  // k_active's k_scan rule
+  const uint32_t e0 = have ? AT(p.row, i, p.N + 1) : 0u;
+  const uint32_t deg = have ? AT(p.row, i + 1, p.N + 1) - e0 : 0u;
+  bool fast = have && deg <= G && !has_start && !has_stop && !tdue;
+  if (fast && x_active) fast = AT(p.seg_off, g + 1, p.NT + 1) == AT(p.seg_off, g, p.NT + 1);
+  if (have && !fast && j == 0) {
+    const uint32_t pos = atomicAdd(&p.act_n[2], 1u);
+    AT(p.act, 2ull * p.NT + pos, 3ull * p.NT) = g;
+  }
+  // this lane's in-slot
+  bool v = false;
+  Rec r{};
+  uint64_t k64 = 0;
+  long long t = 0;
+  uint32_t dt = 0;
+  if (fast && j < deg && flagged) {
+    r = ld_rec(p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0 + j);
+    t = cs + r.t_off;
+    v = (r.flags & RF_VALID) && t >= t_lo && t < t_hi;
+    dt = static_cast<uint32_t>(prop_of_slot(p, e0 + j) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
+    k64 = (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~dt);
+  }
+  // key-order rank within the node's group (ties of (t, dt) by in-slot = origin order)
+  uint32_t rank = 0;
+  for (uint32_t q = 0; q < G; ++q) {
+    const bool vq = __shfl(v ? 1 : 0, gb + q, 64) != 0;
+    const uint64_t kq = (static_cast<uint64_t>(__shfl(static_cast<uint32_t>(k64 >> 32), gb + q, 64)) << 32) |
+                        __shfl(static_cast<uint32_t>(k64), gb + q, 64);
+    if (vq && (kq < k64 || (kq == k64 && q < j))) ++rank;
+  }
+  const int32_t seq = r.f0;
+  const bool blk = v && r.type == GS_BLOCK;
+  const bool inrange = seq >= 0 && static_cast<uint32_t>(seq) < p.pbft_seq_cap;
+  if (blk && !inrange) set_err(p, BCSIM_E_INDEX);
+  bool first = blk && inrange &&
+               AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + seq, static_cast<uint64_t>(p.NT) * p.pbft_seq_cap) == 0;
+  for (uint32_t q = 0; q < G; ++q) {  // an earlier arrival of the window with the same block
+    const bool bq = __shfl(blk ? 1 : 0, gb + q, 64) != 0;
+    const int32_t sq = __shfl(seq, gb + q, 64);
+    const uint32_t rq = __shfl(rank, gb + q, 64);
+    if (bq && sq == seq && rq < rank) first = false;
+  }
+  uint32_t nf = 0, nfb = 0;  // first receipts of the node, and those before this one
+  for (uint32_t q = 0; q < G; ++q) {
+    const bool fq = __shfl(first ? 1 : 0, gb + q, 64) != 0;
+    const uint32_t rq = __shfl(rank, gb + q, 64);
+    if (fq) {
+      ++nf;
+      if (rq < rank) ++nfb;
+    }
+  }
+  // counters (LDS for this workgroup's first replica)
+  uint32_t li = 0;
+  if (v) {
+    if (rep == rep0) {
+      if (r.type < BCSIM_MSG_TYPES) atomicAdd(&s_deliv[r.type], 1u);
+      atomicAdd(&s_ev, 1u);
+      if (r.type != GS_BLOCK) atomicAdd(&s_wr, 1u);
+      atomicMax(&s_tmax, t);
+    } else {
+      unsigned long long* cnt = cnt_stripe(p, rep);
+      if (r.type < BCSIM_MSG_TYPES) {
+        atomicAdd(&cnt[CNT_DELIV + r.type], 1ull);
+        atomicAdd(&cnt[CNT_DELIV_TOTAL], 1ull);
+        atomicAdd(&kst_stripe(p)[KST_DELIV], 1ull);
+      }
+      if (p.echo) atomicAdd(&cnt[CNT_ECHOES], 1ull);
+      if (r.type != GS_BLOCK) atomicAdd(&cnt[CNT_WRONG], 1ull);
+      atomicAdd(&cnt[CNT_EVENTS], 1ull);
+      atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), t);
+    }
+  }
+  if (first) li = atomicAdd(&s_nf, 1u);
+  __syncthreads();
+  if (tid == 0) s_trbase = s_nf ? atomicAdd(p.trace_cnt, s_nf) : 0u;
+  __syncthreads();
+  if (nf) {  // node state: sub (+deg per broadcast), draws (jitter), pending ops
+    const uint32_t sub0 = AT(p.sub, g, p.NT), nops0 = AT(p.n_ops, g, p.NT);
+    const uint64_t draws0 = AT(p.draws, g, p.NT);
+    const uint32_t ocap = op_cap(p, g);
+    if (nops0 + nf > ocap) {
+      if (j == 0) set_err(p, BCSIM_E_OVERFLOW);
+    } else {
+      if (first) {
+        const uint32_t origin = p.mesh ? (j < i ? j : j + 1) : AT(p.col, e0 + j, p.E);
+        const Key key{t, t - static_cast<int64_t>(dt), origin, r.sub};
+        put_trace(p, s_trbase + li, key, rep, i, BCSIM_TR_GOSSIP_DELIVER, seq, r.f1 + 1, static_cast<int32_t>(origin));
+        const Msg m = mkmsg(GS_BLOCK, seq, r.f1 + 1, 0, 1);
+        const uint32_t sb = sub0 + nfb * deg;
+        const Op o = p.delay_mode == BCSIM_DELAY_FIXED
+                         ? mk_op(p, t + p.app_delay, static_cast<uint32_t>(p.app_delay), i, sb, 0, m, OP_BCAST, 0)
+                         : mk_op(p, t, 0, i, sb, static_cast<uint32_t>(draws0 + static_cast<uint64_t>(nfb) * deg), m,
+                                 OP_BCAST_J, 0);
+        st_op(&AT(p.ops + op_base(p, g), nops0 + nfb, ocap), o);
+        AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + seq, static_cast<uint64_t>(p.NT) * p.pbft_seq_cap) = 1;
+      }
+      if (j == 0) {
+        AT(p.sub, g, p.NT) = sub0 + nf * deg;
+        if (p.delay_mode != BCSIM_DELAY_FIXED) AT(p.draws, g, p.NT) = draws0 + static_cast<uint64_t>(nf) * deg;
+        AT(p.n_ops, g, p.NT) = nops0 + nf;
+        AT(p.node_onext, g, p.NT) = LLONG_MIN;  // k_link recomputes
+      }
+    }
+  }
+  if (tid == 0) {
+    unsigned long long* cnt = cnt_stripe(p, rep0);
+    unsigned long long tot = 0;
+    for (int k = 0; k < BCSIM_MSG_TYPES; ++k)
+      if (s_deliv[k]) {
+        atomicAdd(&cnt[CNT_DELIV + k], static_cast<unsigned long long>(s_deliv[k]));
+        tot += s_deliv[k];
+      }
+    if (tot) {
+      atomicAdd(&cnt[CNT_DELIV_TOTAL], tot);
+      atomicAdd(&kst_stripe(p)[KST_DELIV], tot);
+    }
+    if (s_ev) {
+      atomicAdd(&cnt[CNT_EVENTS], static_cast<unsigned long long>(s_ev));
+      if (p.echo) atomicAdd(&cnt[CNT_ECHOES], static_cast<unsigned long long>(s_ev));
+    }
+    if (s_wr) atomicAdd(&cnt[CNT_WRONG], static_cast<unsigned long long>(s_wr));
+    if (s_tmax > LLONG_MIN) atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), s_tmax);
   }
 }
 
@@ -2728,13 +2899,243 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   }
 }
 
-template <bool QM, bool XR>
+// LOOP: a small grid walks list 3 (the nodes k_gossip_link left over)
+template <bool QM, bool XR, bool LOOP = false>
 __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                               long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  if (LOOP) {
+    for (ListRange lr = list_range(p.act_n[3]); lr.k < lr.end; lr.k += lr.step) {
+      link_node<QM, XR>(pk, p.act[3ull * p.NT + lr.k], cell, t_lo, t_hi, final_win);
+      __syncthreads();
+    }
+    return;
+  }
   uint32_t k;
   if (list_one(p.act_n[1], k)) link_node<QM, XR>(pk, p.act[p.NT + k], cell, t_lo, t_hi, final_win);
+}
+
+// ---------------------------------------------------------------------------
+// k_gossip_link (dense layout, BCSIM_GOSSIP, not the full mesh, fixed app delay, infinite
+// queues, one rank, degree <= G): the link stage of a node whose due ops are all broadcasts
+// (<= G pending ops), by a group of G lanes, lane j = out-edge j.  Same result as
+// link_node: per edge the due broadcasts (key order, sub + j) merged with the implicit
+// echo of in-slot j, FIFO busy_until, one record per broadcast into the receiver's
+// in-slot (first record of the edge and arrival cell), its extras list or the overflow
+// list; then the ordered compaction of the ops not yet due.  Other nodes of the k_link
+// The kernel walks all of this rank's gnodes: a node with an echo to send or an op due that
+// is not simple is appended to list 3 for k_link<.., LOOP>.
+__global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                     long long t_hi, int final_win, uint32_t G) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ RawOp sop[256];  // due broadcasts of each group in key order (group base + rank)
+  __shared__ uint32_t s_c[6];  // sends, records, due ops, edges, echoes, kept
+  __shared__ uint8_t s_busy[kMaxBuckets];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, j = tid & (G - 1u), gb = lane & ~(G - 1u);
+  const uint32_t gbase = tid & ~(G - 1u);
+  const uint32_t per_wg = blockDim.x / G;
+  const uint32_t B = p.n_buckets;
+  if (tid < 6) s_c[tid] = 0;
+  for (uint32_t k = tid; k < B; k += blockDim.x) s_busy[k] = 0;
+  __syncthreads();
+  const uint32_t na = p.R * p.nloc;
+  const uint32_t k0 = blockIdx.x * per_wg, kl = k0 + tid / G;
+  const uint32_t g0 = (k0 / p.nloc) * p.N + p.nlo + k0 % p.nloc;
+  const uint32_t g = kl < na ? (kl / p.nloc) * p.N + p.nlo + kl % p.nloc : 0u;
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const uint32_t rep0 = g0 / p.N;
+  const uint32_t ib = static_cast<uint32_t>(cell % B);
+  const bool rx = kl < na && p.impl && node_flagged(p, ib, g, rep, i);
+  const uint32_t n0 = kl < na ? AT(p.n_ops, g, p.NT) : 0u;
+  // nodes link_node would change: an echo to send, or an op due (k_active's rule minus the
+  // nodes for which link_node only recomputes an unchanged node_onext)
+  const bool have = rx || (n0 && AT(p.node_onext, g, p.NT) < t_hi);
+  const uint32_t n = have ? n0 : 0u;
+  const uint32_t e0 = have ? AT(p.row, i, p.N + 1) : 0u;
+  const uint32_t deg = have ? AT(p.row, i + 1, p.N + 1) - e0 : 0u;
+  Op* ops = p.ops + (have ? op_base(p, g) : 0);
+  // this lane's pending op
+  RawOp o = raw_zero();
+  bool due = false, bc = false, keep = false;
+  if (have && n <= G && j < n) {
+    o = ld_raw(ops + j);
+    const uint32_t kind = raw_kind(o);
+    due = kind != OP_BCAST_J && raw_t(o) < t_hi;
+    bc = due && kind == OP_BCAST;
+    keep = !due && (kind != OP_BCAST_J || !(raw_flags(o) & OPF_DONE));
+  }
+  const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
+  const unsigned long long listed = __ballot(due && !bc) & gmask;
+  const bool fast = have && n <= G && deg <= G && listed == 0;
+  if (have && !fast && j == 0) {
+    const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
+    AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
+  }
+  // key-order rank of this lane's due broadcast; the group's broadcasts to LDS in that order
+  uint32_t rank = 0, nb = 0;
+  for (uint32_t q = 0; q < G; ++q) {
+    const bool bq = __shfl(bc ? 1 : 0, gb + q, 64) != 0;
+    RawOp oq;
+    oq.a.x = __shfl(o.a.x, gb + q, 64);
+    oq.a.y = __shfl(o.a.y, gb + q, 64);
+    oq.a.z = __shfl(o.a.z, gb + q, 64);
+    oq.a.w = __shfl(o.a.w, gb + q, 64);
+    oq.b.x = __shfl(o.b.x, gb + q, 64);
+    if (bq) {
+      ++nb;
+      if (bc && raw_key_less(oq, raw_sub(oq), o, raw_sub(o))) ++rank;
+    }
+  }
+  if (fast && bc) sop[gbase + rank] = o;
+  __syncthreads();
+  uint32_t c_rec = 0, c_edges = 0, c_echo = 0;
+  if (fast && j < deg && (nb || rx)) {
+    const uint32_t e = e0 + j;
+    const uint32_t sp = AT(p.col, e, p.E);
+    uint64_t* lwp = p.link + link_index(p, rep, i, e0, j);
+    uint64_t lw = *lwp;
+    bool he = false;
+    RawOp eo = raw_zero();
+    if (rx) {
+      Rec* ir = p.inbox + (static_cast<size_t>(ib) * p.R + rep) * p.E + e;
+      const Rec r0 = ld_rec(ir);
+      const long long ta0 = cell * p.L + r0.t_off;
+      if ((r0.flags & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
+        clr_rec(ir);
+        if (p.echo) {
+          const int bg = (r0.flags & RF_BIG) ? 1 : 0;
+          const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
+          eo = raw_make(ta0, static_cast<uint32_t>(pin + p.tx_last[bg]), sp, r0.sub,
+                        static_cast<uint8_t>(OP_ECHO | (bg ? (OPF_BIG << 2) : 0)));
+          he = true;
+          ++c_echo;
+        }
+      }
+    }
+    if (nb || he) {
+      ++c_edges;
+      int64_t bu = static_cast<int64_t>(lw >> 16);
+      uint32_t lc = static_cast<uint32_t>(lw & 0xFFFFu);
+      const int64_t pr = p.prop_const >= 0 ? p.prop_const : AT(p.prop, e, p.E);
+      const uint32_t slot = AT(p.rev, e, p.E);
+      const uint32_t dg = rep * p.N + sp;
+      uint32_t q = 0;
+      for (;;) {
+        RawOp x = raw_zero();
+        uint32_t sub = 0;
+        int src = -1;
+        if (q < nb) {
+          x = sop[gbase + q];
+          sub = raw_sub(x) + j;
+          src = 1;
+        }
+        if (he && (src < 0 || raw_key_less(eo, raw_sub(eo), x, sub))) {
+          x = eo;
+          sub = raw_sub(eo);
+          src = 3;
+        }
+        if (src < 0) break;
+        if (src == 1)
+          ++q;
+        else
+          he = false;
+        const int big = (raw_flags(x) & OPF_BIG) ? 1 : 0;
+        const int64_t ot = raw_t(x);
+        const int64_t start = bu > ot ? bu : ot;
+        bu = start + p.tx_tot[big];
+        if (src == 3) continue;  // echo: link occupancy only
+        const int64_t ta = bu + pr;
+        const long long ca = ta / p.L;
+        if (ca - cell < 1) {
+          set_err(p, BCSIM_E_TIE);
+          continue;
+        }
+        ++c_rec;
+        const uint32_t tof = static_cast<uint32_t>(ta - ca * p.L);
+        const uint32_t w3 = (x.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+        XRec xr;
+        {
+          const uint4 rv = make_uint4(tof, sub, x.b.z, w3);
+          __builtin_memcpy(&xr.r, &rv, sizeof xr.r);
+        }
+        const bool owner = lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
+        lc = static_cast<uint32_t>(ca) & 0xFFFFu;
+        xr.cell = ca;
+        xr.slot = slot;
+        xr.g = dg;
+        if (ca - cell < static_cast<long long>(B)) {
+          const uint32_t bk = static_cast<uint32_t>(ca % B);
+          if (owner) {
+            st_rec(&AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox), xr.r);
+          } else {
+            const uint32_t pos = atomicAdd(&p.x_cnt[bk], 1u);
+            if (pos >= p.cap_x)
+              set_err(p, BCSIM_E_OVERFLOW);
+            else
+              AT(p.xbuf, static_cast<size_t>(bk) * p.cap_x + pos, p.cap_xbuf) = xr;
+          }
+          AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
+          s_busy[bk] = 1;
+        } else {
+          if (owner) xr.r.flags = static_cast<uint8_t>(xr.r.flags | RF_OWNER);
+          const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+          if (pos >= p.cap_ov)
+            set_err(p, BCSIM_E_OVERFLOW);
+          else
+            AT(p.ov, pos, p.cap_ov) = xr;
+          atomicMin(&p.scal[1], static_cast<long long>(ca));
+        }
+      }
+      if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+      *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
+    }
+  }
+  // ordered compaction of the ops not yet due; their earliest time
+  const unsigned long long km = __ballot(fast && keep) & gmask;
+  long long om = (fast && keep) ? raw_t(o) : LLONG_MAX;
+  for (uint32_t off = 1; off < G; off <<= 1) {
+    const long long y = __shfl_xor(om, off, 64);
+    om = y < om ? y : om;
+  }
+  if (fast && keep) {
+    const uint32_t pos = static_cast<uint32_t>(__popcll(km & ((1ull << lane) - 1ull) & gmask));
+    uint4* w = reinterpret_cast<uint4*>(ops + pos);
+    w[0] = o.a;
+    w[1] = o.b;
+  }
+  const uint32_t kept = static_cast<uint32_t>(__popcll(km));
+  if (fast && j == 0 && (n || rx)) {  // (link_node returns early for a node with neither)
+    AT(p.n_ops, g, p.NT) = kept;
+    AT(p.node_onext, g, p.NT) = om;
+    if (rx && final_win) AT(p.iflag, static_cast<size_t>(ib) * p.NT + g, static_cast<uint64_t>(B) * p.NT) = 0;
+  }
+  // counters
+  {
+    const uint32_t v[6] = {fast && j == 0 && rep == rep0 ? nb * deg : 0u, c_rec, fast && j == 0 ? nb : 0u, c_edges,
+                           c_echo, fast && j == 0 ? kept : 0u};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const uint32_t ws = wave_sum(v[k]);
+      if (lane == 0 && ws) atomicAdd(&s_c[k], ws);
+    }
+    if (fast && rep != rep0 && j == 0 && nb) atomicAdd(&cnt_stripe(p, rep)[CNT_SENDS], static_cast<unsigned long long>(nb * deg));
+  }
+  __syncthreads();
+  for (uint32_t k = tid; k < B; k += blockDim.x)
+    if (s_busy[k]) mark_busy(&p.bucket_cnt[k]);
+  if (tid == 0) {
+    // (sends of another replica's node in this workgroup went straight to its stripe)
+    unsigned long long* cnt = cnt_stripe(p, rep0);
+    if (s_c[0]) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(s_c[0]));
+    unsigned long long* ks = kst_stripe(p);
+    if (s_c[1]) atomicAdd(&ks[KST_REC], static_cast<unsigned long long>(s_c[1]));
+    if (s_c[2]) atomicAdd(&ks[KST_OPS], static_cast<unsigned long long>(s_c[2]));
+    if (s_c[3]) atomicAdd(&ks[KST_EDGES], static_cast<unsigned long long>(s_c[3]));
+    if (s_c[4]) atomicAdd(&ks[KST_ECHO], static_cast<unsigned long long>(s_c[4]));
+    if (s_c[5]) atomicAdd(&ks[KST_KEPT], static_cast<unsigned long long>(s_c[5]));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3189,7 +3590,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
   __shared__ int32_t v_cur, nround0, n_alive, n_ticked;
   __shared__ unsigned long long lmask[64];  // leader flags of the current 4096-node chunk, one bit per node
   const uint32_t rep = blockIdx.x, tid = threadIdx.x;
-  if (rep == 0 && tid < 2) p.act_n[tid] = 0;  // the second window of the cell builds fresh lists
+  if (rep == 0 && tid < 4) p.act_n[tid] = 0;  // the second window of the cell builds fresh lists
   const uint32_t N = p.N;
   const long long ts_tick = tk - p.pbft_period;
   // v = latest v-log write before this tick in canonical order: every thread
@@ -3421,7 +3822,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (blockIdx.x == 0) {
-    if (threadIdx.x < 2) p.act_n[threadIdx.x] = 0;
+    if (threadIdx.x < 4) p.act_n[threadIdx.x] = 0;
     if (clr_b < p.n_buckets) {
       if (threadIdx.x == 0) {
         p.bucket_cnt[clr_b] = 0;
