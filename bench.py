@@ -56,7 +56,8 @@ PMC_ROUND = "r02"
 def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):
     """HBM bytes per launch of `kernel` from this round's committed rocprofv3 PMC
     summary (tools/pmc_summary.py over tests/gpu_prof.sh: FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE, separate passes), same workload; None if absent."""
+    correction + WRITE_SIZE, separate passes), same workload, over the timed window's
+    dispatches when the summary has them; None if absent."""
     path = os.path.join(REPO, "profiles", f"{PMC_ROUND}_pmc_{workload}{n_nodes}.json")
     try:
         with open(path) as f:
@@ -67,7 +68,8 @@ def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):
     cands = [v for k, v in ks.items() if k == kernel or k.startswith(kernel + "<")]
     if not cands:
         return None
-    return max(cands, key=lambda v: v.get("dispatches", 0))["hbm_bytes_per_launch"]
+    best = max(cands, key=lambda v: v.get("dispatches", 0))
+    return best.get("timed_window", {}).get("hbm_bytes_per_launch", best["hbm_bytes_per_launch"])
 
 
 def host_cpu():
@@ -172,9 +174,13 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
 
+    # HIP-event timing around the k_link class only inside the timed region (an event pair
+    # costs a few us of dispatch per launch); the other classes are timed in an extra
+    # untimed breakdown pass after it
+    os.environ["BCSIM_KSTATS"] = "2"
     import bcsim
     period = 50_000_001  # Seconds(0.05f) in ns (round mode)
-    cfg = make_cfg(args.nodes, args.warmup + args.steps + 4, local, args.workload, args.replicas)
+    cfg = make_cfg(args.nodes, args.warmup + 2 * args.steps + 4, local, args.workload, args.replicas)
     if args.workload == "paxos":
         cfg.paxos_decrees = args.decrees
     cfg.engine_mode = {"auto": bcsim.ENGINE_AUTO, "dense": bcsim.ENGINE_DENSE, "sparse": bcsim.ENGINE_SPARSE}[args.engine]
@@ -224,6 +230,7 @@ def main():
                   file=sys.stderr, flush=True)
     c0 = sim.counters()
     cm0 = commit_records(sim, args.workload)
+    link_before = sim.kernel_stats()["link"]["launches"]  # k_link launches before the timed region
     sim.reset_kernel_stats()
     barrier()
     w0 = time.perf_counter()
@@ -237,19 +244,26 @@ def main():
     msgs = c1["delivered_total"] - c0["delivered_total"]
     commits = commit_records(sim, args.workload) - cm0
     dt, msgs, commits = aggregate(dist, f"cuda:{local}", dt, msgs, commits)
+    # breakdown pass (untimed): every kernel class timed over as many more steps
+    os.environ["BCSIM_KSTATS"] = "15"
+    sim.reset_kernel_stats()
+    for _ in range(args.steps):
+        t_sim += period
+        sim.run(t_sim)
+    ks_all = sim.kernel_stats()
     sim.close()
 
     if rank == 0:
         # committed rounds: commit-kind records / N (every node commits each block;
         # block / stop / view records are not counted)
         rounds = commits / args.nodes
-        dom = max(("scan", "link", "group", "aux"), key=lambda k: ks[k]["us"])
+        dom = max(("scan", "link", "group", "aux"), key=lambda k: ks_all[k]["us"])
         lk = ks["link"]
         # roofline of the scatter (k_link): SURVEY.md §8(d) algorithmic bytes = 48 B per record
         # emitted by the timed k_link launches, over their HIP-event time on the engine stream
         ach = (lk["bytes"] / 1e9) / (lk["us"] / 1e6) if lk["us"] > 0 else 0.0
         traffic = pmc_traffic(args.nodes, workload=args.workload)
-        all_us = sum(v["us"] for v in ks.values())
+        all_us = sum(v["us"] for v in ks_all.values())
         if args.workload == "pbft":
             data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, %s)" % (
                 args.nodes, "app delay U{3,4,5} ms per send, counter RNG" if args.jitter else "fixed 3 ms app delay")
@@ -290,10 +304,19 @@ def main():
                          "implementation_bytes_per_launch": impl_launch_bytes,
                          "avg_launch_us": lk["us"] / max(1, lk["launches"]),
                          "launches": lk["launches"],
-                         "pipeline_frac": (48.0 * msgs / 1e9) / (all_us / 1e6) / HBM_PEAK_GBS if all_us else 0.0,
+                         # the timed launches are k_link dispatches [first, first + launches) of the
+                         # process: tools/pmc_summary.py restricts rocprofv3 traces to them
+                         "first_timed_launch": link_before,
                          "dominant_kernel_class": dom},
             "kernel_us": {k: v["us"] for k, v in ks.items()},
             "kernel_launches": {k: v["launches"] for k, v in ks.items()},
+            # untimed pass of as many steps with every kernel class timed (the timed region
+            # times k_link only)
+            "breakdown": {"kernel_us": {k: v["us"] for k, v in ks_all.items()},
+                                 "kernel_launches": {k: v["launches"] for k, v in ks_all.items()},
+                                 "records": ks_all["link"]["bytes"] / 48.0,
+                                 "pipeline_frac": ((ks_all["link"]["bytes"] / 1e9) / (all_us / 1e6) / HBM_PEAK_GBS
+                                                   if all_us else 0.0)},
         }
         if not args.no_cpu_baseline and world == 1:
             try:

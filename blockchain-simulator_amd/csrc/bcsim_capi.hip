@@ -769,15 +769,27 @@ static bool sync_each() {
   return v == 1;
 }
 
+// Kernel-class timing (bcsim_read_kernel_stats): HIP events around the launches of the
+// classes in BCSIM_KSTATS (bit mask over KS_*, default all, read at every launch).  An event
+// pair costs a few microseconds of dispatch per launch (bench.py times the k_link class only).
+static uint32_t kstat_mask() {
+  const char* e = std::getenv("BCSIM_KSTATS");
+  return e && *e ? static_cast<uint32_t>(std::strtol(e, nullptr, 0)) & 15u : 15u;
+}
 template <typename K, typename... Args>
 static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, dim3 block, size_t lds,
                         Args... args) {
-  int rc = ev_begin(s, cls);
+  const bool timed = cls >= 0 && ((kstat_mask() >> cls) & 1u);
+  int rc = timed ? ev_begin(s, cls) : BCSIM_OK;
   if (rc) return rc;
   hipLaunchKernelGGL(kernel, grid, block, lds, s.stream, args...);
   HIPCHK(hipGetLastError());
-  rc = ev_end(s);
-  if (rc) return rc;
+  if (timed) {
+    rc = ev_end(s);
+    if (rc) return rc;
+  } else if (cls >= 0) {
+    s.launches[cls]++;
+  }
   if (sync_each()) {  // debugging aid: pin a failure to one launch
     hipError_t e = hipStreamSynchronize(s.stream);
     if (e != hipSuccess) {
@@ -810,11 +822,17 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     const dim3 gg(static_cast<uint32_t>((static_cast<uint64_t>(s.R) * s.nloc + per_wg - 1) / per_wg));
     if ((rc = launch(s, KS_SCAN, k_gossip_scan, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g)) ||
         (rc = launch(s, KS_SCAN, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), block, lds, s.kp_dev, cell, lo, hi, cs,
-                     fw, xa)) ||
-        (rc = launch(s, KS_LINK, k_gossip_link, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, s.gossip_g)) ||
-        (rc = launch(s, KS_LINK, (k_link<false, false, true>), dim3(256), dim3(s.bs_link), link_lds_bytes(s.kp),
-                     s.kp_dev, cell, lo, hi, fw)))
+                     fw, xa)))
       return rc;
+    // the link stage (both kernels) as ONE timed launch of the k_link class
+    const bool timed = (kstat_mask() >> KS_LINK) & 1u;
+    if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
+    if ((rc = launch(s, -1, k_gossip_link, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, s.gossip_g)) ||
+        (rc = launch(s, -1, (k_link<false, false, true>), dim3(256), dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev,
+                     cell, lo, hi, fw)))
+      return rc;
+    if (timed) return ev_end(s);
+    s.launches[KS_LINK]++;
     return BCSIM_OK;
   }
   uint32_t n_link = 1;

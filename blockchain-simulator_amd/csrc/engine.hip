@@ -3163,33 +3163,49 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
   const uint32_t B = p.n_buckets;
   const long long cs = cell * p.L;
   // ---- 0. broadcasts -> per-edge SEND ops (jitter: per-edge draws; fixed: when due) ----
-  const uint32_t n_in = n;
-  for (uint32_t k = 0; k < n_in; ++k) {  // uniform loop over the node's (few) ops
-    const Op o = AT(ops, k, ocap);
-    const uint8_t kind = op_kind(o);
-    const bool jit = kind == OP_BCAST_J && !(op_flags(o) & OPF_DONE);
-    const bool fix = kind == OP_BCAST && o.t < t_hi;
-    if (!jit && !fix) continue;
-    if (n + deg > ocap) {
+  // The broadcasts to expand are found by a parallel pass over the ops (batches of
+  // kBcastCap, in op order) and expanded one after another by the whole workgroup.
+  for (;;) {
+    if (tid == 0) L.n_bc = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < n; k += bs) {
+      const Op& o = ops[k];
+      const uint8_t kind = op_kind(o);
+      if ((kind == OP_BCAST_J && !(op_flags(o) & OPF_DONE)) || (kind == OP_BCAST && o.t < t_hi)) {
+        const uint32_t pos = atomicAdd(&L.n_bc, 1u);
+        if (pos < kBcastCap) L.bc[pos] = k;
+      }
+    }
+    __syncthreads();
+    const uint32_t nfound = L.n_bc, nb = min(nfound, static_cast<uint32_t>(kBcastCap));
+    if (nb == 0) break;
+    if (n + nb * deg > ocap) {
       if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
       return;
     }
-    const bool paxos = (op_flags(o) & OPF_PAXOS) != 0;
-    for (uint32_t it = tid; it < deg; it += bs) {
-      int64_t d = 0;
-      if (jit) d = delay_from_draw(p, ctr_rand(p.seed, rep, i, static_cast<uint64_t>(o.edge) + it));
-      Op sop = o;
-      sop.t = o.t + d;
-      sop.dt = jit ? static_cast<uint32_t>(d) : o.dt;
-      sop.sub = o.sub + it;  // Paxos: edge it + 1 (peers[0] skipped), the last one *end()
-      sop.edge = paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it;
-      sop.kind_flags = static_cast<uint8_t>(OP_SEND | ((op_flags(o) & OPF_BIG) << 2));
-      AT(ops, n + it, ocap) = sop;
+    for (uint32_t b2 = 0; b2 < nb; ++b2) {
+      const Op o = ops[L.bc[b2]];
+      const bool jit = op_kind(o) == OP_BCAST_J;
+      const bool paxos = (op_flags(o) & OPF_PAXOS) != 0;
+      const uint32_t at = n + b2 * deg;
+      for (uint32_t it = tid; it < deg; it += bs) {
+        int64_t d = 0;
+        if (jit) d = delay_from_draw(p, ctr_rand(p.seed, rep, i, static_cast<uint64_t>(o.edge) + it));
+        Op sop = o;
+        sop.t = o.t + d;
+        sop.dt = jit ? static_cast<uint32_t>(d) : o.dt;
+        sop.sub = o.sub + it;  // Paxos: edge it + 1 (peers[0] skipped), the last one *end()
+        sop.edge = paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it;
+        sop.kind_flags = static_cast<uint8_t>(OP_SEND | ((op_flags(o) & OPF_BIG) << 2));
+        AT(ops, at + it, ocap) = sop;
+      }
     }
     __syncthreads();
-    if (tid == 0) AT(ops, k, ocap).kind_flags = static_cast<uint8_t>(OP_BCAST_J | (OPF_DONE << 2));  // consumed
-    n += deg;
+    for (uint32_t b2 = tid; b2 < nb; b2 += bs)  // consumed
+      AT(ops, L.bc[b2], ocap).kind_flags = static_cast<uint8_t>(OP_BCAST_J | (OPF_DONE << 2));
+    n += nb * deg;
     __syncthreads();
+    if (nfound <= static_cast<uint32_t>(kBcastCap)) break;
   }
   const uint32_t n_lists = B + 1 + (p.nranks > 1 ? p.nranks : 0);
   for (uint32_t k = tid; k < B; k += bs) L.lcnt[k] = 0;

@@ -5,7 +5,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 tag=${1:-prof}; shift
-args=${*:---no-cpu-baseline --steps 2 --warmup 5}
+args=${*:---no-cpu-baseline}
 out=gpurun_out/$tag
 mkdir -p $out
 step() {
