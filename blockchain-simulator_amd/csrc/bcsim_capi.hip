@@ -68,7 +68,8 @@ struct Sim {
   bool sparse = false;
   uint32_t grid_scan = 0, grid_link = 0;  // k_scan / k_link workgroups (walking the active lists)
   uint32_t gossip_g = 0;  // dense gossip: lanes per node of k_gossip_scan (0 = generic k_scan only)
-  bool gossip_link = false;  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
+  bool gossip_link = false;
+  bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
   uint32_t* seg_part = nullptr;  // multi-block segment scan partials
   long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
   long long n_alive = 0;
@@ -479,6 +480,8 @@ static int setup_device(Sim& s) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS, true, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PAXOS, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_GOSSIP, false>),
@@ -591,6 +594,10 @@ static int setup_device(Sim& s) {
     const char* nf = std::getenv("BCSIM_NO_GFAST");
     s.gossip_g = (c.protocol == BCSIM_GOSSIP && p.impl && s.deg_max <= 64 && !(nf && *nf == '1'))
                      ? static_cast<uint32_t>(next_pow2(std::max<uint64_t>(1, s.deg_max))) : 0u;
+    {
+      const char* px = std::getenv("BCSIM_NO_PXFAST");
+      s.paxos_fast = s.sparse && c.protocol == BCSIM_PAXOS && !(px && *px == '1');
+    }
     s.gossip_link = s.gossip_g && !p.mesh && s.P == 1 && c.delay_mode == BCSIM_DELAY_FIXED &&
                     c.queue_model == BCSIM_QUEUE_INFINITE;
     // PBFT replies with a fixed app delay < L (due in the arrival cell or the next)
@@ -837,9 +844,12 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   }
   uint32_t n_link = 1;
   {  // compact lists of the window's active gnodes
-    const uint32_t nb = static_cast<uint32_t>(std::min<uint64_t>(8192, (static_cast<uint64_t>(s.R) * s.nloc + 255) / 256));
-    rc = launch(s, KS_AUX, k_active, dim3(nb), dim3(256), 0, s.kp_dev, lo, hi, static_cast<uint32_t>(cell % s.B),
-                static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing));
+    // contiguous chunks of >= 2048 gnodes (<= kActChunk), at most ~1024 workgroups
+    const uint64_t nl = static_cast<uint64_t>(s.R) * s.nloc;
+    const uint64_t nb = std::max<uint64_t>((nl + kActChunk - 1) / kActChunk, std::min<uint64_t>(1024, (nl + 2047) / 2048));
+    const uint32_t chunk = static_cast<uint32_t>(((nl + nb - 1) / nb + 255) / 256 * 256);
+    rc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, lo, hi,
+                static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk);
     if (rc) return rc;
     if (!s.sparse) {
       // dense layout: read the list lengths back and launch exactly one workgroup per entry
@@ -857,6 +867,13 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
             : launch(s, KS_SCAN, k_scan<P, false>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa))
   if (grid.x == 0)
     rc = BCSIM_OK;  // no node has work in the window
+  else if (s.sparse && s.cfg.protocol == BCSIM_PAXOS && s.paxos_fast) {
+    // sparse Paxos: one lane per node takes the acceptors' request windows; the generic
+    // kernel walks the rest (list 2)
+    rc = launch(s, KS_SCAN, k_paxos_scan, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa);
+    if (!rc)
+      rc = launch(s, KS_SCAN, (k_scan<BCSIM_PAXOS, true, true>), grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa);
+  }
   else if (s.cfg.protocol == BCSIM_PBFT)
     rc = BCSIM_SCAN(BCSIM_PBFT);
   else if (s.cfg.protocol == BCSIM_RAFT)
@@ -899,8 +916,20 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   grid = dim3(s.sparse ? s.grid_link : (n_link + 7) / 8 * 8);
   if (grid.x == 0)
     rc = BCSIM_OK;
-  else if (s.sparse)
-    rc = launch(s, KS_LINK, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw);
+  else if (s.sparse && s.paxos_fast && s.kp.qmodel == 0 && s.P == 1) {
+    // sparse Paxos: one lane per acceptor first, the generic kernel over the rest (list 3)
+    const bool timed = (kstat_mask() >> KS_LINK) & 1u;
+    if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
+    if ((rc = launch(s, -1, k_paxos_link, grid, dim3(128), 0, s.kp_dev, cell, lo, hi)) ||
+        (rc = launch(s, -1, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw, 3)))
+      return rc;
+    if (timed) {
+      if ((rc = ev_end(s))) return rc;
+    } else {
+      s.launches[KS_LINK]++;
+    }
+  } else if (s.sparse)
+    rc = launch(s, KS_LINK, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw, 1);
   else {
     const size_t ll = link_lds_bytes(s.kp);
     const bool qm = s.kp.qmodel != 0, xr = s.kp.nranks > 1;

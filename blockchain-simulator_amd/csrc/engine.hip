@@ -2078,7 +2078,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* __rest
 }
 
 // a fixed grid over the window's active list (k_active); SP: sparse layout (no inbox slots)
-// LOOP (dense gossip): a small grid walks list 2, the nodes k_gossip_scan left over
+// LOOP: a small grid walks list 2, the nodes k_gossip_scan / k_paxos_scan left over
 template <int PROTO, bool SP, bool LOOP = false>
 __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                long long t_hi, long long cs, int final_win, int x_active) {
@@ -2086,7 +2086,7 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   BAIL_IF_ERR();
   if (LOOP) {
     for (ListRange lr = list_range(p.act_n[2]); lr.k < lr.end; lr.k += lr.step) {
-      scan_node<PROTO, false>(pk, p.act[2ull * p.NT + lr.k], cell, t_lo, t_hi, cs, final_win, x_active);
+      scan_node<PROTO, SP>(pk, p.act[2ull * p.NT + lr.k], cell, t_lo, t_hi, cs, final_win, x_active);
       __syncthreads();
     }
     return;
@@ -2099,6 +2099,137 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long l
   for (ListRange lr = list_range(p.act_n[0]); lr.k < lr.end; lr.k += lr.step) {
     scan_node<PROTO, true>(pk, p.act[lr.k], cell, t_lo, t_hi, cs, final_win, x_active);
     __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_paxos_scan (sparse layout, BCSIM_PAXOS): one LANE per active node.  A node whose window
+// holds only acceptor requests (REQ_TICKET / REQ_PROPOSE / REQ_COMMIT, at most kPxCap, no
+// timer, START or STOP due) is handled here in canonical key order exactly as the lane-0
+// loop of scan_node does it (paxos_recv, paxos-node.cc:177-247): per arrival the echo op,
+// the acceptor state of the message's decree, and the reply on the reverse edge with the
+// node's next schedule counter and (jitter) counter-RNG draw.  Every other node of the
+// list (proposers counting responses, START, timers, ...) is appended to list 2 for
+// k_scan<PAXOS, true, LOOP>.  The lane keeps its window's keys in LDS and selects them in
+// order (<= kPxCap^2 LDS reads).
+constexpr int kPxCap = 8;
+__global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                    long long t_hi, long long cs, int x_active) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ uint64_t skey[kPxCap][256];
+  __shared__ uint32_t sref[kPxCap][256];  // slot << 16 | index in the node's list segment
+  const uint32_t tid = threadIdx.x;
+  const uint32_t na = p.act_n[0];
+  const bool has_start = (t_lo <= 0 && 0 < t_hi);
+  const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
+  const bool jit = p.delay_mode != BCSIM_DELAY_FIXED;
+  const bool can = !has_start && !has_stop && t_lo >= p.dbg_tmax && (!jit || p.rng_mode == BCSIM_RNG_COUNTER);
+  for (uint32_t k = blockIdx.x * blockDim.x + tid; k < na; k += gridDim.x * blockDim.x) {
+    const uint32_t g = p.act[k];
+    const uint32_t rep = g / p.N, i = g % p.N;
+    bool fast = can && AT(p.node_tnext, g, p.NT) >= t_hi;
+    uint32_t xb = 0, xn = 0;
+    if (x_active) {
+      xb = AT(p.seg_off, g, p.NT + 1);
+      xn = AT(p.seg_off, g + 1, p.NT + 1) - xb;
+    }
+    const uint32_t e0 = AT(p.row, i, p.N + 1);
+    uint32_t cnt = 0;
+    for (uint32_t j = 0; fast && j < xn; ++j) {
+      const XRec& x = p.xgrp[xb + j];
+      const Rec r = x.r;
+      const long long t = cs + r.t_off;
+      if (!(t >= t_lo && t < t_hi)) continue;
+      if (cnt == static_cast<uint32_t>(kPxCap) || r.type > PX_REQ_COMMIT || r.f2 < 0 ||
+          static_cast<uint32_t>(r.f2) >= p.K || x.slot - e0 > 0xFFFFu) {
+        fast = false;
+        break;
+      }
+      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, x.slot) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
+      skey[cnt][tid] = (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~dt);
+      sref[cnt][tid] = ((x.slot - e0) << 16) | j;
+      ++cnt;
+    }
+    uint32_t nops = 0, ocap = 0;
+    if (fast) {
+      nops = AT(p.n_ops, g, p.NT);
+      ocap = op_cap(p, g);
+      if (nops + 2 * cnt > ocap) fast = false;  // the generic path raises the overflow
+    }
+    if (!fast) {
+      const uint32_t pos = atomicAdd(&p.act_n[2], 1u);
+      AT(p.act, 2ull * p.NT + pos, 4ull * p.NT) = g;
+      continue;
+    }
+    if (cnt == 0) continue;  // only arrivals of a later window of this cell
+    uint32_t sub = AT(p.sub, g, p.NT);
+    uint64_t draws = AT(p.draws, g, p.NT);
+    Op* ops = p.ops + op_base(p, g);
+    unsigned long long* cs_ = cnt_stripe(p, rep);
+    long long tmax = LLONG_MIN;
+    uint32_t done = 0;
+    for (uint32_t s2 = 0; s2 < cnt; ++s2) {
+      uint32_t best = 0;
+      bool have = false;
+      for (uint32_t c2 = 0; c2 < cnt; ++c2) {  // next arrival in (t, ~dt, slot) order
+        if (done & (1u << c2)) continue;
+        if (!have || skey[c2][tid] < skey[best][tid] ||
+            (skey[c2][tid] == skey[best][tid] && sref[c2][tid] < sref[best][tid])) {
+          best = c2;
+          have = true;
+        }
+      }
+      done |= 1u << best;
+      const XRec x = p.xgrp[xb + (sref[best][tid] & 0xFFFFu)];
+      const uint32_t q = x.slot;
+      const Rec r = x.r;
+      const Msg m = rec_msg(r);
+      const int64_t t = cs + r.t_off;
+      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[m.big]);
+      const uint32_t origin = AT(p.col, q, p.E);
+      if (t > tmax) tmax = t;
+      atomicAdd(&cs_[CNT_DELIV + r.type], 1ull);
+      if (p.echo) AT(ops, nops++, ocap) = mk_op(p, t, dt, origin, r.sub, q, m, OP_ECHO, 0);
+      int32_t* a = &AT(p.px, (static_cast<size_t>(g) * p.K + static_cast<uint32_t>(r.f2)) * 4,
+                       static_cast<uint64_t>(p.NT) * p.K * 4);
+      const int32_t tk = c2i(mch(m, 1));
+      Msg rr;
+      if (r.type == PX_REQ_TICKET) {  // :177-198
+        if (tk > a[0]) {
+          a[0] = tk;
+          rr = mkmsg(PX_RES_TICKET, enc_raw(p, 0), a[1], m.f[2], 0);
+        } else {
+          rr = mkmsg(PX_RES_TICKET, enc_raw(p, 1), 0, m.f[2], 0);
+        }
+      } else if (r.type == PX_REQ_PROPOSE) {  // :199-221
+        int32_t st = 1;
+        if (tk == a[0]) {
+          a[1] = mch(m, 2);
+          a[2] = tk;
+          st = 0;
+        }
+        rr = mkmsg(PX_RES_PROPOSE, enc_raw(p, st), 0, m.f[2], 0);
+      } else {  // PX_REQ_COMMIT :222-247
+        int32_t st = 1;
+        if (tk == a[2] && mch(m, 2) == a[1]) {
+          a[3] = 1;
+          st = 0;
+        }
+        rr = mkmsg(PX_RES_COMMIT, enc_raw(p, st), 0, m.f[2], 0);
+      }
+      const int64_t d = jit ? delay_from_draw(p, ctr_rand(p.seed, rep, i, draws++)) : p.app_delay;
+      AT(ops, nops++, ocap) = mk_op(p, t + d, static_cast<uint32_t>(d), i, sub++, q, rr, OP_SEND, 0);
+    }
+    AT(p.sub, g, p.NT) = sub;
+    if (jit) AT(p.draws, g, p.NT) = draws;
+    AT(p.n_ops, g, p.NT) = nops;
+    AT(p.node_onext, g, p.NT) = LLONG_MIN;  // k_link recomputes
+    atomicAdd(&cs_[CNT_DELIV_TOTAL], static_cast<unsigned long long>(cnt));
+    atomicAdd(&kst_stripe(p)[KST_DELIV], static_cast<unsigned long long>(cnt));
+    if (p.echo) atomicAdd(&cs_[CNT_ECHOES], static_cast<unsigned long long>(cnt));
+    atomicAdd(&cs_[CNT_EVENTS], static_cast<unsigned long long>(cnt));
+    atomicMax(reinterpret_cast<long long*>(&cs_[CNT_TLAST]), tmax);
   }
 }
 
@@ -3483,12 +3614,210 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
   (void)cs;
 }
 
+// list 1: the window's k_link list; list 3: the nodes k_paxos_link left over
 __global__ __launch_bounds__(256) void k_link_sparse(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                     long long t_hi, int final_win) {
+                                                     long long t_hi, int final_win, int list) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  for (ListRange lr = list_range(p.act_n[1]); lr.k < lr.end; lr.k += lr.step) {
-    link_node_sparse(p, p.act[p.NT + lr.k], cell, t_lo, t_hi, final_win);
+  const uint32_t li = list == 3 ? 3u : 1u;
+  for (ListRange lr = list_range(p.act_n[li]); lr.k < lr.end; lr.k += lr.step) {
+    link_node_sparse(p, p.act[li * p.NT + lr.k], cell, t_lo, t_hi, final_win);
+    __syncthreads();
+  }
+}
+
+// k_paxos_link (sparse layout, BCSIM_PAXOS, infinite queues): one LANE per node of the
+// k_link list whose pending ops (<= kPxCap) are all unicasts / echoes on real edges -- the
+// acceptors.  Same result as link_node_sparse: the due ops in (edge, canonical key) order
+// through each edge's FIFO, one list record per SEND (staged per workgroup, one global
+// atomic per list and batch), the ops not yet due compacted in order.  Other nodes go to
+// list 3 for k_link_sparse.  128 lanes per workgroup, the lane's ops in LDS (32 KB).
+__global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                    long long t_hi) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ LinkShared L;
+  __shared__ uint4 sa[kPxCap][128], sb[kPxCap][128];
+  __shared__ uint32_t s_c[7];  // records, due ops, edges, echoes, kept, (unused)
+  const uint32_t tid = threadIdx.x, bs = blockDim.x;
+  const uint32_t na = p.act_n[1];
+  const uint32_t B = p.n_buckets;
+  const uint32_t n_lists = B + 1;
+  for (uint32_t base = blockIdx.x * bs; base < na; base += gridDim.x * bs) {  // workgroup-uniform
+    for (uint32_t k = tid; k < B; k += bs) L.lcnt[k] = 0;
+    for (uint32_t k = tid; k < n_lists; k += bs) L.lst[k] = 0;
+    if (tid < 7) s_c[tid] = 0;
+    if (tid == 0) {
+      L.nst = 0;
+      L.ovmin = LLONG_MAX;
+    }
+    __syncthreads();
+    const uint32_t kl = base + tid;
+    const uint32_t g = kl < na ? p.act[p.NT + kl] : 0u;
+    const uint32_t n = kl < na ? AT(p.n_ops, g, p.NT) : 0u;
+    bool fast = kl < na && n <= static_cast<uint32_t>(kPxCap);
+    Op* ops = p.ops + (kl < na ? op_base(p, g) : 0);
+    uint32_t due = 0;  // bit c: op c is due
+    for (uint32_t c = 0; fast && c < n; ++c) {
+      const RawOp o = ld_raw(ops + c);
+      const uint32_t kind = raw_kind(o);
+      if ((kind != OP_SEND && kind != OP_ECHO) || o.b.y == kInvalid) {
+        fast = false;
+        break;
+      }
+      sa[c][tid] = o.a;
+      sb[c][tid] = o.b;
+      if (raw_t(o) < t_hi) due |= 1u << c;
+    }
+    if (kl < na && !fast) {
+      const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
+      AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
+    }
+    uint32_t c_rec = 0, c_ops = 0, c_edges = 0, c_echo = 0, c_sends = 0;
+    long long ovmin = LLONG_MAX;
+    if (fast && due) {
+      const uint32_t rep = g / p.N, i = g % p.N;
+      const uint32_t e0 = AT(p.row, i, p.N + 1);
+      uint32_t left = due;
+      uint32_t cur_e = kInvalid;
+      uint64_t* lwp = nullptr;
+      int64_t bu = 0;
+      uint32_t lc = 0, sn = 0, slot = 0, dg = 0;
+      int64_t pr = 0;
+      while (left) {
+        // next due op in (edge, key) order
+        uint32_t best = 0;
+        bool have = false;
+        for (uint32_t c = 0; c < n; ++c) {
+          if (!(left & (1u << c))) continue;
+          if (!have) {
+            best = c;
+            have = true;
+            continue;
+          }
+          const RawOp oc{sa[c][tid], sb[c][tid]}, ob{sa[best][tid], sb[best][tid]};
+          if (oc.b.y < ob.b.y || (oc.b.y == ob.b.y && raw_key_less(oc, raw_sub(oc), ob, raw_sub(ob)))) best = c;
+        }
+        left &= ~(1u << best);
+        const RawOp o{sa[best][tid], sb[best][tid]};
+        const uint32_t e = o.b.y;
+        if (e != cur_e) {  // a new edge: store the previous one's link word, load this one's
+          if (lwp) {
+            if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+            *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
+          }
+          cur_e = e;
+          const uint32_t le = e - e0;
+          lwp = p.link + link_index(p, rep, i, e0, le);
+          const uint64_t lw = *lwp;
+          bu = static_cast<int64_t>(lw >> 16);
+          lc = static_cast<uint32_t>(lw & 0xFFFFu);
+          sn = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e, p.E);
+          slot = p.mesh ? sn * (p.N - 1) + (i < sn ? i : i - 1) : AT(p.rev, e, p.E);
+          dg = rep * p.N + sn;
+          pr = p.prop_const >= 0 ? p.prop_const : AT(p.prop, e, p.E);
+          ++c_edges;
+        }
+        ++c_ops;
+        const uint32_t kind = raw_kind(o);
+        if (kind == OP_SEND) ++c_sends;
+        const int big = (raw_flags(o) & OPF_BIG) ? 1 : 0;
+        const int64_t ot = raw_t(o);
+        const int64_t start = bu > ot ? bu : ot;
+        bu = start + p.tx_tot[big];
+        if (kind == OP_ECHO) {
+          ++c_echo;
+          continue;
+        }
+        const int64_t ta = bu + pr;
+        const long long ca = ta / p.L;
+        const long long rel = ca - cell;
+        if (rel < 1) {
+          set_err(p, BCSIM_E_TIE);
+          continue;
+        }
+        ++c_rec;
+        lc = static_cast<uint32_t>(ca) & 0xFFFFu;
+        XRec x;
+        {
+          const uint32_t w3 = (o.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+          const uint4 rv = make_uint4(static_cast<uint32_t>(ta - ca * p.L), raw_sub(o), o.b.z, w3);
+          __builtin_memcpy(&x.r, &rv, sizeof x.r);
+        }
+        x.cell = ca;
+        x.slot = slot;
+        x.g = dg;
+        if (rel < static_cast<long long>(B)) {
+          const uint32_t bk = static_cast<uint32_t>(ca % B);
+          link_stage(p, L, g, bk, x);
+          set_flag_once(&AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT));
+          atomicAdd(&L.lcnt[bk], 1u);
+        } else {
+          link_stage(p, L, g, B, x);
+          if (ca < ovmin) ovmin = ca;
+        }
+      }
+      if (lwp) {
+        if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+        *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
+      }
+    }
+    if (fast && (due || n)) {  // ordered compaction of the ops not yet due
+      uint32_t kept = 0;
+      long long omin = LLONG_MAX;
+      for (uint32_t c = 0; c < n; ++c) {
+        if (due & (1u << c)) continue;
+        const RawOp o{sa[c][tid], sb[c][tid]};
+        if (raw_t(o) < omin) omin = raw_t(o);
+        uint4* w = reinterpret_cast<uint4*>(ops + kept);
+        w[0] = o.a;
+        w[1] = o.b;
+        ++kept;
+      }
+      AT(p.n_ops, g, p.NT) = kept;
+      AT(p.node_onext, g, p.NT) = omin;
+      atomicAdd(&s_c[4], kept);
+      if (c_sends) atomicAdd(&cnt_stripe(p, g / p.N)[CNT_SENDS], static_cast<unsigned long long>(c_sends));
+    }
+    if (c_rec) atomicAdd(&s_c[0], c_rec);
+    if (c_ops) atomicAdd(&s_c[1], c_ops);
+    if (c_edges) atomicAdd(&s_c[2], c_edges);
+    if (c_echo) atomicAdd(&s_c[3], c_echo);
+    if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
+    __syncthreads();
+    // flush the staged records: one global atomic per list
+    for (uint32_t k = tid; k < n_lists; k += bs) {
+      const uint32_t c = L.lst[k];
+      if (!c) continue;
+      uint32_t* ctr = k < B ? &p.x_cnt[k] : p.ov_cnt;
+      const uint32_t cap = k < B ? p.cap_x : p.cap_ov;
+      const uint32_t b0 = atomicAdd(ctr, c);
+      if (b0 + c > cap) set_err(p, BCSIM_E_OVERFLOW);
+      L.lbase[k] = b0;
+    }
+    __syncthreads();
+    const uint32_t nst = min(L.nst, p.cap_stage);
+    for (uint32_t k = tid; k < nst; k += bs) {
+      const size_t sidx = static_cast<size_t>(blockIdx.x) * p.cap_stage + k;
+      const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
+      const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
+      if (list == B) {
+        if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
+      } else if (pos < p.cap_x) {
+        p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
+      }
+    }
+    for (uint32_t k = tid; k < B; k += bs)
+      if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
+    if (tid == 0) {
+      if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
+      unsigned long long* ks = kst_stripe(p);
+      if (s_c[0]) atomicAdd(&ks[KST_REC], static_cast<unsigned long long>(s_c[0]));
+      if (s_c[1]) atomicAdd(&ks[KST_OPS], static_cast<unsigned long long>(s_c[1]));
+      if (s_c[2]) atomicAdd(&ks[KST_EDGES], static_cast<unsigned long long>(s_c[2]));
+      if (s_c[3]) atomicAdd(&ks[KST_ECHO], static_cast<unsigned long long>(s_c[3]));
+      if (s_c[4]) atomicAdd(&ks[KST_KEPT], static_cast<unsigned long long>(s_c[4]));
+    }
     __syncthreads();
   }
 }
@@ -3499,39 +3828,63 @@ __global__ __launch_bounds__(256) void k_link_sparse(const KP* __restrict__ pk, 
 // k_scan: arrivals in the bucket, a due timer, START / STOP; k_link: those plus the
 // nodes with an op due -- as two compact lists (one returning atomic per wave; the
 // loop bound is wave-uniform, so every ballot runs with the whole wave active)
+constexpr uint32_t kActChunk = 16384;  // k_active: gnodes per workgroup at most (LDS flags)
 __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long long t_lo, long long t_hi, uint32_t b,
-                                                uint32_t obp) {
+                                                uint32_t obp, uint32_t chunk) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  // each workgroup compacts a contiguous chunk of gnodes: flags to LDS and counts, ONE global
+  // atomic per list for the chunk (a per-wave atomic on the two list counters serialised:
+  // 1.5 ms per launch at 8 M gnodes), then the ordered writes
+  __shared__ uint8_t fl[kActChunk];
+  __shared__ uint32_t s_n[2], s_base[2], wcnt[kMaxWaves];
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t tid = threadIdx.x;
   const uint64_t n_loc = static_cast<uint64_t>(p.R) * p.nloc;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); base < n_loc;
-       base += stride) {
-    const uint64_t k = base + lane;
-    bool sc = false, lk = false;
-    uint32_t g = 0;
-    if (k < n_loc) {
-      g = static_cast<uint32_t>((k / p.nloc) * p.N + p.nlo + k % p.nloc);
-      const uint32_t rep = g / p.N, i = g % p.N;
-      sc = has_start || has_stop || node_flagged(p, b, g, rep, i) || AT(p.node_tnext, g, p.NT) < t_hi;
-      // k_link also runs nodes with reply-slot ops of the previous arrival cell due
-      lk = sc || AT(p.node_onext, g, p.NT) < t_hi ||
-           (p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u));
-    }
-    const unsigned long long ms = __ballot(sc), ml = __ballot(lk);
-    uint32_t ps = 0, pl = 0;
-    if (lane == 0) {
-      if (ms) ps = atomicAdd(&p.act_n[0], static_cast<uint32_t>(__popcll(ms)));
-      if (ml) pl = atomicAdd(&p.act_n[1], static_cast<uint32_t>(__popcll(ml)));
-    }
-    ps = __shfl(ps, 0, 64);
-    pl = __shfl(pl, 0, 64);
-    if (sc) p.act[ps + static_cast<uint32_t>(__popcll(ms & lt))] = g;
-    if (lk) p.act[p.NT + pl + static_cast<uint32_t>(__popcll(ml & lt))] = g;
+  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * chunk;
+  if (c0 >= n_loc) return;  // uniform
+  const uint32_t cn = static_cast<uint32_t>(min(static_cast<uint64_t>(chunk), n_loc - c0));
+  if (tid < 2) s_n[tid] = 0;
+  __syncthreads();
+  uint32_t ns = 0, nl = 0;
+  for (uint32_t j = tid; j < cn; j += blockDim.x) {
+    const uint64_t k = c0 + j;
+    const uint32_t g = static_cast<uint32_t>((k / p.nloc) * p.N + p.nlo + k % p.nloc);
+    const uint32_t rep = g / p.N, i = g % p.N;
+    const bool sc = has_start || has_stop || node_flagged(p, b, g, rep, i) || AT(p.node_tnext, g, p.NT) < t_hi;
+    // k_link also runs nodes with reply-slot ops of the previous arrival cell due
+    const bool lk = sc || AT(p.node_onext, g, p.NT) < t_hi ||
+                    (p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u));
+    fl[j] = static_cast<uint8_t>((sc ? 1u : 0u) | (lk ? 2u : 0u));
+    ns += sc ? 1u : 0u;
+    nl += lk ? 1u : 0u;
+  }
+  ns = wave_sum(ns);
+  nl = wave_sum(nl);
+  if ((tid & 63u) == 0) {
+    if (ns) atomicAdd(&s_n[0], ns);
+    if (nl) atomicAdd(&s_n[1], nl);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    s_base[0] = s_n[0] ? atomicAdd(&p.act_n[0], s_n[0]) : 0u;
+    s_base[1] = s_n[1] ? atomicAdd(&p.act_n[1], s_n[1]) : 0u;
+  }
+  __syncthreads();
+  uint32_t ps = s_base[0], pl = s_base[1];
+  for (uint32_t j0 = 0; j0 < cn; j0 += blockDim.x) {  // uniform
+    const uint32_t j = j0 + tid;
+    const uint32_t f = j < cn ? fl[j] : 0u;
+    const uint64_t k = c0 + j;
+    const uint32_t g = j < cn ? static_cast<uint32_t>((k / p.nloc) * p.N + p.nlo + k % p.nloc) : 0u;
+    uint32_t ts, tl;
+    const uint32_t rs = block_rank((f & 1u) != 0, wcnt, ts);
+    if (f & 1u) p.act[ps + rs] = g;
+    const uint32_t rl = block_rank((f & 2u) != 0, wcnt, tl);
+    if (f & 2u) p.act[p.NT + pl + rl] = g;
+    ps += ts;
+    pl += tl;
   }
 }
 
