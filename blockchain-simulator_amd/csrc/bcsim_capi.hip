@@ -513,6 +513,10 @@ static int setup_device(Sim& s) {
   p.nloc = s.nloc;
   p.rank = s.prank;
   p.nranks = s.P;
+  // rank-local per-edge state: the edges of this rank's rows
+  p.e_lo = static_cast<uint32_t>(s.row[s.nlo]);
+  p.E_loc = static_cast<uint64_t>(s.row[s.nlo + s.nloc]) - s.row[s.nlo];
+  p.cap_inbox = s.sparse ? 1 : static_cast<uint64_t>(s.B) * s.R * p.E_loc;
   {
     std::vector<uint16_t> own(s.N);
     for (uint32_t r = 0; r < s.P; ++r)
@@ -586,7 +590,7 @@ static int setup_device(Sim& s) {
   // per-edge reply slots of main-slot arrivals (kOpRing cells) and implicit
   // echoes; slots off beyond a 16 GiB budget, both off with BCSIM_NO_SLOTS=1 (A/B aid)
   {
-    const uint64_t ne = static_cast<uint64_t>(kOpRing) * s.R * s.E;
+    const uint64_t ne = static_cast<uint64_t>(kOpRing) * s.R * p.E_loc;
     const char* ns = std::getenv("BCSIM_NO_SLOTS");
     const bool off = ns && *ns == '1';
     p.impl = (off || s.sparse) ? 0u : 1u;  // sparse: no slots, echoes listed by k_scan
@@ -612,10 +616,10 @@ static int setup_device(Sim& s) {
   }
   const size_t n_link = p.hubs ? static_cast<size_t>(s.R) * (static_cast<size_t>(p.hubs) * (s.N - 1) +
                                                               static_cast<size_t>(s.N - p.hubs) * p.hubs)
-                               : static_cast<size_t>(s.R) * s.E;
+                               : static_cast<size_t>(s.R) * p.E_loc;
   if ((rc = dalloc(s, &p.link, n_link))) return rc;
   {  // DROPTAIL link queues: ring of cap_q message entries per edge
-    const size_t ne = p.qmodel ? static_cast<size_t>(s.R) * s.E : 1;
+    const size_t ne = p.qmodel ? static_cast<size_t>(s.R) * p.E_loc : 1;
     if (p.cap_q > 65535) {
       g_detail = "cap_queue_msgs must be < 65536";
       return BCSIM_E_INVAL;

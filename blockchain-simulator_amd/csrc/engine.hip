@@ -167,6 +167,10 @@ struct KP {
   // [nlo, nlo + nloc) of every replica; records for other ranks' receivers
   // are staged in sendbuf and exchanged once per cell
   uint32_t nlo, nloc, rank, nranks;
+  // per-edge state (inbox slots, reply slots, link words, queue rings) is rank-local: only the
+  // edges in the rows of this rank's nodes, [e_lo, e_lo + E_loc) of every replica
+  uint32_t e_lo;
+  uint64_t E_loc;
   const uint16_t* owner;    // [N] rank owning node i
   XRec* sendbuf;            // [nranks][cap_send]
   uint32_t* send_cnt;       // [nranks] (control block)
@@ -260,6 +264,14 @@ __device__ inline uint32_t local_gnode(const KP& p, uint32_t b) {
   return (j / p.nloc) * p.N + p.nlo + j % p.nloc;
 }
 
+// rank-local per-edge index of edge / in-slot e of replica rep, and of an inbox slot
+__device__ inline size_t edge_loc(const KP& p, uint32_t rep, uint32_t e) {
+  return static_cast<size_t>(rep) * p.E_loc + (e - p.e_lo);
+}
+__device__ inline size_t inbox_idx(const KP& p, uint32_t b, uint32_t rep, uint32_t slot) {
+  return (static_cast<size_t>(b) * p.R + rep) * p.E_loc + (slot - p.e_lo);
+}
+
 // Active-list launches (k_scan, k_link): a fixed grid (a multiple of 8) walks the list of
 // the window's active gnodes built by k_active.  Workgroups are dispatched round-robin
 // over the 8 XCDs, so XCD x = blockIdx & 7 takes the contiguous list chunk x (neighbouring
@@ -296,7 +308,7 @@ __device__ inline uint32_t op_cap(const KP& p, uint32_t g) { return (g % p.N) < 
 // full mesh): rows of the hub nodes in full, then (node, hub) pairs; an edge between
 // two non-hubs has no state (BCSIM_E_UNSUPPORTED if it ever carries traffic).
 __device__ inline size_t link_index(const KP& p, uint32_t rep, uint32_t i, uint32_t e0, uint32_t le) {
-  if (!p.hubs) return static_cast<size_t>(rep) * p.E + e0 + le;
+  if (!p.hubs) return edge_loc(p, rep, e0 + le);
   const size_t per = static_cast<size_t>(p.hubs) * (p.N - 1) + static_cast<size_t>(p.N - p.hubs) * p.hubs;
   if (i < p.hubs) return rep * per + static_cast<size_t>(i) * (p.N - 1) + le;
   const uint32_t j = le < i ? le : le + 1;  // full mesh peer
@@ -528,7 +540,7 @@ static_assert(offsetof(Op, sub) == 16 && offsetof(Op, f0) == 24 && offsetof(Op, 
 // per-edge op slots
 constexpr uint32_t kOpRing = 4;
 __device__ inline uint4* eslot_at(const KP& p, uint32_t ob, uint32_t rep, uint32_t e) {
-  return &AT(p.eslot, (static_cast<size_t>(ob) * p.R + rep) * p.E + e, p.cap_eslot);
+  return &AT(p.eslot, (static_cast<size_t>(ob) * p.R + rep) * p.E_loc + (e - p.e_lo), p.cap_eslot);
 }
 constexpr uint32_t kPbPrepareRes = 5;  // PBFT PREPARE_RES (pbft-node.h:80-91), the only slot reply
 // the full op of a reply slot: SEND at the stored due time, dt = app delay, origin =
@@ -801,7 +813,7 @@ __global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) 
     const bool owner = (x.r.flags & RF_OWNER) != 0;
     x.r.flags = static_cast<uint8_t>(x.r.flags & ~RF_OWNER);
     if (owner) {
-      st_rec(&AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox), x.r);
+      st_rec(&AT(p.inbox, inbox_idx(p, b, rep, x.slot), p.cap_inbox), x.r);
     } else {
       const uint32_t pos = list_append(&p.x_cnt[b]);
       if (pos >= p.cap_x) {
@@ -1734,7 +1746,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* __rest
 
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
   // sparse mode: no inbox slots, the node's arrivals are all in the cell's grouped lists
-  const Rec* slots = SP ? nullptr : p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0;
+  const Rec* slots = SP ? nullptr : p.inbox + inbox_idx(p, b, rep, e0);
   const uint32_t deg_in = SP ? 0u : deg;
   uint32_t xn = 0;
   const XRec* xs = p.xgrp;
@@ -2286,7 +2298,7 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
   long long t = 0;
   uint32_t dt = 0;
   if (fast && j < deg && flagged) {
-    r = ld_rec(p.inbox + (static_cast<size_t>(b) * p.R + rep) * p.E + e0 + j);
+    r = ld_rec(p.inbox + inbox_idx(p, b, rep, e0 + j));
     t = cs + r.t_off;
     v = (r.flags & RF_VALID) && t >= t_lo && t < t_hi;
     dt = static_cast<uint32_t>(prop_of_slot(p, e0 + j) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
@@ -2540,7 +2552,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   // LDS: ecnt[deg+1] (per-edge counts -> offsets -> ends) | eidx[cap_eidx] (listed due ops
   // grouped by edge; a node with more due ops than cap_eidx uses its global area eidx_g)
   uint32_t* ecnt = reinterpret_cast<uint32_t*>(smem);
-  const size_t eb0 = static_cast<size_t>(rep) * p.E + e0;
+  const size_t eb0 = edge_loc(p, rep, e0);
   const int64_t* prop = p.prop + e0;
   unsigned long long* cnt = cnt_stripe(p, rep);
   const uint32_t B = p.n_buckets;
@@ -2686,7 +2698,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   unsigned long long n_rec = 0, st_edges = 0, st_echo = 0, fdrop = 0, lost = 0;
   long long ovmin = LLONG_MAX;
   const long long cs = cell * p.L;
-  const Rec* in_row = p.inbox + (static_cast<size_t>(ib) * p.R + rep) * p.E;
+  const Rec* in_row = p.inbox + inbox_idx(p, ib, rep, e0);  // this node's row
   for (uint32_t le = tid; le < deg; le += blockDim.x) {
     const uint32_t eb = n_list && le ? ecnt[le - 1] : 0u, ee = n_list ? ecnt[le] : 0u;
     const uint32_t e = e0 + le;
@@ -2710,7 +2722,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     bool he = false;
     RawOp eo = raw_zero();
     if (rx) {
-      Rec* ir = const_cast<Rec*>(in_row) + e;
+      Rec* ir = const_cast<Rec*>(in_row) + le;
       const Rec r0 = ld_rec(ir);
       const long long ta0 = cs + r0.t_off;
       if ((r0.flags & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
@@ -2876,7 +2888,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
           // the receiver's in-slot of this bucket, written directly: a receiver-major 16-byte
           // scatter from XCD-contiguous senders merges in L2 and costs ~2x a coalesced row
           // write, a third of staging sender-major and transposing (tools/microbench/scatter.hip)
-          st_rec(&AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox), r);
+          st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), r);
           if (p.mesh) {
             // receiver-tile flag: one LDS byte per 64-node tile, flushed once per workgroup
             uint32_t tb = kInvalid;
@@ -3130,7 +3142,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
     bool he = false;
     RawOp eo = raw_zero();
     if (rx) {
-      Rec* ir = p.inbox + (static_cast<size_t>(ib) * p.R + rep) * p.E + e;
+      Rec* ir = p.inbox + inbox_idx(p, ib, rep, e);
       const Rec r0 = ld_rec(ir);
       const long long ta0 = cell * p.L + r0.t_off;
       if ((r0.flags & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
@@ -3199,7 +3211,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
         if (ca - cell < static_cast<long long>(B)) {
           const uint32_t bk = static_cast<uint32_t>(ca % B);
           if (owner) {
-            st_rec(&AT(p.inbox, (static_cast<size_t>(bk) * p.R + rep) * p.E + slot, p.cap_inbox), xr.r);
+            st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), xr.r);
           } else {
             const uint32_t pos = atomicAdd(&p.x_cnt[bk], 1u);
             if (pos >= p.cap_x)
@@ -3463,7 +3475,7 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
       uint32_t lc = static_cast<uint32_t>(lw & 0xFFFFu);
       uint64_t qm = 0;
       uint64_t* qr = nullptr;
-      const size_t qe = static_cast<size_t>(rep) * p.E + e;
+      const size_t qe = edge_loc(p, rep, e);
       if (p.qmodel) {
         qm = p.qmeta[qe];
         qr = p.qring + qe * p.cap_q;
@@ -3912,7 +3924,7 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
       const bool owner = (x.r.flags & RF_OWNER) != 0;
       x.r.flags = static_cast<uint8_t>(x.r.flags & ~RF_OWNER);
       if (owner) {
-        st_rec(&AT(p.inbox, (static_cast<size_t>(b) * p.R + rep) * p.E + x.slot, p.cap_inbox), x.r);
+        st_rec(&AT(p.inbox, inbox_idx(p, b, rep, x.slot), p.cap_inbox), x.r);
       } else {
         const uint32_t pos = atomicAdd(&p.x_cnt[b], 1u);
         if (pos < p.cap_x)
