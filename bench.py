@@ -177,7 +177,7 @@ def main():
     # HIP-event timing around the k_link class only inside the timed region (an event pair
     # costs a few us of dispatch per launch); the other classes are timed in an extra
     # untimed breakdown pass after it
-    os.environ["BCSIM_KSTATS"] = "2"
+    os.environ.setdefault("BCSIM_KSTATS", "2")  # (a diagnostic run may time more classes)
     import bcsim
     period = 50_000_001  # Seconds(0.05f) in ns (round mode)
     cfg = make_cfg(args.nodes, args.warmup + 2 * args.steps + 4, local, args.workload, args.replicas)

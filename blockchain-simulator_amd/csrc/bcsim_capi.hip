@@ -380,18 +380,11 @@ static int setup_device(Sim& s) {
   p.sparse = s.sparse ? 1u : 0u;
   p.n_heavy = s.N;
   p.cap_ops_light = p.cap_ops;
-  {
-    const size_t room = kLinkLdsTarget / 4 > s.deg_max + 1 + 1024 ? kLinkLdsTarget / 4 - (s.deg_max + 1) : 1024;
-    p.cap_eidx = static_cast<uint32_t>(std::min<size_t>(p.cap_ops, room));
-  }
-  if (link_lds_bytes(p) > 150 * 1024) {
-    g_detail = "node degree / op capacity exceed the LDS budget of k_link";
-    return BCSIM_E_UNSUPPORTED;
-  }
   s.bs_scan = static_cast<uint32_t>(std::min<uint64_t>(1024, std::max<uint64_t>(64, next_pow2(s.deg_max + 1))));
-  // k_link: two 512-lane workgroups per CU (LDS <= kLinkLdsTarget each) overlap one
-  // another's barrier phases; one 1024-lane group per CU was 15 % slower at N=4096
-  s.bs_link = std::min<uint32_t>(s.bs_scan, 512);
+  // k_link: several smaller workgroups per CU (LDS sized to fit, below) overlap one another's
+  // barrier phases: at N=4096 one 1024-lane group per CU was 15 % slower than two 512-lane
+  // ones, and four 256-lane ones are another 4 % faster
+  s.bs_link = std::min<uint32_t>(s.bs_scan, 256);
   // workgroup size caps (powers of two >= 64; tuning knobs, results do not depend on them)
   auto bs_cap = [](const char* name, uint32_t bs) {
     const char* v = std::getenv(name);
@@ -400,6 +393,15 @@ static int setup_device(Sim& s) {
   };
   s.bs_scan = bs_cap("BCSIM_BS_SCAN", s.bs_scan);
   s.bs_link = bs_cap("BCSIM_BS_LINK", s.bs_link);
+  {  // k_link dynamic LDS: as many workgroups per CU as 1024 lanes make (1024 / bs_link)
+    const size_t target = std::max<size_t>(16 * 1024, kLinkLdsTarget * s.bs_link / 512 - (s.bs_link < 512 ? 4096 : 0));
+    const size_t room = target / 4 > s.deg_max + 1 + 1024 ? target / 4 - (s.deg_max + 1) : 1024;
+    p.cap_eidx = static_cast<uint32_t>(std::min<size_t>(p.cap_ops, room));
+  }
+  if (link_lds_bytes(p) > 150 * 1024) {
+    g_detail = "node degree / op capacity exceed the LDS budget of k_link";
+    return BCSIM_E_UNSUPPORTED;
+  }
   // inbox ring: one 16-byte slot per (bucket, replica, edge); as many buckets
   // as ~8 GiB allows, 8..64
   // full mesh (blockchain-simulator.cc:34-51): records are staged sender-major
@@ -855,7 +857,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     rc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, lo, hi,
                 static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk);
     if (rc) return rc;
-    if (!s.sparse) {
+    if (!s.sparse && s.P == 1) {
       // dense layout: read the list lengths back and launch exactly one workgroup per entry
       // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
       // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
@@ -864,6 +866,11 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       HIPCHK(hipStreamSynchronize(s.stream));
       grid = dim3((s.act_h[0] + 7) / 8 * 8);
       n_link = s.act_h[1];
+    } else if (!s.sparse) {
+      // node-partitioned: a rank holds 1/P of the nodes, so a workgroup per local node costs
+      // less than the round trip (the cell already has several collectives)
+      grid = dim3((s.R * s.nloc + 7) / 8 * 8);
+      n_link = s.R * s.nloc;
     }
   }
 #define BCSIM_SCAN(P)                                                                                   \

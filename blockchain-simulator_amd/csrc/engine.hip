@@ -249,9 +249,12 @@ __device__ inline uint32_t xcd_map(uint32_t b, uint32_t n) {
 // does gnode g (node i of replica rep) have arrivals in bucket b?  (own flag, or its
 // receiver tile's flag in the full mesh)
 __device__ inline bool node_flagged(const KP& p, uint32_t b, uint32_t g, uint32_t rep, uint32_t i) {
-  if (AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT)) return true;
-  return p.mesh && AT(p.rtile, (static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6),
-                      static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles) != 0;
+  // both bytes are loaded together (no dependent second round trip)
+  const uint8_t f = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
+  const uint8_t t = p.mesh ? AT(p.rtile, (static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6),
+                                static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles)
+                           : 0;
+  return (f | t) != 0;
 }
 // set-once byte flag (many writers of the same byte: read first, store only if clear)
 __device__ inline void set_flag_once(uint8_t* f) {
@@ -1722,7 +1725,7 @@ __device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint3
 }
 
 template <int PROTO, bool SP>
-__device__ __attribute__((always_inline)) inline void scan_node(const KP* __restrict__ pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
+__device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
                           long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   // LDS: akey[cap] u64 | asec[cap] u32 | arec[cap] Rec | acls[cap] u32 | timers
@@ -1741,10 +1744,12 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* __rest
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
   const size_t fidx = static_cast<size_t>(b) * p.NT + g;
   const uint32_t rep = g / p.N, i = g % p.N;
+  // the node's row (full mesh: arithmetic, no load) and its flags, loads issued together
+  const uint32_t e0 = p.mesh ? i * (p.N - 1) : AT(p.row, i, p.N + 1);
+  const uint32_t deg = p.mesh ? p.N - 1 : AT(p.row, i + 1, p.N + 1) - e0;
   const bool flag = node_flagged(p, b, g, rep, i);
   if (!flag && AT(p.node_tnext, g, p.NT) >= t_hi && !has_start && !has_stop) return;
 
-  const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
   // sparse mode: no inbox slots, the node's arrivals are all in the cell's grouped lists
   const Rec* slots = SP ? nullptr : p.inbox + inbox_idx(p, b, rep, e0);
   const uint32_t deg_in = SP ? 0u : deg;
@@ -2092,7 +2097,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* __rest
 // a fixed grid over the window's active list (k_active); SP: sparse layout (no inbox slots)
 // LOOP: a small grid walks list 2, the nodes k_gossip_scan / k_paxos_scan left over
 template <int PROTO, bool SP, bool LOOP = false>
-__global__ __launch_bounds__(1024) void k_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
+__global__ __launch_bounds__(1024) void k_scan(const KP* pk, long long cell, long long t_lo,
                                                long long t_hi, long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   BAIL_IF_ERR();
