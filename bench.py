@@ -124,6 +124,57 @@ def cpu_baseline(n_nodes, budget_s, workload="pbft", tweak=None):
                        f"{wall:.1f} s wall)")
 
 
+def _oracle_slice(cfg_fields, budget_s):
+    """One worker of the all-cores baseline: a single-replica oracle run of budget_s CPU."""
+    sys.path[:0] = [REPO, os.path.join(REPO, "blockchain-simulator_amd")]
+    import oracle
+    from bcsim import _abi
+    cfg = _abi.Config()
+    for k, v in cfg_fields.items():
+        if k == "reserved":
+            for i, x in enumerate(v):
+                cfg.reserved[i] = x
+        else:
+            setattr(cfg, k, v)
+    o = oracle.OracleSim(cfg)
+    t0 = time.process_time()
+    t = 0
+    while time.process_time() - t0 < budget_s:
+        t += 1_000_000
+        o.run(t)
+        if o.status()["quiescent"]:
+            break
+    n = o.counters()["delivered_total"]
+    o.close()
+    return n, time.process_time() - t0
+
+
+def cpu_baseline_all_cores(n_nodes, budget_s, workload, tweak, cores):
+    """Monte Carlo replicas are independent (all-cores figure for the replica
+    config): `cores` oracle processes, one replica each (different seeds), run side by side;
+    value = their summed deliveries / the wall time."""
+    import multiprocessing as mp
+    from bcsim import _abi
+    cfg = make_cfg(n_nodes, 100, 0, workload)
+    if tweak:
+        tweak(cfg)
+    jobs = []
+    for k in range(cores):
+        d = _abi.config_dict(cfg)
+        d["seed"] = cfg.seed + k
+        jobs.append(d)
+    w0 = time.time()
+    with mp.get_context("spawn").Pool(cores) as pool:
+        res = pool.starmap(_oracle_slice, [(d, budget_s) for d in jobs])
+    wall = time.time() - w0
+    msgs = sum(r[0] for r in res)
+    model, nproc = host_cpu()
+    return dict(value=msgs / wall, unit="msgs/s", cores=cores, kind="port", cpu_model=model, nproc=nproc,
+                sample=f"{cores} oracle processes side by side, one {workload} n={n_nodes} replica each (seeds "
+                       f"differ), {budget_s:.0f} s CPU each ({msgs} msgs in {wall:.1f} s wall, process start "
+                       f"included)")
+
+
 def aggregate(dist, device, dt, msgs, trace_delta):
     """Whole-job numbers over ranks: max wall time, summed work (the per-rank
     deliveries of a partitioned run, or of independent replicas)."""
@@ -325,6 +376,9 @@ def main():
                     if args.workload == "paxos":
                         c.paxos_decrees = args.decrees
                 out["cpu_baseline"] = cpu_baseline(args.nodes, args.cpu_budget, args.workload, tweak)
+                if args.workload == "paxos":  # replicas: the all-cores figure too (16 = the box's CPU share)
+                    out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(
+                        args.nodes, args.cpu_budget, args.workload, tweak, min(16, os.cpu_count() or 1))
             except Exception as e:  # never let the baseline leg kill the GPU number
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)
