@@ -1184,8 +1184,22 @@ __device__ void paxos_recv(Ctx& c, PaxosState& s, const Msg& m, uint32_t back_ed
 // twice at the same instant).  The common full-mesh case (all arrivals of a
 // phase at one instant) is already sorted and skips the LDS bitonic sort.
 constexpr int kScanMaxArr = 4096;  // LDS staging window (28 B per arrival)
-constexpr int kRidxBits = 12;
-constexpr uint32_t kRidxMask = (1u << kRidxBits) - 1u;
+// staged arrival id (asec): in-slot << kSlotShift | (extras record ? kXBit | index in the node's
+// extras segment : 0).  The records themselves are not copied to LDS: a main-slot record is
+// read from the node's inbox row (L2-resident after the stage), an extras record from the
+// grouped list, so a staged arrival costs 16 B of LDS (key, id, class) and two 512-lane
+// workgroups fit a CU at N=4096.
+constexpr int kSlotShift = 14;
+constexpr uint32_t kXBit = 1u << 13;
+constexpr uint32_t kXIdx = kXBit - 1u;
+struct RecSrc {
+  const Rec* slots;  // the node's inbox row (nullptr in the sparse layout)
+  const XRec* xs;    // the node's extras of the cell
+};
+__device__ inline Rec rec_of(const RecSrc& rs, uint32_t sec) {
+  return (sec & kXBit) ? rs.xs[sec & kXIdx].r : ld_rec(rs.slots + (sec >> kSlotShift));
+}
+__device__ inline bool is_main(uint32_t sec) { return (sec & kXBit) == 0; }
 constexpr int kQuorumTab = 256;    // distinct (phase, sequence) pairs per window
 
 // PBFT class word per staged arrival (acls): bits 30-31 class, 29 crossing, 0-28 index
@@ -1229,7 +1243,7 @@ __device__ inline uint64_t arr_key(const KP& p, const Rec& r, uint32_t q) {
 // then extras.  Returns the total count (entries beyond cap are not stored).
 __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, uint32_t e0, uint32_t deg,
                                  const XRec* xs, uint32_t xn, long long cs, long long wa, long long wb,
-                                 uint64_t* akey, uint32_t* asec, Rec* arec, bool store) {
+                                 uint64_t* akey, uint32_t* asec, bool store) {
   const uint32_t tid = threadIdx.x;
   uint32_t n = 0;
   for (uint32_t base = 0; base < deg; base += 4 * blockDim.x) {
@@ -1254,8 +1268,7 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
     for (uint32_t j = 0; j < 4; ++j) {
       const uint32_t k = base + j * blockDim.x + tid, pos = pos4[j];
       if (store && vv[j] && pos < p.cap_arr) {
-        arec[pos] = rr[j];
-        asec[pos] = (k << kRidxBits) | pos;
+        asec[pos] = k << kSlotShift;
         akey[pos] = arr_key(p, rr[j], e0 + k);
       }
     }
@@ -1274,8 +1287,7 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
     uint32_t tot;
     const uint32_t pos = n + block_rank(v, S.wcnt, tot);
     if (store && v && pos < p.cap_arr) {
-      arec[pos] = x.r;
-      asec[pos] = ((x.slot - e0) << kRidxBits) | pos;
+      asec[pos] = ((x.slot - e0) << kSlotShift) | kXBit | k;
       akey[pos] = arr_key(p, x.r, x.slot);
     }
     n += tot;
@@ -1353,7 +1365,7 @@ __device__ inline uint32_t quorum_slot(const KP& p, ScanShared& S, uint32_t key,
 // window 64 arrivals at a time, grouping lanes by ballot.
 __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep, uint32_t i, uint32_t e0,
                             uint32_t deg, uint32_t n, uint32_t n_main, long long cell, long long cs, long long t_lo,
-                            const uint64_t* akey, const uint32_t* asec, const Rec* arec, uint32_t* acls) {
+                            const uint64_t* akey, const uint32_t* asec, const RecSrc rs, uint32_t* acls) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const size_t base = static_cast<size_t>(g) * p.pbft_seq_cap;
   const int32_t N = static_cast<int32_t>(p.N);
@@ -1367,7 +1379,7 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
   }
   __syncthreads();
   for (uint32_t r = tid; r < n; r += blockDim.x) {
-    const Rec rec = arec[asec[r] & kRidxMask];
+    const Rec rec = rec_of(rs, asec[r]);
     const Msg m = rec_msg(rec);
     uint32_t w = 0;
     switch (rec.type) {
@@ -1484,10 +1496,10 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
 #pragma nounroll
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
-    const Rec rec = arec[sec & kRidxMask];
+    const Rec rec = rec_of(rs, sec);
     const uint32_t w = acls[r];
     const bool cross = (w & kCross) != 0;
-    const bool main_rec = (sec & kRidxMask) < n_main;
+    const bool main_rec = is_main(sec);
     const bool main_slot = slots && main_rec;
     uint32_t si = 0, di = 0, ci = 0, oi = (p.impl && main_rec) ? 0u : ech;
     if (rec.type == PB_PRE_PREPARE) {
@@ -1533,8 +1545,8 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
 #pragma nounroll
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
-    const Rec rec = arec[sec & kRidxMask];
-    const uint32_t q = e0 + (sec >> kRidxBits);  // in-slot = reverse (reply) edge
+    const Rec rec = rec_of(rs, sec);
+    const uint32_t q = e0 + (sec >> kSlotShift);  // in-slot = reverse (reply) edge
     const uint32_t w = acls[r];
     const bool cross = (w & kCross) != 0;
     const Msg m = rec_msg(rec);
@@ -1546,7 +1558,7 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
     if (t == ((t / p.pbft_period) * p.pbft_period) && key.ts <= t - p.pbft_period)
       set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
     // pbft-node.cc:175 echo: implicit for main-slot records (k_link), listed otherwise
-    if (ech && !(p.impl && (sec & kRidxMask) < n_main)) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);
+    if (ech && !(p.impl && is_main(sec))) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);
     switch (rec.type) {
       case PB_PRE_PREPARE: {  // :193-211
         const Msg rr = mkmsg(PB_PREPARE, mch(m, 1), mch(m, 2), mch(m, 3), 0);
@@ -1621,7 +1633,7 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
   for (uint32_t j = 0; j < per; ++j) {
     const uint32_t r = r0 + j;
     const bool act = r < r1;
-    const uint32_t ty = act ? arec[asec[r] & kRidxMask].type : 0u;
+    const uint32_t ty = act ? rec_of(rs, asec[r]).type : 0u;
     wave_add_by_key(act && ty < BCSIM_MSG_TYPES, ty, 1u, S.deliv);
   }
   if (wrong) atomicAdd(&S.wrong, wrong);
@@ -1698,18 +1710,18 @@ __device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender, bool first, u
 // earlier arrival of this window carries the same sequence -- writes the flag to acls[r], and
 // the first receipts are marked seen.  The lane-0 event loop then reads the flags from LDS.
 __device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint32_t n, const uint32_t* asec,
-                                   const Rec* arec, uint32_t* acls) {
+                                   const RecSrc rs, uint32_t* acls) {
   const uint32_t tid = threadIdx.x;
   if (tid == 0) S.tr_n = 0;
   __syncthreads();
   for (uint32_t r = tid; r < n; r += blockDim.x) {
-    const Rec& rc = arec[asec[r] & kRidxMask];
+    const Rec rc = rec_of(rs, asec[r]);
     const int32_t seq = rc.f0;
     bool first = rc.type == GS_BLOCK && seq >= 0 && static_cast<uint32_t>(seq) < p.pbft_seq_cap &&
                  AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + seq,
                     static_cast<uint64_t>(p.NT) * p.pbft_seq_cap) == 0;
     for (uint32_t r2 = 0; first && r2 < r; ++r2) {
-      const Rec& o = arec[asec[r2] & kRidxMask];
+      const Rec o = rec_of(rs, asec[r2]);
       if (o.type == GS_BLOCK && o.f0 == seq) first = false;
     }
     acls[r] = first ? 1u : 0u;
@@ -1720,7 +1732,7 @@ __device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint3
   if (tid == 0) S.tr_pos = S.tr_n ? atomicAdd(p.trace_cnt, S.tr_n) : 0u;
   for (uint32_t r = tid; r < n; r += blockDim.x)
     if (acls[r])
-      AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + arec[asec[r] & kRidxMask].f0,
+      AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + rec_of(rs, asec[r]).f0,
          static_cast<uint64_t>(p.NT) * p.pbft_seq_cap) = 1;
 }
 
@@ -1728,14 +1740,13 @@ template <int PROTO, bool SP>
 __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
                           long long cs, int final_win, int x_active) {
   const KP& p = *pk;
-  // LDS: akey[cap] u64 | asec[cap] u32 | arec[cap] Rec | acls[cap] u32 | timers
+  // LDS: akey[cap] u64 | asec[cap] u32 | acls[cap] u32 | timers
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ ScanShared S;
   const uint32_t cap = p.cap_arr;
   uint64_t* akey = reinterpret_cast<uint64_t*>(smem);
   uint32_t* asec = reinterpret_cast<uint32_t*>(akey + cap);
-  Rec* arec = reinterpret_cast<Rec*>(asec + cap);
-  uint32_t* acls = reinterpret_cast<uint32_t*>(arec + cap);
+  uint32_t* acls = asec + cap;
   TimerEnt* tm = reinterpret_cast<TimerEnt*>(acls + cap);
 
   const uint32_t tid = threadIdx.x;
@@ -1759,6 +1770,10 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
     const uint32_t xb = AT(p.seg_off, g, p.NT + 1);
     xn = AT(p.seg_off, g + 1, p.NT + 1) - xb;
     xs = p.xgrp + xb;
+    if (xn > kXIdx + 1) {  // staged ids index at most 8192 extras records per node and cell
+      if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
+      return;
+    }
   }
   if (PROTO != BCSIM_PBFT && tid < p.cap_timers)
     tm[tid] = AT(p.timers, static_cast<size_t>(g) * p.cap_timers + tid, static_cast<uint64_t>(p.NT) * p.cap_timers);
@@ -1832,12 +1847,12 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
   long long wa = t_lo;
   for (;;) {
     long long wb = t_hi;
-    uint32_t n = flag ? stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, wb, akey, asec, arec, true) : 0u;
+    uint32_t n = flag ? stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, wb, akey, asec, true) : 0u;
     if (n > cap) {  // more than cap arrivals: shrink the window (rare)
       long long lo = wa, hi = t_hi;  // count(lo) <= cap < count(hi)
       while (hi - lo > 1) {
         const long long mid = lo + (hi - lo) / 2;
-        if (stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, mid, akey, asec, arec, false) <= cap)
+        if (stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, mid, akey, asec, false) <= cap)
           lo = mid;
         else
           hi = mid;
@@ -1847,16 +1862,17 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
         if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
         return;
       }
-      n = stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, wb, akey, asec, arec, true);
+      n = stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, wb, akey, asec, true);
     }
     const uint32_t n_main = S.n_main;
     SPH(1);
     sort_window(S, n, akey, asec);
     SPH(2);
 
-    if (PROTO == BCSIM_GOSSIP) gossip_first_flags(p, S, g, n, asec, arec, acls);
+    const RecSrc rsrc{slots, xs};
+    if (PROTO == BCSIM_GOSSIP) gossip_first_flags(p, S, g, n, asec, rsrc, acls);
     if (PROTO == BCSIM_PBFT) {
-      pbft_window(p, S, g, rep, i, e0, deg, n, n_main, cell, cs, t_lo, akey, asec, arec, acls);
+      pbft_window(p, S, g, rep, i, e0, deg, n, n_main, cell, cs, t_lo, akey, asec, rsrc, acls);
       events += (tid == 0) ? n : 0;
     } else if (tid == 0) {
       c.sub = S.sub;
@@ -1871,8 +1887,8 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
         int tsel = -1;
         if (ai < n) {
           const uint32_t sec = asec[ai];
-          rec = arec[sec & kRidxMask];
-          q = e0 + (sec >> kRidxBits);
+          rec = rec_of(rsrc, sec);
+          q = e0 + (sec >> kSlotShift);
           const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
           best.t = cs + rec.t_off;
           best.ts = best.t - dt;
@@ -1923,7 +1939,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
           if (p.echo) {  // socket->SendTo(packet, 0, from): reverse-link occupancy
             const Op eo = mk_op(p, best.t, static_cast<uint32_t>(best.t - best.ts), best.origin, rec.sub, q, msg,
                                 OP_ECHO, 0);
-            if (!(p.impl && (asec[ai - 1] & kRidxMask) < n_main)) ctx_op(c, eo);  // else implicit (k_link)
+            if (!(p.impl && is_main(asec[ai - 1]))) ctx_op(c, eo);  // else implicit (k_link)
             ++c.echoes;
           }
           if (PROTO == BCSIM_RAFT)
@@ -2003,7 +2019,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
     // consumed slots are free again
     for (uint32_t r = tid; r < n; r += blockDim.x) {
       const uint32_t sec = asec[r];
-      if (!p.impl && (sec & kRidxMask) < n_main) clr_rec(const_cast<Rec*>(slots) + (sec >> kRidxBits));
+      if (!p.impl && is_main(sec)) clr_rec(const_cast<Rec*>(slots) + (sec >> kSlotShift));
     }
     __syncthreads();
     if (wb >= t_hi) break;
