@@ -168,11 +168,12 @@ def cpu_baseline_all_cores(n_nodes, budget_s, workload, tweak, cores):
         res = pool.starmap(_oracle_slice, [(d, budget_s) for d in jobs])
     wall = time.time() - w0
     msgs = sum(r[0] for r in res)
+    cpu = sum(r[1] for r in res)
     model, nproc = host_cpu()
     return dict(value=msgs / wall, unit="msgs/s", cores=cores, kind="port", cpu_model=model, nproc=nproc,
                 sample=f"{cores} oracle processes side by side, one {workload} n={n_nodes} replica each (seeds "
-                       f"differ), {budget_s:.0f} s CPU each ({msgs} msgs in {wall:.1f} s wall, process start "
-                       f"included)")
+                       f"differ), each until {budget_s:.0f} s CPU or the end of its run ({msgs} msgs, {cpu:.1f} s CPU "
+                       f"in total, {wall:.1f} s wall incl. process start)")
 
 
 def aggregate(dist, device, dt, msgs, trace_delta):
@@ -313,7 +314,8 @@ def main():
         # roofline of the scatter (k_link): SURVEY.md §8(d) algorithmic bytes = 48 B per record
         # emitted by the timed k_link launches, over their HIP-event time on the engine stream
         ach = (lk["bytes"] / 1e9) / (lk["us"] / 1e6) if lk["us"] > 0 else 0.0
-        traffic = pmc_traffic(args.nodes, workload=args.workload)
+        # PMC traffic of this workload's committed profile (none for the jittered variant)
+        traffic = None if args.jitter else pmc_traffic(args.nodes, workload=args.workload)
         all_us = sum(v["us"] for v in ks_all.values())
         if args.workload == "pbft":
             data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, %s)" % (
