@@ -288,6 +288,10 @@ static int setup_device(Sim& s) {
   p.stop_ns = c.stop_ns;
   p.pbft_rounds = c.pbft_rounds;
   p.pbft_seq_cap = c.pbft_seq_cap ? c.pbft_seq_cap : 1000;
+  if (p.pbft_seq_cap >= (1u << 21)) {  // k_scan's class word holds the sequence index in 21 bits
+    g_detail = "pbft_seq_cap must be < 2^21";
+    return BCSIM_E_INVAL;
+  }
   p.pbft_view_change = c.pbft_view_change;
   p.raft_blocks = c.raft_blocks;
   p.raft_prop_rounds = c.raft_proposal_rounds;

@@ -1203,8 +1203,13 @@ __device__ inline bool is_main(uint32_t sec) { return (sec & kXBit) == 0; }
 constexpr int kQuorumTab = 256;    // distinct (phase, sequence) pairs per window
 
 // PBFT class word per staged arrival (acls): bits 30-31 class, 29 crossing, 0-28 index
+// PBFT class word per staged arrival (acls): bits 30-31 class, 29 crossing, 21-28 message type
+// (phases C and D and the delivery counts read it instead of the record), 0-20 sequence index
 constexpr uint32_t kClsPres = 1u << 30, kClsCommit = 2u << 30, kCross = 1u << 29;
-constexpr uint32_t kIdxMask = kCross - 1u;
+constexpr int kTypeShift = 21;
+constexpr uint32_t kTypeMask = 0xFFu << kTypeShift;
+constexpr uint32_t kIdxMask = (1u << kTypeShift) - 1u;
+__device__ inline uint32_t cls_type(uint32_t w) { return (w & kTypeMask) >> kTypeShift; }
 
 struct ScanShared {
   uint32_t wcnt[kMaxWaves];
@@ -1413,7 +1418,7 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
       default:
         break;
     }
-    acls[r] = w;
+    acls[r] = w | (static_cast<uint32_t>(rec.type) << kTypeShift);
   }
   __syncthreads();
   SPH(3);
@@ -1431,7 +1436,7 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
     for (int pass = 0; pass < 2; ++pass) {
       for (uint32_t b0 = rb; b0 < re; b0 += 64) {  // wave-uniform bounds
         const uint32_t r = b0 + lane;
-        const uint32_t w = r < re ? acls[r] : 0u;
+        const uint32_t w = r < re ? (acls[r] & ~kTypeMask) : 0u;  // (phase, sequence) key
         unsigned long long rem = __ballot(w != 0);
         while (rem) {
           const int ld = __ffsll(static_cast<long long>(rem)) - 1;
@@ -1449,7 +1454,7 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
             if (mine) {
               const uint32_t v = cnt + static_cast<uint32_t>(__popcll(same & ((1ull << lane) - 1ull))) + 1u;
               const bool cross = (w >> 30) == 1u ? (v % T1 == 0) : (v % T2 == 0);
-              if (cross) acls[r] = w | kCross;
+              if (cross) acls[r] |= kCross;
             }
           }
           rem &= ~same;
@@ -1496,17 +1501,17 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
 #pragma nounroll
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
-    const Rec rec = rec_of(rs, sec);
     const uint32_t w = acls[r];
+    const uint32_t type = cls_type(w);
     const bool cross = (w & kCross) != 0;
     const bool main_rec = is_main(sec);
     const bool main_slot = slots && main_rec;
     uint32_t si = 0, di = 0, ci = 0, oi = (p.impl && main_rec) ? 0u : ech;
-    if (rec.type == PB_PRE_PREPARE) {
+    if (type == PB_PRE_PREPARE) {
       si = deg;
       di = fixed ? 0u : deg;
       oi += 1;
-    } else if (rec.type == PB_PREPARE) {
+    } else if (type == PB_PREPARE) {
       si = 1;
       di = fixed ? 0u : 1u;
       // the reply of a main-slot arrival owns its edge's slot of this arrival cell
@@ -1514,11 +1519,11 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
         rslot |= 1u << (r - r0);
       else
         oi += 1;
-    } else if (rec.type == PB_PREPARE_RES && cross) {
+    } else if (type == PB_PREPARE_RES && cross) {
       si = deg;
       di = fixed ? 0u : deg;
       oi += 1;
-    } else if (rec.type == PB_COMMIT && cross) {
+    } else if (type == PB_COMMIT && cross) {
       ci = 1;
     }
     loc.x += si;
@@ -1633,7 +1638,7 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
   for (uint32_t j = 0; j < per; ++j) {
     const uint32_t r = r0 + j;
     const bool act = r < r1;
-    const uint32_t ty = act ? rec_of(rs, asec[r]).type : 0u;
+    const uint32_t ty = act ? cls_type(acls[r]) : 0u;
     wave_add_by_key(act && ty < BCSIM_MSG_TYPES, ty, 1u, S.deliv);
   }
   if (wrong) atomicAdd(&S.wrong, wrong);
