@@ -1550,21 +1550,29 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
 #pragma nounroll
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
-    const Rec rec = rec_of(rs, sec);
     const uint32_t q = e0 + (sec >> kSlotShift);  // in-slot = reverse (reply) edge
     const uint32_t w = acls[r];
+    const uint32_t type = cls_type(w);
     const bool cross = (w & kCross) != 0;
+    // t and dt from the staged key; the record is read only by arrivals that produce output
+    // (the PREPARE_RES / COMMIT waves are almost all non-crossing: nothing to read)
+    const uint64_t kk = akey[r];
+    const int64_t t = cs + static_cast<int64_t>(kk >> 32);
+    const uint32_t dt = ~static_cast<uint32_t>(kk);
+    const bool lecho = ech && !(p.impl && is_main(sec));
+    const bool need = lecho || type == PB_PRE_PREPARE || type == PB_PREPARE || type == PB_VIEW_CHANGE ||
+                      (cross && (type == PB_PREPARE_RES || type == PB_COMMIT));
+    Rec rec{};
+    if (need) rec = rec_of(rs, sec);
     const Msg m = rec_msg(rec);
-    const int64_t t = cs + rec.t_off;
-    const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[m.big]);
     const uint32_t le = q - e0;
     const uint32_t origin = p.mesh ? (le < i ? le : le + 1) : AT(p.col, q, p.E);
     const Key key{t, t - static_cast<int64_t>(dt), origin, rec.sub};
     if (t == ((t / p.pbft_period) * p.pbft_period) && key.ts <= t - p.pbft_period)
       set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
     // pbft-node.cc:175 echo: implicit for main-slot records (k_link), listed otherwise
-    if (ech && !(p.impl && is_main(sec))) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);
-    switch (rec.type) {
+    if (lecho) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);
+    switch (type) {
       case PB_PRE_PREPARE: {  // :193-211
         const Msg rr = mkmsg(PB_PREPARE, mch(m, 1), mch(m, 2), mch(m, 3), 0);
         ops[op++] = fixed ? mk_op(p, t + p.app_delay, static_cast<uint32_t>(p.app_delay), i, sp, 0, rr, OP_BCAST, 0)
