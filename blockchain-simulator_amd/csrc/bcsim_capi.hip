@@ -32,7 +32,7 @@ struct Ctl {
   int32_t err;
   uint32_t trace_cnt, vlog_cnt, dreq_cnt, ov_cnt;
   int32_t dbg;
-  long long scal[4];  // next_local, ov_min_cell, n_alive_ticks, spare
+  long long scal[4];  // next_local, ov_min_cell, n_alive_ticks, next timer
   // followed by bucket_cnt[B] and x_cnt[B]
 };
 
@@ -69,6 +69,7 @@ struct Sim {
   uint32_t grid_scan = 0, grid_link = 0;  // k_scan / k_link workgroups (walking the active lists)
   uint32_t gossip_g = 0;  // dense gossip: lanes per node of k_gossip_scan (0 = generic k_scan only)
   bool gossip_link = false;
+  long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
   uint32_t* seg_part = nullptr;  // multi-block segment scan partials
   long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
@@ -684,7 +685,7 @@ static int setup_device(Sim& s) {
   p.dreq_cnt = &cd->dreq_cnt;
   p.ov_cnt = &cd->ov_cnt;
   p.scal = cd->scal;
-  if ((rc = dalloc(s, &p.nxt_part, kNextBlocks)) || (rc = dalloc(s, &p.nxt_done, 1))) return rc;
+  if ((rc = dalloc(s, &p.nxt_part, 2 * kNextBlocks)) || (rc = dalloc(s, &p.nxt_done, 1))) return rc;
   HIPCHK(hipMemset(p.nxt_done, 0, 4));
   p.bucket_cnt = reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl));
   p.x_cnt = p.bucket_cnt + s.B;
@@ -844,16 +845,21 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   if (s.gossip_link && s.kp.dbg_tmax <= lo) {
     const uint32_t per_wg = 256 / s.gossip_g;
     const dim3 gg(static_cast<uint32_t>((static_cast<uint64_t>(s.R) * s.nloc + per_wg - 1) / per_wg));
-    if ((rc = launch(s, KS_SCAN, k_gossip_scan, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g)) ||
-        (rc = launch(s, KS_SCAN, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), block, lds, s.kp_dev, cell, lo, hi, cs,
-                     fw, xa)))
+    // the generic kernel only has work with a timer, START/STOP or extras in the window
+    const int loop = lo <= 0 || xa || s.next_timer < hi || (s.cfg.stop_ns >= 0 && s.cfg.stop_ns < hi);
+    if ((rc = launch(s, KS_SCAN, k_gossip_scan, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g, loop)) ||
+        (loop &&
+         (rc = launch(s, KS_SCAN, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), block, lds, s.kp_dev, cell, lo, hi,
+                      cs, fw, xa))))
       return rc;
     // the link stage (both kernels) as ONE timed launch of the k_link class
     const bool timed = (kstat_mask() >> KS_LINK) & 1u;
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
     if ((rc = launch(s, -1, k_gossip_link, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, s.gossip_g)) ||
-        (rc = launch(s, -1, (k_link<false, false, true>), dim3(256), dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev,
-                     cell, lo, hi, fw)))
+        // (the looped grid may not exceed the workgroups the per-workgroup staging areas
+        // were allocated for: xstage / xmeta hold grid_link of them)
+        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(256, s.grid_link)), dim3(s.bs_link),
+                     link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
       return rc;
     if (timed) return ev_end(s);
     s.launches[KS_LINK]++;
@@ -868,7 +874,11 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     rc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, lo, hi,
                 static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk);
     if (rc) return rc;
-    if (!s.sparse && s.P == 1) {
+    static const bool no_sync = [] {
+      const char* e = std::getenv("BCSIM_NO_ACTSYNC");
+      return e && *e == '1';
+    }();
+    if (!s.sparse && s.P == 1 && !no_sync) {
       // dense layout: read the list lengths back and launch exactly one workgroup per entry
       // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
       // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
@@ -1065,6 +1075,7 @@ static int readback(Sim& s) {
     s.xcnt[k] = s.xcnt_h[k];
   }
   s.next_local = s.ctl_h->scal[0];
+  s.next_timer = s.ctl_h->scal[3];
   s.ov_min = s.ctl_h->scal[1];
   if (s.ctl_h->err) {
     g_detail = std::string(bcsim_strerror(s.ctl_h->err)) + " raised at engine.hip:" + std::to_string(s.ctl_h->dbg) +

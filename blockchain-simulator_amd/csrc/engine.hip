@@ -2290,7 +2290,8 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
 // The kernel walks all of this rank's gnodes (no k_active): a node with work in the window
 // (k_active's rule) that is not simple is appended to list 2 for k_scan<.., LOOP>.
 __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                     long long t_hi, long long cs, int x_active, uint32_t G) {
+                                                     long long t_hi, long long cs, int x_active, uint32_t G,
+                                                     int loop) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ uint32_t s_deliv[BCSIM_MSG_TYPES];
@@ -2322,6 +2323,9 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
   bool fast = have && deg <= G && !has_start && !has_stop && !tdue;
   if (fast && x_active) fast = AT(p.seg_off, g + 1, p.NT + 1) == AT(p.seg_off, g, p.NT + 1);
   if (have && !fast && j == 0) {
+    // (loop == 0: the host skips k_scan<.., LOOP> -- no timer, START, STOP or extras can be
+    // due in the window -- so no node may be left over)
+    if (!loop) set_err(p, BCSIM_E_TIE);
     const uint32_t pos = atomicAdd(&p.act_n[2], 1u);
     AT(p.act, 2ull * p.NT + pos, 3ull * p.NT) = g;
   }
@@ -2389,12 +2393,19 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
     }
   }
   if (first) li = atomicAdd(&s_nf, 1u);
+  // node state: sub (+deg per broadcast), draws (jitter), pending ops -- read by every lane
+  // of the group before the barrier, written by lane 0 after it
+  uint32_t sub0 = 0, nops0 = 0;
+  uint64_t draws0 = 0;
+  if (nf) {
+    sub0 = AT(p.sub, g, p.NT);
+    nops0 = AT(p.n_ops, g, p.NT);
+    draws0 = AT(p.draws, g, p.NT);
+  }
   __syncthreads();
   if (tid == 0) s_trbase = s_nf ? atomicAdd(p.trace_cnt, s_nf) : 0u;
   __syncthreads();
-  if (nf) {  // node state: sub (+deg per broadcast), draws (jitter), pending ops
-    const uint32_t sub0 = AT(p.sub, g, p.NT), nops0 = AT(p.n_ops, g, p.NT);
-    const uint64_t draws0 = AT(p.draws, g, p.NT);
+  if (nf) {
     const uint32_t ocap = op_cap(p, g);
     if (nops0 + nf > ocap) {
       if (j == 0) set_err(p, BCSIM_E_OVERFLOW);
@@ -2752,12 +2763,19 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     // ROCm 7.2 (a record took f0 from a broadcast and the rest from a listed op; the Raft
     // N>=300 parity gap).  Integer word selects are what the compiler sees.
     // implicit echo: this node's main inbox record of in-slot le, delivered in
-    // [t_lo, t_hi), goes back out on out-edge le (the same peer); release the slot
+    // [t_lo, t_hi), goes back out on out-edge le (the same peer); release the slot.
+    // All of the edge's loads (link word above, inbox record, reply slots) are issued before
+    // the slot release: a load after that store could not be moved above it (possible
+    // alias) and would cost a second memory round trip per edge.
+    Rec* ir = const_cast<Rec*>(in_row) + le;
+    Rec r0{};
+    if (rx) r0 = ld_rec(ir);
+    uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
+    if (sl0) w0 = *eslot_at(p, ob, rep, e);
+    if (sl1) w1 = *eslot_at(p, obp, rep, e);
     bool he = false;
     RawOp eo = raw_zero();
     if (rx) {
-      Rec* ir = const_cast<Rec*>(in_row) + le;
-      const Rec r0 = ld_rec(ir);
       const long long ta0 = cs + r0.t_off;
       if ((r0.flags & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
         clr_rec(ir);
@@ -2775,12 +2793,12 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     bool hr = false, hr2 = false;
     RawOp ro = raw_zero(), ro2 = raw_zero();
     if (sl0) {
-      ro = slot_op(p, *eslot_at(p, ob, rep, e), i, e);
+      ro = slot_op(p, w0, i, e);
       hr = raw_t(ro) >= t_lo && raw_t(ro) < t_hi;
       if (hr) ++st_ops;
     }
     if (sl1) {
-      ro2 = slot_op(p, *eslot_at(p, obp, rep, e), i, e);
+      ro2 = slot_op(p, w1, i, e);
       hr2 = raw_t(ro2) >= t_lo && raw_t(ro2) < t_hi;
       if (hr2) ++st_ops;
     }
@@ -4248,32 +4266,43 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
           p.rtile[static_cast<size_t>(clr_b) * p.R * p.n_tiles + k] = 0;
     }
   }
-  __shared__ long long red[1024];
-  long long m = LLONG_MAX;
+  // scal[0] = the next event time (timers and pending ops), scal[3] = the next timer alone
+  __shared__ long long red[1024], redt[1024];
+  long long m = LLONG_MAX, mt = LLONG_MAX;
   const uint32_t nb = gridDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < p.NT; k += nb * blockDim.x) {
     const long long a = AT(p.node_tnext, k, p.NT), b = AT(p.node_onext, k, p.NT);
     m = min(m, min(a, b));
+    mt = min(mt, a);
   }
   red[threadIdx.x] = m;
+  redt[threadIdx.x] = mt;
   __syncthreads();
   for (uint32_t s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] = min(red[threadIdx.x], red[threadIdx.x + s]);
+    if (threadIdx.x < s) {
+      red[threadIdx.x] = min(red[threadIdx.x], red[threadIdx.x + s]);
+      redt[threadIdx.x] = min(redt[threadIdx.x], redt[threadIdx.x + s]);
+    }
     __syncthreads();
   }
   if (threadIdx.x != 0) return;
   if (nb == 1) {
     p.scal[0] = red[0];
+    p.scal[3] = redt[0];
     return;
   }
   __hip_atomic_store(&p.nxt_part[blockIdx.x], red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&p.nxt_part[kNextBlocks + blockIdx.x], redt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __threadfence();
   if (atomicAdd(p.nxt_done, 1u) != nb - 1) return;
   __threadfence();
-  long long mm = LLONG_MAX;
-  for (uint32_t b = 0; b < nb; ++b)
+  long long mm = LLONG_MAX, mmt = LLONG_MAX;
+  for (uint32_t b = 0; b < nb; ++b) {
     mm = min(mm, __hip_atomic_load(&p.nxt_part[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    mmt = min(mmt, __hip_atomic_load(&p.nxt_part[kNextBlocks + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
   p.scal[0] = mm;
+  p.scal[3] = mmt;
   __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
