@@ -69,6 +69,7 @@ struct Sim {
   uint32_t grid_scan = 0, grid_link = 0;  // k_scan / k_link workgroups (walking the active lists)
   uint32_t gossip_g = 0;  // dense gossip: lanes per node of k_gossip_scan (0 = generic k_scan only)
   bool gossip_link = false;
+  bool mesh_link = false;  // full mesh, fixed delay: k_link_mesh first, k_link over list 3
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
   uint32_t* seg_part = nullptr;  // multi-block segment scan partials
@@ -618,6 +619,13 @@ static int setup_device(Sim& s) {
     }
     s.gossip_link = s.gossip_g && !p.mesh && s.P == 1 && c.delay_mode == BCSIM_DELAY_FIXED &&
                     c.queue_model == BCSIM_QUEUE_INFINITE;
+    // full mesh, fixed app delay: k_link_mesh takes the nodes whose due ops are all broadcasts
+    // (BCSIM_NO_MFAST=1: off)
+    {
+      const char* mf = std::getenv("BCSIM_NO_MFAST");
+      s.mesh_link = p.mesh && !s.sparse && s.P == 1 && c.delay_mode == BCSIM_DELAY_FIXED &&
+                    c.queue_model == BCSIM_QUEUE_INFINITE && !(mf && *mf == '1');
+    }
     // PBFT replies with a fixed app delay < L (due in the arrival cell or the next)
     const bool on = ne * 16 <= (16ull << 30) && !off && !s.sparse && c.protocol == BCSIM_PBFT &&
                     c.delay_mode == BCSIM_DELAY_FIXED && c.app_delay_ns < s.L;
@@ -962,7 +970,22 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     }
   } else if (s.sparse)
     rc = launch(s, KS_LINK, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw, 1);
-  else {
+  else if (s.mesh_link) {
+    // full mesh, fixed app delay: the lean kernel takes the nodes whose due ops are all
+    // broadcasts, the generic kernel (a small looped grid) the rest (list 3); timed as ONE
+    // launch of the k_link class
+    const bool timed = (kstat_mask() >> KS_LINK) & 1u;
+    if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
+    if ((rc = launch(s, -1, k_link_mesh, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
+        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(256, s.grid_link)), dim3(s.bs_link),
+                     link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
+      return rc;
+    if (timed) {
+      if ((rc = ev_end(s))) return rc;
+    } else {
+      s.launches[KS_LINK]++;
+    }
+  } else {
     const size_t ll = link_lds_bytes(s.kp);
     const bool qm = s.kp.qmodel != 0, xr = s.kp.nranks > 1;
     rc = qm ? (xr ? launch(s, KS_LINK, k_link<true, true>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw)

@@ -801,13 +801,8 @@ __global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   AT(p.xgrp, pos, p.cap_x) = x;
 }
 
-// move far-future arrivals whose cell entered the ring into their bucket
-__global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) {
-  const KP& p = *pk;
-  BAIL_IF_ERR();
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  XRec& o = AT(p.ov, k, p.cap_ov);
+// one overflow record: into its bucket if its cell entered the ring, else `stay` = its cell
+__device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long long& stay) {
   if (o.cell < 0) return;
   if (o.cell < g_cur + static_cast<long long>(p.n_buckets)) {
     const uint32_t b = static_cast<uint32_t>(o.cell % p.n_buckets);
@@ -829,7 +824,32 @@ __global__ void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) 
     mark_busy(&p.bucket_cnt[b]);
     o.cell = -1;
   } else {
-    atomicMin(&p.scal[1], o.cell);
+    stay = o.cell;
+  }
+}
+
+// move far-future arrivals whose cell entered the ring into their bucket.
+// The overflow horizon of the records that stay is reduced per workgroup (one atomicMin
+// each): a saturated PBFT leader keeps tens of thousands of PRE_PREPAREs in the list and a
+// same-address atomic per record took 0.3-0.5 ms per launch.
+__global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ long long wmin[4];
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  long long stay = LLONG_MAX;
+  if (k < n) rebin_one(p, g_cur, AT(p.ov, k, p.cap_ov), stay);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const long long y = __shfl_xor(stay, off, 64);
+    stay = y < stay ? y : stay;
+  }
+  if ((threadIdx.x & 63u) == 0) wmin[threadIdx.x >> 6] = stay;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long m = wmin[0];
+    for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) m = wmin[w] < m ? wmin[w] : m;
+    if (m != LLONG_MAX) atomicMin(&p.scal[1], m);
   }
 }
 
@@ -2567,6 +2587,116 @@ __device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32
   }
 }
 
+// per-lane statistics of a link stage: dropped, sends, records, due ops, edges, echoes,
+// refused frames, lost messages (summed per workgroup in link_finish)
+struct LinkCounts {
+  uint32_t v[8];
+};
+
+// The end of a node's link stage (link_node, k_link_mesh): ordered compaction of the ops
+// not yet due, flush of the staged extras / overflow / cross-rank records (one atomic per
+// list), counters, and the node's op count and next op time.
+__device__ __attribute__((always_inline)) inline void link_finish(const KP& p, LinkShared& L, uint32_t g, Op* ops, uint32_t n,
+                                                                  long long t_hi, uint32_t n_lists, long long ovmin,
+                                                                  const LinkCounts& c8, bool clr_slots, bool clr_rx,
+                                                                  uint32_t obp, size_t fidx, unsigned long long wg_t0,
+                                                                  unsigned long long* ph, uint32_t n_in) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t B = p.n_buckets;
+  unsigned long long* cnt = cnt_stripe(p, g / p.N);
+  // ---- 3. compact the ops that are not due yet ----
+  // ordered in-place compaction: an op moves to the count of kept ops before
+  // it (<= its own index); every lane has read its op before any lane writes
+  long long omin = LLONG_MAX;
+  uint32_t kept = 0;
+  if (p.wgt && tid == 0) ph[3] = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t k0 = 0; k0 < n; k0 += blockDim.x) {
+    const uint32_t k = k0 + tid;
+    Op o{};
+    bool keep = false;
+    if (k < n) {
+      o = ops[k];
+      const uint8_t kind = op_kind(o);
+      if (kind == OP_BCAST_J)
+        keep = !(op_flags(o) & OPF_DONE);  // unexpanded (fixed mode never creates these)
+      else if (o.t >= t_hi) {
+        keep = true;
+        if (o.t < omin) omin = o.t;
+      }
+    }
+    uint32_t tot;
+    const uint32_t pos = kept + block_rank(keep, L.wcnt, tot);
+    if (keep) ops[pos] = o;
+    kept += tot;
+  }
+  if (tid == 0) L.n_keep = kept;
+  if (omin != LLONG_MAX) atomicMin(&L.omin, omin);
+  if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
+  // ---- 4. flush the staged extras / overflow records: one atomic per list ----
+  for (uint32_t k = tid; k < n_lists; k += blockDim.x) {
+    const uint32_t c = L.lst[k];
+    if (!c) continue;
+    uint32_t* ctr = k < B ? &p.x_cnt[k] : k == B ? p.ov_cnt : &p.send_cnt[k - B - 1];
+    const uint32_t cap = k < B ? p.cap_x : k == B ? p.cap_ov : p.cap_send;
+    const uint32_t base = atomicAdd(ctr, c);
+    if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
+    L.lbase[k] = base;
+  }
+  __syncthreads();
+  const uint32_t nst = min(L.nst, p.cap_stage);
+  for (uint32_t k = tid; k < nst; k += blockDim.x) {
+    const size_t sidx = static_cast<size_t>(blockIdx.x) * p.cap_stage + k;
+    const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
+    const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
+    if (list > B) {
+      if (pos < p.cap_send) p.sendbuf[static_cast<size_t>(list - B - 1) * p.cap_send + pos] = p.xstage[sidx];
+    } else if (list == B) {
+      if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
+    } else if (pos < p.cap_x) {
+      p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
+    }
+  }
+  // ---- 5. counters: wave sums, LDS atomics, one global atomic per workgroup ----
+  {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t ws = wave_sum(c8.v[k]);
+      if ((tid & 63u) == 0 && ws) atomicAdd(&L.csum[k], ws);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (L.csum[0]) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(L.csum[0]));
+    if (L.csum[1]) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(L.csum[1]));
+    if (L.csum[2]) atomicAdd(&kst_stripe(p)[KST_REC], static_cast<unsigned long long>(L.csum[2]));
+    if (L.csum[3]) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(L.csum[3]));
+    if (L.csum[4]) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(L.csum[4]));
+    if (L.csum[5]) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(L.csum[5]));
+    if (L.csum[6]) atomicAdd(&cnt[CNT_FDROP], static_cast<unsigned long long>(L.csum[6]));
+    if (L.csum[7]) atomicAdd(&cnt[CNT_LOST], static_cast<unsigned long long>(L.csum[7]));
+  }
+  for (uint32_t k = tid; k < B; k += blockDim.x)
+    if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
+  if (p.wgt && tid == 0) {
+    p.wgt[8ull * g] = wg_t0;
+    p.wgt[8ull * g + 1] = __builtin_amdgcn_s_memrealtime();
+    p.wgt[8ull * g + 2] = (static_cast<unsigned long long>(n_in) << 32) | L.n_keep;
+    p.wgt[8ull * g + 3] = ph[0];
+    p.wgt[8ull * g + 4] = ph[1];
+    p.wgt[8ull * g + 5] = ph[2];
+    p.wgt[8ull * g + 6] = ph[3];
+  }
+  if (tid == 0) {
+    if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
+    // the previous arrival cell's replies are all consumed now
+    if (clr_slots) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 0;
+    if (clr_rx) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
+    AT(p.n_ops, g, p.NT) = L.n_keep;
+    AT(p.node_onext, g, p.NT) = L.omin;
+    atomicAdd(&kst_stripe(p)[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
+  }
+}
+
 // QM: DROPTAIL queue model; XR: node-partitioned run (records for other ranks).  Both are
 // template flags so the common case (infinite queues, one rank) carries none of their
 // registers through the per-edge loop.
@@ -2599,7 +2729,6 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   uint32_t* ecnt = reinterpret_cast<uint32_t*>(smem);
   const size_t eb0 = edge_loc(p, rep, e0);
   const int64_t* prop = p.prop + e0;
-  unsigned long long* cnt = cnt_stripe(p, rep);
   const uint32_t B = p.n_buckets;
 
   // ---- 0. expand jitter broadcasts into per-edge SEND ops ----
@@ -2998,100 +3127,10 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   }
 
   if (p.wgt && tid == 0) ph[2] = __builtin_amdgcn_s_memrealtime();
-  // ---- 3. compact the ops that are not due yet ----
-  // ordered in-place compaction: an op moves to the count of kept ops before
-  // it (<= its own index); every lane has read its op before any lane writes
-  long long omin = LLONG_MAX;
-  uint32_t kept = 0;
-  if (p.wgt && tid == 0) ph[3] = __builtin_amdgcn_s_memrealtime();
-  for (uint32_t k0 = 0; k0 < n; k0 += blockDim.x) {
-    const uint32_t k = k0 + tid;
-    Op o{};
-    bool keep = false;
-    if (k < n) {
-      o = ops[k];
-      const uint8_t kind = op_kind(o);
-      if (kind == OP_BCAST_J)
-        keep = !(op_flags(o) & OPF_DONE);  // unexpanded (fixed mode never creates these)
-      else if (o.t >= t_hi) {
-        keep = true;
-        if (o.t < omin) omin = o.t;
-      }
-    }
-    uint32_t tot;
-    const uint32_t pos = kept + block_rank(keep, L.wcnt, tot);
-    if (keep) ops[pos] = o;
-    kept += tot;
-  }
-  if (tid == 0) L.n_keep = kept;
-  if (omin != LLONG_MAX) atomicMin(&L.omin, omin);
-  if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
-  // ---- 4. flush the staged extras / overflow records: one atomic per list ----
-  for (uint32_t k = tid; k < n_lists; k += blockDim.x) {
-    const uint32_t c = L.lst[k];
-    if (!c) continue;
-    uint32_t* ctr = k < B ? &p.x_cnt[k] : k == B ? p.ov_cnt : &p.send_cnt[k - B - 1];
-    const uint32_t cap = k < B ? p.cap_x : k == B ? p.cap_ov : p.cap_send;
-    const uint32_t base = atomicAdd(ctr, c);
-    if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
-    L.lbase[k] = base;
-  }
-  __syncthreads();
-  const uint32_t nst = min(L.nst, p.cap_stage);
-  for (uint32_t k = tid; k < nst; k += blockDim.x) {
-    const size_t sidx = static_cast<size_t>(blockIdx.x) * p.cap_stage + k;
-    const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
-    const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
-    if (list > B) {
-      if (pos < p.cap_send) p.sendbuf[static_cast<size_t>(list - B - 1) * p.cap_send + pos] = p.xstage[sidx];
-    } else if (list == B) {
-      if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
-    } else if (pos < p.cap_x) {
-      p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
-    }
-  }
-  // ---- 5. counters: wave sums, LDS atomics, one global atomic per workgroup ----
-  {
-    const uint32_t v[8] = {static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends), static_cast<uint32_t>(n_rec),
-                           static_cast<uint32_t>(st_ops), static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo),
-                           static_cast<uint32_t>(fdrop), static_cast<uint32_t>(lost)};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t ws = wave_sum(v[k]);
-      if ((tid & 63u) == 0 && ws) atomicAdd(&L.csum[k], ws);
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    if (L.csum[0]) atomicAdd(&cnt[CNT_DROPPED], static_cast<unsigned long long>(L.csum[0]));
-    if (L.csum[1]) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(L.csum[1]));
-    if (L.csum[2]) atomicAdd(&kst_stripe(p)[KST_REC], static_cast<unsigned long long>(L.csum[2]));
-    if (L.csum[3]) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(L.csum[3]));
-    if (L.csum[4]) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(L.csum[4]));
-    if (L.csum[5]) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(L.csum[5]));
-    if (L.csum[6]) atomicAdd(&cnt[CNT_FDROP], static_cast<unsigned long long>(L.csum[6]));
-    if (L.csum[7]) atomicAdd(&cnt[CNT_LOST], static_cast<unsigned long long>(L.csum[7]));
-  }
-  for (uint32_t k = tid; k < B; k += blockDim.x)
-    if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
-  if (p.wgt && tid == 0) {
-    p.wgt[8ull * g] = wg_t0;
-    p.wgt[8ull * g + 1] = __builtin_amdgcn_s_memrealtime();
-    p.wgt[8ull * g + 2] = (static_cast<unsigned long long>(n_in) << 32) | L.n_keep;
-    p.wgt[8ull * g + 3] = ph[0];
-    p.wgt[8ull * g + 4] = ph[1];
-    p.wgt[8ull * g + 5] = ph[2];
-    p.wgt[8ull * g + 6] = ph[3];
-  }
-  if (tid == 0) {
-    if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
-    // the previous arrival cell's replies are all consumed now
-    if (sl1 && final_win) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 0;
-    if (rx && final_win) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
-    AT(p.n_ops, g, p.NT) = L.n_keep;
-    AT(p.node_onext, g, p.NT) = L.omin;
-    atomicAdd(&kst_stripe(p)[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
-  }
+  const LinkCounts lc8{static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends), static_cast<uint32_t>(n_rec),
+                       static_cast<uint32_t>(st_ops),  static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo),
+                       static_cast<uint32_t>(fdrop),   static_cast<uint32_t>(lost)};
+  link_finish(p, L, g, ops, n, t_hi, n_lists, ovmin, lc8, sl1 && final_win, rx && final_win, obp, fidx, wg_t0, ph, n_in);
 }
 
 // LOOP: a small grid walks list 3 (the nodes k_gossip_link left over)
@@ -3109,6 +3148,317 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   }
   uint32_t k;
   if (list_one(p.act_n[1], k)) link_node<QM, XR>(pk, p.act[p.NT + k], cell, t_lo, t_hi, final_win);
+}
+
+// ---------------------------------------------------------------------------
+// k_link_mesh (dense layout, full mesh, fixed app delay, infinite queues, one rank): the
+// link stage of a node whose due ops are all broadcasts -- the PBFT heavy waves, where
+// every out-edge carries a broadcast record, a reply-slot PREPARE_RES and/or the implicit
+// echo.  Same result as link_node (the merge of the four sources in key order per edge,
+// the FIFO, the record into the receiver's in-slot / extras / overflow), with the
+// per-edge state held as compact words instead of 32-byte ops (link_node: 127 VGPRs and
+// a scratch spill), and kU out-edges per lane per iteration whose loads (link word, inbox
+// record, reply slots) are all issued before the first edge's stores, so a lane has kU
+// memory round trips in flight instead of one.  A node with a listed op due (unicast /
+// echo op), too many broadcasts or an unexpanded jitter broadcast goes to list 3, which
+// k_link<false, false, LOOP> finishes after this kernel.
+constexpr int kMeshU = 2;
+__device__ inline bool kless(int64_t ta, uint32_t dta, uint32_t oa, uint32_t sa, int64_t tb, uint32_t dtb, uint32_t ob,
+                             uint32_t sb) {
+  if (ta != tb) return ta < tb;
+  const int64_t xa = ta - dta, xb = tb - dtb;
+  if (xa != xb) return xa < xb;
+  if (oa != ob) return oa < ob;
+  return sa < sb;
+}
+
+__global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                   long long t_hi, int final_win) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ LinkShared L;
+  uint32_t kk;
+  if (!list_one(p.act_n[1], kk)) return;
+  const uint32_t g = p.act[p.NT + kk];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = AT(p.n_ops, g, p.NT);
+  const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
+  const bool sl0 = p.eslot && (AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u);
+  const bool sl1 = p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u);
+  const uint32_t B = p.n_buckets;
+  const uint32_t ib = static_cast<uint32_t>(cell % B);
+  const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const bool rx = p.impl && node_flagged(p, ib, g, rep, i);
+  if (n == 0 && !sl0 && !sl1 && !rx) return;
+  const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
+  Op* ops = p.ops + op_base(p, g);
+
+  // ---- classify the due ops: broadcasts to LDS; anything else sends the node to list 3 ----
+  for (uint32_t k = tid; k < B; k += blockDim.x) L.lcnt[k] = 0;
+  for (uint32_t k = tid; k <= B; k += blockDim.x) L.lst[k] = 0;
+  const bool tmap = p.n_tiles <= static_cast<uint32_t>(kMaxTiles);
+  if (tmap)
+    for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x) L.tflag[k] = 0;
+  if (tid < 8) L.csum[tid] = 0;
+  if (tid == 0) {
+    L.n_bc = 0;
+    L.n_list = 0;
+    L.nst = 0;
+    L.omin = LLONG_MAX;
+    L.ovmin = LLONG_MAX;
+    L.tbk = kInvalid;
+  }
+  __syncthreads();
+  const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
+  uint32_t sends = 0, dropped = 0, st_ops = 0, other = 0;
+  for (uint32_t k = tid; k < n; k += blockDim.x) {
+    const Op& o = ops[k];
+    const uint8_t kind = op_kind(o);
+    if (kind == OP_BCAST_J) {
+      other += (op_flags(o) & OPF_DONE) ? 0u : 1u;
+      continue;
+    }
+    if (o.t >= t_hi) continue;
+    if (kind != OP_BCAST) {
+      ++other;
+      continue;
+    }
+    ++st_ops;
+    const uint32_t pos = atomicAdd(&L.n_bc, 1u);
+    if (pos < kBcastCap) L.bc[pos] = k;
+    sends += deg;
+    if (op_flags(o) & OPF_PAXOS) dropped += 1;
+  }
+  {
+    const uint32_t ws = wave_sum(other);
+    if ((tid & 63u) == 0 && ws) atomicAdd(&L.n_list, ws);
+  }
+  __syncthreads();
+  const uint32_t n_bc = L.n_bc;
+  if (L.n_list || n_bc > static_cast<uint32_t>(kBcastCap)) {  // not a simple node: the generic kernel
+    if (tid == 0) {
+      const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
+      AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
+    }
+    return;
+  }
+  // the due broadcasts in key order (LDS copies: every lane reads them per edge)
+  if (tid < n_bc) L.bco[tid] = ld_op(&ops[L.bc[tid]]);
+  __syncthreads();
+  if (tid == 0) {
+    for (uint32_t a = 1; a < n_bc; ++a) {
+      const Op ox = L.bco[a];
+      uint32_t b2 = a;
+      while (b2 > 0 && op_key_less(ox, ox.sub, L.bco[b2 - 1], L.bco[b2 - 1].sub)) {
+        st_op(&L.bco[b2], L.bco[b2 - 1]);
+        --b2;
+      }
+      st_op(&L.bco[b2], ox);
+    }
+  }
+  __syncthreads();
+
+  // ---- per out-edge: merge broadcasts / reply slots / implicit echo in key order, FIFO, emit ----
+  uint32_t n_rec = 0, st_edges = 0, st_echo = 0;
+  long long ovmin = LLONG_MAX;
+  uint32_t cb = kInvalid, cbn = 0;
+  const long long cs = cell * p.L;
+  const uint32_t N1 = p.N - 1;
+  Rec* in_row = p.inbox + inbox_idx(p, ib, rep, e0);
+  const int64_t app = p.app_delay;
+  const uint32_t f2r = static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0)));
+  const uint32_t w3r = f2r | (kPbPrepareRes << 16);  // a reply slot's (f2, type) word
+  const uint32_t bs = blockDim.x;
+  for (uint32_t base = tid; base < deg; base += kMeshU * bs) {
+    // all loads of the kU edges first (independent addresses), then the per-edge work
+    uint64_t lw[kMeshU];
+    uint4 r0[kMeshU], w0[kMeshU], w1[kMeshU];
+    uint64_t* lwp[kMeshU];
+#pragma unroll
+    for (int u = 0; u < kMeshU; ++u) {
+      const uint32_t le = base + u * bs;
+      const bool v = le < deg;
+      lwp[u] = p.link + edge_loc(p, rep, e0 + (v ? le : 0u));
+      lw[u] = v ? *lwp[u] : 0ull;
+      r0[u] = (v && rx) ? *reinterpret_cast<const uint4*>(in_row + le) : make_uint4(0, 0, 0, 0);
+      w0[u] = (v && sl0) ? *eslot_at(p, ob, rep, e0 + le) : make_uint4(0, 0, 0, 0);
+      w1[u] = (v && sl1) ? *eslot_at(p, obp, rep, e0 + le) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kMeshU; ++u) {
+      const uint32_t le = base + u * bs;
+      if (le >= deg) break;
+      const uint32_t e = e0 + le;
+      const uint32_t s = le < i ? le : le + 1;  // full mesh: peers ascending without self
+      // implicit echo of in-slot le (record {t_off, sub, f0|f1, f2|type|flags})
+      bool he = false;
+      int64_t et = 0;
+      uint32_t edt = 0, esub = 0;
+      int ebig = 0;
+      if (rx) {
+        const uint32_t fl = r0[u].w >> 24;
+        const long long ta0 = cs + r0[u].x;
+        if ((fl & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
+          clr_rec(in_row + le);
+          if (p.echo) {
+            ebig = (fl & RF_BIG) ? 1 : 0;
+            const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
+            et = ta0;
+            edt = static_cast<uint32_t>(pin + p.tx_last[ebig]);
+            esub = r0[u].y;
+            he = true;
+            ++st_echo;
+          }
+        }
+      }
+      // reply slots {due t lo, hi, sub, f0 | f1 << 16} of this arrival cell and the previous one
+      const int64_t rt1 = static_cast<int64_t>((static_cast<uint64_t>(w0[u].y) << 32) | w0[u].x);
+      const int64_t rt2 = static_cast<int64_t>((static_cast<uint64_t>(w1[u].y) << 32) | w1[u].x);
+      bool hr = sl0 && rt1 >= t_lo && rt1 < t_hi;
+      bool hr2 = sl1 && rt2 >= t_lo && rt2 < t_hi;
+      st_ops += (hr ? 1u : 0u) + (hr2 ? 1u : 0u);
+      if (n_bc == 0 && !he && !hr && !hr2) continue;
+      ++st_edges;
+      int64_t bu = static_cast<int64_t>(lw[u] >> 16);
+      uint32_t lc = static_cast<uint32_t>(lw[u] & 0xFFFFu);
+      const int64_t pr = p.prop_const >= 0 ? p.prop_const : p.prop[e];
+      const uint32_t slot = s * N1 + (i < s ? i : i - 1);
+      const uint32_t dg = rep * p.N + s;
+      uint32_t bi = 0;
+      for (;;) {
+        while (bi < n_bc && (op_flags(L.bco[bi]) & OPF_PAXOS) && le == 0) ++bi;
+        // the earliest source: 1 broadcast, 2 / 4 reply slots, 3 echo
+        int src = 0;
+        int64_t ot = 0;
+        uint32_t odt = 0, oor = 0, osub = 0, ow2 = 0, ow3 = 0;
+        int big = 0;
+        if (bi < n_bc) {
+          const uint4* bw = reinterpret_cast<const uint4*>(&L.bco[bi]);
+          const uint4 a = bw[0], b = bw[1];
+          ot = static_cast<int64_t>((static_cast<uint64_t>(a.y) << 32) | a.x);
+          odt = a.z;
+          oor = a.w;
+          osub = b.x + (((b.w >> 26) & OPF_PAXOS) ? le - 1 : le);
+          ow2 = b.z;
+          ow3 = b.w & 0x00FFFFFFu;
+          big = ((b.w >> 26) & OPF_BIG) ? 1 : 0;
+          src = 1;
+        }
+        if (hr && (src == 0 || kless(rt1, static_cast<uint32_t>(app), i, w0[u].z, ot, odt, oor, osub))) {
+          ot = rt1;
+          odt = static_cast<uint32_t>(app);
+          oor = i;
+          osub = w0[u].z;
+          ow2 = w0[u].w;
+          ow3 = w3r;
+          big = 0;
+          src = 2;
+        }
+        if (hr2 && (src == 0 || kless(rt2, static_cast<uint32_t>(app), i, w1[u].z, ot, odt, oor, osub))) {
+          ot = rt2;
+          odt = static_cast<uint32_t>(app);
+          oor = i;
+          osub = w1[u].z;
+          ow2 = w1[u].w;
+          ow3 = w3r;
+          big = 0;
+          src = 4;
+        }
+        if (he && (src == 0 || kless(et, edt, s, esub, ot, odt, oor, osub))) {
+          ot = et;
+          big = ebig;
+          src = 3;
+        }
+        if (src == 0) break;
+        if (src == 1)
+          ++bi;
+        else if (src == 2)
+          hr = false;
+        else if (src == 4)
+          hr2 = false;
+        else
+          he = false;
+        if (src == 2 || src == 4) ++sends;
+        const int64_t start = bu > ot ? bu : ot;
+        const int64_t end = start + p.tx_tot[big];
+        bu = end;
+        if (src == 3) continue;  // the echo only occupies the link
+        const int64_t ta = end + pr;
+        const long long ca = ta / p.L;
+        const long long rel = ca - cell;
+        if (rel < 1) {
+          set_err(p, BCSIM_E_TIE);  // lookahead violated
+          continue;
+        }
+        ++n_rec;
+        const uint32_t tof = static_cast<uint32_t>(ta - ca * p.L);
+        const uint32_t w3 = ow3 | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+        Rec r;
+        {
+          const uint4 rv = make_uint4(tof, osub, ow2, w3);
+          __builtin_memcpy(&r, &rv, sizeof r);
+        }
+        const bool owner = lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
+        lc = static_cast<uint32_t>(ca) & 0xFFFFu;
+        if (rel < static_cast<long long>(B)) {
+          const uint32_t bk = static_cast<uint32_t>(ca % B);
+          if (owner) {
+            st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), r);
+            uint32_t tb = kInvalid;
+            if (tmap) {  // the first bucket seen owns the LDS tile map; others flag directly
+              tb = L.tbk;
+              if (tb == kInvalid) {
+                const uint32_t old = atomicCAS(&L.tbk, kInvalid, bk);
+                tb = old == kInvalid ? bk : old;
+              }
+            }
+            if (tb == bk)
+              L.tflag[s >> 6] = 1;
+            else
+              set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
+                                static_cast<uint64_t>(B) * p.R * p.n_tiles));
+          } else {
+            XRec x;
+            x.r = r;
+            x.cell = ca;
+            x.slot = slot;
+            x.g = dg;
+            link_stage(p, L, g, bk, x);
+            AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
+          }
+          if (bk != cb) {
+            if (cbn) atomicAdd(&L.lcnt[cb], cbn);
+            cb = bk;
+            cbn = 0;
+          }
+          ++cbn;
+        } else {
+          XRec x;
+          x.r = r;
+          if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+          x.cell = ca;
+          x.slot = slot;
+          x.g = dg;
+          link_stage(p, L, g, B, x);
+          if (ca < ovmin) ovmin = ca;
+        }
+      }
+      if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+      *lwp[u] = (static_cast<uint64_t>(bu) << 16) | lc;
+    }
+  }
+  if (cbn) atomicAdd(&L.lcnt[cb], cbn);
+  __syncthreads();
+  if (tmap && L.tbk != kInvalid) {  // flush the receiver-tile flags of this sender's records
+    const size_t tb = (static_cast<size_t>(L.tbk) * p.R + rep) * p.n_tiles;
+    for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x)
+      if (L.tflag[k]) set_flag_once(&AT(p.rtile, tb + k, static_cast<uint64_t>(B) * p.R * p.n_tiles));
+  }
+  const unsigned long long t0 = p.wgt ? wg_t0 : 0ull;
+  unsigned long long ph[4] = {t0, t0, t0, t0};
+  const LinkCounts c8{dropped, sends, n_rec, st_ops, st_edges, st_echo, 0u, 0u};
+  link_finish(p, L, g, ops, n, t_hi, B + 1, ovmin, c8, sl1 && final_win, rx && final_win, obp, fidx, t0, ph, n);
 }
 
 // ---------------------------------------------------------------------------
