@@ -61,3 +61,39 @@ def test_cpu_baselines_small():
         c.paxos_decrees = 2
     allc = bench.cpu_baseline_all_cores(16, 0.3, "paxos", tweak, 2)
     assert allc["value"] > 0 and allc["cores"] == 2
+
+
+def test_pmc_summary_link_class_groups(tmp_path):
+    """A timed k_link-class launch = fast-path dispatch + looped generic dispatch: the
+    link_class entry sums both over the bench's timed window."""
+    import pmc_summary
+    src = tmp_path / "prof"
+    mesh = "bcsim::k_link_mesh(bcsim::KP const*, long long, long long, long long, int)"
+    loop = "void bcsim::k_link<false, false, true>(bcsim::KP const*, long long, long long, long long, int)"
+    scan = "void bcsim::k_scan<0, false, false>(bcsim::KP const*)"
+    rows_f, rows_w, trace = [], [], []
+    t, d = 0, 0
+    for k in range(5):
+        for name, fv, wv, us in ((scan, 1.0, 1.0, 1), (mesh, float(k), 10.0, 10 * (k + 1)), (loop, 1.0, 2.0, 2)):
+            rows_f.append((d, name, [fv]))
+            rows_w.append((d, name, [wv, 0, 0]))
+            trace.append((d, name, t, t + 1000 * us))
+            t += 100000
+            d += 1
+    _write_pass(str(src / "fetch"), rows_f, ["FETCH_SIZE"])
+    _write_pass(str(src / "write"), rows_w, ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"])
+    os.makedirs(src / "trace")
+    with open(src / "trace" / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        for row in trace:
+            w.writerow(row)
+    with open(src / "trace.log", "w") as f:
+        f.write(json.dumps({"roofline": {"first_timed_launch": 1, "launches": 3}}) + "\n")
+    dst = tmp_path / "out.json"
+    pmc_summary.main(str(src), str(dst))
+    tw = json.load(open(dst))["kernels"]["link_class"]["timed_window"]
+    assert tw["first"] == 1 and tw["launches"] == 3
+    # groups 1..3: mesh FETCH 1,2,3 + loop FETCH 1 (x2), WRITE 10 + 2
+    assert abs(tw["hbm_bytes_per_launch"] - (2 * 1024 * (2.0 + 1.0) + 12 * 1024)) < 1e-6
+    assert abs(tw["rocprof_avg_us"] - (30.0 + 2.0)) < 1e-9  # mesh 20, 30, 40 us + loop 2 us
