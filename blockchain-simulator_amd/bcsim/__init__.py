@@ -44,6 +44,8 @@ def lib():
         _LIB.bcsim_read_kernel_stats.argtypes = [C.c_void_p, C.POINTER(C.c_double),
                                                  C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
         _LIB.bcsim_read_kernel_stats.restype = C.c_int
+        _LIB.bcsim_read_engine_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        _LIB.bcsim_read_engine_counters.restype = C.c_int
         _LIB.bcsim_reset_kernel_stats.argtypes = [C.c_void_p]
         _LIB.bcsim_reset_kernel_stats.restype = C.c_int
         _LIB.bcsim_topology_random_regular.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64,
@@ -97,6 +99,13 @@ class Simulator(_abi.Handle):
         self._call("read_kernel_stats", self.h, us, by, ln)
         names = ("scan", "link", "group", "aux")
         return {n: dict(us=us[k], bytes=by[k], launches=ln[k]) for k, n in enumerate(names)}
+
+    def engine_counters(self):
+        """Raw work counters (include/bcsim.h bcsim_read_engine_counters)."""
+        out = (C.c_uint64 * 8)()
+        self._call("read_engine_counters", self.h, out)
+        names = ("records", "due_ops", "edges", "kept_ops", "delivered", "scan_ops", "echoes", "split_windows")
+        return dict(zip(names, out))
 
     def reset_kernel_stats(self):
         self._call("reset_kernel_stats", self.h)

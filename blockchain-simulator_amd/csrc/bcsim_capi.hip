@@ -369,6 +369,10 @@ static int setup_device(Sim& s) {
   // k_scan stages up to cap_arr arrivals per window in LDS (32 B each); a
   // cell with more is split into windows, so cap_arr only bounds one instant
   p.cap_arr = static_cast<uint32_t>(std::min<uint64_t>(kScanMaxArr, next_pow2(std::max<uint64_t>(64, s.deg_max + 64))));
+  if (const char* ca = std::getenv("BCSIM_CAP_ARR"); ca && *ca) {  // testing aid: smaller windows (>= 64)
+    const uint32_t v = static_cast<uint32_t>(next_pow2(std::max<uint64_t>(64, std::strtoull(ca, nullptr, 0))));
+    if (v < p.cap_arr) p.cap_arr = v;
+  }
   if (s.deg_max >= (1u << (32 - kSlotShift))) {  // staged arrival ids carry the in-slot in 18 bits
     g_detail = "node degree above 2^18";
     return BCSIM_E_UNSUPPORTED;
@@ -658,6 +662,7 @@ static int setup_device(Sim& s) {
   }
   const size_t n_rtile = p.mesh ? static_cast<size_t>(s.B) * s.R * p.n_tiles : 1;
   if ((rc = dalloc(s, &p.rtile, n_rtile))) return rc;
+  if ((rc = dalloc(s, &p.bmin, s.B))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
       (rc = dalloc(s, &p.xbuf, p.cap_xbuf)) || (rc = dalloc(s, &p.xgrp, p.cap_x)) ||
       (rc = dalloc(s, &p.xstage, static_cast<size_t>(s.grid_link) * p.cap_stage)) ||
@@ -749,6 +754,10 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemset(p.inbox, 0, p.cap_inbox * sizeof(Rec)));
   HIPCHK(hipMemset(p.rtile, 0, n_rtile));
   HIPCHK(hipMemset(p.iflag, 0, static_cast<size_t>(s.B) * NT));
+  {
+    const std::vector<long long> none(s.B, LLONG_MAX);  // every bucket empty
+    HIPCHK(hipMemcpy(p.bmin, none.data(), s.B * sizeof(long long), hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMemset(p.seg_cnt, 0, NT * 4));
   HIPCHK(hipMemset(p.seg_off, 0, (NT + 1) * 4));
   HIPCHK(hipMemset(p.cursor, 0, NT * 4));
@@ -875,9 +884,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   }
   uint32_t n_link = 1;
   {  // compact lists of the window's active gnodes
-    // contiguous chunks of >= 2048 gnodes (<= kActChunk), at most ~1024 workgroups
+    // contiguous chunks of >= 256 gnodes (<= kActChunk), at most ~1024 workgroups (N=4096:
+    // 16 workgroups of one gnode per lane; 2 of 2048 took 14-22 us of dependent loads per lane)
     const uint64_t nl = static_cast<uint64_t>(s.R) * s.nloc;
-    const uint64_t nb = std::max<uint64_t>((nl + kActChunk - 1) / kActChunk, std::min<uint64_t>(1024, (nl + 2047) / 2048));
+    const uint64_t nb = std::max<uint64_t>((nl + kActChunk - 1) / kActChunk, std::min<uint64_t>(1024, (nl + 255) / 256));
     const uint32_t chunk = static_cast<uint32_t>(((nl + nb - 1) / nb + 255) / 256 * 256);
     rc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, lo, hi,
                 static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk);
@@ -1644,6 +1654,18 @@ int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, u
     bytes_out4[bcsim::KS_AUX] = 32.0 * ks[bcsim::KST_OPS] + 16.0 * ks[bcsim::KST_REC] + 16.0 * ks[bcsim::KST_EDGES] +
                                 32.0 * ks[bcsim::KST_KEPT] + 32.0 * ks[bcsim::KST_ECHO];
   }
+  return BCSIM_OK;
+}
+
+int bcsim_read_engine_counters(bcsim_sim* h, uint64_t* out8) {
+  if (!h || !out8) return BCSIM_E_INVAL;
+  Sim& s = *h->s;
+  for (int k = 0; k < 8; ++k) out8[k] = 0;
+  if (!s.started) return BCSIM_OK;
+  unsigned long long kss[8 * bcsim::kKstStripes];
+  if (hipMemcpy(kss, s.kp.kstat, sizeof kss, hipMemcpyDeviceToHost) != hipSuccess) return BCSIM_E_HIP;
+  for (uint32_t st = 0; st < bcsim::kKstStripes; ++st)
+    for (int k = 0; k < 8; ++k) out8[k] += kss[8 * st + k];
   return BCSIM_OK;
 }
 

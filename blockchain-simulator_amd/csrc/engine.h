@@ -137,6 +137,6 @@ enum {
 enum { KS_SCAN = 0, KS_LINK = 1, KS_GROUP = 2, KS_AUX = 3 };
 
 // link-kernel algorithmic counters (KP::kstat)
-enum { KST_REC = 0, KST_OPS = 1, KST_EDGES = 2, KST_KEPT = 3, KST_DELIV = 4, KST_SCAN_OPS = 5, KST_ECHO = 6 };
+enum { KST_REC = 0, KST_OPS = 1, KST_EDGES = 2, KST_KEPT = 3, KST_DELIV = 4, KST_SCAN_OPS = 5, KST_ECHO = 6, KST_SPLIT = 7 };
 
 }  // namespace bcsim

@@ -123,6 +123,8 @@ struct KP {
                          // tile sits in the bucket (senders set one byte per tile, not one per node)
   uint32_t mesh, n_tiles;  // full-mesh topology (arithmetic peers / in-slots)
   uint8_t* iflag;        // [B][NT] node has records in the bucket
+  long long* bmin;       // [B] lower bound of the arrival times of the bucket's records (LLONG_MAX: none):
+                         // a window that ends before it skips the flagged rows (node_flagged_w)
   uint32_t* bucket_cnt;  // [B] nonzero = the bucket holds records (slots + extras); see mark_busy
   uint32_t* x_cnt;       // [B] extras in the bucket
   uint32_t n_buckets;
@@ -255,6 +257,25 @@ __device__ inline bool node_flagged(const KP& p, uint32_t b, uint32_t g, uint32_
                                 static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles)
                            : 0;
   return (f | t) != 0;
+}
+// node_flagged for the window [.., t_hi): false when no record of the bucket arrives before
+// t_hi (a cell split by a tick or a run() limit: the rows are read once, in the window that
+// holds the arrivals, instead of in every window)
+__device__ inline bool node_flagged_w(const KP& p, uint32_t b, uint32_t g, uint32_t rep, uint32_t i, long long t_hi) {
+  const long long bm = p.bmin[b];
+  const bool f = node_flagged(p, b, g, rep, i);
+  return f && bm < t_hi;
+}
+// lower the bucket's arrival-time bound (read first: most writers find it already lower)
+__device__ inline void bmin_lower(const KP& p, uint32_t b, long long t) {
+  if (t < *reinterpret_cast<volatile long long*>(&p.bmin[b])) atomicMin(&p.bmin[b], t);
+}
+// start time of the cell that bucket k holds, seen from cell `cell` (records are emitted
+// 1 .. B-1 cells ahead)
+__device__ inline long long bucket_t0(const KP& p, long long cell, uint32_t k) {
+  const uint32_t B = p.n_buckets;
+  const long long rel = (static_cast<long long>(k) + B - cell % B) % B;
+  return (cell + rel) * p.L;
 }
 // set-once byte flag (many writers of the same byte: read first, store only if clear)
 __device__ inline void set_flag_once(uint8_t* f) {
@@ -821,6 +842,7 @@ __device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long lon
       AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
     }
     AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(p.n_buckets) * p.NT) = 1;
+    bmin_lower(p, b, o.cell * p.L + static_cast<long long>(x.r.t_off));
     mark_busy(&p.bucket_cnt[b]);
     o.cell = -1;
   } else {
@@ -1235,6 +1257,7 @@ struct ScanShared {
   uint32_t wcnt[kMaxWaves];
   uint4 wsum[kMaxWaves];
   uint32_t n, n_main, unsorted, cnt;
+  uint32_t hsel, hcnt;  // window split: selected bin, arrivals before it
   // PBFT window state
   uint32_t sub, nops, tn, npp, last_vc;
   uint64_t draws;
@@ -1320,6 +1343,82 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
   if (tid == 0) S.n_main = n_main;
   __syncthreads();
   return n;
+}
+
+// The end wb of a window starting at wa: the largest wb <= hi with at most cap of the node's
+// arrivals in [wa, wb), given more than cap in [wa, hi) (count(wa, wb) is monotone, so this
+// is the same bound a binary search over stage_window counts finds).  Radix select over time:
+// each pass histograms the arrivals of [lo, hi) into 2^kb-ns bins (LDS atomics into `hist`,
+// the not yet used staging area), so ~3 passes over the row replace ~22 counting passes.
+__device__ long long window_split(const KP& p, ScanShared& S, const Rec* slots, uint32_t deg, const XRec* xs,
+                                  uint32_t xn, long long cs, long long wa, long long hi, uint32_t* hist) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t lg = p.cap_arr >= 128 ? 8u : 6u;  // 2^lg bins (<= 2 * cap_arr u32 of staging)
+  const uint32_t nb = 1u << lg;
+  long long lo = wa;
+  uint32_t c_lo = 0;  // arrivals in [wa, lo)
+  while (hi - lo > 1) {
+    uint32_t sh = 0;
+    while ((static_cast<long long>(nb) << sh) < hi - lo) ++sh;
+    for (uint32_t k = tid; k < nb; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < deg; base += 4 * blockDim.x) {
+      Rec rr[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t k = base + j * blockDim.x + tid;
+        rr[j] = k < deg ? ld_rec(slots + k) : Rec{};
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t k = base + j * blockDim.x + tid;
+        const long long t = cs + rr[j].t_off;
+        if (k < deg && (rr[j].flags & RF_VALID) && t >= lo && t < hi)
+          atomicAdd(&hist[static_cast<uint32_t>((t - lo) >> sh)], 1u);
+      }
+    }
+    for (uint32_t k = tid; k < xn; k += blockDim.x) {
+      const long long t = cs + xs[k].r.t_off;
+      if (t >= lo && t < hi) atomicAdd(&hist[static_cast<uint32_t>((t - lo) >> sh)], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: boundaries b = 0 .. nb-1 at lo + (b << sh), count c_lo + prefix(b)
+      const uint32_t per = nb / 64;
+      uint32_t h[4] = {0, 0, 0, 0}, sum = 0;
+      for (uint32_t j = 0; j < per; ++j) {
+        h[j] = hist[lane * per + j];
+        sum += h[j];
+      }
+      uint32_t inc = sum;
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += v;
+      }
+      uint32_t c = c_lo + inc - sum, ok = 0;
+      for (uint32_t j = 0; j < per; ++j) {
+        const uint32_t b = lane * per + j;
+        if (c <= p.cap_arr && (static_cast<long long>(b) << sh) < hi - lo) ++ok;  // monotone in b
+        c += h[j];
+      }
+      const uint32_t tot_ok = wave_sum(ok);  // boundaries with count <= cap: 0 .. tot_ok - 1
+      const uint32_t best = tot_ok - 1;
+      if (lane == best / per) {
+        uint32_t cb = c_lo + inc - sum;
+        for (uint32_t j = 0; j < best % per; ++j) cb += h[j];
+        S.hsel = best;
+        S.hcnt = cb;
+      }
+    }
+    __syncthreads();
+    const uint32_t best = S.hsel;
+    c_lo = S.hcnt;
+    const long long nlo = lo + (static_cast<long long>(best) << sh);
+    const long long nhi = lo + (static_cast<long long>(best + 1) << sh);
+    lo = nlo;
+    if (nhi < hi) hi = nhi;
+    __syncthreads();  // S.hsel / hist reuse
+  }
+  return lo;
 }
 
 __device__ inline bool sec_less(uint64_t ka, uint32_t sa, uint64_t kb, uint32_t sb) {
@@ -1791,7 +1890,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
   // the node's row (full mesh: arithmetic, no load) and its flags, loads issued together
   const uint32_t e0 = p.mesh ? i * (p.N - 1) : AT(p.row, i, p.N + 1);
   const uint32_t deg = p.mesh ? p.N - 1 : AT(p.row, i + 1, p.N + 1) - e0;
-  const bool flag = node_flagged(p, b, g, rep, i);
+  const bool flag = node_flagged_w(p, b, g, rep, i, t_hi);
   if (!flag && AT(p.node_tnext, g, p.NT) >= t_hi && !has_start && !has_stop) return;
 
   // sparse mode: no inbox slots, the node's arrivals are all in the cell's grouped lists
@@ -1882,15 +1981,8 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
     long long wb = t_hi;
     uint32_t n = flag ? stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, wb, akey, asec, true) : 0u;
     if (n > cap) {  // more than cap arrivals: shrink the window (rare)
-      long long lo = wa, hi = t_hi;  // count(lo) <= cap < count(hi)
-      while (hi - lo > 1) {
-        const long long mid = lo + (hi - lo) / 2;
-        if (stage_window(p, S, slots, e0, deg_in, xs, xn, cs, wa, mid, akey, asec, false) <= cap)
-          lo = mid;
-        else
-          hi = mid;
-      }
-      wb = lo;
+      wb = window_split(p, S, slots, deg_in, xs, xn, cs, wa, t_hi, reinterpret_cast<uint32_t*>(akey));
+      if (tid == 0) atomicAdd(&kst_stripe(p)[KST_SPLIT], 1ull);
       if (wb == wa) {  // > cap arrivals at one instant
         if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
         return;
@@ -2335,7 +2427,7 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
   const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
-  const bool flagged = kl < na && node_flagged(p, b, g, rep, i);
+  const bool flagged = kl < na && node_flagged_w(p, b, g, rep, i, t_hi);
   const bool tdue = kl < na && AT(p.node_tnext, g, p.NT) < t_hi;
   const bool have = kl < na && (has_start || has_stop || flagged || tdue);  // k_active's k_scan rule
   const uint32_t e0 = have ? AT(p.row, i, p.N + 1) : 0u;
@@ -2540,6 +2632,7 @@ struct LinkShared {
   uint32_t bc[kBcastCap];
   Op bco[kBcastCap];         // the due broadcasts in key order (LDS copies: every lane reads them per edge)
   uint32_t lcnt[kMaxBuckets];
+  uint32_t lmin[kMaxBuckets];  // earliest arrival offset of this workgroup's records per bucket (-> bmin)
   uint4 wsum[kMaxWaves];
   uint32_t wcnt[kMaxWaves];
   uint32_t nst;                      // staged extras / overflow records
@@ -2676,7 +2769,10 @@ __device__ __attribute__((always_inline)) inline void link_finish(const KP& p, L
     if (L.csum[7]) atomicAdd(&cnt[CNT_LOST], static_cast<unsigned long long>(L.csum[7]));
   }
   for (uint32_t k = tid; k < B; k += blockDim.x)
-    if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
+    if (L.lcnt[k]) {
+      mark_busy(&p.bucket_cnt[k]);
+      bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + L.lmin[k]);
+    }
   if (p.wgt && tid == 0) {
     p.wgt[8ull * g] = wg_t0;
     p.wgt[8ull * g + 1] = __builtin_amdgcn_s_memrealtime();
@@ -2715,7 +2811,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   const uint32_t ib = static_cast<uint32_t>(cell % p.n_buckets);
   const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
   const uint32_t rep = g / p.N, i = g % p.N;
-  const bool rx = p.impl && node_flagged(p, ib, g, rep, i);
+  const bool rx = p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
   if (n == 0 && !sl && !rx) return;
   const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
   unsigned long long ph[4] = {0, 0, 0, 0};
@@ -2780,7 +2876,10 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   }
 
   // ---- 1. classify due ops: broadcast list, listed-op count ----
-  for (uint32_t k = tid; k < B; k += blockDim.x) L.lcnt[k] = 0;
+  for (uint32_t k = tid; k < B; k += blockDim.x) {
+    L.lcnt[k] = 0;
+    L.lmin[k] = ~0u;
+  }
   const uint32_t n_lists = B + 1 + (XR ? p.nranks : 0);
   for (uint32_t k = tid; k < n_lists; k += blockDim.x) L.lst[k] = 0;
   const bool tmap = p.mesh && p.n_tiles <= static_cast<uint32_t>(kMaxTiles);
@@ -2799,6 +2898,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   __syncthreads();
   unsigned long long dropped = 0, sends = 0, st_ops = 0;
   uint32_t cb = kInvalid, cbn = 0;  // run-length bucket count of this thread's records
+  uint32_t cmn = ~0u;               // and their earliest arrival offset in the cell
   uint32_t my_list = 0;
   for (uint32_t k = tid; k < n; k += blockDim.x) {
     const Op& o = ops[k];
@@ -3097,11 +3197,16 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
         }
         if (flag_rx) AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
         if (bk != cb) {
-          if (cbn) atomicAdd(&L.lcnt[cb], cbn);
+          if (cbn) {
+            atomicAdd(&L.lcnt[cb], cbn);
+            atomicMin(&L.lmin[cb], cmn);
+          }
           cb = bk;
           cbn = 0;
+          cmn = ~0u;
         }
         ++cbn;
+        if (tof < cmn) cmn = tof;
       } else {
         XRec x;
         x.r = r;
@@ -3117,7 +3222,10 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
     if (QM) p.qmeta[eb0 + le] = qm;
   }
-  if (cbn) atomicAdd(&L.lcnt[cb], cbn);
+  if (cbn) {
+    atomicAdd(&L.lcnt[cb], cbn);
+    atomicMin(&L.lmin[cb], cmn);
+  }
   __syncthreads();
   // flush the receiver-tile flags of this sender's full-mesh records
   if (tmap && L.tbk != kInvalid) {
@@ -3189,13 +3297,16 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   const uint32_t ib = static_cast<uint32_t>(cell % B);
   const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
   const uint32_t rep = g / p.N, i = g % p.N;
-  const bool rx = p.impl && node_flagged(p, ib, g, rep, i);
+  const bool rx = p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
   if (n == 0 && !sl0 && !sl1 && !rx) return;
   const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
   Op* ops = p.ops + op_base(p, g);
 
   // ---- classify the due ops: broadcasts to LDS; anything else sends the node to list 3 ----
-  for (uint32_t k = tid; k < B; k += blockDim.x) L.lcnt[k] = 0;
+  for (uint32_t k = tid; k < B; k += blockDim.x) {
+    L.lcnt[k] = 0;
+    L.lmin[k] = ~0u;
+  }
   for (uint32_t k = tid; k <= B; k += blockDim.x) L.lst[k] = 0;
   const bool tmap = p.n_tiles <= static_cast<uint32_t>(kMaxTiles);
   if (tmap)
@@ -3263,6 +3374,7 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   uint32_t n_rec = 0, st_edges = 0, st_echo = 0;
   long long ovmin = LLONG_MAX;
   uint32_t cb = kInvalid, cbn = 0;
+  uint32_t cmn = ~0u;
   const long long cs = cell * p.L;
   const uint32_t N1 = p.N - 1;
   Rec* in_row = p.inbox + inbox_idx(p, ib, rep, e0);
@@ -3428,11 +3540,16 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
             AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
           }
           if (bk != cb) {
-            if (cbn) atomicAdd(&L.lcnt[cb], cbn);
+            if (cbn) {
+              atomicAdd(&L.lcnt[cb], cbn);
+              atomicMin(&L.lmin[cb], cmn);
+            }
             cb = bk;
             cbn = 0;
+            cmn = ~0u;
           }
           ++cbn;
+          if (tof < cmn) cmn = tof;
         } else {
           XRec x;
           x.r = r;
@@ -3448,7 +3565,10 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
       *lwp[u] = (static_cast<uint64_t>(bu) << 16) | lc;
     }
   }
-  if (cbn) atomicAdd(&L.lcnt[cb], cbn);
+  if (cbn) {
+    atomicAdd(&L.lcnt[cb], cbn);
+    atomicMin(&L.lmin[cb], cmn);
+  }
   __syncthreads();
   if (tmap && L.tbk != kInvalid) {  // flush the receiver-tile flags of this sender's records
     const size_t tb = (static_cast<size_t>(L.tbk) * p.R + rep) * p.n_tiles;
@@ -3478,12 +3598,16 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
   __shared__ RawOp sop[256];  // due broadcasts of each group in key order (group base + rank)
   __shared__ uint32_t s_c[6];  // sends, records, due ops, edges, echoes, kept
   __shared__ uint8_t s_busy[kMaxBuckets];
+  __shared__ long long s_bmin[kMaxBuckets];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, j = tid & (G - 1u), gb = lane & ~(G - 1u);
   const uint32_t gbase = tid & ~(G - 1u);
   const uint32_t per_wg = blockDim.x / G;
   const uint32_t B = p.n_buckets;
   if (tid < 6) s_c[tid] = 0;
-  for (uint32_t k = tid; k < B; k += blockDim.x) s_busy[k] = 0;
+  for (uint32_t k = tid; k < B; k += blockDim.x) {
+    s_busy[k] = 0;
+    s_bmin[k] = LLONG_MAX;
+  }
   __syncthreads();
   const uint32_t na = p.R * p.nloc;
   const uint32_t k0 = blockIdx.x * per_wg, kl = k0 + tid / G;
@@ -3492,7 +3616,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
   const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t rep0 = g0 / p.N;
   const uint32_t ib = static_cast<uint32_t>(cell % B);
-  const bool rx = kl < na && p.impl && node_flagged(p, ib, g, rep, i);
+  const bool rx = kl < na && p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
   const uint32_t n0 = kl < na ? AT(p.n_ops, g, p.NT) : 0u;
   // nodes link_node would change: an echo to send, or an op due (k_active's rule minus the
   // nodes for which link_node only recomputes an unchanged node_onext)
@@ -3623,6 +3747,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
           }
           AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
           s_busy[bk] = 1;
+          atomicMin(&s_bmin[bk], static_cast<long long>(ta));
         } else {
           if (owner) xr.r.flags = static_cast<uint8_t>(xr.r.flags | RF_OWNER);
           const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
@@ -3669,7 +3794,10 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
   }
   __syncthreads();
   for (uint32_t k = tid; k < B; k += blockDim.x)
-    if (s_busy[k]) mark_busy(&p.bucket_cnt[k]);
+    if (s_busy[k]) {
+      mark_busy(&p.bucket_cnt[k]);
+      bmin_lower(p, k, s_bmin[k]);
+    }
   if (tid == 0) {
     // (sends of another replica's node in this workgroup went straight to its stripe)
     unsigned long long* cnt = cnt_stripe(p, rep0);
@@ -3753,7 +3881,10 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
     if (nfound <= static_cast<uint32_t>(kBcastCap)) break;
   }
   const uint32_t n_lists = B + 1 + (p.nranks > 1 ? p.nranks : 0);
-  for (uint32_t k = tid; k < B; k += bs) L.lcnt[k] = 0;
+  for (uint32_t k = tid; k < B; k += bs) {
+    L.lcnt[k] = 0;
+    L.lmin[k] = ~0u;
+  }
   for (uint32_t k = tid; k < n_lists; k += bs) L.lst[k] = 0;
   if (tid == 0) {
     L.nst = 0;
@@ -3938,6 +4069,7 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
           link_stage(p, L, g, bk, x);
           set_flag_once(&AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT));
           atomicAdd(&L.lcnt[bk], 1u);
+          atomicMin(&L.lmin[bk], static_cast<uint32_t>(ta - ca * p.L));
         } else {
           link_stage(p, L, g, B, x);
           if (ca < ovmin) ovmin = ca;
@@ -4017,7 +4149,10 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
   }
   __syncthreads();
   for (uint32_t k = tid; k < B; k += bs)
-    if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
+    if (L.lcnt[k]) {
+      mark_busy(&p.bucket_cnt[k]);
+      bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + L.lmin[k]);
+    }
   if (tid == 0) {
     if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
     AT(p.n_ops, g, p.NT) = L.n_keep;
@@ -4058,7 +4193,10 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
   const uint32_t B = p.n_buckets;
   const uint32_t n_lists = B + 1;
   for (uint32_t base = blockIdx.x * bs; base < na; base += gridDim.x * bs) {  // workgroup-uniform
-    for (uint32_t k = tid; k < B; k += bs) L.lcnt[k] = 0;
+    for (uint32_t k = tid; k < B; k += bs) {
+      L.lcnt[k] = 0;
+      L.lmin[k] = ~0u;
+    }
     for (uint32_t k = tid; k < n_lists; k += bs) L.lst[k] = 0;
     if (tid < 7) s_c[tid] = 0;
     if (tid == 0) {
@@ -4166,6 +4304,7 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
           link_stage(p, L, g, bk, x);
           set_flag_once(&AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT));
           atomicAdd(&L.lcnt[bk], 1u);
+          atomicMin(&L.lmin[bk], static_cast<uint32_t>(ta - ca * p.L));
         } else {
           link_stage(p, L, g, B, x);
           if (ca < ovmin) ovmin = ca;
@@ -4222,7 +4361,10 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
       }
     }
     for (uint32_t k = tid; k < B; k += bs)
-      if (L.lcnt[k]) mark_busy(&p.bucket_cnt[k]);
+      if (L.lcnt[k]) {
+      mark_busy(&p.bucket_cnt[k]);
+      bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + L.lmin[k]);
+    }
     if (tid == 0) {
       if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
       unsigned long long* ks = kst_stripe(p);
@@ -4266,7 +4408,7 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
     const uint64_t k = c0 + j;
     const uint32_t g = static_cast<uint32_t>((k / p.nloc) * p.N + p.nlo + k % p.nloc);
     const uint32_t rep = g / p.N, i = g % p.N;
-    const bool sc = has_start || has_stop || node_flagged(p, b, g, rep, i) || AT(p.node_tnext, g, p.NT) < t_hi;
+    const bool sc = has_start || has_stop || node_flagged_w(p, b, g, rep, i, t_hi) || AT(p.node_tnext, g, p.NT) < t_hi;
     // k_link also runs nodes with reply-slot ops of the previous arrival cell due
     const bool lk = sc || AT(p.node_onext, g, p.NT) < t_hi ||
                     (p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u));
@@ -4335,6 +4477,7 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
           set_err(p, BCSIM_E_OVERFLOW);
       }
       set_flag_once(&AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(B) * p.NT));
+      bmin_lower(p, b, x.cell * p.L + static_cast<long long>(x.r.t_off));
       atomicAdd(&lb[b], 1u);
     } else {
       const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
@@ -4610,6 +4753,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
       if (threadIdx.x == 0) {
         p.bucket_cnt[clr_b] = 0;
         p.x_cnt[clr_b] = 0;
+        p.bmin[clr_b] = LLONG_MAX;
       }
       if (p.mesh)
         for (uint32_t k = threadIdx.x; k < p.R * p.n_tiles; k += blockDim.x)

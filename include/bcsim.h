@@ -294,6 +294,11 @@ int bcsim_set_partition_rccl(bcsim_sim* s, uint32_t rank, uint32_t nranks, const
 int bcsim_reset_kernel_stats(bcsim_sim* s);
 int bcsim_read_kernel_stats(bcsim_sim* s, double* us_out4, double* bytes_out4,
                             uint64_t* launches_out4);
+/* Raw engine work counters since the last bcsim_reset_kernel_stats (testing and
+ * profiling aid, no reference counterpart): [0] records emitted, [1] due ops, [2] touched
+ * edges, [3] kept ops, [4] delivered records, [5] k_scan ops, [6] implicit echoes,
+ * [7] k_scan windows split because a node had more arrivals than its LDS staging. */
+int bcsim_read_engine_counters(bcsim_sim* s, uint64_t* out8);
 
 #ifdef __cplusplus
 }
