@@ -137,8 +137,10 @@ static int dalloc(Sim& s, T** p, size_t count) {
 static int ev_begin(Sim& s, int cls) {
   if (s.ev_used == s.ev_pool.size()) {
     hipEvent_t a, b;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
+    // timing only: no system-scope fence (an L2 writeback + invalidate at every record cost
+    // ~10 us of dispatch gap per event on the MI355X, the gossip step 20 %)
+    HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+    HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
     s.ev_pool.push_back({a, b});
     s.ev_class.push_back(cls);
   }
@@ -957,10 +959,23 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       }
       acc[0] += static_cast<double>(q[7] - q[0]);
     }
-    if (nw && tmax - tmin > 40000) {
+    if (nw && tmax - tmin > 10000) {
       std::fprintf(stderr, "[wgs] cell %lld k_scan span %.2f ms, %u WGs, mean us: total %.1f stage %.1f sort %.1f A %.1f B %.1f C %.1f D %.1f E+wb %.1f\n",
                    cell, (tmax - tmin) / 1e5, nw, acc[0] / nw / 100, acc[1] / nw / 100, acc[2] / nw / 100,
                    acc[3] / nw / 100, acc[4] / nw / 100, acc[5] / nw / 100, acc[6] / nw / 100, acc[7] / nw / 100);
+      uint32_t gs = 0;  // the slowest workgroup's phases
+      unsigned long long ws = 0;
+      for (uint32_t g = 0; g < s.NT; ++g) {
+        const unsigned long long* q = &w[8ull * g];
+        if (q[7] && q[0] && q[7] - q[0] > ws) {
+          ws = q[7] - q[0];
+          gs = g;
+        }
+      }
+      const unsigned long long* q = &w[8ull * gs];
+      std::fprintf(stderr, "[wgs]   slowest g%u %.1f us:", gs, ws / 100.0);
+      for (int k = 1; k < 8; ++k) std::fprintf(stderr, " %.1f", q[k] >= q[k - 1] ? (q[k] - q[k - 1]) / 100.0 : -1.0);
+      std::fprintf(stderr, "\n");
     }
   }
   grid = dim3(s.sparse ? s.grid_link : (n_link + 7) / 8 * 8);

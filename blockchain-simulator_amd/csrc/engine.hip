@@ -1666,6 +1666,21 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
   uint64_t dp = draws0 + ex.y;
   unsigned long long wrong = 0;
   uint32_t n_slot0 = 0, n_slot1 = 0;  // slot replies due in this cell / the next (app delay < L)
+  // the first tick time at or after the window start: an arrival at a tick time is checked
+  // against it without a 64-bit division per arrival
+  const int64_t tk0 = ((t_lo + p.pbft_period - 1) / p.pbft_period) * p.pbft_period;
+  // t and dt come from the staged key; the record is read only by arrivals that produce output
+  // (the PREPARE_RES / COMMIT waves are almost all non-crossing: nothing to read), one arrival
+  // ahead, so its load is in flight while the previous arrival's output is written
+  auto needs_rec = [&](uint32_t r) -> bool {
+    const uint32_t w = acls[r];
+    const uint32_t type = cls_type(w);
+    const bool cross = (w & kCross) != 0;
+    return (ech && !(p.impl && is_main(asec[r]))) || type == PB_PRE_PREPARE || type == PB_PREPARE ||
+           type == PB_VIEW_CHANGE || (cross && (type == PB_PREPARE_RES || type == PB_COMMIT));
+  };
+  Rec nrec{};
+  if (r0 < r1 && needs_rec(r0)) nrec = rec_of(rs, asec[r0]);
 #pragma nounroll
   for (uint32_t r = r0; r < r1; ++r) {
     const uint32_t sec = asec[r];
@@ -1673,21 +1688,18 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
     const uint32_t w = acls[r];
     const uint32_t type = cls_type(w);
     const bool cross = (w & kCross) != 0;
-    // t and dt from the staged key; the record is read only by arrivals that produce output
-    // (the PREPARE_RES / COMMIT waves are almost all non-crossing: nothing to read)
     const uint64_t kk = akey[r];
     const int64_t t = cs + static_cast<int64_t>(kk >> 32);
     const uint32_t dt = ~static_cast<uint32_t>(kk);
     const bool lecho = ech && !(p.impl && is_main(sec));
-    const bool need = lecho || type == PB_PRE_PREPARE || type == PB_PREPARE || type == PB_VIEW_CHANGE ||
-                      (cross && (type == PB_PREPARE_RES || type == PB_COMMIT));
-    Rec rec{};
-    if (need) rec = rec_of(rs, sec);
+    const Rec rec = nrec;  // zero unless needs_rec(r)
+    nrec = Rec{};
+    if (r + 1 < r1 && needs_rec(r + 1)) nrec = rec_of(rs, asec[r + 1]);
     const Msg m = rec_msg(rec);
     const uint32_t le = q - e0;
     const uint32_t origin = p.mesh ? (le < i ? le : le + 1) : AT(p.col, q, p.E);
     const Key key{t, t - static_cast<int64_t>(dt), origin, rec.sub};
-    if (t == ((t / p.pbft_period) * p.pbft_period) && key.ts <= t - p.pbft_period)
+    if (t >= tk0 && (t == tk0 || (t - tk0) % p.pbft_period == 0) && key.ts <= t - p.pbft_period)
       set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
     // pbft-node.cc:175 echo: implicit for main-slot records (k_link), listed otherwise
     if (lecho) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);
