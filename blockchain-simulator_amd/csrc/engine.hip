@@ -1443,22 +1443,40 @@ __device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t*
     asec[k] = ~0u;
   }
   __syncthreads();
+  // bitonic network; the stages with j < 64 compare inside aligned 64-element blocks, so each
+  // wave runs them over its own blocks without workgroup barriers (78 -> 33 barriers at 4096)
+  const uint32_t lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
+  const uint32_t blk = P2 < 64u ? P2 : 64u, ppb = blk / 2, nblk = P2 / blk;
+  const uint32_t own = nblk > wv ? (nblk - wv + nwv - 1) / nwv : 0u;  // blocks of this wave
+  auto ce = [&](uint32_t t, uint32_t j, uint32_t k2) {
+    const uint32_t lo = 2 * t - (t & (j - 1)), hi = lo + j;
+    const bool up = (lo & k2) == 0;
+    const uint64_t ka = akey[lo], kb = akey[hi];
+    const uint32_t sa = asec[lo], sb = asec[hi];
+    if (up == sec_less(kb, sb, ka, sa)) {
+      akey[lo] = kb;
+      akey[hi] = ka;
+      asec[lo] = sb;
+      asec[hi] = sa;
+    }
+  };
   for (uint32_t k2 = 2; k2 <= P2; k2 <<= 1) {
-    for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
-      for (uint32_t t = tid; t < P2 / 2; t += blockDim.x) {
-        const uint32_t lo = 2 * t - (t & (j - 1)), hi = lo + j;
-        const bool up = (lo & k2) == 0;
-        const uint64_t ka = akey[lo], kb = akey[hi];
-        const uint32_t sa = asec[lo], sb = asec[hi];
-        if (up == sec_less(kb, sb, ka, sa)) {
-          akey[lo] = kb;
-          akey[hi] = ka;
-          asec[lo] = sb;
-          asec[hi] = sa;
-        }
-      }
+    uint32_t j = k2 >> 1;
+    for (; j >= blk; j >>= 1) {
+      for (uint32_t t = tid; t < P2 / 2; t += blockDim.x) ce(t, j, k2);
       __syncthreads();
     }
+    for (; j > 0; j >>= 1) {
+      for (uint32_t u = lane; u < own * ppb; u += 64) {
+        const uint32_t b = wv + nwv * (u / ppb);
+        ce(b * ppb + u % ppb, j, k2);
+      }
+      // the wave's LDS writes complete before its next stage reads them
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
   }
 }
 
@@ -4772,8 +4790,9 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
           p.rtile[static_cast<size_t>(clr_b) * p.R * p.n_tiles + k] = 0;
     }
   }
-  // scal[0] = the next event time (timers and pending ops), scal[3] = the next timer alone
-  __shared__ long long red[1024], redt[1024];
+  // scal[0] = the next event time (timers and pending ops), scal[3] = the next timer alone;
+  // wave minima by shuffles, one LDS slot per wave, one barrier
+  __shared__ long long red[kMaxWaves], redt[kMaxWaves];
   long long m = LLONG_MAX, mt = LLONG_MAX;
   const uint32_t nb = gridDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < p.NT; k += nb * blockDim.x) {
@@ -4781,32 +4800,49 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     m = min(m, min(a, b));
     mt = min(mt, a);
   }
-  red[threadIdx.x] = m;
-  redt[threadIdx.x] = mt;
-  __syncthreads();
-  for (uint32_t s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      red[threadIdx.x] = min(red[threadIdx.x], red[threadIdx.x + s]);
-      redt[threadIdx.x] = min(redt[threadIdx.x], redt[threadIdx.x + s]);
-    }
-    __syncthreads();
+  for (int d = 32; d > 0; d >>= 1) {
+    m = min(m, static_cast<long long>(__shfl_xor(m, d, 64)));
+    mt = min(mt, static_cast<long long>(__shfl_xor(mt, d, 64)));
   }
-  if (threadIdx.x != 0) return;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  if (lane == 0) {
+    red[wv] = m;
+    redt[wv] = mt;
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  m = lane < nwv ? red[lane] : LLONG_MAX;
+  mt = lane < nwv ? redt[lane] : LLONG_MAX;
+  for (int d = 32; d > 0; d >>= 1) {
+    m = min(m, static_cast<long long>(__shfl_xor(m, d, 64)));
+    mt = min(mt, static_cast<long long>(__shfl_xor(mt, d, 64)));
+  }
   if (nb == 1) {
-    p.scal[0] = red[0];
-    p.scal[3] = redt[0];
+    if (lane == 0) {
+      p.scal[0] = m;
+      p.scal[3] = mt;
+    }
     return;
   }
-  __hip_atomic_store(&p.nxt_part[blockIdx.x], red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&p.nxt_part[kNextBlocks + blockIdx.x], redt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __threadfence();
-  if (atomicAdd(p.nxt_done, 1u) != nb - 1) return;
+  bool last = false;
+  if (lane == 0) {
+    __hip_atomic_store(&p.nxt_part[blockIdx.x], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&p.nxt_part[kNextBlocks + blockIdx.x], mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    last = atomicAdd(p.nxt_done, 1u) == nb - 1;
+  }
+  if (!__shfl(static_cast<int>(last), 0, 64)) return;
   __threadfence();
   long long mm = LLONG_MAX, mmt = LLONG_MAX;
-  for (uint32_t b = 0; b < nb; ++b) {
+  for (uint32_t b = lane; b < nb; b += 64) {  // the last workgroup's first wave combines the partials
     mm = min(mm, __hip_atomic_load(&p.nxt_part[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     mmt = min(mmt, __hip_atomic_load(&p.nxt_part[kNextBlocks + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
+  for (int d = 32; d > 0; d >>= 1) {
+    mm = min(mm, static_cast<long long>(__shfl_xor(mm, d, 64)));
+    mmt = min(mmt, static_cast<long long>(__shfl_xor(mmt, d, 64)));
+  }
+  if (lane != 0) return;
   p.scal[0] = mm;
   p.scal[3] = mmt;
   __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
