@@ -53,6 +53,10 @@ struct Sim {
   hipStream_t stream = nullptr;
   KP kp{};
   KP* kp_dev = nullptr;  // device copy of kp passed to every kernel
+  // PBFT, dense: kp with a doubled k_scan staging window, for launches of few nodes (the
+  // leader's oversized cells: one window instead of several, occupancy is moot there)
+  KP* kp_dev_big = nullptr;
+  size_t lds_big = 0;
   std::vector<void*> allocs;
   // host mirrors
   Ctl* ctl_h = nullptr;  // pinned
@@ -797,6 +801,18 @@ static int setup_device(Sim& s) {
   HIPCHK(hipDeviceSynchronize());
   if ((rc = dalloc(s, &s.kp_dev, 1))) return rc;
   HIPCHK(hipMemcpy(s.kp_dev, &s.kp, sizeof(KP), hipMemcpyHostToDevice));
+  if (!s.sparse && s.P == 1 && c.protocol == BCSIM_PBFT) {
+    KP kb = s.kp;
+    kb.cap_arr = 2 * s.kp.cap_arr;
+    const size_t lb = scan_lds_bytes(kb);
+    if (lb + sizeof(ScanShared) <= 160 * 1024) {
+      if ((rc = dalloc(s, &s.kp_dev_big, 1))) return rc;
+      HIPCHK(hipMemcpy(s.kp_dev_big, &kb, sizeof(KP), hipMemcpyHostToDevice));
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, false>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lb)));
+      s.lds_big = lb;
+    }
+  }
   s.bcnt.assign(s.B, 0);
   s.xcnt.assign(s.B, 0);
   s.next_tick = (c.protocol == BCSIM_PBFT) ? p.pbft_period : INT64_MAX;
@@ -854,6 +870,7 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
 }
 #define launch(s, cls, kernel, ...) launch_named(s, #kernel, cls, kernel, __VA_ARGS__)
 
+constexpr uint32_t kFewScan = 64;  // k_scan launches of at most this many nodes use kp_dev_big
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
   dim3 grid(s.grid_scan), block(s.bs_scan);
@@ -919,6 +936,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
             : launch(s, KS_SCAN, k_scan<P, false>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa))
   if (grid.x == 0)
     rc = BCSIM_OK;  // no node has work in the window
+  else if (s.kp_dev_big && !s.sparse && s.P == 1 && grid.x <= kFewScan)
+    // a few nodes (the leader's cells): the doubled staging window, a 1024-lane workgroup each
+    rc = launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false>), grid, dim3(1024), s.lds_big, s.kp_dev_big, cell, lo, hi, cs, fw,
+                xa);
   else if (s.sparse && s.cfg.protocol == BCSIM_PAXOS && s.paxos_fast) {
     // sparse Paxos: one lane per node takes the acceptors' request windows; the generic
     // kernel walks the rest (list 2)
