@@ -1374,6 +1374,12 @@ static int run(Sim& s, int64_t t_until) {
     if (s.cfg.stop_ns >= 0 && s.cfg.stop_ns < hi) s.stop_pending = false;
     s.t_done = hi;
     ++s.cells;
+    if (hi == ce && !s.sparse && (c / s.B) % 32 == 31) {
+      // inbox-slot tags (engine.hip cell_tag) repeat every 32 ring turns: zero the finished
+      // bucket once per 32 turns instead of clearing every delivered slot
+      const size_t per = static_cast<size_t>(s.R) * s.kp.E_loc;
+      HIPCHK(hipMemsetAsync(s.kp.inbox + static_cast<size_t>(c % s.B) * per, 0, per * sizeof(Rec), s.stream));
+    }
     if (hi == ce) {
       s.grouped_cell = -1;
       s.bcnt[c % s.B] = 0;

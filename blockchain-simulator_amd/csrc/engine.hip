@@ -508,6 +508,21 @@ __device__ inline void st_rec(Rec* p, const Rec& r) {
   *reinterpret_cast<uint4*>(p) = v;
 }
 __device__ inline void clr_rec(Rec* p) { *reinterpret_cast<uint4*>(p) = make_uint4(0, 0, 0, 0); }
+// Inbox-slot records carry a ring-turn tag in flags bits 3-7: (arrival cell / B) mod 32.  A slot
+// is live for cell c only with the tag of c, so a delivered record needs no clear: it goes stale
+// when the bucket comes round again, and the host zeroes a bucket once every 32 turns
+// (bcsim_capi.hip run()) before a tag can repeat.
+__device__ inline uint32_t cell_tag(const KP& p, long long cell) {
+  return static_cast<uint32_t>((cell / p.n_buckets) & 31);
+}
+__device__ inline bool slot_live(uint32_t flags, uint32_t tag) {
+  return (flags & RF_VALID) && ((flags >> 3) & 31u) == tag;
+}
+// the tag of a record emitted in cell `cell` for cell + rel (1 <= rel < B), without a division:
+// cq = cell / B, cr = cell % B
+__device__ inline uint32_t emit_tag(long long cq, uint32_t cr, long long rel, uint32_t B) {
+  return static_cast<uint32_t>((cq + ((cr + rel) >= B ? 1 : 0)) & 31);
+}
 
 // 32-byte ops as two dwordx4 accesses
 __device__ inline Op ld_op(const Op* q) {
@@ -830,7 +845,7 @@ __device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long lon
     const uint32_t rep = o.g / p.N;
     XRec x = o;
     const bool owner = (x.r.flags & RF_OWNER) != 0;
-    x.r.flags = static_cast<uint8_t>(x.r.flags & ~RF_OWNER);
+    x.r.flags = static_cast<uint8_t>((x.r.flags & (RF_VALID | RF_BIG)) | (cell_tag(p, o.cell) << 3));
     if (owner) {
       st_rec(&AT(p.inbox, inbox_idx(p, b, rep, x.slot), p.cap_inbox), x.r);
     } else {
@@ -1293,6 +1308,7 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
                                  const XRec* xs, uint32_t xn, long long cs, long long wa, long long wb,
                                  uint64_t* akey, uint32_t* asec, bool store) {
   const uint32_t tid = threadIdx.x;
+  const uint32_t tag = cell_tag(p, cs / p.L);
   uint32_t n = 0;
   for (uint32_t base = 0; base < deg; base += 4 * blockDim.x) {
     Rec rr[4];
@@ -1306,7 +1322,7 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
     for (uint32_t j = 0; j < 4; ++j) {
       const uint32_t k = base + j * blockDim.x + tid;
       const long long t = cs + rr[j].t_off;
-      vv[j] = k < deg && (rr[j].flags & RF_VALID) && t >= wa && t < wb;
+      vv[j] = k < deg && slot_live(rr[j].flags, tag) && t >= wa && t < wb;
     }
     // one block scan ranks all four chunks: chunk j's records follow chunks < j (slot order)
     uint4 tot;
@@ -1353,6 +1369,7 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
 __device__ long long window_split(const KP& p, ScanShared& S, const Rec* slots, uint32_t deg, const XRec* xs,
                                   uint32_t xn, long long cs, long long wa, long long hi, uint32_t* hist) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t tag = cell_tag(p, cs / p.L);
   const uint32_t lg = p.cap_arr >= 128 ? 8u : 6u;  // 2^lg bins (<= 2 * cap_arr u32 of staging)
   const uint32_t nb = 1u << lg;
   long long lo = wa;
@@ -1373,7 +1390,7 @@ __device__ long long window_split(const KP& p, ScanShared& S, const Rec* slots, 
       for (uint32_t j = 0; j < 4; ++j) {
         const uint32_t k = base + j * blockDim.x + tid;
         const long long t = cs + rr[j].t_off;
-        if (k < deg && (rr[j].flags & RF_VALID) && t >= lo && t < hi)
+        if (k < deg && slot_live(rr[j].flags, tag) && t >= lo && t < hi)
           atomicAdd(&hist[static_cast<uint32_t>((t - lo) >> sh)], 1u);
       }
     }
@@ -2480,7 +2497,7 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
   if (fast && j < deg && flagged) {
     r = ld_rec(p.inbox + inbox_idx(p, b, rep, e0 + j));
     t = cs + r.t_off;
-    v = (r.flags & RF_VALID) && t >= t_lo && t < t_hi;
+    v = slot_live(r.flags, cell_tag(p, cell)) && t >= t_lo && t < t_hi;
     dt = static_cast<uint32_t>(prop_of_slot(p, e0 + j) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
     k64 = (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~dt);
   }
@@ -3036,8 +3053,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     RawOp eo = raw_zero();
     if (rx) {
       const long long ta0 = cs + r0.t_off;
-      if ((r0.flags & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
-        clr_rec(ir);
+      if (slot_live(r0.flags, cell_tag(p, cell)) && ta0 >= t_lo && ta0 < t_hi) {
         if (p.echo) {
           const int bg = (r0.flags & RF_BIG) ? 1 : 0;
           const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
@@ -3170,7 +3186,8 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       ++n_rec;
       // the record: t_off | sub | payload word (f0, f1) | (f2, type, flags) -- raw words only
       const uint32_t tof = static_cast<uint32_t>(ta - ca * p.L);
-      const uint32_t w3 = (o.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+      const uint32_t w3 = (o.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24) |
+          (emit_tag(cell / p.n_buckets, static_cast<uint32_t>(cell % p.n_buckets), ca - cell, p.n_buckets) << 27);
       Rec r;
       {
         const uint4 rv = make_uint4(tof, sub, o.b.z, w3);
@@ -3441,8 +3458,7 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
       if (rx) {
         const uint32_t fl = r0[u].w >> 24;
         const long long ta0 = cs + r0[u].x;
-        if ((fl & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
-          clr_rec(in_row + le);
+        if (slot_live(fl, cell_tag(p, cell)) && ta0 >= t_lo && ta0 < t_hi) {
           if (p.echo) {
             ebig = (fl & RF_BIG) ? 1 : 0;
             const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
@@ -3535,7 +3551,8 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
         }
         ++n_rec;
         const uint32_t tof = static_cast<uint32_t>(ta - ca * p.L);
-        const uint32_t w3 = ow3 | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+        const uint32_t w3 = ow3 | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24) |
+            (emit_tag(cell / p.n_buckets, static_cast<uint32_t>(cell % p.n_buckets), ca - cell, p.n_buckets) << 27);
         Rec r;
         {
           const uint4 rv = make_uint4(tof, osub, ow2, w3);
@@ -3701,8 +3718,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
       Rec* ir = p.inbox + inbox_idx(p, ib, rep, e);
       const Rec r0 = ld_rec(ir);
       const long long ta0 = cell * p.L + r0.t_off;
-      if ((r0.flags & RF_VALID) && ta0 >= t_lo && ta0 < t_hi) {
-        clr_rec(ir);
+      if (slot_live(r0.flags, cell_tag(p, cell)) && ta0 >= t_lo && ta0 < t_hi) {
         if (p.echo) {
           const int bg = (r0.flags & RF_BIG) ? 1 : 0;
           const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
@@ -3753,7 +3769,8 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
         }
         ++c_rec;
         const uint32_t tof = static_cast<uint32_t>(ta - ca * p.L);
-        const uint32_t w3 = (x.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+        const uint32_t w3 = (x.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24) |
+            (emit_tag(cell / p.n_buckets, static_cast<uint32_t>(cell % p.n_buckets), ca - cell, p.n_buckets) << 27);
         XRec xr;
         {
           const uint4 rv = make_uint4(tof, sub, x.b.z, w3);
@@ -4496,7 +4513,7 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
     if (x.cell < g_cur + static_cast<long long>(B)) {
       const uint32_t b = static_cast<uint32_t>(x.cell % B);
       const bool owner = (x.r.flags & RF_OWNER) != 0;
-      x.r.flags = static_cast<uint8_t>(x.r.flags & ~RF_OWNER);
+      x.r.flags = static_cast<uint8_t>((x.r.flags & (RF_VALID | RF_BIG)) | (cell_tag(p, x.cell) << 3));
       if (owner) {
         st_rec(&AT(p.inbox, inbox_idx(p, b, rep, x.slot), p.cap_inbox), x.r);
       } else {
