@@ -1085,9 +1085,9 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
 static int group_cell(Sim& s, long long cell) {
   const uint32_t b = static_cast<uint32_t>(cell % s.B);
   if (s.ov_min <= cell + static_cast<long long>(s.B) - 1) {
-    uint32_t nov = 0;
-    HIPCHK(hipMemcpyAsync(&nov, s.kp.ov_cnt, 4, hipMemcpyDeviceToHost, s.stream));
-    HIPCHK(hipStreamSynchronize(s.stream));
+    // the overflow count as of the last read-back (nothing appends to the list between the
+    // end-of-cell read-back and here)
+    const uint32_t nov = s.ctl_h->ov_cnt;
     long long big = LLONG_MAX;
     HIPCHK(hipMemcpyAsync(s.kp.scal + 1, &big, 8, hipMemcpyHostToDevice, s.stream));
     if (nov) {

@@ -3625,7 +3625,9 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   const unsigned long long t0 = p.wgt ? wg_t0 : 0ull;
   unsigned long long ph[4] = {t0, t0, t0, t0};
   const LinkCounts c8{dropped, sends, n_rec, st_ops, st_edges, st_echo, 0u, 0u};
-  link_finish(p, L, g, ops, n, t_hi, B + 1, ovmin, c8, sl1 && final_win, rx && final_win, obp, fidx, t0, ph, n);
+  // every op due (the broadcasts just sent): nothing to compact, no op to read again
+  link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, B + 1, ovmin, c8, sl1 && final_win, rx && final_win, obp, fidx, t0,
+              ph, n);
 }
 
 // ---------------------------------------------------------------------------
