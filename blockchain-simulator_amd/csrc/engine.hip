@@ -1480,10 +1480,12 @@ __device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t*
   for (uint32_t k2 = 2; k2 <= P2; k2 <<= 1) {
     uint32_t j = k2 >> 1;
     for (; j >= blk; j >>= 1) {
+#pragma unroll 4
       for (uint32_t t = tid; t < P2 / 2; t += blockDim.x) ce(t, j, k2);
       __syncthreads();
     }
     for (; j > 0; j >>= 1) {
+#pragma unroll 4
       for (uint32_t u = lane; u < own * ppb; u += 64) {
         const uint32_t b = wv + nwv * (u / ppb);
         ce(b * ppb + u % ppb, j, k2);
