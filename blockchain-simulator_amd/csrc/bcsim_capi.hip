@@ -1022,9 +1022,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     // launch of the k_link class
     const bool timed = (kstat_mask() >> KS_LINK) & 1u;
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
+    // (list 3 holds a few nodes, the leader's cells among them: wide workgroups)
     if ((rc = launch(s, -1, k_link_mesh, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
-        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(256, s.grid_link)), dim3(s.bs_link),
-                     link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
+        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(256, s.grid_link)),
+                     dim3(std::min<uint32_t>(1024, 4 * s.bs_link)), link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
       return rc;
     if (timed) {
       if ((rc = ev_end(s))) return rc;
