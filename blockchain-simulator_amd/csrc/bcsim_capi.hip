@@ -47,6 +47,7 @@ struct Sim {
   int64_t L = 0;
   int64_t t_done = 0;
   long long grouped_cell = -1;
+  long long last_full = -1;  // last cell processed to its end (hi == ce)
   int64_t next_tick = INT64_MAX;  // PBFT
   bool start_pending = true;
   bool stop_pending = true;   // Application::Stop at cfg.stop_ns (if >= 0)
@@ -80,6 +81,8 @@ struct Sim {
   long long next_local = LLONG_MAX, ov_min = LLONG_MAX;
   long long n_alive = 0;
   uint64_t cells = 0;
+  uint64_t tag_zeroes = 0;  // bucket zeroings of the slot-tag invariant (zero_tag_buckets)
+  std::vector<long long> zeroed_turn;  // per bucket: the ring turn after which it was last zeroed
   // timing
   double us[4] = {0, 0, 0, 0};
   uint64_t launches[4] = {0, 0, 0, 0};
@@ -815,6 +818,7 @@ static int setup_device(Sim& s) {
   }
   s.bcnt.assign(s.B, 0);
   s.xcnt.assign(s.B, 0);
+  s.zeroed_turn.assign(s.B, -1);  // hipMemset above: every bucket is clean before turn 0
   s.next_tick = (c.protocol == BCSIM_PBFT) ? p.pbft_period : INT64_MAX;
   s.n_alive = (c.protocol == BCSIM_PBFT) ? 1 : 0;  // STARTs arm the ticks
   return BCSIM_OK;
@@ -1267,6 +1271,49 @@ static int ensure_topology(Sim& s) {
   return BCSIM_OK;
 }
 
+// Inbox-slot records carry a 5-bit ring-turn tag (engine.hip cell_tag: (cell / B) mod 32), so
+// a delivered record needs no clear; the invariant that makes a matching tag mean "live" is
+// that bucket b holds no record of turn T - 32k when turn T of b begins.  It holds because
+// every cell s whose turn ends a 32-turn period ((s / B) % 32 == 31) zeroes its bucket once it
+// is over -- the cells run() processes to their end AND the cells it skips for lack of work
+// (no live record sits in a skipped cell's bucket, and none for a later turn of it exists
+// yet: such a record is emitted at a cell > s, or rebinned by group_cell of a cell > s, both
+// after this call).  Cells [a, b] are finished or skipped; at most B memsets.
+static int zero_tag_buckets(Sim& s, long long a, long long b) {
+  if (s.sparse || b < a) return BCSIM_OK;
+  const size_t per = static_cast<size_t>(s.R) * s.kp.E_loc;
+  std::vector<uint8_t> hit(s.B, 0);
+  if (b - a + 1 >= 32ll * s.B) {
+    std::fill(hit.begin(), hit.end(), 1);
+  } else {
+    for (long long x = a; x <= b; ++x)
+      if ((x / s.B) % 32 == 31) hit[x % s.B] = 1;
+  }
+  for (uint32_t k = 0; k < s.B; ++k)
+    if (hit[k]) {
+      HIPCHK(hipMemsetAsync(s.kp.inbox + static_cast<size_t>(k) * per, 0, per * sizeof(Rec), s.stream));
+      ++s.tag_zeroes;
+      // the latest turn of bucket k in [a, b]
+      const long long lastk = b - ((b % s.B - k + s.B) % s.B);
+      s.zeroed_turn[k] = std::max(s.zeroed_turn[k], lastk / s.B);
+    }
+  return BCSIM_OK;
+}
+
+// The invariant itself, checked before turn c / B of bucket c % B begins: records of turns
+// Z+1 .. T-1 (Z = the turn after which the bucket was last zeroed) may still sit in it, and
+// none of them may carry the tag of T, i.e. T - Z <= 32.
+static int check_tag_invariant(Sim& s, long long c) {
+  if (s.sparse) return BCSIM_OK;
+  const long long T = c / s.B, Z = s.zeroed_turn[c % s.B];
+  if (T - Z > 32) {
+    g_detail = "inbox-slot tag invariant broken: bucket " + std::to_string(c % s.B) + " last zeroed after turn " +
+               std::to_string(Z) + ", turn " + std::to_string(T) + " begins";
+    return BCSIM_E_STATE;
+  }
+  return BCSIM_OK;
+}
+
 static int run(Sim& s, int64_t t_until) {
   int rc;
   if (!s.started) {
@@ -1332,7 +1379,13 @@ static int run(Sim& s, int64_t t_until) {
       break;
     }
     int lrc = 0;  // this rank's status of the cell
-    if (s.grouped_cell != c) lrc = group_cell(s, c);
+    if (s.grouped_cell != c) {
+      // cells (last_full, c) had no work and were skipped: their buckets still owe the
+      // once-per-32-turns zeroing of the inbox-slot tags (before group_cell can rebin into them)
+      if (c > s.last_full + 1) lrc = zero_tag_buckets(s, s.last_full + 1, c - 1);
+      if (!lrc) lrc = check_tag_invariant(s, c);
+      if (!lrc) lrc = group_cell(s, c);
+    }
     const bool tick = s.cfg.protocol == BCSIM_PBFT && s.n_alive > 0 && s.next_tick >= lo && s.next_tick < hi;
     if (tick) {
       const long long tk = s.next_tick;
@@ -1375,13 +1428,10 @@ static int run(Sim& s, int64_t t_until) {
     if (s.cfg.stop_ns >= 0 && s.cfg.stop_ns < hi) s.stop_pending = false;
     s.t_done = hi;
     ++s.cells;
-    if (hi == ce && !s.sparse && (c / s.B) % 32 == 31) {
-      // inbox-slot tags (engine.hip cell_tag) repeat every 32 ring turns: zero the finished
-      // bucket once per 32 turns instead of clearing every delivered slot
-      const size_t per = static_cast<size_t>(s.R) * s.kp.E_loc;
-      HIPCHK(hipMemsetAsync(s.kp.inbox + static_cast<size_t>(c % s.B) * per, 0, per * sizeof(Rec), s.stream));
-    }
     if (hi == ce) {
+      // (a failure rides the next cell's collective like any other rank-local one)
+      if (!lerr) lerr = zero_tag_buckets(s, c, c);
+      s.last_full = c;
       s.grouped_cell = -1;
       s.bcnt[c % s.B] = 0;
       s.xcnt[c % s.B] = 0;

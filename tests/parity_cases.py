@@ -99,7 +99,33 @@ def cases():
         # the reference protocols on a non-mesh graph (CSR path without the mesh transpose)
         "pbft32_d6_ctr": _cfg(P, 32, delay_mode=J, rng_mode=K, seed=4, pbft_rounds=6, pbft_block_bytes=1500),
         "raft48_d6_ctr": _cfg(R, 48, delay_mode=J, rng_mode=K, seed=2, t_end_ns=3_000_000_000),
+        # a 2-bucket ring: the inbox-slot ring-turn tags (engine.hip cell_tag, 32 turns) wrap
+        # every 64 cells (~0.2 s), across idle cells the engine skips (run() zero_tag_buckets),
+        # with jittered sends beyond the ring (overflow + rebin) and varying slot use
+        "pbft12_jitter_b2": _cfg(P, 12, delay_mode=J, rng_mode=K, seed=19, pbft_rounds=40, n_buckets=2,
+                                 pbft_block_bytes=1500),
+        "raft16_fixed_b2": _cfg(R, 16, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=3_000_000_000, n_buckets=2),
+        "gossip64_d4_b2": _cfg(GS, 64, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=20, pbft_block_bytes=1000,
+                               stop_ns=-1, n_buckets=2),
     }
+
+
+def fullsize_cases():
+    """BASELINE configs at full size (too big for the oracle): the bench configurations
+    themselves, compared between engine runs (partitioned vs single, tests/test_partition.py)
+    and through size-independent properties (tests/test_fullsize.py)."""
+    import bcsim
+    c4 = bcsim.preset("c4_pbft4096")   # bench.py: 50 KB blocks, glibc lottery on, fixed 3 ms
+    c4.pbft_rounds = 4
+    c4.stop_ns = -1
+    c5 = bcsim.preset("c5_gossip65536")  # bench.py --workload gossip (echo on)
+    c5.pbft_rounds = 3
+    return {"c4_bench_r4": c4, "c5_gossip_r3": c5}
+
+
+def any_case(name):
+    c = cases()
+    return c[name] if name in c else fullsize_cases()[name]
 
 
 # non-mesh cases: name -> (n, degree, seed) of bcsim.random_regular
@@ -110,6 +136,7 @@ TOPOLOGY = {
     "pbft32_d6_ctr": (32, 6, 3),
     "gossip64_d4_droptail": (64, 4, 1),
     "raft48_d6_ctr": (48, 6, 8),
+    "gossip64_d4_b2": (64, 4, 1),
 }
 
 
@@ -120,6 +147,7 @@ TOPOLOGY_PROP = {
     "gossip96_d6_hetero_prop": (3_000_000, 2_000_000),
 }
 TOPOLOGY["gossip96_d6_hetero_prop"] = (96, 6, 11)
+TOPOLOGY["c5_gossip_r3"] = (65536, 8, 1)
 
 
 def hetero_prop(row, col, base, spread):
@@ -141,7 +169,7 @@ def topology(name):
     if name in TOPOLOGY:
         row, col = bcsim.random_regular(*TOPOLOGY[name])
     else:
-        n = cases()[name].n_nodes
+        n = any_case(name).n_nodes
         row, col = bcsim.full_mesh(n)
     prop = hetero_prop(row, col, *TOPOLOGY_PROP[name]) if name in TOPOLOGY_PROP else None
     return row, col, prop

@@ -25,13 +25,12 @@ def _worker(rank, world, port, names, transport, q):
     sys.path[:0] = [REPO, os.path.join(REPO, "tests"), os.path.join(REPO, "blockchain-simulator_amd")]
     import torch.distributed as dist
     import bcsim
-    from parity_cases import cases, topology
+    from parity_cases import any_case, topology
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        allc = cases()
         for name in names:
-            cfg = allc[name]
+            cfg = any_case(name)
             try:
                 with bcsim.Simulator(cfg) as s:
                     topo = topology(name)

@@ -1,6 +1,11 @@
 """BASELINE configs at full size on the GPU, checked through size-independent
 properties (the oracle is too slow at these sizes):
 
+* C4  the bench configuration itself (bench.py: 50 KB blocks on saturated 3 Mbps links,
+      fixed 3 ms app delay, the glibc rand()%100==5 lottery on, pbft-node.cc:371-411) run
+      to quiescence over 66 blocks, so that the lottery hits at draws 60 and 65 (the glibc
+      seed-1 stream, tests/golden/glibc_rand_seed1.json): deliveries per type, one commit
+      per (node, block) in order with the leader's value, two VIEW records.
 * C4  PBFT n=4096 full mesh, unsaturated blocks, view change off: every round
       delivers exactly 3(N-1)^2 + (N-1) messages (pbft-node.cc:193-265) and every
       node commits each sequence once, in order, with the leader's value.
@@ -53,6 +58,15 @@ def test_c4_pbft4096_message_and_commit_kats(engine_lib):
     assert per_node[0] == [(k, 0) for k in range(rounds)]
     blocks = [r for r in tr if r[6] == TR["PBFT_BLOCK"]]
     assert [r[7] for r in sorted(blocks)] == list(range(rounds)) and {r[5] for r in blocks} == {0}
+
+
+@pytest.mark.timeout(170)
+def test_c4_bench_config_saturated_lottery_kats(engine_lib):
+    import bcsim
+    from fullsize_props import bench_config, check_bench_config
+    c = bench_config(4096)
+    tr, cnt, st = bcsim.run(c)
+    check_bench_config(tr, cnt, st, c)
 
 
 def bfs(row, col, src):

@@ -103,7 +103,7 @@ def test_merge_matches_single_process_shape():
 
 # cases whose RNG is per node (counter) or absent: the glibc global stream of
 # Raft is a single-GPU configuration (bcsim_run returns E_UNSUPPORTED)
-PART_CASES = ["pbft16_fixed_100", "pbft5_odd", "pbft12_jitter_ctr", "pbft8_rep3_ctr", "pbft8_compat",
+PART_CASES = ["pbft12_jitter_b2", "pbft16_fixed_100", "pbft5_odd", "pbft12_jitter_ctr", "pbft8_rep3_ctr", "pbft8_compat",
               "raft16_jitter_ctr", "paxos8_fixed", "paxos32_jitter_ctr", "paxos16_jitter_rep4",
               "gossip64_d4_fixed", "gossip200_d8_jitter_ctr", "gossip24_mesh", "pbft32_d6_ctr",
               "pbft16_droptail_100", "gossip64_d4_droptail", "pbft12_hetero_prop", "paxos32_jitter_k4"]
@@ -134,6 +134,28 @@ def test_partitioned_n512_matches_oracle(engine_lib):
     assert err is None, err
     d = compare(oracle.run(cases()[name]), merged)
     assert d is None, d
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["c4_bench_r4", "c5_gossip_r3"])
+def test_partitioned_fullsize_equals_single(name, engine_lib):
+    """SURVEY.md §4 item 4 at BASELINE size: the bench configurations themselves --
+    C4 PBFT n=4096 (50 KB blocks, glibc lottery on, 4 rounds; blockchain-simulator.cc:34-51
+    mesh) and C5 gossip n=65536 on the random 8-regular graph (3 rounds, echoes on) --
+    node-partitioned over 2 ranks sharing the GPU (host transport) give merged traces and
+    counters identical to the single-process run, bit for bit."""
+    import bcsim
+    import partition_run
+    from parity_cases import any_case
+    topo = topology(name)
+    single = bcsim.run(any_case(name), topology=topo)
+    assert single[2]["error"] == 0 and single[2]["quiescent"]
+    assert single[1]["delivered_total"] > 0
+    merged, err = partition_run.run(2, [name], transport="host", timeout=540)[name]
+    assert err is None, err
+    d = compare(single, merged)
+    assert d is None, f"{name} world=2: {d}"
 
 
 def _rccl1_worker(port, names, q):
