@@ -202,7 +202,18 @@ constexpr int kMaxRanks = 16;
 __device__ inline void set_err_(const KP& p, int32_t code, int line) {
   if (atomicCAS(p.err, 0, code) == 0) atomicCAS(p.dbg, 0, line);
 }
-#define set_err(pp, code) set_err_((pp), (code), __LINE__)
+// The code and line are materialised by volatile asm INSIDE the (cold) error branch: as plain
+// constants, loop-invariant code motion hoisted every call site's pair out of the per-arrival
+// loops into registers live across the whole kernel, and in the 128-VGPR kernels those got
+// spilled to scratch (k_scan<PBFT>: most of its 116 B/lane, written by every lane of every
+// workgroup).
+#define set_err(pp, code)                                                      \
+  do {                                                                         \
+    int32_t c_, l_;                                                            \
+    asm volatile("v_mov_b32 %0, %1" : "=v"(c_) : "i"(static_cast<int32_t>(code))); \
+    asm volatile("v_mov_b32 %0, %1" : "=v"(l_) : "i"(__LINE__));              \
+    set_err_((pp), c_, l_);                                                    \
+  } while (0)
 
 // Checked array access.  In BCSIM_CHECKED builds an out-of-range index is
 // recorded (source line in p.dbg, BCSIM_E_OVERFLOW in p.err) and the wave
@@ -590,13 +601,23 @@ __device__ inline RawOp slot_op(const KP& p, const uint4 w, uint32_t i, uint32_t
                make_uint4(w.z, e, w.w, f2 | (kPbPrepareRes << 16) | (static_cast<uint32_t>(OP_SEND) << 24))};
 }
 
+// threadIdx.x behind an empty volatile asm: values derived from it (lane, wave, loop bounds
+// and trip counts of the strided loops) are recomputed in each phase instead of being hoisted
+// by loop-invariant code motion into registers live across the whole kernel -- in the
+// 128-VGPR kernels those were spilled to scratch and reloaded by every lane
+__device__ inline uint32_t tidx() {
+  uint32_t t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 // ---- block-wide primitives (blockDim.x a multiple of 64, <= 1024) ----------
 constexpr int kMaxWaves = 16;
 
 // Ordered compaction rank: exclusive position of this thread's flag among
 // the block's set flags in thread order; `total` = number of set flags.
 __device__ inline uint32_t block_rank(bool f, uint32_t* wcnt, uint32_t& total) {
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t lane = tidx() & 63u, w = tidx() >> 6, nw = blockDim.x >> 6;
   const unsigned long long m = __ballot(f);
   const uint32_t below = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
   if (lane == 0) wcnt[w] = static_cast<uint32_t>(__popcll(m));
@@ -617,7 +638,7 @@ __device__ inline uint32_t list_append(uint32_t* counter) { return atomicAdd(cou
 
 // Exclusive block scan of four u32 lanes at once; totals in `tot`.
 __device__ inline uint4 block_scan4(uint4 v, uint4* wsum, uint4& tot) {
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t lane = tidx() & 63u, w = tidx() >> 6, nw = blockDim.x >> 6;
   uint4 x = v;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -655,7 +676,7 @@ __device__ inline uint4 block_scan4(uint4 v, uint4* wsum, uint4& tot) {
 // returns the total.  All threads must call it.
 __device__ inline uint32_t block_scan_array(uint32_t* a, uint32_t n, uint4* wsum) {
   const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
-  const uint32_t b0 = min(n, threadIdx.x * per), b1 = min(n, b0 + per);
+  const uint32_t b0 = min(n, tidx() * per), b1 = min(n, b0 + per);
   uint32_t s = 0;
   for (uint32_t k = b0; k < b1; ++k) s += a[k];
   uint4 tot;
@@ -681,7 +702,7 @@ __device__ inline uint32_t wave_sum(uint32_t v) {
 // LDS atomics; all lanes of the wave must call it).
 __device__ inline void wave_add_by_key(bool act, uint32_t key, uint32_t inc, unsigned long long* lds) {
   unsigned long long rem = __ballot(act);
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = tidx() & 63u;
   while (rem) {
     const int ld = __ffsll(static_cast<long long>(rem)) - 1;
     const uint32_t kl = __shfl(key, ld, 64);
@@ -703,7 +724,7 @@ __device__ inline void wave_add_by_key(bool act, uint32_t key, uint32_t inc, uns
 __global__ void k_xcount(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = blockIdx.x * blockDim.x + tidx();
   if (k >= n) return;
   const uint32_t g = AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf).g;
   atomicAdd(&AT(p.seg_cnt, g, p.NT), 1u);
@@ -715,7 +736,7 @@ __global__ __launch_bounds__(1024) void k_offsets(const KP* __restrict__ pk) {
   BAIL_IF_ERR();
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t carry;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t tid = tidx(), lane = tid & 63, w = tid >> 6;
   if (tid == 0) carry = 0;
   __syncthreads();
   for (uint32_t base = 0; base < p.NT; base += 1024) {
@@ -754,20 +775,20 @@ __global__ __launch_bounds__(1024) void k_seg_sums(const KP* __restrict__ pk, ui
   __shared__ uint32_t red[1024];
   const size_t b0 = static_cast<size_t>(blockIdx.x) * kSegChunk;
   uint32_t acc = 0;
-  for (uint32_t k = threadIdx.x; k < kSegChunk; k += blockDim.x)
+  for (uint32_t k = tidx(); k < kSegChunk; k += blockDim.x)
     if (b0 + k < p.NT) acc += p.seg_cnt[b0 + k];
-  red[threadIdx.x] = acc;
+  red[tidx()] = acc;
   __syncthreads();
   for (uint32_t o = blockDim.x / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    if (tidx() < o) red[tidx()] += red[tidx() + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+  if (tidx() == 0) part[blockIdx.x] = red[0];
 }
 __global__ __launch_bounds__(1024) void k_seg_top(uint32_t* part, uint32_t nparts) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t carry;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const uint32_t tid = tidx(), lane = tid & 63u, w = tid >> 6;
   if (tid == 0) carry = 0;
   __syncthreads();
   for (uint32_t base = 0; base < nparts; base += 1024) {
@@ -800,7 +821,7 @@ __global__ __launch_bounds__(1024) void k_seg_top(uint32_t* part, uint32_t npart
 __global__ __launch_bounds__(1024) void k_seg_apply(const KP* __restrict__ pk, const uint32_t* part) {
   const KP& p = *pk;
   __shared__ uint32_t wsum[16];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  const uint32_t tid = tidx(), lane = tid & 63u, w = tid >> 6;
   const size_t b0 = static_cast<size_t>(blockIdx.x) * kSegChunk + static_cast<size_t>(tid) * 8;
   uint32_t v[8], sum = 0;
 #pragma unroll
@@ -830,7 +851,7 @@ __global__ __launch_bounds__(1024) void k_seg_apply(const KP* __restrict__ pk, c
 __global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = blockIdx.x * blockDim.x + tidx();
   if (k >= n) return;
   const XRec x = AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf);
   const uint32_t pos = AT(p.seg_off, x.g, p.NT + 1) + atomicAdd(&AT(p.cursor, x.g, p.NT), 1u);
@@ -873,7 +894,7 @@ __global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long l
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ long long wmin[4];
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = blockIdx.x * blockDim.x + tidx();
   long long stay = LLONG_MAX;
   if (k < n) rebin_one(p, g_cur, AT(p.ov, k, p.cap_ov), stay);
 #pragma unroll
@@ -881,9 +902,9 @@ __global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long l
     const long long y = __shfl_xor(stay, off, 64);
     stay = y < stay ? y : stay;
   }
-  if ((threadIdx.x & 63u) == 0) wmin[threadIdx.x >> 6] = stay;
+  if ((tidx() & 63u) == 0) wmin[tidx() >> 6] = stay;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tidx() == 0) {
     long long m = wmin[0];
     for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) m = wmin[w] < m ? wmin[w] : m;
     if (m != LLONG_MAX) atomicMin(&p.scal[1], m);
@@ -1291,7 +1312,7 @@ struct ScanShared {
 };
 #define SPH(k)                                                         \
   do {                                                                 \
-    if (p.wgs && threadIdx.x == 0) S.ph[k] = __builtin_amdgcn_s_memrealtime(); \
+    if (p.wgs && tidx() == 0) S.ph[k] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 __device__ inline int64_t prop_of_slot(const KP& p, uint32_t q) {
@@ -1307,7 +1328,7 @@ __device__ inline uint64_t arr_key(const KP& p, const Rec& r, uint32_t q) {
 __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, uint32_t e0, uint32_t deg,
                                  const XRec* xs, uint32_t xn, long long cs, long long wa, long long wb,
                                  uint64_t* akey, uint32_t* asec, bool store) {
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   const uint32_t tag = cell_tag(p, cs / p.L);
   uint32_t n = 0;
   for (uint32_t base = 0; base < deg; base += 4 * blockDim.x) {
@@ -1368,7 +1389,7 @@ __device__ uint32_t stage_window(const KP& p, ScanShared& S, const Rec* slots, u
 // the not yet used staging area), so ~3 passes over the row replace ~22 counting passes.
 __device__ long long window_split(const KP& p, ScanShared& S, const Rec* slots, uint32_t deg, const XRec* xs,
                                   uint32_t xn, long long cs, long long wa, long long hi, uint32_t* hist) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t tid = tidx(), lane = tid & 63u;
   const uint32_t tag = cell_tag(p, cs / p.L);
   const uint32_t lg = p.cap_arr >= 128 ? 8u : 6u;  // 2^lg bins (<= 2 * cap_arr u32 of staging)
   const uint32_t nb = 1u << lg;
@@ -1444,7 +1465,7 @@ __device__ inline bool sec_less(uint64_t ka, uint32_t sa, uint64_t kb, uint32_t 
 
 // Sort (akey, asec) pairs of [0, n) unless already ordered.
 __device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec) {
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   if (tid == 0) S.unsorted = 0;
   __syncthreads();
   bool bad = false;
@@ -1527,7 +1548,7 @@ __device__ inline uint32_t quorum_slot(const KP& p, ScanShared& S, uint32_t key,
 __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, ScanShared& S, uint32_t g, uint32_t rep, uint32_t i, uint32_t e0,
                             uint32_t deg, uint32_t n, uint32_t n_main, long long cell, long long cs, long long t_lo,
                             const uint64_t* akey, const uint32_t* asec, const RecSrc rs, uint32_t* acls) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t tid = tidx(), lane = tid & 63u;
   const size_t base = static_cast<size_t>(g) * p.pbft_seq_cap;
   const int32_t N = static_cast<int32_t>(p.N);
   const uint32_t T1 = static_cast<uint32_t>(N / 2), T2 = T1 + 1;
@@ -1892,7 +1913,7 @@ __device__ void gossip_recv(Ctx& c, const Msg& m, uint32_t sender, bool first, u
 // the first receipts are marked seen.  The lane-0 event loop then reads the flags from LDS.
 __device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint32_t n, const uint32_t* asec,
                                    const RecSrc rs, uint32_t* acls) {
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   if (tid == 0) S.tr_n = 0;
   __syncthreads();
   for (uint32_t r = tid; r < n; r += blockDim.x) {
@@ -1930,7 +1951,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
   uint32_t* acls = asec + cap;
   TimerEnt* tm = reinterpret_cast<TimerEnt*>(acls + cap);
 
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
@@ -2326,7 +2347,7 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
   BAIL_IF_ERR();
   __shared__ uint64_t skey[kPxCap][256];
   __shared__ uint32_t sref[kPxCap][256];  // slot << 16 | index in the node's list segment
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   const uint32_t na = p.act_n[0];
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
@@ -2458,7 +2479,7 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
   __shared__ uint32_t s_deliv[BCSIM_MSG_TYPES];
   __shared__ uint32_t s_ev, s_wr, s_nf, s_trbase;
   __shared__ long long s_tmax;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, j = tid & (G - 1u), gb = lane & ~(G - 1u);
+  const uint32_t tid = tidx(), lane = tid & 63u, j = tid & (G - 1u), gb = lane & ~(G - 1u);
   const uint32_t per_wg = blockDim.x / G;
   if (tid < BCSIM_MSG_TYPES) s_deliv[tid] = 0;
   if (tid == 0) {
@@ -2743,7 +2764,7 @@ __device__ __attribute__((always_inline)) inline void link_finish(const KP& p, L
                                                                   const LinkCounts& c8, bool clr_slots, bool clr_rx,
                                                                   uint32_t obp, size_t fidx, unsigned long long wg_t0,
                                                                   unsigned long long* ph, uint32_t n_in) {
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   const uint32_t B = p.n_buckets;
   unsigned long long* cnt = cnt_stripe(p, g / p.N);
   // ---- 3. compact the ops that are not due yet ----
@@ -2865,7 +2886,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
   unsigned long long ph[4] = {0, 0, 0, 0};
   const uint32_t n_in = n;
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
   Op* ops = p.ops + op_base(p, g);
   const uint32_t ocap = op_cap(p, g);
@@ -3337,7 +3358,7 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   uint32_t kk;
   if (!list_one(p.act_n[1], kk)) return;
   const uint32_t g = p.act[p.NT + kk];
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   const uint32_t n = AT(p.n_ops, g, p.NT);
   const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
   const bool sl0 = p.eslot && (AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u);
@@ -3650,7 +3671,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
   __shared__ uint32_t s_c[6];  // sends, records, due ops, edges, echoes, kept
   __shared__ uint8_t s_busy[kMaxBuckets];
   __shared__ long long s_bmin[kMaxBuckets];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, j = tid & (G - 1u), gb = lane & ~(G - 1u);
+  const uint32_t tid = tidx(), lane = tid & 63u, j = tid & (G - 1u), gb = lane & ~(G - 1u);
   const uint32_t gbase = tid & ~(G - 1u);
   const uint32_t per_wg = blockDim.x / G;
   const uint32_t B = p.n_buckets;
@@ -3878,7 +3899,7 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
   __shared__ uint32_t s_cnt;
   uint32_t n = AT(p.n_ops, g, p.NT);
   if (n == 0) return;
-  const uint32_t tid = threadIdx.x, bs = blockDim.x;
+  const uint32_t tid = tidx(), bs = blockDim.x;
   const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t e0 = AT(p.row, i, p.N + 1), deg = AT(p.row, i + 1, p.N + 1) - e0;
   Op* ops = p.ops + op_base(p, g);
@@ -4239,7 +4260,7 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
   __shared__ LinkShared L;
   __shared__ uint4 sa[kPxCap][128], sb[kPxCap][128];
   __shared__ uint32_t s_c[7];  // records, due ops, edges, echoes, kept, (unused)
-  const uint32_t tid = threadIdx.x, bs = blockDim.x;
+  const uint32_t tid = tidx(), bs = blockDim.x;
   const uint32_t na = p.act_n[1];
   const uint32_t B = p.n_buckets;
   const uint32_t n_lists = B + 1;
@@ -4447,7 +4468,7 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
   __shared__ uint32_t s_n[2], s_base[2], wcnt[kMaxWaves];
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = tidx();
   const uint64_t n_loc = static_cast<uint64_t>(p.R) * p.nloc;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * chunk;
   if (c0 >= n_loc) return;  // uniform
@@ -4507,10 +4528,10 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
   __shared__ uint32_t lb[kMaxBuckets];
   __shared__ long long ovmin;
   const uint32_t B = p.n_buckets;
-  for (uint32_t k = threadIdx.x; k < B; k += blockDim.x) lb[k] = 0;
-  if (threadIdx.x == 0) ovmin = LLONG_MAX;
+  for (uint32_t k = tidx(); k < B; k += blockDim.x) lb[k] = 0;
+  if (tidx() == 0) ovmin = LLONG_MAX;
   __syncthreads();
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = blockIdx.x * blockDim.x + tidx();
   if (k < n) {
     XRec x = rx[k];
     const uint32_t rep = x.g / p.N;
@@ -4540,16 +4561,16 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
     }
   }
   __syncthreads();
-  for (uint32_t q = threadIdx.x; q < B; q += blockDim.x)
+  for (uint32_t q = tidx(); q < B; q += blockDim.x)
     if (lb[q]) mark_busy(&p.bucket_cnt[q]);
-  if (threadIdx.x == 0 && ovmin != LLONG_MAX) atomicMin(&p.scal[1], ovmin);
+  if (tidx() == 0 && ovmin != LLONG_MAX) atomicMin(&p.scal[1], ovmin);
 }
 
 // k_lead (multi-GPU, PBFT): this rank's "ticking leader" flags for k_pbft_tick
 __global__ __launch_bounds__(1024) void k_lead(const KP* __restrict__ pk) {
   const KP& p = *pk;
   const uint32_t rep = blockIdx.x;
-  for (uint32_t k = threadIdx.x; k < p.nloc; k += blockDim.x) {
+  for (uint32_t k = tidx(); k < p.nloc; k += blockDim.x) {
     const uint32_t i = p.nlo + k, g = rep * p.N + i;
     p.lead_loc[g] = (p.tick_alive[g] && p.leader[g] == static_cast<int32_t>(i)) ? 1 : 0;
   }
@@ -4566,7 +4587,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
   uint8_t* lead = reinterpret_cast<uint8_t*>(smem);  // N flags
   __shared__ int32_t v_cur, nround0, n_alive, n_ticked;
   __shared__ unsigned long long lmask[64];  // leader flags of the current 4096-node chunk, one bit per node
-  const uint32_t rep = blockIdx.x, tid = threadIdx.x;
+  const uint32_t rep = blockIdx.x, tid = tidx();
   if (rep == 0 && tid < 4) p.act_n[tid] = 0;  // the second window of the cell builds fresh lists
   const uint32_t N = p.N;
   const long long ts_tick = tk - p.pbft_period;
@@ -4748,7 +4769,7 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
 // glibc election-timeout draws (Raft), canonical global order per replica.
 __global__ void k_draws(const KP* __restrict__ pk, uint32_t) {
   const KP& p = *pk;
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (tidx() != 0 || blockIdx.x != 0) return;
   const uint32_t n = min(*p.dreq_cnt, p.cap_dreq);
   if (n == 0) return;
   // insertion sort by (rep, t, ts, origin, sub, target): n is small
@@ -4799,15 +4820,15 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (blockIdx.x == 0) {
-    if (threadIdx.x < 4) p.act_n[threadIdx.x] = 0;
+    if (tidx() < 4) p.act_n[tidx()] = 0;
     if (clr_b < p.n_buckets) {
-      if (threadIdx.x == 0) {
+      if (tidx() == 0) {
         p.bucket_cnt[clr_b] = 0;
         p.x_cnt[clr_b] = 0;
         p.bmin[clr_b] = LLONG_MAX;
       }
       if (p.mesh)
-        for (uint32_t k = threadIdx.x; k < p.R * p.n_tiles; k += blockDim.x)
+        for (uint32_t k = tidx(); k < p.R * p.n_tiles; k += blockDim.x)
           p.rtile[static_cast<size_t>(clr_b) * p.R * p.n_tiles + k] = 0;
     }
   }
@@ -4816,7 +4837,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
   __shared__ long long red[kMaxWaves], redt[kMaxWaves];
   long long m = LLONG_MAX, mt = LLONG_MAX;
   const uint32_t nb = gridDim.x;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < p.NT; k += nb * blockDim.x) {
+  for (uint32_t k = blockIdx.x * blockDim.x + tidx(); k < p.NT; k += nb * blockDim.x) {
     const long long a = AT(p.node_tnext, k, p.NT), b = AT(p.node_onext, k, p.NT);
     m = min(m, min(a, b));
     mt = min(mt, a);
@@ -4825,7 +4846,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     m = min(m, static_cast<long long>(__shfl_xor(m, d, 64)));
     mt = min(mt, static_cast<long long>(__shfl_xor(mt, d, 64)));
   }
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const uint32_t lane = tidx() & 63u, wv = tidx() >> 6, nwv = blockDim.x >> 6;
   if (lane == 0) {
     red[wv] = m;
     redt[wv] = mt;
