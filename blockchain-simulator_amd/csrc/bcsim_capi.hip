@@ -75,6 +75,8 @@ struct Sim {
   uint32_t gossip_g = 0;  // dense gossip: lanes per node of k_gossip_scan (0 = generic k_scan only)
   bool gossip_link = false;
   bool mesh_link = false;  // full mesh, fixed delay: k_link_mesh first, k_link over list 3
+  bool scan_fast = false;  // dense PBFT, fixed delay, reply slots: k_scan_pbft first, k_scan over list 2
+  uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
   uint32_t* seg_part = nullptr;  // multi-block segment scan partials
@@ -500,6 +502,8 @@ static int setup_device(Sim& s) {
     }
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, false, true>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_RAFT, false>),
@@ -643,6 +647,13 @@ static int setup_device(Sim& s) {
     const bool on = ne * 16 <= (16ull << 30) && !off && !s.sparse && c.protocol == BCSIM_PBFT &&
                     c.delay_mode == BCSIM_DELAY_FIXED && c.app_delay_ns < s.L;
     p.cap_eslot = on ? ne : 1;
+    {  // BCSIM_NO_SFAST=1: off (A/B aid)
+      const char* sf = std::getenv("BCSIM_NO_SFAST");
+      s.scan_fast = on && p.impl && s.deg_max <= kFastLanes * kFastRPL && !(sf && *sf == '1');
+      // testing aid: BCSIM_FEW_SCAN=0 sends small launches (every launch of a small parity case)
+      // through k_scan_pbft too
+      if (const char* fs = std::getenv("BCSIM_FEW_SCAN"); fs && *fs) s.few_scan = static_cast<uint32_t>(std::atoi(fs));
+    }
     if ((rc = dalloc(s, &p.eslot, p.cap_eslot)) || (rc = dalloc(s, &p.sflag, static_cast<size_t>(kOpRing) * NT)))
       return rc;
     HIPCHK(hipMemset(p.eslot, 0xFF, p.cap_eslot * 16));  // due t = -1: no live reply
@@ -813,6 +824,8 @@ static int setup_device(Sim& s) {
       HIPCHK(hipMemcpy(s.kp_dev_big, &kb, sizeof(KP), hipMemcpyHostToDevice));
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, false>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lb)));
+      HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, false, true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lb)));
       s.lds_big = lb;
     }
   }
@@ -874,7 +887,6 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
 }
 #define launch(s, cls, kernel, ...) launch_named(s, #kernel, cls, kernel, __VA_ARGS__)
 
-constexpr uint32_t kFewScan = 64;  // k_scan launches of at most this many nodes use kp_dev_big
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
   dim3 grid(s.grid_scan), block(s.bs_scan);
@@ -940,11 +952,21 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
             : launch(s, KS_SCAN, k_scan<P, false>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa))
   if (grid.x == 0)
     rc = BCSIM_OK;  // no node has work in the window
-  else if (s.kp_dev_big && !s.sparse && s.P == 1 && grid.x <= kFewScan)
+  else if (s.kp_dev_big && !s.sparse && s.P == 1 && grid.x <= s.few_scan)
     // a few nodes (the leader's cells): the doubled staging window, a 1024-lane workgroup each
     rc = launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false>), grid, dim3(1024), s.lds_big, s.kp_dev_big, cell, lo, hi, cs, fw,
                 xa);
-  else if (s.sparse && s.cfg.protocol == BCSIM_PAXOS && s.paxos_fast) {
+  else if (s.scan_fast && !(lo <= 0 && 0 < hi) && !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi)) {
+    // PBFT heavy waves: one pass over each row in registers; the nodes it leaves (list 2) to
+    // the generic kernel -- a small looped grid, with the doubled staging window if there is one
+    rc = launch(s, KS_SCAN, k_scan_pbft, grid, dim3(kFastLanes), 0, s.kp_dev, cell, lo, hi, cs, xa);
+    if (!rc)
+      rc = s.kp_dev_big
+               ? launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false, true>), dim3(std::min<uint32_t>(grid.x, 256)), dim3(1024),
+                        s.lds_big, s.kp_dev_big, cell, lo, hi, cs, fw, xa)
+               : launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false, true>), dim3(std::min<uint32_t>(grid.x, 512)), block, lds,
+                        s.kp_dev, cell, lo, hi, cs, fw, xa);
+  } else if (s.sparse && s.cfg.protocol == BCSIM_PAXOS && s.paxos_fast) {
     // sparse Paxos: one lane per node takes the acceptors' request windows; the generic
     // kernel walks the rest (list 2)
     rc = launch(s, KS_SCAN, k_paxos_scan, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa);

@@ -2331,6 +2331,382 @@ __global__ __launch_bounds__(1024) void k_scan(const KP* pk, long long cell, lon
 }
 
 // ---------------------------------------------------------------------------
+// k_scan_pbft (dense layout, PBFT, fixed app delay < L with reply slots, degree <= 4096): the
+// k_scan of a node whose window holds only main-slot PRE_PREPARE / PREPARE / PREPARE_RES /
+// COMMIT arrivals that all carry one canonical key prefix (t, dt) -- the PBFT heavy waves,
+// where a row holds one record per in-edge, all at one instant.  The same state changes and
+// outputs as scan_node + pbft_window (pbft-node.cc:166-265) for such a node, in ONE pass over
+// its inbox row: every lane keeps kFastRPL records in registers (slot j * 512 + lane: the row
+// is read with coalesced 16-byte loads, all in flight at once).  With equal (t, dt) the
+// canonical order is the slot order (sort_window breaks ties by slot), so every prefix the
+// handler needs -- quorum ranks per (phase, sequence), the schedule counter, op positions,
+// commit numbers -- is a count of flagged arrivals before this one: wave ballots + popcounts
+// plus per-(chunk, wave) totals in LDS.  No key staging, no sort, no second or third read of
+// the row, 3 KB of LDS instead of 76 KB.  A node that does not qualify (an extras record,
+// another message type, arrivals at different instants, more than kFastKeys (phase, sequence)
+// groups or kFastPP PRE_PREPAREs, a bad index, START / STOP, a due timer) is appended to
+// list 2, untouched, for k_scan<PBFT, false, LOOP>.
+constexpr uint32_t kFastLanes = 512, kFastRPL = 8, kFastWaves = kFastLanes / 64, kFastKeys = 8, kFastPP = 16;
+constexpr uint32_t kFastSeg = kFastRPL * kFastWaves;  // (chunk, wave) segments in arrival order
+struct FastShared {
+  uint4 seg[kFastSeg];                 // per segment (PREPAREs, deg-steps, commits, arrivals); then exclusive bases
+  uint32_t qc[kFastSeg][kFastKeys];    // quorum group counts per segment, then bases
+  uint32_t tkey[kFastKeys];            // (phase, sequence) groups of the window
+  uint32_t tcnt[kFastKeys];            // stored vote count + the window's
+  unsigned long long kmin, kmax;       // (t_off, ~dt) of the arrivals
+  uint32_t bad, npp;
+  uint32_t pp_k[kFastPP];
+  int32_t pp_idx[kFastPP], pp_val[kFastPP];
+  uint32_t tcount[4];  // deliveries: PRE_PREPARE, PREPARE, COMMIT, PREPARE_RES
+  uint32_t ocnt[2];    // reply slots due in this cell / the next
+};
+
+// record words {t_off, sub, f0 | f1 << 16, f2 | type << 16 | flags << 24} -> payload chars after
+// getPacketContent's NUL truncation (mch)
+__device__ inline int32_t fr_f0(const uint4& r) { return static_cast<int16_t>(r.z & 0xFFFFu); }
+__device__ inline int32_t fr_m2(const uint4& r) { return fr_f0(r) ? static_cast<int16_t>(r.z >> 16) : 0; }
+__device__ inline int32_t fr_m3(const uint4& r) {
+  return (fr_f0(r) && static_cast<int16_t>(r.z >> 16)) ? static_cast<int16_t>(r.w & 0xFFFFu) : 0;
+}
+__device__ inline uint32_t fr_type(const uint4& r) { return (r.w >> 16) & 0xFFu; }
+// quorum group of an arrival (kClsPres / kClsCommit | sequence) or 0; indices checked in pass 1
+__device__ inline uint32_t fr_group(const uint4& r) {
+  const uint32_t type = fr_type(r);
+  const uint32_t idx = static_cast<uint32_t>(c2i(fr_m2(r))) & kIdxMask;
+  if (type == PB_COMMIT) return kClsCommit | idx;
+  if (type == PB_PREPARE_RES && c2i(fr_m3(r)) == 0) return kClsPres | idx;
+  return 0u;
+}
+
+__device__ inline uint32_t fast_key_slot(FastShared& F, uint32_t key) {
+  for (uint32_t k = 0; k < kFastKeys; ++k) {
+    const uint32_t t = __hip_atomic_load(&F.tkey[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (t == key) return k;
+    if (t == 0u) {
+      const uint32_t old = atomicCAS(&F.tkey[k], 0u, key);
+      if (old == 0u || old == key) return k;
+    }
+  }
+  F.bad = 1;
+  return kFastKeys;
+}
+__device__ inline uint32_t fast_key_find(const FastShared& F, uint32_t key) {
+  uint32_t s = 0;
+  for (uint32_t k = 0; k < kFastKeys; ++k)
+    if (F.tkey[k] == key) s = k;
+  return s;
+}
+
+__global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                   long long t_hi, long long cs, int x_active) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ FastShared F;
+  uint32_t kk;
+  if (!list_one(p.act_n[0], kk)) return;
+  const uint32_t g = p.act[kk];
+  const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6;
+  const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const uint32_t e0 = p.mesh ? i * (p.N - 1) : AT(p.row, i, p.N + 1);
+  const uint32_t deg = p.mesh ? p.N - 1 : AT(p.row, i + 1, p.N + 1) - e0;
+  const bool flag = node_flagged_w(p, b, g, rep, i, t_hi);
+  const bool has_ss = (t_lo <= 0 && 0 < t_hi) || (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
+  const bool timer = AT(p.node_tnext, g, p.NT) < t_hi;
+  uint32_t xn = 0;
+  if (x_active) xn = AT(p.seg_off, g + 1, p.NT + 1) - AT(p.seg_off, g, p.NT + 1);
+  if (!flag && !has_ss && !timer) return;  // nothing in the window (scan_node returns too)
+  if (!flag || has_ss || timer || xn || deg > kFastLanes * kFastRPL || deg > p.cap_arr || blockDim.x != kFastLanes ||
+      !p.impl || !p.eslot || p.delay_mode != BCSIM_DELAY_FIXED) {
+    if (tid == 0) AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+    return;
+  }
+  const Rec* slots = p.inbox + inbox_idx(p, b, rep, e0);
+  uint4 rv[kFastRPL];
+#pragma unroll
+  for (uint32_t j = 0; j < kFastRPL; ++j) {  // the whole row in flight at once
+    const uint32_t k = j * kFastLanes + tid;
+    rv[j] = k < deg ? *reinterpret_cast<const uint4*>(slots + k) : make_uint4(0, 0, 0, 0);
+  }
+  if (tid == 0) {
+    F.bad = 0;
+    F.npp = 0;
+    F.kmin = ~0ull;
+    F.kmax = 0ull;
+  }
+  if (tid < kFastKeys) F.tkey[tid] = 0;
+  if (tid < 4) F.tcount[tid] = 0;
+  if (tid < 2) F.ocnt[tid] = 0;
+  for (uint32_t k = tid; k < kFastSeg * kFastKeys; k += kFastLanes) (&F.qc[0][0])[k] = 0;
+  __syncthreads();
+  const uint32_t tag = cell_tag(p, cell);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  auto key_of = [&](const uint4& r, uint32_t k) -> unsigned long long {
+    const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, e0 + k) + p.tx_last[((r.w >> 24) & RF_BIG) ? 1 : 0]);
+    return (static_cast<unsigned long long>(r.x) << 32) | static_cast<uint32_t>(~dt);
+  };
+  // ---- pass 1: window membership, message types and indices, quorum group counts, key range ----
+  uint32_t vmask = 0;  // bit j: slot j * 512 + tid holds an arrival of the window
+  bool bad = false;
+  unsigned long long kmn = ~0ull, kmx = 0ull;
+#pragma unroll
+  for (uint32_t j = 0; j < kFastRPL; ++j) {
+    const uint32_t k = j * kFastLanes + tid;
+    const uint4 r = rv[j];
+    const long long t = cs + r.x;
+    const bool v = k < deg && slot_live(r.w >> 24, tag) && t >= t_lo && t < t_hi;
+    uint32_t w = 0;
+    if (v) {
+      vmask |= 1u << j;
+      const unsigned long long key = key_of(r, k);
+      kmn = min(kmn, key);
+      kmx = max(kmx, key);
+      const uint32_t type = fr_type(r);
+      const int32_t idx = c2i(fr_m2(r));
+      const bool inr = idx >= 0 && static_cast<uint32_t>(idx) < p.pbft_seq_cap;
+      if (type == PB_PRE_PREPARE) {
+        const uint32_t q = inr ? atomicAdd(&F.npp, 1u) : kFastPP;
+        if (q < kFastPP) {
+          F.pp_k[q] = k;
+          F.pp_idx[q] = idx;
+          F.pp_val[q] = c2i(fr_m3(r));
+        } else {
+          bad = true;
+        }
+      } else if (type == PB_PREPARE_RES || type == PB_COMMIT) {
+        if (!inr) bad = true;
+        else w = fr_group(r);
+      } else if (type != PB_PREPARE) {
+        bad = true;  // VIEW_CHANGE / "Wrong msg": the generic path
+      }
+    }
+    unsigned long long rem = __ballot(w != 0);
+    while (rem) {
+      const int ld = __ffsll(static_cast<long long>(rem)) - 1;
+      const uint32_t wl = __shfl(w, ld, 64);
+      const unsigned long long same = __ballot(w == wl);
+      if (lane == static_cast<uint32_t>(ld)) {
+        const uint32_t s = fast_key_slot(F, wl);
+        if (s < kFastKeys) F.qc[j * kFastWaves + wv][s] = static_cast<uint32_t>(__popcll(same));
+      }
+      rem &= ~same;
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    kmn = min(kmn, static_cast<unsigned long long>(__shfl_xor(kmn, d, 64)));
+    kmx = max(kmx, static_cast<unsigned long long>(__shfl_xor(kmx, d, 64)));
+  }
+  if (lane == 0) {
+    atomicMin(&F.kmin, kmn);
+    atomicMax(&F.kmax, kmx);
+  }
+  if (bad) F.bad = 1;
+  __syncthreads();
+  // group bases: the stored vote counters, then the segments in arrival order
+  const size_t base = static_cast<size_t>(g) * p.pbft_seq_cap;
+  if (tid < kFastKeys) {
+    const uint32_t wl = F.tkey[tid];
+    if (wl) {
+      const uint32_t idx = wl & kIdxMask;
+      uint32_t run = static_cast<uint32_t>((wl >> 30) == 1u ? AT(p.tx_pv, base + idx, p.cap_txn)
+                                                            : AT(p.tx_cv, base + idx, p.cap_txn));
+      for (uint32_t s = 0; s < kFastSeg; ++s) {
+        const uint32_t c = F.qc[s][tid];
+        F.qc[s][tid] = run;
+        run += c;
+      }
+      F.tcnt[tid] = run;
+    }
+  }
+  __syncthreads();
+  // uniform: several instants in the window (the slot order may not be the key order), or
+  // anything else the generic path must take -- nothing has been written
+  if (F.bad || F.kmin != F.kmax) {
+    if (tid == 0) AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+    return;
+  }
+  const int32_t N = static_cast<int32_t>(p.N);
+  const uint32_t T1 = static_cast<uint32_t>(N / 2), T2 = T1 + 1;
+  // ---- pass 2: quorum crossings; per-segment counts of the flagged arrivals ----
+  uint32_t xmask = 0;  // bit j: the arrival crosses its quorum
+#pragma unroll
+  for (uint32_t j = 0; j < kFastRPL; ++j) {
+    const uint4 r = rv[j];
+    const bool v = (vmask >> j) & 1u;
+    const uint32_t w = v ? fr_group(r) : 0u;
+    unsigned long long rem = __ballot(w != 0);
+    while (rem) {
+      const int ld = __ffsll(static_cast<long long>(rem)) - 1;
+      const uint32_t wl = __shfl(w, ld, 64);
+      const unsigned long long same = __ballot(w == wl);
+      if (w == wl) {
+        const uint32_t vv = F.qc[j * kFastWaves + wv][fast_key_find(F, wl)] + static_cast<uint32_t>(__popcll(same & lt)) + 1u;
+        if ((wl >> 30) == 1u ? (vv % T1 == 0) : (vv % T2 == 0)) xmask |= 1u << j;
+      }
+      rem &= ~same;
+    }
+    const uint32_t type = fr_type(r);
+    const bool cross = (xmask >> j) & 1u;
+    const unsigned long long mp = __ballot(v && type == PB_PREPARE);
+    const unsigned long long md = __ballot(v && (type == PB_PRE_PREPARE || (type == PB_PREPARE_RES && cross)));
+    const unsigned long long mc = __ballot(v && type == PB_COMMIT && cross);
+    const unsigned long long mv = __ballot(v);
+    if (lane == 0)
+      F.seg[j * kFastWaves + wv] = make_uint4(static_cast<uint32_t>(__popcll(mp)), static_cast<uint32_t>(__popcll(md)),
+                                              static_cast<uint32_t>(__popcll(mc)), static_cast<uint32_t>(__popcll(mv)));
+  }
+  // write back the vote counters (tx[idx].prepare_vote / commit_vote)
+  if (tid < kFastKeys) {
+    const uint32_t wl = F.tkey[tid];
+    if (wl) {
+      const uint32_t idx = wl & kIdxMask;
+      if ((wl >> 30) == 1u)
+        AT(p.tx_pv, base + idx, p.cap_txn) = static_cast<int32_t>(F.tcnt[tid] % T1);
+      else
+        AT(p.tx_cv, base + idx, p.cap_txn) = static_cast<int32_t>(F.tcnt[tid] % T2);
+    }
+  }
+  __syncthreads();
+  // exclusive segment bases (wave 0: one segment per lane); totals to every lane
+  uint4 tot;
+  {
+    const uint4 x = lane < kFastSeg ? F.seg[lane] : make_uint4(0, 0, 0, 0);
+    uint4 in = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t a = __shfl_up(in.x, off, 64), bq = __shfl_up(in.y, off, 64);
+      const uint32_t c = __shfl_up(in.z, off, 64), d = __shfl_up(in.w, off, 64);
+      if (lane >= static_cast<uint32_t>(off)) {
+        in.x += a;
+        in.y += bq;
+        in.z += c;
+        in.w += d;
+      }
+    }
+    tot = make_uint4(__shfl(in.x, 63, 64), __shfl(in.y, 63, 64), __shfl(in.z, 63, 64), __shfl(in.w, 63, 64));
+    __syncthreads();  // every wave has read its totals before wave 0 overwrites the counts
+    if (wv == 0 && lane < kFastSeg) F.seg[lane] = make_uint4(in.x - x.x, in.y - x.y, in.z - x.z, in.w - x.w);
+  }
+  const uint32_t sub0 = AT(p.sub, g, p.NT), nops0 = AT(p.n_ops, g, p.NT);
+  const int32_t bn0 = AT(p.block_num, g, p.NT);
+  if (nops0 + tot.y > op_cap(p, g)) {
+    if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
+    return;
+  }
+  __syncthreads();
+  // ---- pass 3: outputs, every arrival with its counter values from the bases + popcounts ----
+  Op* ops = p.ops + op_base(p, g);
+  const int64_t app = p.app_delay;
+  const int64_t tk0 = ((t_lo + p.pbft_period - 1) / p.pbft_period) * p.pbft_period;
+  const uint32_t deg_u = deg;
+  uint32_t n_slot0 = 0, n_slot1 = 0, cnt_t[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (uint32_t j = 0; j < kFastRPL; ++j) {
+    const uint4 r = rv[j];
+    const bool v = (vmask >> j) & 1u;
+    const uint32_t type = fr_type(r);
+    const bool cross = (xmask >> j) & 1u;
+    const unsigned long long mp = __ballot(v && type == PB_PREPARE);
+    const unsigned long long md = __ballot(v && (type == PB_PRE_PREPARE || (type == PB_PREPARE_RES && cross)));
+    const unsigned long long mc = __ballot(v && type == PB_COMMIT && cross);
+    if (!v) continue;
+    const uint4 sb = F.seg[j * kFastWaves + wv];
+    const uint32_t np = sb.x + static_cast<uint32_t>(__popcll(mp & lt));
+    const uint32_t nd = sb.y + static_cast<uint32_t>(__popcll(md & lt));
+    const uint32_t nc = sb.z + static_cast<uint32_t>(__popcll(mc & lt));
+    const uint32_t sp = sub0 + np + nd * deg_u, op = nops0 + nd;
+    const uint32_t k = j * kFastLanes + tid;
+    const uint32_t q = e0 + k;  // in-slot = the reverse (reply) edge
+    const uint32_t dt = ~static_cast<uint32_t>(key_of(r, k));
+    const int64_t t = cs + static_cast<int64_t>(r.x);
+    const uint32_t origin = p.mesh ? (k < i ? k : k + 1) : AT(p.col, q, p.E);
+    const Key key{t, t - static_cast<int64_t>(dt), origin, r.y};
+    if (t >= tk0 && (t == tk0 || (t - tk0) % p.pbft_period == 0) && key.ts <= t - p.pbft_period)
+      set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
+    const int32_t m1 = fr_f0(r), m2 = fr_m2(r);
+    if (type == PB_PRE_PREPARE) {  // :193-211
+      ++cnt_t[0];
+      st_op(&ops[op], mk_op(p, t + app, static_cast<uint32_t>(app), i, sp, 0, mkmsg(PB_PREPARE, m1, m2, fr_m3(r), 0),
+                            OP_BCAST, 0));
+    } else if (type == PB_PREPARE) {  // :212-222, the reply into its edge's slot of this arrival cell
+      ++cnt_t[1];
+      const int64_t due = t + app;
+      const uint64_t ut = static_cast<uint64_t>(due);
+      *eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q) =
+          make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), sp,
+                     static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m1))) |
+                         (static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m2))) << 16));
+      if (due / p.L == cell)
+        ++n_slot0;
+      else
+        ++n_slot1;
+    } else if (type == PB_PREPARE_RES) {  // :223-240
+      ++cnt_t[3];
+      if (cross)
+        st_op(&ops[op], mk_op(p, t + app, static_cast<uint32_t>(app), i, sp, 0, mkmsg(PB_COMMIT, m1, m2, 0, 0), OP_BCAST, 0));
+    } else {  // PB_COMMIT :241-265
+      ++cnt_t[2];
+      if (cross) {
+        const int32_t idx = c2i(m2);
+        int32_t val = 0, best = -1;  // tx[idx].val as of this event
+        for (uint32_t u = 0; u < F.npp; ++u)
+          if (F.pp_idx[u] == idx && F.pp_k[u] < k && static_cast<int32_t>(F.pp_k[u]) > best) {
+            best = static_cast<int32_t>(F.pp_k[u]);
+            val = F.pp_val[u];
+          }
+        if (best < 0) val = AT(p.tx_val, base + idx, p.cap_txn);
+        emit_trace(p, key, rep, i, BCSIM_TR_PBFT_COMMIT, INT32_MIN, bn0 + static_cast<int32_t>(nc), val);
+      }
+    }
+  }
+#pragma unroll
+  for (int t4 = 0; t4 < 4; ++t4) {
+    const uint32_t s = wave_sum(cnt_t[t4]);
+    if (lane == 0 && s) atomicAdd(&F.tcount[t4], s);
+  }
+  {
+    const uint32_t s0 = wave_sum(n_slot0), s1 = wave_sum(n_slot1);
+    if (lane == 0) {
+      if (s0) atomicAdd(&F.ocnt[0], s0);
+      if (s1) atomicAdd(&F.ocnt[1], s1);
+    }
+  }
+  __syncthreads();
+  // ---- tx[n].val of the window's PRE_PREPAREs (the last one per index wins) ----
+  for (uint32_t u = tid; u < F.npp; u += kFastLanes) {
+    bool last = true;
+    for (uint32_t u2 = 0; u2 < F.npp; ++u2)
+      if (F.pp_idx[u2] == F.pp_idx[u] && F.pp_k[u2] > F.pp_k[u]) last = false;
+    if (last) AT(p.tx_val, base + F.pp_idx[u], p.cap_txn) = F.pp_val[u];
+  }
+  // slot replies make their cells busy and flag this node for k_link
+  if (tid < 2 && F.ocnt[tid]) mark_busy(&p.bucket_cnt[(cell + tid) % p.n_buckets]);
+  if (tid != 0) return;
+  const uint32_t sm = (F.ocnt[0] ? 1u : 0u) | (F.ocnt[1] ? 2u : 0u);
+  if (sm) {
+    uint8_t& f = AT(p.sflag, (cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT);
+    f = static_cast<uint8_t>(f | sm);
+  }
+  AT(p.sub, g, p.NT) = sub0 + tot.x + tot.y * deg_u;
+  AT(p.n_ops, g, p.NT) = nops0 + tot.y;
+  if (tot.y) AT(p.node_onext, g, p.NT) = LLONG_MIN;  // the link stage recomputes
+  AT(p.block_num, g, p.NT) = bn0 + static_cast<int32_t>(tot.z);
+  unsigned long long* cnt = cnt_stripe(p, rep);
+  const uint32_t type_of[4] = {PB_PRE_PREPARE, PB_PREPARE, PB_COMMIT, PB_PREPARE_RES};
+  for (int t4 = 0; t4 < 4; ++t4)
+    if (F.tcount[t4]) atomicAdd(&cnt[CNT_DELIV + type_of[t4]], static_cast<unsigned long long>(F.tcount[t4]));
+  const unsigned long long n = tot.w;
+  if (n) {
+    atomicAdd(&cnt[CNT_DELIV_TOTAL], n);
+    if (p.echo) atomicAdd(&cnt[CNT_ECHOES], n);
+    atomicAdd(&kst_stripe(p)[KST_DELIV], n);
+    atomicAdd(&cnt[CNT_EVENTS], n);
+    // every arrival is at one instant: t = cs + t_off of any of them
+    atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), cs + static_cast<long long>(F.kmax >> 32));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_paxos_scan (sparse layout, BCSIM_PAXOS): one LANE per active node.  A node whose window
 // holds only acceptor requests (REQ_TICKET / REQ_PROPOSE / REQ_COMMIT, at most kPxCap, no
 // timer, START or STOP due) is handled here in canonical key order exactly as the lane-0

@@ -1,10 +1,14 @@
-"""Lane-group fast paths against the generic kernels at full size.
+"""Fast paths against the generic kernels at full size.
 
 The dense-gossip kernels (k_gossip_scan / k_gossip_link) and the sparse-Paxos acceptor
 kernels (k_paxos_scan / k_paxos_link) restate scan_node / link_node for the simple nodes of
 a window.  The oracle parity cases cover them at the sizes the oracle runs; here the same
 run with the fast paths switched off (BCSIM_NO_GFAST=1, BCSIM_NO_PXFAST=1: every node through
 the generic kernels) must give identical traces and counters at BASELINE sizes.
+
+k_scan_pbft (the PBFT heavy waves, one pass over each row in registers) is checked the same
+way on the bench configuration (BCSIM_NO_SFAST=1: off), and against the oracle on every PBFT
+parity case with BCSIM_FEW_SCAN=0, so that even the small cases' launches take it.
 """
 import os
 
@@ -59,3 +63,29 @@ def test_c3_paxos_sparse_fast_equals_generic(engine_lib):
     gen = _run(cfg, None, {"BCSIM_NO_PXFAST": "1"})
     assert fast[1]["delivered_total"] > 1_000_000
     assert compare(gen, fast) is None
+
+
+@pytest.mark.timeout(170)
+def test_c4_bench_config_fast_scan_equals_generic(engine_lib):
+    from fullsize_props import bench_config
+    cfg = bench_config(4096, rounds=6)
+    fast = _run(cfg, None, {"BCSIM_NO_SFAST": "0"})
+    gen = _run(cfg, None, {"BCSIM_NO_SFAST": "1"})
+    assert fast[1]["delivered_total"] == 6 * (3 * 4095 ** 2 + 4095)
+    assert compare(gen, fast) is None
+
+
+def _pbft_cases():
+    from parity_cases import cases
+    return sorted(n for n, c in cases().items() if c.protocol == _abi.PBFT)
+
+
+@pytest.mark.parametrize("name", _pbft_cases())
+def test_fast_scan_every_launch_matches_oracle(name, engine_lib):
+    import oracle
+    from parity_cases import cases, topology
+    cfg = cases()[name]
+    topo = topology(name)
+    got = _run(cfg, topo, {"BCSIM_FEW_SCAN": "0", "BCSIM_NO_SFAST": "0"})
+    d = compare(oracle.run(cfg, topology=topo), got)
+    assert d is None, f"{name} (k_scan_pbft on every launch): {d}"
