@@ -704,7 +704,8 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.counters, static_cast<size_t>(p.cnt_stripes) * s.R * CNT_N)) ||
       (rc = dalloc(s, &p.kstat, 8 * kKstStripes)))
     return rc;
-  if ((rc = dalloc(s, &p.node_tnext, NT)) || (rc = dalloc(s, &p.node_onext, NT))) return rc;
+  if ((rc = dalloc(s, &p.node_tnext, NT)) || (rc = dalloc(s, &p.node_onext, NT)) || (rc = dalloc(s, &p.eapp, NT)))
+    return rc;
   // control block: Ctl + bucket counts + extras counts, contiguous for one read-back
   const size_t ctl_bytes = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
   char* ctl = nullptr;
@@ -808,6 +809,10 @@ static int setup_device(Sim& s) {
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p.node_onext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
+  {
+    const std::vector<long long> never(NT, LLONG_MIN);
+    HIPCHK(hipMemcpy(p.eapp, never.data(), NT * 8, hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMemset(s.ctl_d, 0, ctl_bytes));
   long long sc0[4] = {LLONG_MAX, LLONG_MAX, 0, 0};
   HIPCHK(hipMemcpy(p.scal, sc0, sizeof sc0, hipMemcpyHostToDevice));

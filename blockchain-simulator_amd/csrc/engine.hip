@@ -107,6 +107,9 @@ struct KP {
   // in-slot index is the reverse out-edge) and releases the slots; k_scan
   // writes echo ops only for extras records
   uint32_t impl;
+  // window stamp per gnode: k_scan_pbft applied the implicit echoes of the window starting at
+  // eapp[g] itself (the link kernels skip them); LLONG_MIN = never
+  long long* eapp;
   int64_t prop_const;    // propagation delay of every edge, or -1 (per-edge array)
   // links
   uint64_t* link;  // per edge: busy_until << 16 | (arrival cell of the last record & 0xFFFF)
@@ -2589,6 +2592,16 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   }
   const uint32_t sub0 = AT(p.sub, g, p.NT), nops0 = AT(p.n_ops, g, p.NT);
   const int32_t bn0 = AT(p.block_num, g, p.NT);
+  // The implicit echoes (pbft-node.cc:175: every delivery goes back out on the reverse edge,
+  // occupying it) are applied here, on the link words of the node's out-edges, when no op of
+  // the node is due in the window apart from the ones this scan creates -- those are due
+  // app_delay after the arrivals, so they follow the echoes in key order (t, then t - dt).
+  // The link kernels then skip the echoes of this window (eapp stamp) instead of reading the
+  // row a second time; otherwise they do them, merged with the due ops, as before.
+  const bool echo_here =
+      p.echo && p.qmodel == 0 && AT(p.node_onext, g, p.NT) >= t_hi &&
+      !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u) &&
+      !(AT(p.sflag, static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u);
   if (nops0 + tot.y > op_cap(p, g)) {
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
     return;
@@ -2659,6 +2672,22 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
       }
     }
   }
+  if (echo_here) {  // one link word per arrival (distinct in-slots = distinct out-edges), coalesced
+    uint64_t lw[kFastRPL];
+#pragma unroll
+    for (uint32_t j = 0; j < kFastRPL; ++j)
+      lw[j] = ((vmask >> j) & 1u) ? p.link[edge_loc(p, rep, e0 + j * kFastLanes + tid)] : 0ull;
+#pragma unroll
+    for (uint32_t j = 0; j < kFastRPL; ++j) {
+      if (!((vmask >> j) & 1u)) continue;
+      const uint4 r = rv[j];
+      const int64_t t = cs + static_cast<int64_t>(r.x);
+      const int64_t bu0 = static_cast<int64_t>(lw[j] >> 16);
+      const int64_t bu = (bu0 > t ? bu0 : t) + p.tx_tot[((r.w >> 24) & RF_BIG) ? 1 : 0];
+      if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+      p.link[edge_loc(p, rep, e0 + j * kFastLanes + tid)] = (static_cast<uint64_t>(bu) << 16) | (lw[j] & 0xFFFFull);
+    }
+  }
 #pragma unroll
   for (int t4 = 0; t4 < 4; ++t4) {
     const uint32_t s = wave_sum(cnt_t[t4]);
@@ -2691,6 +2720,10 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   AT(p.n_ops, g, p.NT) = nops0 + tot.y;
   if (tot.y) AT(p.node_onext, g, p.NT) = LLONG_MIN;  // the link stage recomputes
   AT(p.block_num, g, p.NT) = bn0 + static_cast<int32_t>(tot.z);
+  if (echo_here) {
+    AT(p.eapp, g, p.NT) = t_lo;
+    if (tot.w) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(tot.w));
+  }
   unsigned long long* cnt = cnt_stripe(p, rep);
   const uint32_t type_of[4] = {PB_PRE_PREPARE, PB_PREPARE, PB_COMMIT, PB_PREPARE_RES};
   for (int t4 = 0; t4 < 4; ++t4)
@@ -3258,7 +3291,12 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
   const uint32_t rep = g / p.N, i = g % p.N;
   const bool rx = p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
-  if (n == 0 && !sl && !rx) return;
+  // the implicit echoes, unless k_scan_pbft applied them in this window
+  const bool rxe = rx && AT(p.eapp, g, p.NT) != t_lo;
+  if (n == 0 && !sl && !rxe) {
+    if (rx && final_win && tidx() == 0) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
+    return;
+  }
   const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
   unsigned long long ph[4] = {0, 0, 0, 0};
   const uint32_t n_in = n;
@@ -3444,13 +3482,13 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     // alias) and would cost a second memory round trip per edge.
     Rec* ir = const_cast<Rec*>(in_row) + le;
     Rec r0{};
-    if (rx) r0 = ld_rec(ir);
+    if (rxe) r0 = ld_rec(ir);
     uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
     if (sl0) w0 = *eslot_at(p, ob, rep, e);
     if (sl1) w1 = *eslot_at(p, obp, rep, e);
     bool he = false;
     RawOp eo = raw_zero();
-    if (rx) {
+    if (rxe) {
       const long long ta0 = cs + r0.t_off;
       if (slot_live(r0.flags, cell_tag(p, cell)) && ta0 >= t_lo && ta0 < t_hi) {
         if (p.echo) {
@@ -3744,7 +3782,11 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
   const uint32_t rep = g / p.N, i = g % p.N;
   const bool rx = p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
-  if (n == 0 && !sl0 && !sl1 && !rx) return;
+  const bool rxe = rx && AT(p.eapp, g, p.NT) != t_lo;  // (see link_node)
+  if (n == 0 && !sl0 && !sl1 && !rxe) {
+    if (rx && final_win && tid == 0) AT(p.iflag, fidx, static_cast<uint64_t>(B) * p.NT) = 0;
+    return;
+  }
   const unsigned long long wg_t0 = p.wgt ? __builtin_amdgcn_s_memrealtime() : 0;
   Op* ops = p.ops + op_base(p, g);
 
@@ -3839,7 +3881,7 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
       const bool v = le < deg;
       lwp[u] = p.link + edge_loc(p, rep, e0 + (v ? le : 0u));
       lw[u] = v ? *lwp[u] : 0ull;
-      r0[u] = (v && rx) ? *reinterpret_cast<const uint4*>(in_row + le) : make_uint4(0, 0, 0, 0);
+      r0[u] = (v && rxe) ? *reinterpret_cast<const uint4*>(in_row + le) : make_uint4(0, 0, 0, 0);
       w0[u] = (v && sl0) ? *eslot_at(p, ob, rep, e0 + le) : make_uint4(0, 0, 0, 0);
       w1[u] = (v && sl1) ? *eslot_at(p, obp, rep, e0 + le) : make_uint4(0, 0, 0, 0);
     }
@@ -3854,7 +3896,7 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
       int64_t et = 0;
       uint32_t edt = 0, esub = 0;
       int ebig = 0;
-      if (rx) {
+      if (rxe) {
         const uint32_t fl = r0[u].w >> 24;
         const long long ta0 = cs + r0[u].x;
         if (slot_live(fl, cell_tag(p, cell)) && ta0 >= t_lo && ta0 < t_hi) {
