@@ -2400,6 +2400,11 @@ __device__ inline uint32_t fast_key_find(const FastShared& F, uint32_t key) {
   return s;
 }
 
+// BCSIM_WGT=1 (debug): per-workgroup phase clock of k_scan_pbft, same slots as scan_node's SPH
+#define FPH(k)                                                                              \
+  do {                                                                                      \
+    if (p.wgs && tid == 0) p.wgs[8ull * g + (k)] = __builtin_amdgcn_s_memrealtime();       \
+  } while (0)
 __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                    long long t_hi, long long cs, int x_active) {
   const KP& p = *pk;
@@ -2424,6 +2429,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     if (tid == 0) AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
     return;
   }
+  FPH(0);
   const Rec* slots = p.inbox + inbox_idx(p, b, rep, e0);
   uint4 rv[kFastRPL];
 #pragma unroll
@@ -2505,6 +2511,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   }
   if (bad) F.bad = 1;
   __syncthreads();
+  FPH(1);
   // group bases: the stored vote counters, then the segments in arrival order
   const size_t base = static_cast<size_t>(g) * p.pbft_seq_cap;
   if (tid < kFastKeys) {
@@ -2528,6 +2535,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     if (tid == 0) AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
     return;
   }
+  FPH(2);
   const int32_t N = static_cast<int32_t>(p.N);
   const uint32_t T1 = static_cast<uint32_t>(N / 2), T2 = T1 + 1;
   // ---- pass 2: quorum crossings; per-segment counts of the flagged arrivals ----
@@ -2570,6 +2578,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     }
   }
   __syncthreads();
+  FPH(3);
   // exclusive segment bases (wave 0: one segment per lane); totals to every lane
   uint4 tot;
   {
@@ -2607,6 +2616,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     return;
   }
   __syncthreads();
+  FPH(4);
   // ---- pass 3: outputs, every arrival with its counter values from the bases + popcounts ----
   Op* ops = p.ops + op_base(p, g);
   const int64_t app = p.app_delay;
@@ -2672,6 +2682,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
       }
     }
   }
+  FPH(5);
   if (echo_here) {  // one link word per arrival (distinct in-slots = distinct out-edges), coalesced
     uint64_t lw[kFastRPL];
 #pragma unroll
@@ -2701,6 +2712,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     }
   }
   __syncthreads();
+  FPH(6);
   // ---- tx[n].val of the window's PRE_PREPAREs (the last one per index wins) ----
   for (uint32_t u = tid; u < F.npp; u += kFastLanes) {
     bool last = true;
@@ -2720,6 +2732,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   AT(p.n_ops, g, p.NT) = nops0 + tot.y;
   if (tot.y) AT(p.node_onext, g, p.NT) = LLONG_MIN;  // the link stage recomputes
   AT(p.block_num, g, p.NT) = bn0 + static_cast<int32_t>(tot.z);
+  FPH(7);
   if (echo_here) {
     AT(p.eapp, g, p.NT) = t_lo;
     if (tot.w) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(tot.w));
@@ -3870,7 +3883,10 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   const uint32_t f2r = static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0)));
   const uint32_t w3r = f2r | (kPbPrepareRes << 16);  // a reply slot's (f2, type) word
   const uint32_t bs = blockDim.x;
-  for (uint32_t base = tid; base < deg; base += kMeshU * bs) {
+  // (a node whose broadcasts are not due yet and that has no reply slot or echo to send skips
+  // the edges: their link words would be loaded for nothing)
+  const uint32_t deg_w = (n_bc || sl0 || sl1 || rxe) ? deg : 0u;
+  for (uint32_t base = tid; base < deg_w; base += kMeshU * bs) {
     // all loads of the kU edges first (independent addresses), then the per-edge work
     uint64_t lw[kMeshU];
     uint4 r0[kMeshU], w0[kMeshU], w1[kMeshU];
