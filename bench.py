@@ -202,7 +202,7 @@ def main():
                          "paxos: configs[2] shape (jittered links, batched Monte Carlo replicas)")
     ap.add_argument("--nodes", type=int, default=0, help="default 4096 (pbft, paxos) / 65536 (gossip)")
     ap.add_argument("--replicas", type=int, default=0,
-                    help="paxos: replicas in one engine (default 2048, sparse layout; configs[2] names 10k)")
+                    help="paxos: replicas in one engine (default 10000 = configs[2], sparse layout)")
     ap.add_argument("--decrees", type=int, default=2, help="paxos: decrees per proposer (multi-decree extension)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -216,8 +216,8 @@ def main():
     args = ap.parse_args()
     if args.nodes <= 0:
         args.nodes = 65536 if args.workload == "gossip" else 4096
-    if args.replicas <= 0:
-        args.replicas = 2048 if args.workload == "paxos" else 1
+    if args.replicas <= 0:  # configs[2]: 10k batched Monte Carlo replicas
+        args.replicas = 10000 if args.workload == "paxos" else 1
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -334,6 +334,10 @@ def main():
                     "1000 B blocks, fixed 3 ms app delay)" % args.nodes)
             wl = f"PBFT-style gossip n={args.nodes} random 8-regular (BASELINE configs[4])"
         lk_launch_bytes = lk["bytes"] / max(1, lk["launches"])
+        # the whole scan -> link pipeline priced the same way: 48 B per record over the time of
+        # both classes (untimed breakdown pass, every class timed)
+        sl_us = ks_all["scan"]["us"] + ks_all["link"]["us"]
+        pipe_ach = (ks_all["link"]["bytes"] / 1e9) / (sl_us / 1e6) if sl_us > 0 else 0.0
         impl_launch_bytes = ks["aux"]["bytes"] / max(1, lk["launches"])
         out = {
             "metric": METRIC,
@@ -363,7 +367,10 @@ def main():
                          # the timed launches are k_link dispatches [first, first + launches) of the
                          # process: tools/pmc_summary.py restricts rocprofv3 traces to them
                          "first_timed_launch": link_before,
-                         "dominant_kernel_class": dom},
+                         "dominant_kernel_class": dom,
+                         "pipeline": {"kernels": "k_scan + k_link classes", "achieved": pipe_ach,
+                                      "frac": pipe_ach / HBM_PEAK_GBS, "us": sl_us,
+                                      "records": ks_all["link"]["bytes"] / 48.0}},
             "kernel_us": {k: v["us"] for k, v in ks.items()},
             "kernel_launches": {k: v["launches"] for k, v in ks.items()},
             # untimed pass of as many steps with every kernel class timed (the timed region

@@ -45,6 +45,7 @@ class TorchTransport:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.error = None
+        self.bytes = 0  # payload bytes this rank sent through alltoallv (exchange volume)
         # keep the ctypes thunks alive as long as the transport
         self._ar = ALLREDUCE_FN(self._allreduce)
         self._a2a = ALLTOALLV_FN(self._alltoallv)
@@ -68,6 +69,7 @@ class TorchTransport:
             import torch
             P = self.world
             sb = [int(send_bytes[r]) for r in range(P)]
+            self.bytes += sum(b for r, b in enumerate(sb) if b < PEER_ERR and r != self.rank)
             # sizes: row r of the gathered matrix = what rank r sends to each rank
             sz = torch.tensor(sb, dtype=torch.int64)
             rows = [torch.empty(P, dtype=torch.int64) for _ in range(P)]

@@ -76,6 +76,7 @@ struct Sim {
   bool gossip_link = false;
   bool mesh_link = false;  // full mesh, fixed delay: k_link_mesh first, k_link over list 3
   bool scan_fast = false;  // dense PBFT, fixed delay, reply slots: k_scan_pbft first, k_scan over list 2
+  uint32_t mesh_u = 2;     // k_link_mesh out-edges per lane per iteration (BCSIM_MESH_U=4: tuning A/B)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -524,6 +525,7 @@ static int setup_device(Sim& s) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_scan)));
     for (const void* f : {reinterpret_cast<const void*>(k_link<false, false>), reinterpret_cast<const void*>(k_link<false, true>),
                           reinterpret_cast<const void*>(k_link<false, false, true>),
+                          reinterpret_cast<const void*>(k_link<false, true, true>),
                           reinterpret_cast<const void*>(k_link<true, false>), reinterpret_cast<const void*>(k_link<true, true>)})
       HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(link_lds_bytes(p))));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_pbft_tick),
@@ -640,7 +642,7 @@ static int setup_device(Sim& s) {
     // (BCSIM_NO_MFAST=1: off)
     {
       const char* mf = std::getenv("BCSIM_NO_MFAST");
-      s.mesh_link = p.mesh && !s.sparse && s.P == 1 && c.delay_mode == BCSIM_DELAY_FIXED &&
+      s.mesh_link = p.mesh && !s.sparse && c.delay_mode == BCSIM_DELAY_FIXED &&
                     c.queue_model == BCSIM_QUEUE_INFINITE && !(mf && *mf == '1');
     }
     // PBFT replies with a fixed app delay < L (due in the arrival cell or the next)
@@ -653,6 +655,7 @@ static int setup_device(Sim& s) {
       // testing aid: BCSIM_FEW_SCAN=0 sends small launches (every launch of a small parity case)
       // through k_scan_pbft too
       if (const char* fs = std::getenv("BCSIM_FEW_SCAN"); fs && *fs) s.few_scan = static_cast<uint32_t>(std::atoi(fs));
+      if (const char* mu = std::getenv("BCSIM_MESH_U"); mu && std::atoi(mu) == 4) s.mesh_u = 4;
     }
     if ((rc = dalloc(s, &p.eslot, p.cap_eslot)) || (rc = dalloc(s, &p.sflag, static_cast<size_t>(kOpRing) * NT)))
       return rc;
@@ -1054,9 +1057,13 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     const bool timed = (kstat_mask() >> KS_LINK) & 1u;
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
     // (list 3 holds a few nodes, the leader's cells among them: wide workgroups)
-    if ((rc = launch(s, -1, k_link_mesh, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
-        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(256, s.grid_link)),
-                     dim3(std::min<uint32_t>(1024, 4 * s.bs_link)), link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
+    // (node-partitioned: the kernels that stage records for other ranks)
+    const dim3 gl(std::min<uint32_t>(256, s.grid_link)), bl(std::min<uint32_t>(1024, 4 * s.bs_link));
+    if (s.P > 1 ? ((rc = launch(s, -1, k_link_mesh<true, 2>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
+                   (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
+                : ((rc = (s.mesh_u == 4 ? launch(s, -1, k_link_mesh<false, 4>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)
+                                        : launch(s, -1, k_link_mesh<false, 2>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw))) ||
+                   (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw))))
       return rc;
     if (timed) {
       if ((rc = ev_end(s))) return rc;

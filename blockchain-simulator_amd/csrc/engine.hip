@@ -2362,6 +2362,7 @@ struct FastShared {
   int32_t pp_idx[kFastPP], pp_val[kFastPP];
   uint32_t tcount[4];  // deliveries: PRE_PREPARE, PREPARE, COMMIT, PREPARE_RES
   uint32_t ocnt[2];    // reply slots due in this cell / the next
+  uint64_t lw[kFastRPL * kFastLanes];  // link words of the node's out-edges (echo pass)
 };
 
 // record words {t_off, sub, f0 | f1 << 16, f2 | type << 16 | flags << 24} -> payload chars after
@@ -2430,12 +2431,34 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     return;
   }
   FPH(0);
+  // The implicit echoes (pbft-node.cc:175: every delivery goes back out on the reverse edge,
+  // occupying it) are applied here, on the link words of the node's out-edges, when no op of
+  // the node is due in the window apart from the ones this scan creates -- those are due
+  // app_delay after the arrivals, so they follow the echoes in key order (t, then t - dt).
+  // The link kernels then skip the echoes of this window (eapp stamp) instead of reading the
+  // row a second time; otherwise they do them, merged with the due ops, as before.
+  const bool echo_here =
+      p.echo && p.qmodel == 0 && AT(p.node_onext, g, p.NT) >= t_hi &&
+      !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u) &&
+      !(AT(p.sflag, static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u);
   const Rec* slots = p.inbox + inbox_idx(p, b, rep, e0);
   uint4 rv[kFastRPL];
 #pragma unroll
   for (uint32_t j = 0; j < kFastRPL; ++j) {  // the whole row in flight at once
     const uint32_t k = j * kFastLanes + tid;
     rv[j] = k < deg ? *reinterpret_cast<const uint4*>(slots + k) : make_uint4(0, 0, 0, 0);
+  }
+  // ... and the link words of its out-edges with it (LDS; used by the echo pass at the end)
+  if (echo_here) {
+    const uint64_t* lrow = p.link + edge_loc(p, rep, e0);
+    uint64_t lv[kFastRPL];
+#pragma unroll
+    for (uint32_t j = 0; j < kFastRPL; ++j) {
+      const uint32_t k = j * kFastLanes + tid;
+      lv[j] = k < deg ? lrow[k] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kFastRPL; ++j) F.lw[j * kFastLanes + tid] = lv[j];
   }
   if (tid == 0) {
     F.bad = 0;
@@ -2601,16 +2624,6 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   }
   const uint32_t sub0 = AT(p.sub, g, p.NT), nops0 = AT(p.n_ops, g, p.NT);
   const int32_t bn0 = AT(p.block_num, g, p.NT);
-  // The implicit echoes (pbft-node.cc:175: every delivery goes back out on the reverse edge,
-  // occupying it) are applied here, on the link words of the node's out-edges, when no op of
-  // the node is due in the window apart from the ones this scan creates -- those are due
-  // app_delay after the arrivals, so they follow the echoes in key order (t, then t - dt).
-  // The link kernels then skip the echoes of this window (eapp stamp) instead of reading the
-  // row a second time; otherwise they do them, merged with the due ops, as before.
-  const bool echo_here =
-      p.echo && p.qmodel == 0 && AT(p.node_onext, g, p.NT) >= t_hi &&
-      !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u) &&
-      !(AT(p.sflag, static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u);
   if (nops0 + tot.y > op_cap(p, g)) {
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
     return;
@@ -2684,19 +2697,17 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   }
   FPH(5);
   if (echo_here) {  // one link word per arrival (distinct in-slots = distinct out-edges), coalesced
-    uint64_t lw[kFastRPL];
-#pragma unroll
-    for (uint32_t j = 0; j < kFastRPL; ++j)
-      lw[j] = ((vmask >> j) & 1u) ? p.link[edge_loc(p, rep, e0 + j * kFastLanes + tid)] : 0ull;
+    uint64_t* lrow = p.link + edge_loc(p, rep, e0);
 #pragma unroll
     for (uint32_t j = 0; j < kFastRPL; ++j) {
       if (!((vmask >> j) & 1u)) continue;
       const uint4 r = rv[j];
+      const uint64_t lw = F.lw[j * kFastLanes + tid];
       const int64_t t = cs + static_cast<int64_t>(r.x);
-      const int64_t bu0 = static_cast<int64_t>(lw[j] >> 16);
+      const int64_t bu0 = static_cast<int64_t>(lw >> 16);
       const int64_t bu = (bu0 > t ? bu0 : t) + p.tx_tot[((r.w >> 24) & RF_BIG) ? 1 : 0];
       if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
-      p.link[edge_loc(p, rep, e0 + j * kFastLanes + tid)] = (static_cast<uint64_t>(bu) << 16) | (lw[j] & 0xFFFFull);
+      lrow[j * kFastLanes + tid] = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
     }
   }
 #pragma unroll
@@ -3767,7 +3778,7 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
 // memory round trips in flight instead of one.  A node with a listed op due (unicast /
 // echo op), too many broadcasts or an unexpanded jitter broadcast goes to list 3, which
 // k_link<false, false, LOOP> finishes after this kernel.
-constexpr int kMeshU = 2;
+// kMeshU (template): out-edges per lane per iteration, their loads issued together
 __device__ inline bool kless(int64_t ta, uint32_t dta, uint32_t oa, uint32_t sa, int64_t tb, uint32_t dtb, uint32_t ob,
                              uint32_t sb) {
   if (ta != tb) return ta < tb;
@@ -3777,6 +3788,50 @@ __device__ inline bool kless(int64_t ta, uint32_t dta, uint32_t oa, uint32_t sa,
   return sa < sb;
 }
 
+// Cross-rank broadcast de-duplication (SURVEY.md §8e "Collective"): a wave of k_link_mesh
+// covers 64 consecutive out-edges of one sender, i.e. 64 consecutive receivers (skipping the
+// sender itself).  When the lanes holding a record for one other rank form a contiguous run and
+// their records are equal up to the schedule counter, which steps by one per edge (a
+// broadcast: sub + le, pbft-node.cc:360-367), the run is shipped as ONE range record -- the
+// first record, sender node in `slot`, first receiver in `g`, count and a range bit in the top
+// bits of `cell` -- and k_import expands it on the receiving rank.  Anything else is shipped
+// record by record.  Convergent: every lane of the wave calls it.
+constexpr uint64_t kXRange = 1ull << 62;
+constexpr int kXCountShift = 48;
+constexpr uint64_t kXCellMask = (1ull << kXCountShift) - 1;
+__device__ inline void xr_ship(const KP& p, LinkShared& L, uint32_t g, uint32_t i, uint32_t le, bool hp, const XRec& x,
+                               uint32_t orank) {
+  const uint32_t lane = tidx() & 63u;
+  unsigned long long rem = __ballot(hp);
+  const uint4 rw = *reinterpret_cast<const uint4*>(&x.r);
+  while (rem) {
+    const int ld = __ffsll(static_cast<long long>(rem)) - 1;
+    const uint32_t rk = __shfl(orank, ld, 64);
+    const unsigned long long grp = __ballot(hp && orank == rk);
+    const uint32_t l_tof = __shfl(rw.x, ld, 64), l_sub = __shfl(rw.y, ld, 64);
+    const uint32_t l_z = __shfl(rw.z, ld, 64), l_w = __shfl(rw.w, ld, 64);
+    const long long l_cell = __shfl(x.cell, ld, 64);
+    const uint32_t l_le = __shfl(le, ld, 64);
+    const bool mine = hp && orank == rk;
+    const bool ok = mine && rw.x == l_tof && rw.z == l_z && rw.w == l_w && x.cell == l_cell && rw.y == l_sub + (le - l_le);
+    const unsigned long long okm = __ballot(ok);
+    const unsigned long long run = grp >> ld;  // contiguous lanes ld .. ld + n - 1
+    const uint32_t n = static_cast<uint32_t>(__popcll(grp));
+    if (okm == grp && n >= 2 && (run & (run + 1)) == 0) {
+      if (lane == static_cast<uint32_t>(ld)) {
+        XRec xr = x;
+        xr.cell = static_cast<long long>(static_cast<uint64_t>(x.cell) | kXRange | (static_cast<uint64_t>(n) << kXCountShift));
+        xr.slot = i;  // the sender (range records: full mesh only)
+        link_stage(p, L, g, p.n_buckets + 1 + rk, xr);
+      }
+    } else if (mine) {
+      link_stage(p, L, g, p.n_buckets + 1 + rk, x);
+    }
+    rem &= ~grp;
+  }
+}
+
+template <bool XR, int kMeshU>
 __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                    long long t_hi, int final_win) {
   const KP& p = *pk;
@@ -3808,7 +3863,8 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
     L.lcnt[k] = 0;
     L.lmin[k] = ~0u;
   }
-  for (uint32_t k = tid; k <= B; k += blockDim.x) L.lst[k] = 0;
+  const uint32_t n_lists = B + 1 + (XR ? p.nranks : 0);  // extras..., overflow, ranks...
+  for (uint32_t k = tid; k < n_lists; k += blockDim.x) L.lst[k] = 0;
   const bool tmap = p.n_tiles <= static_cast<uint32_t>(kMaxTiles);
   if (tmap)
     for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x) L.tflag[k] = 0;
@@ -3886,7 +3942,20 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   // (a node whose broadcasts are not due yet and that has no reply slot or echo to send skips
   // the edges: their link words would be loaded for nothing)
   const uint32_t deg_w = (n_bc || sl0 || sl1 || rxe) ? deg : 0u;
-  for (uint32_t base = tid; base < deg_w; base += kMeshU * bs) {
+  const bool xr = XR;  // (a template flag: the one-rank kernel carries no staging registers)
+  // (a wave-uniform trip count: the cross-rank range step after the edges is convergent)
+  for (uint32_t b0 = 0; b0 < deg_w; b0 += kMeshU * bs) {
+    const uint32_t base = b0 + tid;
+    // node-partitioned run: each edge's first record for another rank's receiver waits here,
+    // so that a wave can ship a run of them as one range record (xr_ship)
+    XRec xp[kMeshU];
+    bool hp[kMeshU];
+    uint32_t xo[kMeshU];
+#pragma unroll
+    for (int u = 0; u < kMeshU; ++u) {
+      hp[u] = false;
+      xo[u] = 0;
+    }
     // all loads of the kU edges first (independent addresses), then the per-edge work
     uint64_t lw[kMeshU];
     uint4 r0[kMeshU], w0[kMeshU], w1[kMeshU];
@@ -4017,6 +4086,25 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
         }
         const bool owner = lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
         lc = static_cast<uint32_t>(ca) & 0xFFFFu;
+        if (xr) {
+          const uint32_t orank = p.owner[s];
+          if (orank != p.rank) {  // receiver on another GPU: shipped, k_import places it
+            XRec x;
+            x.r = r;
+            if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+            x.cell = ca;
+            x.slot = slot;
+            x.g = dg;
+            if (!hp[u]) {
+              xp[u] = x;
+              hp[u] = true;
+              xo[u] = orank;
+            } else {
+              link_stage(p, L, g, B + 1 + orank, x);
+            }
+            continue;
+          }
+        }
         if (rel < static_cast<long long>(B)) {
           const uint32_t bk = static_cast<uint32_t>(ca % B);
           if (owner) {
@@ -4068,6 +4156,10 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
       if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
       *lwp[u] = (static_cast<uint64_t>(bu) << 16) | lc;
     }
+    if (xr) {
+#pragma unroll
+      for (int u = 0; u < kMeshU; ++u) xr_ship(p, L, g, i, base + u * bs, hp[u], xp[u], xo[u]);
+    }
   }
   if (cbn) {
     atomicAdd(&L.lcnt[cb], cbn);
@@ -4083,7 +4175,7 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   unsigned long long ph[4] = {t0, t0, t0, t0};
   const LinkCounts c8{dropped, sends, n_rec, st_ops, st_edges, st_echo, 0u, 0u};
   // every op due (the broadcasts just sent): nothing to compact, no op to read again
-  link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, B + 1, ovmin, c8, sl1 && final_win, rx && final_win, obp, fidx, t0,
+  link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, n_lists, ovmin, c8, sl1 && final_win, rx && final_win, obp, fidx, t0,
               ph, n);
 }
 
@@ -4951,53 +5043,82 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
 }
 
 // ---------------------------------------------------------------------------
-// k_import (multi-GPU): place the records received from other ranks -- the
-// same rules as a local k_link emission (slot owner -> inbox, or outbox +
-// tile flag for the full mesh; second record of an edge -> extras; beyond
-// the ring -> overflow).  g_cur = the cell just processed.
+// place one received record (the rules of a local emission)
+__device__ inline void import_one(const KP& p, long long g_cur, XRec x, uint32_t* lb, long long& ovmin) {
+  const uint32_t B = p.n_buckets;
+  const uint32_t rep = x.g / p.N;
+  if (x.cell < g_cur + static_cast<long long>(B)) {
+    const uint32_t b = static_cast<uint32_t>(x.cell % B);
+    const bool owner = (x.r.flags & RF_OWNER) != 0;
+    x.r.flags = static_cast<uint8_t>((x.r.flags & (RF_VALID | RF_BIG)) | (cell_tag(p, x.cell) << 3));
+    if (owner) {
+      st_rec(&AT(p.inbox, inbox_idx(p, b, rep, x.slot), p.cap_inbox), x.r);
+    } else {
+      const uint32_t pos = atomicAdd(&p.x_cnt[b], 1u);
+      if (pos < p.cap_x)
+        AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
+      else
+        set_err(p, BCSIM_E_OVERFLOW);
+    }
+    set_flag_once(&AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(B) * p.NT));
+    bmin_lower(p, b, x.cell * p.L + static_cast<long long>(x.r.t_off));
+    atomicAdd(&lb[b], 1u);
+  } else {
+    const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+    if (pos < p.cap_ov)
+      AT(p.ov, pos, p.cap_ov) = x;
+    else
+      set_err(p, BCSIM_E_OVERFLOW);
+    ovmin = min(ovmin, static_cast<long long>(x.cell));
+  }
+}
+
+// k_import (multi-GPU): place the records received from other ranks -- the same rules as a
+// local k_link emission (slot owner -> inbox, second record of an edge -> extras, beyond the
+// ring -> overflow); a range record (xr_ship) is expanded here into its per-edge records
+// (receiver s, its in-slot and sub + k follow from the sender and the first receiver).
+// g_cur = the cell just processed.
 __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long long g_cur, const XRec* __restrict__ rx,
                                                 uint32_t n) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ uint32_t lb[kMaxBuckets];
-  __shared__ long long ovmin;
+  __shared__ long long ovmin_s;
   const uint32_t B = p.n_buckets;
   for (uint32_t k = tidx(); k < B; k += blockDim.x) lb[k] = 0;
-  if (tidx() == 0) ovmin = LLONG_MAX;
+  if (tidx() == 0) ovmin_s = LLONG_MAX;
   __syncthreads();
   const uint32_t k = blockIdx.x * blockDim.x + tidx();
+  long long ovmin = LLONG_MAX;
   if (k < n) {
     XRec x = rx[k];
-    const uint32_t rep = x.g / p.N;
-    if (x.cell < g_cur + static_cast<long long>(B)) {
-      const uint32_t b = static_cast<uint32_t>(x.cell % B);
-      const bool owner = (x.r.flags & RF_OWNER) != 0;
-      x.r.flags = static_cast<uint8_t>((x.r.flags & (RF_VALID | RF_BIG)) | (cell_tag(p, x.cell) << 3));
-      if (owner) {
-        st_rec(&AT(p.inbox, inbox_idx(p, b, rep, x.slot), p.cap_inbox), x.r);
+    const uint64_t cw = static_cast<uint64_t>(x.cell);
+    if (cw & kXRange) {
+      const uint32_t cnt = static_cast<uint32_t>((cw >> kXCountShift) & 0x3FFFu);
+      const uint32_t i = x.slot, rep = x.g / p.N, s0 = x.g % p.N, N1 = p.N - 1;
+      if (!p.mesh || i >= p.N || s0 == i) {
+        set_err(p, BCSIM_E_STATE);
       } else {
-        const uint32_t pos = atomicAdd(&p.x_cnt[b], 1u);
-        if (pos < p.cap_x)
-          AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
-        else
-          set_err(p, BCSIM_E_OVERFLOW);
+        const uint32_t le0 = s0 < i ? s0 : s0 - 1, sub0 = x.r.sub;
+        x.cell = static_cast<long long>(cw & kXCellMask);
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const uint32_t le = le0 + j, s = le < i ? le : le + 1;
+          XRec y = x;
+          y.r.sub = sub0 + j;
+          y.slot = s * N1 + (i < s ? i : i - 1);
+          y.g = rep * p.N + s;
+          import_one(p, g_cur, y, lb, ovmin);
+        }
       }
-      set_flag_once(&AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(B) * p.NT));
-      bmin_lower(p, b, x.cell * p.L + static_cast<long long>(x.r.t_off));
-      atomicAdd(&lb[b], 1u);
     } else {
-      const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
-      if (pos < p.cap_ov)
-        AT(p.ov, pos, p.cap_ov) = x;
-      else
-        set_err(p, BCSIM_E_OVERFLOW);
-      atomicMin(&ovmin, x.cell);
+      import_one(p, g_cur, x, lb, ovmin);
     }
   }
+  if (ovmin != LLONG_MAX) atomicMin(&ovmin_s, ovmin);
   __syncthreads();
   for (uint32_t q = tidx(); q < B; q += blockDim.x)
     if (lb[q]) mark_busy(&p.bucket_cnt[q]);
-  if (tidx() == 0 && ovmin != LLONG_MAX) atomicMin(&p.scal[1], ovmin);
+  if (tidx() == 0 && ovmin_s != LLONG_MAX) atomicMin(&p.scal[1], ovmin_s);
 }
 
 // k_lead (multi-GPU, PBFT): this rank's "ticking leader" flags for k_pbft_tick

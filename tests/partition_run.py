@@ -38,7 +38,10 @@ def _worker(rank, world, port, names, transport, q):
                         s.set_topology(*topo)
                     s.set_partition(dist, transport=transport)
                     s.run()
-                    q.put((name, rank, s.trace(), s.counters(), None))
+                    cnt = s.counters()
+                    if transport == "host":  # exchange volume (bytes this rank sent to the others)
+                        cnt["xfer_bytes"] = s._transport.bytes
+                    q.put((name, rank, s.trace(), cnt, None))
             except Exception as e:  # report, keep the other ranks' collectives aligned
                 q.put((name, rank, None, None, repr(e)))
                 raise

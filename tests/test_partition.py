@@ -156,6 +156,12 @@ def test_partitioned_fullsize_equals_single(name, engine_lib):
     assert err is None, err
     d = compare(single, merged)
     assert d is None, f"{name} world=2: {d}"
+    if name.startswith("c4"):
+        # broadcast de-dup (k_link_mesh xr_ship -> k_import): about half the 16.8 M records of
+        # a heavy cell cross ranks, shipped as range records of up to 64 edges, so the volume
+        # is far below one 32-byte record per cross-rank delivery
+        cross = single[1]["delivered_total"] // 2
+        assert merged[1]["xfer_bytes"] < cross * 32 // 16, (merged[1]["xfer_bytes"], cross)
 
 
 def _rccl1_worker(port, names, q):

@@ -67,7 +67,22 @@ def test_c3_paxos4096_10k_replicas_fit(engine_lib):
     c.t_end_ns = 100_000_000
     with bcsim.Simulator(c) as s:
         s.run()
-        cnt, st = s.counters(), s.status()
+        cnt, st, tr = s.counters(), s.status(), s.trace()
     assert st["error"] == 0
     d = cnt["delivered"]
     assert d[0] > 10_000 * (n_min := 3 * 4000) and d[3] <= d[0]
+    # per replica: the three proposers request their first ticket at t = 0 (paxos-node.cc:136-138,
+    # :510-522), and every ticket broadcast of the window is logged once (:518)
+    from collections import defaultdict
+    t0 = defaultdict(set)
+    tickets = 0
+    for r in tr:
+        if r[6] == _abi.TR["PAXOS_TICKET"]:
+            tickets += 1
+            if r[1] == 0:
+                t0[r[0]].add(r[5])
+    assert len(t0) == 10_000 and all(v == {0, 1, 2} for v in t0.values())
+    # a ticket broadcast reaches at most N-2 peers (:481-496: the *end() send is dropped)
+    assert d[0] <= (4096 - 2) * tickets
+    # one response per delivered request, never more (:177-247)
+    assert d[3] <= d[0] and d[4] <= d[1] and d[5] <= d[2]
