@@ -46,6 +46,8 @@ def lib():
         _LIB.bcsim_read_kernel_stats.restype = C.c_int
         _LIB.bcsim_read_engine_counters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         _LIB.bcsim_read_engine_counters.restype = C.c_int
+        _LIB.bcsim_read_loop_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        _LIB.bcsim_read_loop_stats.restype = C.c_int
         _LIB.bcsim_reset_kernel_stats.argtypes = [C.c_void_p]
         _LIB.bcsim_reset_kernel_stats.restype = C.c_int
         _LIB.bcsim_topology_random_regular.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64,
@@ -106,6 +108,12 @@ class Simulator(_abi.Handle):
         self._call("read_engine_counters", self.h, out)
         names = ("records", "due_ops", "edges", "kept_ops", "delivered", "scan_ops", "echoes", "split_windows")
         return dict(zip(names, out))
+
+    def loop_stats(self):
+        """Cell-loop statistics (include/bcsim.h bcsim_read_loop_stats)."""
+        out = (C.c_uint64 * 4)()
+        self._call("read_loop_stats", self.h, out)
+        return dict(windows=out[0], collectives=out[1], tag_zeroes=out[2])
 
     def reset_kernel_stats(self):
         self._call("reset_kernel_stats", self.h)

@@ -32,7 +32,7 @@ struct Ctl {
   int32_t err;
   uint32_t trace_cnt, vlog_cnt, dreq_cnt, ov_cnt;
   int32_t dbg;
-  long long scal[4];  // next_local, ov_min_cell, n_alive_ticks, next timer
+  long long scal[6];  // next_local, ov_min_cell, n_alive_ticks, next timer, min shipped cell, (pad)
   // followed by bucket_cnt[B] and x_cnt[B]
 };
 
@@ -76,7 +76,6 @@ struct Sim {
   bool gossip_link = false;
   bool mesh_link = false;  // full mesh, fixed delay: k_link_mesh first, k_link over list 3
   bool scan_fast = false;  // dense PBFT, fixed delay, reply slots: k_scan_pbft first, k_scan over list 2
-  uint32_t mesh_u = 2;     // k_link_mesh out-edges per lane per iteration (BCSIM_MESH_U=4: tuning A/B)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -104,6 +103,9 @@ struct Sim {
   XRec* recvbuf = nullptr;
   uint64_t cap_recv = 0;
   uint32_t vsync = 0;          // v-log entries already exchanged
+  long long next_cell = 0;     // node-partitioned: the next cell of the whole system, agreed by the
+  bool next_known = false;     // last cell's control exchange (no separate all-reduce needed)
+  uint64_t ctl_collectives = 0;  // collectives + host syncs of the cell loop (engine counters)
   std::vector<int64_t> lead_w; // leader flags packed for the all-reduce
 };
 
@@ -655,7 +657,6 @@ static int setup_device(Sim& s) {
       // testing aid: BCSIM_FEW_SCAN=0 sends small launches (every launch of a small parity case)
       // through k_scan_pbft too
       if (const char* fs = std::getenv("BCSIM_FEW_SCAN"); fs && *fs) s.few_scan = static_cast<uint32_t>(std::atoi(fs));
-      if (const char* mu = std::getenv("BCSIM_MESH_U"); mu && std::atoi(mu) == 4) s.mesh_u = 4;
     }
     if ((rc = dalloc(s, &p.eslot, p.cap_eslot)) || (rc = dalloc(s, &p.sflag, static_cast<size_t>(kOpRing) * NT)))
       return rc;
@@ -817,7 +818,7 @@ static int setup_device(Sim& s) {
     HIPCHK(hipMemcpy(p.eapp, never.data(), NT * 8, hipMemcpyHostToDevice));
   }
   HIPCHK(hipMemset(s.ctl_d, 0, ctl_bytes));
-  long long sc0[4] = {LLONG_MAX, LLONG_MAX, 0, 0};
+  long long sc0[6] = {LLONG_MAX, LLONG_MAX, 0, 0, LLONG_MAX, 0};
   HIPCHK(hipMemcpy(p.scal, sc0, sizeof sc0, hipMemcpyHostToDevice));
   // counters' t_last slot starts at 0 (max)
   HIPCHK(hipDeviceSynchronize());
@@ -1061,8 +1062,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     const dim3 gl(std::min<uint32_t>(256, s.grid_link)), bl(std::min<uint32_t>(1024, 4 * s.bs_link));
     if (s.P > 1 ? ((rc = launch(s, -1, k_link_mesh<true, 2>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
                    (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
-                : ((rc = (s.mesh_u == 4 ? launch(s, -1, k_link_mesh<false, 4>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)
-                                        : launch(s, -1, k_link_mesh<false, 2>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw))) ||
+                // (a few nodes -- the leader's block broadcast at a tick -- get 1024-lane workgroups:
+                // the launch is one workgroup's latency)
+                : ((rc = launch(s, -1, k_link_mesh<false, 2>, grid, dim3(n_link <= 64 ? 1024 : 256), 0, s.kp_dev, cell, lo,
+                                hi, fw)) ||
                    (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw))))
       return rc;
     if (timed) {
@@ -1199,27 +1202,69 @@ static int readback(Sim& s) {
 // `lrc` is this rank's status of the cell so far: a failed rank sends the kPeerErr
 // count to everyone instead of data, so every rank leaves together (no rank is left
 // waiting in a collective the failed one never joins).
-static int exchange(Sim& s, long long cell, int lrc) {
-  std::vector<uint64_t> sb(s.P), rb(s.P);
-  for (uint32_t r = 0; r < s.P && !lrc; ++r)
+static long long local_next_cell(const Sim& s, bool with_tick);
+
+// The per-cell exchange of a node-partitioned run: ONE control all-to-all --
+// per peer the byte size of the records staged for it (kPeerErr: this rank failed), this
+// rank's next-cell candidate, the earliest arrival cell it ships to anyone, and (tick cells)
+// its ticking PBFT nodes -- from which every rank derives the same next cell, PBFT n_alive
+// and status; then the records themselves (sizes known on both sides) and k_import.
+static int exchange(Sim& s, long long cell, int lrc, bool tick) {
+  const uint32_t P = s.P, W = Xport::kCtlWords;
+  for (uint32_t r = 0; r < P && !lrc; ++r)
     if (s.scnt_h[r] > s.kp.cap_send) {
       g_detail = "multi-GPU send list overflowed";
       lrc = BCSIM_E_OVERFLOW;
     }
-  for (uint32_t r = 0; r < s.P; ++r) sb[r] = lrc ? kPeerErr : static_cast<uint64_t>(s.scnt_h[r]) * sizeof(XRec);
-  int rc = s.xp->alltoallv_dev(s.stream, reinterpret_cast<const char*>(s.kp.sendbuf),
-                               static_cast<uint64_t>(s.kp.cap_send) * sizeof(XRec), sb.data(),
-                               reinterpret_cast<char*>(s.recvbuf), s.cap_recv * sizeof(XRec), rb.data());
+  const long long cand = lrc ? LLONG_MAX : local_next_cell(s, false);
+  const long long xmin = lrc ? LLONG_MAX : s.ctl_h->scal[4];
+  const int64_t alive = (tick && !lrc) ? s.ctl_h->scal[2] : 0;
+  std::vector<int64_t> snd(static_cast<size_t>(P) * W), rcv(static_cast<size_t>(P) * W);
+  std::vector<uint64_t> sb(P), rb(P);
+  for (uint32_t r = 0; r < P; ++r) {
+    sb[r] = lrc ? kPeerErr : static_cast<uint64_t>(s.scnt_h[r]) * sizeof(XRec);
+    snd[r * W + 0] = static_cast<int64_t>(sb[r]);
+    snd[r * W + 1] = cand;
+    snd[r * W + 2] = xmin;
+    snd[r * W + 3] = alive;
+  }
+  int rc = s.xp->ctl_exchange(s.stream, snd.data(), rcv.data());
+  ++s.ctl_collectives;
   if (rc) return rc;
   if (lrc) return lrc;
-  for (uint32_t r = 0; r < s.P; ++r)
+  long long nx = LLONG_MAX;
+  int64_t na = 0;
+  uint64_t n = 0;
+  for (uint32_t r = 0; r < P; ++r) {
+    rb[r] = static_cast<uint64_t>(rcv[r * W + 0]);
     if (rb[r] == kPeerErr) {
       g_detail = "rank " + std::to_string(r) + " of the partition failed";
       return BCSIM_E_PEER;
     }
+    nx = std::min<long long>(nx, rcv[r * W + 1]);
+    nx = std::min<long long>(nx, rcv[r * W + 2]);
+    na += rcv[r * W + 3];
+    n += rb[r] / sizeof(XRec);
+  }
+  if (tick) {
+    s.n_alive = na;
+    s.next_tick += s.kp.pbft_period;
+  }
+  if (s.n_alive > 0 && s.next_tick != INT64_MAX) nx = std::min<long long>(nx, s.next_tick / s.L);
+  s.next_cell = nx;
+  s.next_known = true;
+  if (n > s.cap_recv) {
+    g_detail = "multi-GPU receive buffer too small";
+    return BCSIM_E_OVERFLOW;
+  }
+  if ((rc = s.xp->sendrecv_dev(s.stream, reinterpret_cast<const char*>(s.kp.sendbuf),
+                               static_cast<uint64_t>(s.kp.cap_send) * sizeof(XRec), sb.data(),
+                               reinterpret_cast<char*>(s.recvbuf), rb.data())))
+    return rc;
+  ++s.ctl_collectives;
+  static const long long kNone = LLONG_MAX;
   HIPCHK(hipMemsetAsync(s.kp.send_cnt, 0, 4ull * kMaxRanks, s.stream));
-  uint64_t n = 0;
-  for (uint32_t r = 0; r < s.P; ++r) n += rb[r] / sizeof(XRec);
+  HIPCHK(hipMemcpyAsync(s.kp.scal + 4, &kNone, 8, hipMemcpyHostToDevice, s.stream));
   if (n) {
     rc = launch(s, KS_GROUP, k_import, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s.kp_dev, cell,
                 static_cast<const XRec*>(s.recvbuf), static_cast<uint32_t>(n));
@@ -1284,9 +1329,10 @@ static int sync_leaders(Sim& s) {
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(s.lead_w.data(), s.kp.lead_loc, s.NT, hipMemcpyDeviceToHost, s.stream));
   HIPCHK(hipStreamSynchronize(s.stream));
-  for (size_t k = 0; k < s.lead_w.size(); k += 64) {
-    const uint32_t n = static_cast<uint32_t>(std::min<size_t>(64, s.lead_w.size() - k));
+  for (size_t k = 0; k < s.lead_w.size(); k += 4096) {  // (one call for N <= 32768 nodes)
+    const uint32_t n = static_cast<uint32_t>(std::min<size_t>(4096, s.lead_w.size() - k));
     if ((rc = s.xp->allreduce_i64(s.stream, s.lead_w.data() + k, n, 1))) return rc;
+    ++s.ctl_collectives;
   }
   HIPCHK(hipMemcpyAsync(const_cast<uint8_t*>(s.kp.lead_all), s.lead_w.data(), s.NT, hipMemcpyHostToDevice, s.stream));
   return BCSIM_OK;
@@ -1348,6 +1394,27 @@ static int check_tag_invariant(Sim& s, long long c) {
   return BCSIM_OK;
 }
 
+// The earliest cell with work on this rank (the state after the cells processed so far).
+// with_tick: include the PBFT tick (n_alive must then be the global one).
+static long long local_next_cell(const Sim& s, bool with_tick) {
+  const long long L = s.L;
+  long long c = LLONG_MAX;
+  const long long cdone = s.t_done / L;
+  if (s.start_pending) c = 0;
+  if (s.grouped_cell >= 0) c = std::min(c, s.grouped_cell);  // partially processed cell
+  for (uint32_t b = 0; b < s.B; ++b) {
+    if (!s.bcnt[b]) continue;
+    // bucket b holds the cell c == b (mod B) in [cdone, cdone + B)
+    const long long cb = cdone + ((static_cast<long long>(b) - cdone % s.B) % s.B + s.B) % s.B;
+    c = std::min(c, cb);
+  }
+  if (s.next_local != LLONG_MAX) c = std::min(c, std::max<long long>(s.next_local, s.t_done) / L);
+  if (s.ov_min != LLONG_MAX) c = std::min(c, s.ov_min);
+  if (with_tick && s.n_alive > 0 && s.next_tick != INT64_MAX) c = std::min(c, s.next_tick / L);
+  if (s.stop_pending && s.cfg.stop_ns >= 0 && s.cfg.stop_ns >= s.t_done) c = std::min(c, s.cfg.stop_ns / L);
+  return c;
+}
+
 static int run(Sim& s, int64_t t_until) {
   int rc;
   if (!s.started) {
@@ -1375,34 +1442,45 @@ static int run(Sim& s, int64_t t_until) {
   } while (0)
   for (;;) {
     // earliest cell with work
-    long long c = LLONG_MAX;
-    const long long cdone = s.t_done / L;
-    if (s.start_pending) c = 0;
-    if (s.grouped_cell >= 0) c = std::min(c, s.grouped_cell);  // partially processed cell
-    for (uint32_t b = 0; b < s.B; ++b) {
-      if (!s.bcnt[b]) continue;
-      // bucket b holds the cell c == b (mod B) in [cdone, cdone + B)
-      const long long cb = cdone + ((static_cast<long long>(b) - cdone % s.B) % s.B + s.B) % s.B;
-      c = std::min(c, cb);
-    }
-    if (s.next_local != LLONG_MAX) c = std::min(c, std::max<long long>(s.next_local, s.t_done) / L);
-    if (s.ov_min != LLONG_MAX) c = std::min(c, s.ov_min);
-    if (s.n_alive > 0 && s.next_tick != INT64_MAX) c = std::min(c, s.next_tick / L);
-    if (s.stop_pending && s.cfg.stop_ns >= 0 && s.cfg.stop_ns >= s.t_done) c = std::min(c, s.cfg.stop_ns / L);
-    if (s.xp) {  // the next cell of the whole system, and every rank's status
-      int64_t cv[2] = {c, lerr};
-      if ((rc = s.xp->allreduce_i64(s.stream, cv, 2, 0))) return rc;
-      if (cv[1] < 0) {
-        if (lerr) return lerr;
-        g_detail = "another rank of the partition failed";
-        return BCSIM_E_PEER;
+    long long c;
+    int carried = 0;  // node-partitioned: a failure after the last exchange, carried by this cell's
+    if (s.xp && s.next_known) {
+      // the last cell's control exchange agreed on this cell already
+      s.next_known = false;
+      c = s.next_cell;
+      carried = lerr;
+      lerr = 0;
+    } else {
+      c = local_next_cell(s, true);
+      if (s.xp) {  // the next cell of the whole system, and every rank's status
+        int64_t cv[2] = {c, lerr};
+        if ((rc = s.xp->allreduce_i64(s.stream, cv, 2, 0))) return rc;
+        ++s.ctl_collectives;
+        if (cv[1] < 0) {
+          if (lerr) return lerr;
+          g_detail = "another rank of the partition failed";
+          return BCSIM_E_PEER;
+        }
+        c = cv[0];
+      } else if (lerr) {
+        return lerr;
       }
-      c = cv[0];
-    } else if (lerr) {
-      return lerr;
     }
     if (c == LLONG_MAX || c * L >= lim) {
       if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
+      if (s.xp && carried) {  // every rank leaves here: tell them, then leave with the failure
+        int64_t cv[2] = {LLONG_MAX, carried};
+        (void)s.xp->allreduce_i64(s.stream, cv, 2, 0);
+        return carried;
+      }
+      if (s.xp) {  // the others may carry a failure into this exit
+        int64_t cv[2] = {LLONG_MAX, 0};
+        if ((rc = s.xp->allreduce_i64(s.stream, cv, 2, 0))) return rc;
+        if (cv[1] < 0) {
+          g_detail = "another rank of the partition failed";
+          return BCSIM_E_PEER;
+        }
+      }
       break;
     }
     const long long cs = c * L, ce = cs + L;
@@ -1412,8 +1490,8 @@ static int run(Sim& s, int64_t t_until) {
       if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
       break;
     }
-    int lrc = 0;  // this rank's status of the cell
-    if (s.grouped_cell != c) {
+    int lrc = carried;  // this rank's status of the cell
+    if (!lrc && s.grouped_cell != c) {
       // cells (last_full, c) had no work and were skipped: their buckets still owe the
       // once-per-32-turns zeroing of the inbox-slot tags (before group_cell can rebin into them)
       if (c > s.last_full + 1) lrc = zero_tag_buckets(s, s.last_full + 1, c - 1);
@@ -1448,28 +1526,32 @@ static int run(Sim& s, int64_t t_until) {
       lrc = BCSIM_E_OVERFLOW;
     }
     if (!s.xp && lrc) return lrc;
-    if (s.xp) {  // ship records for other ranks' nodes, place the received ones
-      if ((rc = exchange(s, c, lrc))) return rc;
-      lerr = readback(s);  // a failure here rides the next cell's MIN
-    }
-    if (tick) {
-      int64_t na = lerr ? 0 : s.ctl_h->scal[2];
-      if (s.xp && (rc = s.xp->allreduce_i64(s.stream, &na, 1, 1))) return rc;
-      s.n_alive = na;
-      s.next_tick += s.kp.pbft_period;
-    }
+    // host bookkeeping of the finished window (before the exchange: the next-cell candidate a
+    // rank announces there is its state after this window)
     s.start_pending = false;
     if (s.cfg.stop_ns >= 0 && s.cfg.stop_ns < hi) s.stop_pending = false;
     s.t_done = hi;
     ++s.cells;
     if (hi == ce) {
-      // (a failure rides the next cell's collective like any other rank-local one)
-      if (!lerr) lerr = zero_tag_buckets(s, c, c);
+      const int zr = zero_tag_buckets(s, c, c);
+      if (!lrc) lrc = zr;  // (node-partitioned: rides the exchange like any other rank-local failure)
       s.last_full = c;
       s.grouped_cell = -1;
       s.bcnt[c % s.B] = 0;
       s.xcnt[c % s.B] = 0;
       s.x_active = 0;
+    }
+    if (s.xp) {
+      // ONE control exchange (segment sizes, next-cell candidates, status, PBFT n_alive), the
+      // records for other ranks' nodes, k_import; the next cell is agreed there
+      if ((rc = exchange(s, c, lrc, tick))) return rc;
+      lerr = readback(s);  // a failure here rides the next cell's exchange
+    } else {
+      if (lrc) return lrc;
+      if (tick) {
+        s.n_alive = s.ctl_h->scal[2];
+        s.next_tick += s.kp.pbft_period;
+      }
     }
   }
 #undef LOCAL
@@ -1781,6 +1863,16 @@ int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, u
     bytes_out4[bcsim::KS_AUX] = 32.0 * ks[bcsim::KST_OPS] + 16.0 * ks[bcsim::KST_REC] + 16.0 * ks[bcsim::KST_EDGES] +
                                 32.0 * ks[bcsim::KST_KEPT] + 32.0 * ks[bcsim::KST_ECHO];
   }
+  return BCSIM_OK;
+}
+
+int bcsim_read_loop_stats(bcsim_sim* h, uint64_t* out4) {
+  if (!h || !out4) return BCSIM_E_INVAL;
+  const Sim& s = *h->s;
+  out4[0] = s.cells;
+  out4[1] = s.ctl_collectives;
+  out4[2] = s.tag_zeroes;
+  out4[3] = 0;
   return BCSIM_OK;
 }
 

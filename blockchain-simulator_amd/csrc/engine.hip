@@ -165,7 +165,8 @@ struct KP {
   unsigned long long* wgs;    // BCSIM_WGT: per-workgroup k_scan phase timing [NT][8] (debug)
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   long long *node_tnext, *node_onext;
-  long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks
+  long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks, [3] next timer,
+                    // [4] earliest arrival cell shipped to another rank (node-partitioned)
   long long* nxt_part;  // [kNextBlocks] k_next per-workgroup minima
   uint32_t* nxt_done;   // k_next workgroups finished (the last one reduces and resets it)
   // node partition (multi-GPU PDES): this rank owns nodes
@@ -724,13 +725,24 @@ __device__ inline void wave_add_by_key(bool act, uint32_t key, uint32_t inc, uns
 
 // ---------------------------------------------------------------------------
 // extras grouping: counting sort of the cell's extras by receiver gnode
+// Group the cell's extras by receiver: counts, then placement.  The records of one receiver
+// arrive in runs (the leader's cell: ~N of them for one node), so the per-receiver atomics are
+// wave-aggregated -- one atomic per (wave, receiver) instead of one per record, which
+// serialised ~4 k same-address atomics (~50 us) per kernel.
 __global__ void k_xcount(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  const uint32_t k = blockIdx.x * blockDim.x + tidx();
-  if (k >= n) return;
-  const uint32_t g = AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf).g;
-  atomicAdd(&AT(p.seg_cnt, g, p.NT), 1u);
+  const uint32_t k = blockIdx.x * blockDim.x + tidx(), lane = tidx() & 63u;
+  const bool v = k < n;
+  const uint32_t g = v ? AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf).g : 0u;
+  unsigned long long rem = __ballot(v);
+  while (rem) {
+    const int ld = __ffsll(static_cast<long long>(rem)) - 1;
+    const uint32_t gl = __shfl(g, ld, 64);
+    const unsigned long long same = __ballot(v && g == gl);
+    if (lane == static_cast<uint32_t>(ld)) atomicAdd(&AT(p.seg_cnt, gl, p.NT), static_cast<uint32_t>(__popcll(same)));
+    rem &= ~same;
+  }
 }
 
 // single-block exclusive scan of seg_cnt[0..NT) -> seg_off[0..NT]
@@ -854,11 +866,24 @@ __global__ __launch_bounds__(1024) void k_seg_apply(const KP* __restrict__ pk, c
 __global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  const uint32_t k = blockIdx.x * blockDim.x + tidx();
-  if (k >= n) return;
-  const XRec x = AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf);
-  const uint32_t pos = AT(p.seg_off, x.g, p.NT + 1) + atomicAdd(&AT(p.cursor, x.g, p.NT), 1u);
-  AT(p.xgrp, pos, p.cap_x) = x;
+  const uint32_t k = blockIdx.x * blockDim.x + tidx(), lane = tidx() & 63u;
+  const bool v = k < n;
+  XRec x{};
+  if (v) x = AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf);
+  unsigned long long rem = __ballot(v);
+  uint32_t pos = 0;
+  while (rem) {
+    const int ld = __ffsll(static_cast<long long>(rem)) - 1;
+    const uint32_t gl = __shfl(x.g, ld, 64);
+    const unsigned long long same = __ballot(v && x.g == gl);
+    uint32_t base = 0;
+    if (lane == static_cast<uint32_t>(ld))
+      base = AT(p.seg_off, gl, p.NT + 1) + atomicAdd(&AT(p.cursor, gl, p.NT), static_cast<uint32_t>(__popcll(same)));
+    base = __shfl(base, ld, 64);
+    if (v && x.g == gl) pos = base + static_cast<uint32_t>(__popcll(same & ((1ull << lane) - 1ull)));
+    rem &= ~same;
+  }
+  if (v) AT(p.xgrp, pos, p.cap_x) = x;
 }
 
 // one overflow record: into its bucket if its cell entered the ring, else `stay` = its cell
@@ -2437,8 +2462,9 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   // app_delay after the arrivals, so they follow the echoes in key order (t, then t - dt).
   // The link kernels then skip the echoes of this window (eapp stamp) instead of reading the
   // row a second time; otherwise they do them, merged with the due ops, as before.
+  const long long onext0 = AT(p.node_onext, g, p.NT);  // earliest pending op (LLONG_MIN: unknown)
   const bool echo_here =
-      p.echo && p.qmodel == 0 && AT(p.node_onext, g, p.NT) >= t_hi &&
+      p.echo && p.qmodel == 0 && onext0 >= t_hi &&
       !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u) &&
       !(AT(p.sflag, static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u);
   const Rec* slots = p.inbox + inbox_idx(p, b, rep, e0);
@@ -2741,7 +2767,12 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   }
   AT(p.sub, g, p.NT) = sub0 + tot.x + tot.y * deg_u;
   AT(p.n_ops, g, p.NT) = nops0 + tot.y;
-  if (tot.y) AT(p.node_onext, g, p.NT) = LLONG_MIN;  // the link stage recomputes
+  // the new ops are all due at t + app_delay (one instant): the earliest pending op stays exact,
+  // so a link stage with nothing due can skip the node (k_link_mesh)
+  if (tot.y) {
+    const long long on = AT(p.node_onext, g, p.NT);  // (re-read: not kept live across the passes)
+    AT(p.node_onext, g, p.NT) = on == LLONG_MIN ? LLONG_MIN : min(on, cs + static_cast<long long>(F.kmax >> 32) + app);
+  }
   AT(p.block_num, g, p.NT) = bn0 + static_cast<int32_t>(tot.z);
   FPH(7);
   if (echo_here) {
@@ -3160,6 +3191,7 @@ __device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32
   }
   if (list > p.n_buckets) {  // another rank's receiver
     const uint32_t r = list - p.n_buckets - 1;
+    atomicMin(&p.scal[4], static_cast<long long>(static_cast<uint64_t>(x.cell) & ((1ull << 48) - 1)));
     const uint32_t pos = atomicAdd(&p.send_cnt[r], 1u);
     if (pos >= p.cap_send) {
       set_err(p, BCSIM_E_OVERFLOW);
@@ -3240,17 +3272,24 @@ __device__ __attribute__((always_inline)) inline void link_finish(const KP& p, L
   }
   __syncthreads();
   const uint32_t nst = min(L.nst, p.cap_stage);
+  long long xmin = LLONG_MAX;  // earliest arrival cell shipped to another rank (scal[4]: the next-cell bound)
   for (uint32_t k = tid; k < nst; k += blockDim.x) {
     const size_t sidx = static_cast<size_t>(blockIdx.x) * p.cap_stage + k;
     const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
     const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
     if (list > B) {
-      if (pos < p.cap_send) p.sendbuf[static_cast<size_t>(list - B - 1) * p.cap_send + pos] = p.xstage[sidx];
+      const XRec x = p.xstage[sidx];
+      xmin = min(xmin, static_cast<long long>(static_cast<uint64_t>(x.cell) & ((1ull << 48) - 1)));
+      if (pos < p.cap_send) p.sendbuf[static_cast<size_t>(list - B - 1) * p.cap_send + pos] = x;
     } else if (list == B) {
       if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
     } else if (pos < p.cap_x) {
       p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
     }
+  }
+  if (n_lists > B + 1) {
+    for (int d = 32; d > 0; d >>= 1) xmin = min(xmin, static_cast<long long>(__shfl_xor(xmin, d, 64)));
+    if ((tid & 63u) == 0 && xmin != LLONG_MAX) atomicMin(&p.scal[4], xmin);
   }
   // ---- 5. counters: wave sums, LDS atomics, one global atomic per workgroup ----
   {
@@ -3832,7 +3871,7 @@ __device__ inline void xr_ship(const KP& p, LinkShared& L, uint32_t g, uint32_t 
 }
 
 template <bool XR, int kMeshU>
-__global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
+__global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                    long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
@@ -3851,7 +3890,9 @@ __global__ __launch_bounds__(256) void k_link_mesh(const KP* __restrict__ pk, lo
   const uint32_t rep = g / p.N, i = g % p.N;
   const bool rx = p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
   const bool rxe = rx && AT(p.eapp, g, p.NT) != t_lo;  // (see link_node)
-  if (n == 0 && !sl0 && !sl1 && !rxe) {
+  // nothing due in the window: no op before t_hi (node_onext is exact unless LLONG_MIN; fixed
+  // app delays only, so no unexpanded jitter broadcast hides behind it), no reply slot, no echo
+  if ((n == 0 || AT(p.node_onext, g, p.NT) >= t_hi) && !sl0 && !sl1 && !rxe) {
     if (rx && final_win && tid == 0) AT(p.iflag, fidx, static_cast<uint64_t>(B) * p.NT) = 0;
     return;
   }
@@ -4717,18 +4758,22 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
   }
   __syncthreads();
   const uint32_t nst = min(L.nst, p.cap_stage);
+  long long xmin = LLONG_MAX;  // earliest arrival cell shipped to another rank (scal[4])
   for (uint32_t k = tid; k < nst; k += bs) {
     const size_t sidx = static_cast<size_t>(blockIdx.x) * p.cap_stage + k;
     const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
     const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
     if (list > B) {
-      if (pos < p.cap_send) p.sendbuf[static_cast<size_t>(list - B - 1) * p.cap_send + pos] = p.xstage[sidx];
+      const XRec x = p.xstage[sidx];
+      xmin = min(xmin, static_cast<long long>(static_cast<uint64_t>(x.cell) & ((1ull << 48) - 1)));
+      if (pos < p.cap_send) p.sendbuf[static_cast<size_t>(list - B - 1) * p.cap_send + pos] = x;
     } else if (list == B) {
       if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
     } else if (pos < p.cap_x) {
       p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
     }
   }
+  if (xmin != LLONG_MAX) atomicMin(&p.scal[4], xmin);
   // ---- 5. counters ----
   uint4 t1, t2;
   (void)block_scan4(make_uint4(static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends),

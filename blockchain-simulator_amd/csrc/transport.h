@@ -29,6 +29,21 @@ struct Xport {
   // the same on host memory (send segments back to back)
   virtual int alltoallv_host(hipStream_t st, const char* send, const uint64_t* send_bytes, char* recv,
                              uint64_t recv_cap, uint64_t* recv_bytes) = 0;
+  // all-to-all of kCtlWords int64 per peer (host arrays [nranks][kCtlWords]): the per-cell
+  // control exchange -- segment sizes, next-cell candidates, status -- in ONE collective
+  static constexpr uint32_t kCtlWords = 4;
+  virtual int ctl_exchange(hipStream_t st, const int64_t* send, int64_t* recv) {
+    std::vector<uint64_t> sb(nranks, kCtlWords * 8ull), rb(nranks);
+    const int rc = alltoallv_host(st, reinterpret_cast<const char*>(send), sb.data(), reinterpret_cast<char*>(recv),
+                                  nranks * kCtlWords * 8ull, rb.data());
+    if (rc) return rc;
+    for (uint32_t r = 0; r < nranks; ++r)
+      if (rb[r] != kCtlWords * 8ull) return BCSIM_E_HIP;
+    return BCSIM_OK;
+  }
+  // device segments of known sizes (both sides know them from ctl_exchange)
+  virtual int sendrecv_dev(hipStream_t st, const char* send_dev, uint64_t stride, const uint64_t* send_bytes,
+                           char* recv_dev, const uint64_t* recv_bytes) = 0;
 };
 
 #ifndef HIPEMU  // tools/hipemu (debug host emulator) has no RCCL
@@ -54,16 +69,37 @@ struct RcclXport : Xport {
     if (d_cnt) (void)hipFree(d_cnt);
     if (d_host) (void)hipFree(d_host);
   }
+  static constexpr uint32_t kRedMax = 4096;  // int64 per all-reduce call
   int init(uint32_t r, uint32_t n, const ncclUniqueId& id) {
     rank = r;
     nranks = n;
     NCCLCHK(ncclCommInitRank(&comm, static_cast<int>(n), id, static_cast<int>(r)));
-    HIPCHK(hipMalloc(&d_red, 64 * sizeof(int64_t)));
-    HIPCHK(hipMalloc(&d_cnt, 2ull * n * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&d_red, kRedMax * sizeof(int64_t)));
+    HIPCHK(hipMalloc(&d_cnt, 2ull * n * kCtlWords * sizeof(uint64_t)));
+    return BCSIM_OK;
+  }
+  int ctl_exchange(hipStream_t st, const int64_t* send, int64_t* recv) override {
+    HIPCHK(hipMemcpyAsync(d_cnt, send, nranks * kCtlWords * 8ull, hipMemcpyHostToDevice, st));
+    NCCLCHK(ncclAllToAll(d_cnt, d_cnt + nranks * kCtlWords, kCtlWords, ncclInt64, comm, st));
+    HIPCHK(hipMemcpyAsync(recv, d_cnt + nranks * kCtlWords, nranks * kCtlWords * 8ull, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return BCSIM_OK;
+  }
+  int sendrecv_dev(hipStream_t st, const char* send_dev, uint64_t stride, const uint64_t* send_bytes, char* recv_dev,
+                   const uint64_t* recv_bytes) override {
+    NCCLCHK(ncclGroupStart());
+    uint64_t off = 0;
+    for (uint32_t r = 0; r < nranks; ++r) {
+      if (send_bytes[r]) NCCLCHK(ncclSend(send_dev + r * stride, send_bytes[r], ncclUint8, static_cast<int>(r), comm, st));
+      if (recv_bytes[r]) NCCLCHK(ncclRecv(recv_dev + off, recv_bytes[r], ncclUint8, static_cast<int>(r), comm, st));
+      off += recv_bytes[r];
+    }
+    NCCLCHK(ncclGroupEnd());
+    // (no host sync: k_import follows on the same stream)
     return BCSIM_OK;
   }
   int allreduce_i64(hipStream_t st, int64_t* v, uint32_t n, int op) override {
-    if (n > 64) return BCSIM_E_INVAL;
+    if (n > kRedMax) return BCSIM_E_INVAL;
     HIPCHK(hipMemcpyAsync(d_red, v, n * 8ull, hipMemcpyHostToDevice, st));
     NCCLCHK(ncclAllReduce(d_red, d_red, n, ncclInt64, op == 0 ? ncclMin : ncclSum, comm, st));
     HIPCHK(hipMemcpyAsync(v, d_red, n * 8ull, hipMemcpyDeviceToHost, st));
@@ -130,6 +166,20 @@ struct RcclXport : Xport {
 struct CbXport : Xport {
   bcsim_transport t{};
   std::vector<char> hs, hr;
+  int sendrecv_dev(hipStream_t st, const char* send_dev, uint64_t stride, const uint64_t* send_bytes, char* recv_dev,
+                   const uint64_t* recv_bytes) override {
+    uint64_t cap = 0;
+    for (uint32_t r = 0; r < nranks; ++r) cap += recv_bytes[r];
+    std::vector<uint64_t> rb(nranks);
+    const int rc = alltoallv_dev(st, send_dev, stride, send_bytes, recv_dev, cap, rb.data());
+    if (rc) return rc;
+    for (uint32_t r = 0; r < nranks; ++r)
+      if (rb[r] != recv_bytes[r]) {
+        g_detail = "transport: received segment sizes differ from the announced ones";
+        return BCSIM_E_HIP;
+      }
+    return BCSIM_OK;
+  }
   int allreduce_i64(hipStream_t, int64_t* v, uint32_t n, int op) override {
     if (t.allreduce_i64(t.ctx, v, n, op) != 0) {
       g_detail = "transport allreduce_i64 callback failed";

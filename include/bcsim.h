@@ -299,6 +299,10 @@ int bcsim_read_kernel_stats(bcsim_sim* s, double* us_out4, double* bytes_out4,
  * edges, [3] kept ops, [4] delivered records, [5] k_scan ops, [6] implicit echoes,
  * [7] k_scan windows split because a node had more arrivals than its LDS staging. */
 int bcsim_read_engine_counters(bcsim_sim* s, uint64_t* out8);
+/* Cell-loop statistics since bcsim_create (profiling aid): [0] windows processed, [1]
+ * collectives of a node-partitioned run (control exchanges, record exchanges, all-reduces;
+ * DESIGN.md §5), [2] inbox buckets zeroed for the ring-turn tag invariant, [3] 0. */
+int bcsim_read_loop_stats(bcsim_sim* s, uint64_t* out4);
 
 #ifdef __cplusplus
 }

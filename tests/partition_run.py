@@ -41,6 +41,8 @@ def _worker(rank, world, port, names, transport, q):
                     cnt = s.counters()
                     if transport == "host":  # exchange volume (bytes this rank sent to the others)
                         cnt["xfer_bytes"] = s._transport.bytes
+                    ls = s.loop_stats()  # per-rank cell-loop collectives (summed over ranks by merge)
+                    cnt["windows"], cnt["collectives"] = ls["windows"], ls["collectives"]
                     q.put((name, rank, s.trace(), cnt, None))
             except Exception as e:  # report, keep the other ranks' collectives aligned
                 q.put((name, rank, None, None, repr(e)))

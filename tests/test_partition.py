@@ -162,6 +162,9 @@ def test_partitioned_fullsize_equals_single(name, engine_lib):
         # is far below one 32-byte record per cross-rank delivery
         cross = single[1]["delivered_total"] // 2
         assert merged[1]["xfer_bytes"] < cross * 32 // 16, (merged[1]["xfer_bytes"], cross)
+    # one control exchange + one record exchange per window, plus the PBFT
+    # tick's leader-flag all-reduce and the first / last agreement of a run() call
+    assert merged[1]["collectives"] <= 2 * merged[1]["windows"] + 8 * 2 * 8, merged[1]
 
 
 def _rccl1_worker(port, names, q):
