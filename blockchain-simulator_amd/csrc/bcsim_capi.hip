@@ -76,6 +76,7 @@ struct Sim {
   bool gossip_link = false;
   bool mesh_link = false;  // full mesh, fixed delay: k_link_mesh first, k_link over list 3
   bool scan_fast = false;  // dense PBFT, fixed delay, reply slots: k_scan_pbft first, k_scan over list 2
+  bool mesh_pf = true;     // k_link_mesh parks the node's link words in LDS first (BCSIM_MESH_PF=0: off)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -657,6 +658,8 @@ static int setup_device(Sim& s) {
       // testing aid: BCSIM_FEW_SCAN=0 sends small launches (every launch of a small parity case)
       // through k_scan_pbft too
       if (const char* fs = std::getenv("BCSIM_FEW_SCAN"); fs && *fs) s.few_scan = static_cast<uint32_t>(std::atoi(fs));
+      if (const char* pf = std::getenv("BCSIM_MESH_PF"); pf && *pf == '0') s.mesh_pf = false;
+      if (static_cast<size_t>(s.deg_max) * 8 > 64 * 1024) s.mesh_pf = false;  // (dynamic LDS without an opt-in)
     }
     if ((rc = dalloc(s, &p.eslot, p.cap_eslot)) || (rc = dalloc(s, &p.sflag, static_cast<size_t>(kOpRing) * NT)))
       return rc;
@@ -1060,12 +1063,15 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     // (list 3 holds a few nodes, the leader's cells among them: wide workgroups)
     // (node-partitioned: the kernels that stage records for other ranks)
     const dim3 gl(std::min<uint32_t>(256, s.grid_link)), bl(std::min<uint32_t>(1024, 4 * s.bs_link));
-    if (s.P > 1 ? ((rc = launch(s, -1, k_link_mesh<true, 2>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
+    const size_t mlds = static_cast<size_t>(s.deg_max) * 8;  // (the PF variant's link words)
+    if (s.P > 1 ? ((rc = launch(s, -1, k_link_mesh<true, 2, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
                    (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
                 // (a few nodes -- the leader's block broadcast at a tick -- get 1024-lane workgroups:
                 // the launch is one workgroup's latency)
-                : ((rc = launch(s, -1, k_link_mesh<false, 2>, grid, dim3(n_link <= 64 ? 1024 : 256), 0, s.kp_dev, cell, lo,
-                                hi, fw)) ||
+                : ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<false, 2, true>, grid, dim3(n_link <= 64 ? 1024 : 256), mlds,
+                                            s.kp_dev, cell, lo, hi, fw)
+                                   : launch(s, -1, k_link_mesh<false, 2, false>, grid, dim3(n_link <= 64 ? 1024 : 256), 0,
+                                            s.kp_dev, cell, lo, hi, fw)) ||
                    (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw))))
       return rc;
     if (timed) {

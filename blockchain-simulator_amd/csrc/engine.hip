@@ -3240,21 +3240,24 @@ __device__ __attribute__((always_inline)) inline void link_finish(const KP& p, L
   if (p.wgt && tid == 0) ph[3] = __builtin_amdgcn_s_memrealtime();
   for (uint32_t k0 = 0; k0 < n; k0 += blockDim.x) {
     const uint32_t k = k0 + tid;
-    Op o{};
+    RawOp o = raw_zero();  // (raw words: an Op struct here went through scratch)
     bool keep = false;
     if (k < n) {
-      o = ops[k];
-      const uint8_t kind = op_kind(o);
-      if (kind == OP_BCAST_J)
-        keep = !(op_flags(o) & OPF_DONE);  // unexpanded (fixed mode never creates these)
-      else if (o.t >= t_hi) {
+      o = ld_raw(&ops[k]);
+      if (raw_kind(o) == OP_BCAST_J)
+        keep = !(raw_flags(o) & OPF_DONE);  // unexpanded (fixed mode never creates these)
+      else if (raw_t(o) >= t_hi) {
         keep = true;
-        if (o.t < omin) omin = o.t;
+        if (raw_t(o) < omin) omin = raw_t(o);
       }
     }
     uint32_t tot;
     const uint32_t pos = kept + block_rank(keep, L.wcnt, tot);
-    if (keep) ops[pos] = o;
+    if (keep) {
+      uint4* q = reinterpret_cast<uint4*>(&ops[pos]);
+      q[0] = o.a;
+      q[1] = o.b;
+    }
     kept += tot;
   }
   if (tid == 0) L.n_keep = kept;
@@ -3870,7 +3873,7 @@ __device__ inline void xr_ship(const KP& p, LinkShared& L, uint32_t g, uint32_t 
   }
 }
 
-template <bool XR, int kMeshU>
+template <bool XR, int kMeshU, bool PF>
 __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                    long long t_hi, int final_win) {
   const KP& p = *pk;
@@ -3984,6 +3987,28 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   // the edges: their link words would be loaded for nothing)
   const uint32_t deg_w = (n_bc || sl0 || sl1 || rxe) ? deg : 0u;
   const bool xr = XR;  // (a template flag: the one-rank kernel carries no staging registers)
+  // PF: the link words of all the node's out-edges in flight at once, parked in LDS (dynamic,
+  // deg_max words), so that the edge loop of a pure broadcast has no dependent global load --
+  // instead of one round trip per kMeshU edges per lane
+  extern __shared__ __attribute__((aligned(16))) uint64_t mlw[];
+  if (PF) {
+    constexpr int kPF = 8;
+    const uint64_t* lrow = p.link + edge_loc(p, rep, e0);
+    for (uint32_t k0 = 0; k0 < deg_w; k0 += kPF * bs) {
+      uint64_t v[kPF];
+#pragma unroll
+      for (int q = 0; q < kPF; ++q) {
+        const uint32_t k = k0 + q * bs + tid;
+        v[q] = k < deg_w ? lrow[k] : 0ull;
+      }
+#pragma unroll
+      for (int q = 0; q < kPF; ++q) {
+        const uint32_t k = k0 + q * bs + tid;
+        if (k < deg_w) mlw[k] = v[q];
+      }
+    }
+    __syncthreads();
+  }
   // (a wave-uniform trip count: the cross-rank range step after the edges is convergent)
   for (uint32_t b0 = 0; b0 < deg_w; b0 += kMeshU * bs) {
     const uint32_t base = b0 + tid;
@@ -4006,7 +4031,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
       const uint32_t le = base + u * bs;
       const bool v = le < deg;
       lwp[u] = p.link + edge_loc(p, rep, e0 + (v ? le : 0u));
-      lw[u] = v ? *lwp[u] : 0ull;
+      lw[u] = v ? (PF ? mlw[le] : *lwp[u]) : 0ull;
       r0[u] = (v && rxe) ? *reinterpret_cast<const uint4*>(in_row + le) : make_uint4(0, 0, 0, 0);
       w0[u] = (v && sl0) ? *eslot_at(p, ob, rep, e0 + le) : make_uint4(0, 0, 0, 0);
       w1[u] = (v && sl1) ? *eslot_at(p, obp, rep, e0 + le) : make_uint4(0, 0, 0, 0);
