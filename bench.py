@@ -50,7 +50,7 @@ def make_topology(n_nodes, workload):
     return bcsim.random_regular(n_nodes, 8, 1)
 
 
-PMC_ROUND = "r02"
+PMC_ROUND = "r03"
 
 
 def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):

@@ -56,14 +56,19 @@ def kernel_durations(path, prefix):
 LINK_PRIMARY = ("bcsim::k_link_mesh", "bcsim::k_gossip_link", "bcsim::k_paxos_link")
 
 
+def is_primary(n):
+    """A fast-path link kernel (templated names included: k_link_mesh<false, 2, true>)."""
+    return n is not None and any(n == x or n.startswith(x + "<") for x in LINK_PRIMARY)
+
+
 def link_groups(names):
     """Dispatch ids of the k_link class grouped into bench launches (see the module doc)."""
     groups, prev = [], None
     for d in sorted(names):
         n = names[d]
-        if not (n.startswith("bcsim::k_link") or n in LINK_PRIMARY):
+        if not (n.startswith("bcsim::k_link") or is_primary(n)):
             continue
-        follower = (groups and prev in LINK_PRIMARY and
+        follower = (groups and is_primary(prev) and
                     ((n.startswith("bcsim::k_link<") and n.endswith("true>")) or
                      (n == "bcsim::k_link_sparse" and prev == "bcsim::k_paxos_link")))
         if follower:
@@ -124,6 +129,27 @@ def main(src, dst):
                 first=a, launches=len(gf), hbm_bytes_per_launch=fb + wb,
                 fetch_bytes_per_launch=fb, write_bytes_per_launch=wb,
                 rocprof_avg_us=(sum(dur[d] for g in gt for d in g) / len(gt) / 1000.0) if gt else None))
+    # SQ pass (when present): per kernel, the counters summed over its dispatches and the
+    # stall / issue shares of the wave cycles
+    try:
+        sq, names_s = per_dispatch(f"{src}/sq/run_counter_collection.csv")
+    except OSError:
+        sq, names_s = {}, {}
+    for kern in sorted(set(names_s.values())):
+        tot = defaultdict(float)
+        nd = 0
+        for d, v in sq.items():
+            if names_s[d] != kern:
+                continue
+            nd += 1
+            for c, x in v.items():
+                tot[c] += x
+        cyc = tot.get("SQ_WAVE_CYCLES", 0.0)
+        if kern in res and cyc > 0:
+            res[kern]["sq"] = dict(dispatches=nd, counters_per_launch={c: x / nd for c, x in sorted(tot.items())},
+                                   wait_any_frac=tot.get("SQ_WAIT_ANY", 0.0) / cyc,
+                                   wait_inst_any_frac=tot.get("SQ_WAIT_INST_ANY", 0.0) / cyc,
+                                   active_inst_any_frac=tot.get("SQ_ACTIVE_INST_ANY", 0.0) / cyc)
     json.dump(dict(source=src, correction="FETCH_SIZE x2 (gfx950), KiB->bytes", kernels=res),
               open(dst, "w"), indent=1)
     for k, v in res.items():
@@ -132,8 +158,10 @@ def main(src, dst):
             print(f"link class {v['kernels']}: timed window [{t['first']}, +{t['launches']}) HBM/launch "
                   f"{t['hbm_bytes_per_launch'] / 1e6:.2f} MB, rocprof avg {t['rocprof_avg_us']} us")
             continue
+        q = v.get("sq")
+        sqs = (f"  wait {q['wait_any_frac']:.2f} issue {q['active_inst_any_frac']:.2f}" if q else "")
         print(f"{k:28s} {v['dispatches']:4d} disp  HBM/launch {v['hbm_bytes_per_launch'] / 1e6:10.2f} MB  "
-              f"L2 hit {v['l2_hit_rate']:.2f}")
+              f"L2 hit {v['l2_hit_rate']:.2f}{sqs}")
         if "timed_window" in v:
             t = v["timed_window"]
             print(f"  timed window: dispatches [{t['first']}, +{t['launches']}) HBM/launch "
