@@ -666,6 +666,19 @@ static int setup_device(Sim& s) {
     HIPCHK(hipMemset(p.eslot, 0xFF, p.cap_eslot * 16));  // due t = -1: no live reply
     HIPCHK(hipMemset(p.sflag, 0, static_cast<size_t>(kOpRing) * NT));
     if (!on) p.eslot = nullptr;
+    // k_scan_pbft -> k_link_mesh reply / echo descriptors (BCSIM_NO_DESC=1: off)
+    const char* nd = std::getenv("BCSIM_NO_DESC");
+    // (k_link_mesh applies pending echoes to its LDS-parked link words: the PF variant)
+    p.desc = (s.scan_fast && s.mesh_link && s.mesh_pf && s.deg_max <= 32 * kDescWords && !(nd && *nd == '1')) ? 1u : 0u;
+    p.dwords = p.desc ? static_cast<uint32_t>((s.deg_max + 31) / 32) : 1u;
+    const size_t nrb = p.desc ? static_cast<size_t>(kOpRing) * NT * p.dwords : 1;
+    const size_t neb = p.desc ? static_cast<size_t>(NT) * kEDesc * p.dwords : 1;
+    if ((rc = dalloc(s, &p.rdesc, p.desc ? static_cast<size_t>(kOpRing) * NT : 1)) || (rc = dalloc(s, &p.rbits, nrb)) ||
+        (rc = dalloc(s, &p.edesc, p.desc ? static_cast<size_t>(NT) * kEDesc : 1)) || (rc = dalloc(s, &p.ebits, neb)) ||
+        (rc = dalloc(s, &p.en, p.desc ? NT : 1)))
+      return rc;
+    HIPCHK(hipMemset(p.rdesc, 0xFF, (p.desc ? static_cast<size_t>(kOpRing) * NT : 1) * 16));  // due -1: sent
+    HIPCHK(hipMemset(p.en, 0, p.desc ? NT : 1));
   }
   const size_t n_link = p.hubs ? static_cast<size_t>(s.R) * (static_cast<size_t>(p.hubs) * (s.N - 1) +
                                                               static_cast<size_t>(s.N - p.hubs) * p.hubs)
@@ -805,6 +818,10 @@ static int setup_device(Sim& s) {
     }
   }
 #endif
+  if (const char* fv = std::getenv("BCSIM_FDBG"); fv && *fv == '1') {  // debug: fast-kernel leave reasons
+    if ((rc = dalloc(s, &p.fdbg, 16))) return rc;
+    HIPCHK(hipMemset(p.fdbg, 0, 16 * 8));
+  }
   if (const char* wv = std::getenv("BCSIM_WGT"); wv && *wv == '1') {  // debug: k_link per-WG timing
     if ((rc = dalloc(s, &p.wgt, NT * 8)) || (rc = dalloc(s, &p.wgs, NT * 8))) return rc;
     HIPCHK(hipMemset(p.wgt, 0, NT * 64));
@@ -995,6 +1012,17 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     rc = BCSIM_SCAN(BCSIM_PAXOS);
 #undef BCSIM_SCAN
   if (rc) return rc;
+  if (s.kp.fdbg) {  // debug (BCSIM_FDBG=1): why nodes of this window left the fast scan kernel
+    unsigned long long fc[16];
+    HIPCHK(hipStreamSynchronize(s.stream));
+    HIPCHK(hipMemcpy(fc, s.kp.fdbg, sizeof fc, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(s.kp.fdbg, 0, sizeof fc));
+    unsigned long long any = 0;
+    for (int k = 0; k < 8; ++k) any |= fc[k];
+    if (any)
+      std::fprintf(stderr, "[fdbg] cell %lld [%lld,%lld) scan grid %u: nowork %llu ss %llu timer %llu extras %llu deg %llu cfg %llu bad %llu instants %llu\n",
+                   cell, lo, hi, grid.x, fc[0], fc[1], fc[2], fc[3], fc[4], fc[5], fc[6], fc[7]);
+  }
   if (s.kp.wgs) {  // debug (BCSIM_WGT=1): mean k_scan phase times of a heavy launch
     std::vector<unsigned long long> w(8ull * s.NT);
     HIPCHK(hipStreamSynchronize(s.stream));
@@ -1064,7 +1092,8 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     // (node-partitioned: the kernels that stage records for other ranks)
     const dim3 gl(std::min<uint32_t>(256, s.grid_link)), bl(std::min<uint32_t>(1024, 4 * s.bs_link));
     const size_t mlds = static_cast<size_t>(s.deg_max) * 8;  // (the PF variant's link words)
-    if (s.P > 1 ? ((rc = launch(s, -1, k_link_mesh<true, 2, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
+    if (s.P > 1 ? ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<true, 2, true>, grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw)
+                                   : launch(s, -1, k_link_mesh<true, 2, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
                    (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
                 // (a few nodes -- the leader's block broadcast at a tick -- get 1024-lane workgroups:
                 // the launch is one workgroup's latency)
@@ -1086,6 +1115,15 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
                   : launch(s, KS_LINK, k_link<true, false>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw))
             : (xr ? launch(s, KS_LINK, k_link<false, true>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw)
                   : launch(s, KS_LINK, k_link<false, false>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw));
+  }
+  if (!rc && s.kp.fdbg) {  // debug (BCSIM_FDBG=1): nodes k_link_mesh left to the generic kernel
+    unsigned long long fc[16];
+    HIPCHK(hipStreamSynchronize(s.stream));
+    HIPCHK(hipMemcpy(fc, s.kp.fdbg, sizeof fc, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(s.kp.fdbg, 0, sizeof fc));
+    if (fc[8] | fc[9])
+      std::fprintf(stderr, "[fdbg] cell %lld [%lld,%lld) link grid %u: listed %llu bcasts %llu\n", cell, lo, hi, grid.x,
+                   fc[8], fc[9]);
   }
   if (rc || !s.kp.wgt) return rc;
   // debug (BCSIM_WGT=1): report the slowest k_link workgroups of this launch

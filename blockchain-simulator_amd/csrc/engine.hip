@@ -110,6 +110,17 @@ struct KP {
   // window stamp per gnode: k_scan_pbft applied the implicit echoes of the window starting at
   // eapp[g] itself (the link kernels skip them); LLONG_MIN = never
   long long* eapp;
+  // PBFT heavy-wave descriptors (k_scan_pbft -> k_link_mesh): a PREPARE wave's
+  // replies as ONE descriptor {due, first sub, payload} + the bitmap of in-slots that replied
+  // (sub + rank), and the waves' echoes as pending {t, big} + bitmap, applied by the node's next
+  // link stage that walks its edges (k_link_mesh: the link words are loaded there anyway)
+  uint32_t desc;          // enabled: dense full mesh with k_link_mesh as the link stage
+  uint32_t dwords;        // bitmap words per descriptor: ceil(deg_max / 32) <= kDescWords
+  uint4* rdesc;           // [kOpRing][NT] {due lo, due hi, sub, f0 | f1 << 16} of the arrival cell
+  uint32_t* rbits;        // [kOpRing][NT][dwords]
+  uint4* edesc;           // [NT][kEDesc] {t lo, t hi, big, 0}
+  uint32_t* ebits;        // [NT][kEDesc][dwords]
+  uint8_t* en;            // [NT] pending echo descriptors
   int64_t prop_const;    // propagation delay of every edge, or -1 (per-edge array)
   // links
   uint64_t* link;  // per edge: busy_until << 16 | (arrival cell of the last record & 0xFFFF)
@@ -163,6 +174,7 @@ struct KP {
   unsigned long long* trail;  // BCSIM_CHECKED + BCSIM_TRAIL: host-mapped breadcrumbs
   unsigned long long* wgt;    // BCSIM_WGT: per-workgroup k_link timing [NT][8] (debug)
   unsigned long long* wgs;    // BCSIM_WGT: per-workgroup k_scan phase timing [NT][8] (debug)
+  unsigned long long* fdbg;   // BCSIM_FDBG: why nodes leave the fast kernels [16] (debug; see FDBG)
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   long long *node_tnext, *node_onext;
   long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks, [3] next timer,
@@ -197,6 +209,10 @@ struct KP {
 };
 
 constexpr int kMaxRanks = 16;
+constexpr uint32_t kDescWords = 128;  // descriptor bitmaps: in-slots of degree <= 4096
+constexpr uint32_t kEDesc = 4;        // pending echo descriptors per node
+// sflag bits of a reply descriptor of the arrival cell (bits 0..3: reply slots due in cell + k)
+constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in this cell / the next
 
 
 // ---------------------------------------------------------------------------
@@ -2387,6 +2403,8 @@ struct FastShared {
   int32_t pp_idx[kFastPP], pp_val[kFastPP];
   uint32_t tcount[4];  // deliveries: PRE_PREPARE, PREPARE, COMMIT, PREPARE_RES
   uint32_t ocnt[2];    // reply slots due in this cell / the next
+  uint32_t fmin, fmax;  // PREPAREs' reply payload words (one reply descriptor if equal)
+  uint32_t bigs;        // bit 0: a big arrival, bit 1: a small one (one echo descriptor if not both)
   uint64_t lw[kFastRPL * kFastLanes];  // link words of the node's out-edges (echo pass)
 };
 
@@ -2426,6 +2444,12 @@ __device__ inline uint32_t fast_key_find(const FastShared& F, uint32_t key) {
   return s;
 }
 
+// BCSIM_FDBG=1 (debug): count why a node leaves k_scan_pbft (0 no work .. 7 several instants) /
+// k_link_mesh (8 listed ops, 9 too many broadcasts) for the generic kernels
+#define FDBG(k)                                             \
+  do {                                                      \
+    if (p.fdbg) atomicAdd(&p.fdbg[(k)], 1ull);              \
+  } while (0)
 // BCSIM_WGT=1 (debug): per-workgroup phase clock of k_scan_pbft, same slots as scan_node's SPH
 #define FPH(k)                                                                              \
   do {                                                                                      \
@@ -2452,7 +2476,10 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   if (!flag && !has_ss && !timer) return;  // nothing in the window (scan_node returns too)
   if (!flag || has_ss || timer || xn || deg > kFastLanes * kFastRPL || deg > p.cap_arr || blockDim.x != kFastLanes ||
       !p.impl || !p.eslot || p.delay_mode != BCSIM_DELAY_FIXED) {
-    if (tid == 0) AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+    if (tid == 0) {
+      AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+      FDBG(!flag ? 0 : has_ss ? 1 : timer ? 2 : xn ? 3 : (deg > kFastLanes * kFastRPL || deg > p.cap_arr) ? 4 : 5);
+    }
     return;
   }
   FPH(0);
@@ -2462,11 +2489,18 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   // app_delay after the arrivals, so they follow the echoes in key order (t, then t - dt).
   // The link kernels then skip the echoes of this window (eapp stamp) instead of reading the
   // row a second time; otherwise they do them, merged with the due ops, as before.
+  // With descriptors (p.desc) the echoes are not applied here but recorded as one pending echo
+  // descriptor {t, big} + the bitmap of the arrivals' in-slots, which the node's next link
+  // stage that walks its edges applies before anything else (k_link_mesh: it loads and stores
+  // those link words anyway) -- unless kEDesc descriptors are pending: then the link stage
+  // does the echoes of this window from the row (no eapp stamp), after the pending ones.
   const long long onext0 = AT(p.node_onext, g, p.NT);  // earliest pending op (LLONG_MIN: unknown)
   const bool echo_here =
       p.echo && p.qmodel == 0 && onext0 >= t_hi &&
-      !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u) &&
-      !(AT(p.sflag, static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u);
+      !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & (1u | kSfD0)) &&
+      !(AT(p.sflag, static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) &
+        (2u | kSfD1));
+  const bool echo_dir = echo_here && !p.desc;
   const Rec* slots = p.inbox + inbox_idx(p, b, rep, e0);
   uint4 rv[kFastRPL];
 #pragma unroll
@@ -2475,7 +2509,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     rv[j] = k < deg ? *reinterpret_cast<const uint4*>(slots + k) : make_uint4(0, 0, 0, 0);
   }
   // ... and the link words of its out-edges with it (LDS; used by the echo pass at the end)
-  if (echo_here) {
+  if (echo_dir) {
     const uint64_t* lrow = p.link + edge_loc(p, rep, e0);
     uint64_t lv[kFastRPL];
 #pragma unroll
@@ -2495,6 +2529,11 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   if (tid < kFastKeys) F.tkey[tid] = 0;
   if (tid < 4) F.tcount[tid] = 0;
   if (tid < 2) F.ocnt[tid] = 0;
+  if (tid == 0) {
+    F.fmin = ~0u;
+    F.fmax = 0u;
+    F.bigs = 0u;
+  }
   for (uint32_t k = tid; k < kFastSeg * kFastKeys; k += kFastLanes) (&F.qc[0][0])[k] = 0;
   __syncthreads();
   const uint32_t tag = cell_tag(p, cell);
@@ -2581,7 +2620,10 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   // uniform: several instants in the window (the slot order may not be the key order), or
   // anything else the generic path must take -- nothing has been written
   if (F.bad || F.kmin != F.kmax) {
-    if (tid == 0) AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+    if (tid == 0) {
+      AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+      FDBG(F.bad ? 6 : 7);
+    }
     return;
   }
   FPH(2);
@@ -2611,6 +2653,21 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     const unsigned long long md = __ballot(v && (type == PB_PRE_PREPARE || (type == PB_PREPARE_RES && cross)));
     const unsigned long long mc = __ballot(v && type == PB_COMMIT && cross);
     const unsigned long long mv = __ballot(v);
+    if (p.desc) {  // descriptor checks: one reply payload over the PREPAREs, one frame size
+      if (mp) {
+        const int fl = __ffsll(static_cast<long long>(mp)) - 1;
+        const uint32_t f01 = static_cast<uint32_t>(static_cast<uint16_t>(to16(p, fr_f0(r)))) |
+                             (static_cast<uint32_t>(static_cast<uint16_t>(to16(p, fr_m2(r)))) << 16);
+        const uint32_t ref = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(f01), fl));
+        const unsigned long long dif = __ballot(v && type == PB_PREPARE && f01 != ref);
+        if (lane == 0) {
+          atomicMin(&F.fmin, dif ? 0u : ref);
+          atomicMax(&F.fmax, dif ? ~0u : ref);
+        }
+      }
+      const unsigned long long mb = __ballot(v && ((r.w >> 24) & RF_BIG));
+      if (lane == 0 && mv) atomicOr(&F.bigs, (mb ? 1u : 0u) | (mb != mv ? 2u : 0u));
+    }
     if (lane == 0)
       F.seg[j * kFastWaves + wv] = make_uint4(static_cast<uint32_t>(__popcll(mp)), static_cast<uint32_t>(__popcll(md)),
                                               static_cast<uint32_t>(__popcll(mc)), static_cast<uint32_t>(__popcll(mv)));
@@ -2644,12 +2701,30 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
         in.w += d;
       }
     }
-    tot = make_uint4(__shfl(in.x, 63, 64), __shfl(in.y, 63, 64), __shfl(in.z, 63, 64), __shfl(in.w, 63, 64));
+    // (wave-uniform: readlane puts the totals in scalar registers)
+    tot = make_uint4(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(in.x), 63)),
+                     static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(in.y), 63)),
+                     static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(in.z), 63)),
+                     static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(in.w), 63)));
     __syncthreads();  // every wave has read its totals before wave 0 overwrites the counts
     if (wv == 0 && lane < kFastSeg) F.seg[lane] = make_uint4(in.x - x.x, in.y - x.y, in.z - x.z, in.w - x.w);
   }
   const uint32_t sub0 = AT(p.sub, g, p.NT), nops0 = AT(p.n_ops, g, p.NT);
   const int32_t bn0 = AT(p.block_num, g, p.NT);
+  // descriptors (uniform): the echoes of the window (one instant, one frame size), and the
+  // replies when every arrival is a PREPARE with one reply payload (one due instant, subs
+  // sub0 + rank) and the arrival cell's descriptor is free (none, or one already sent)
+  // (re-read here, not kept live across the passes: the pending echo count, the slot flags)
+  const uint32_t ne0 = p.desc ? AT(p.en, g, p.NT) : 0u;
+  const bool echo_desc = p.desc && echo_here && ne0 < kEDesc && F.bigs != 3u;
+  bool rdesc_on = false;
+  if (p.desc && tot.x == tot.w && tot.x != 0 && F.fmin == F.fmax) {
+    rdesc_on = !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & kSfD);
+    if (!rdesc_on) {
+      const uint4 od = p.rdesc[static_cast<size_t>(cell % kOpRing) * p.NT + g];
+      rdesc_on = static_cast<long long>((static_cast<uint64_t>(od.y) << 32) | od.x) < t_lo;
+    }
+  }
   if (nops0 + tot.y > op_cap(p, g)) {
     if (tid == 0) set_err(p, BCSIM_E_OVERFLOW);
     return;
@@ -2694,10 +2769,11 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
       ++cnt_t[1];
       const int64_t due = t + app;
       const uint64_t ut = static_cast<uint64_t>(due);
-      *eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q) =
-          make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), sp,
-                     static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m1))) |
-                         (static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m2))) << 16));
+      if (!rdesc_on)
+        *eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q) =
+            make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), sp,
+                       static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m1))) |
+                           (static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m2))) << 16));
       if (due / p.L == cell)
         ++n_slot0;
       else
@@ -2722,7 +2798,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     }
   }
   FPH(5);
-  if (echo_here) {  // one link word per arrival (distinct in-slots = distinct out-edges), coalesced
+  if (echo_dir) {  // one link word per arrival (distinct in-slots = distinct out-edges), coalesced
     uint64_t* lrow = p.link + edge_loc(p, rep, e0);
 #pragma unroll
     for (uint32_t j = 0; j < kFastRPL; ++j) {
@@ -2734,6 +2810,20 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
       const int64_t bu = (bu0 > t ? bu0 : t) + p.tx_tot[((r.w >> 24) & RF_BIG) ? 1 : 0];
       if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
       lrow[j * kFastLanes + tid] = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
+    }
+  }
+  if (rdesc_on || echo_desc) {  // descriptor bitmaps: bit k = in-slot k holds an arrival
+    uint32_t* rb = p.rbits + (static_cast<size_t>(cell % kOpRing) * p.NT + g) * p.dwords;
+    uint32_t* eb = p.ebits + (static_cast<size_t>(g) * kEDesc + ne0) * p.dwords;
+#pragma unroll 1
+    for (uint32_t j = 0; j < kFastRPL; ++j) {
+      const unsigned long long mv = __ballot((vmask >> j) & 1u);
+      const uint32_t w0 = j * (kFastLanes / 32) + wv * 2 + lane;
+      if (lane < 2 && w0 < p.dwords) {
+        const uint32_t word = static_cast<uint32_t>(mv >> (32 * lane));
+        if (rdesc_on) rb[w0] = word;
+        if (echo_desc) eb[w0] = word;
+      }
     }
   }
 #pragma unroll
@@ -2763,7 +2853,14 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   const uint32_t sm = (F.ocnt[0] ? 1u : 0u) | (F.ocnt[1] ? 2u : 0u);
   if (sm) {
     uint8_t& f = AT(p.sflag, (cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT);
-    f = static_cast<uint8_t>(f | sm);
+    if (rdesc_on) {  // kSfD0 / kSfD1: the descriptor's replies are due in this cell / the next
+      const uint64_t ud = static_cast<uint64_t>(cs + static_cast<long long>(F.kmax >> 32) + app);
+      p.rdesc[static_cast<size_t>(cell % kOpRing) * p.NT + g] =
+          make_uint4(static_cast<uint32_t>(ud), static_cast<uint32_t>(ud >> 32), sub0, F.fmin);
+      f = static_cast<uint8_t>((f & ~kSfD) | (sm << 4));
+    } else {
+      f = static_cast<uint8_t>(f | sm);
+    }
   }
   AT(p.sub, g, p.NT) = sub0 + tot.x + tot.y * deg_u;
   AT(p.n_ops, g, p.NT) = nops0 + tot.y;
@@ -2775,7 +2872,13 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   }
   AT(p.block_num, g, p.NT) = bn0 + static_cast<int32_t>(tot.z);
   FPH(7);
-  if (echo_here) {
+  if (echo_desc) {
+    const uint64_t ut = static_cast<uint64_t>(cs + static_cast<long long>(F.kmax >> 32));
+    p.edesc[static_cast<size_t>(g) * kEDesc + ne0] = make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32),
+                                                                F.bigs == 1u ? 1u : 0u, 0u);
+    AT(p.en, g, p.NT) = static_cast<uint8_t>(ne0 + 1);
+  }
+  if (echo_dir || echo_desc) {
     AT(p.eapp, g, p.NT) = t_lo;
     if (tot.w) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(tot.w));
   }
@@ -3873,20 +3976,96 @@ __device__ inline void xr_ship(const KP& p, LinkShared& L, uint32_t g, uint32_t 
   }
 }
 
+// k_link_mesh's view of the node's descriptors (k_scan_pbft): the live reply descriptors of
+// this arrival cell (0) and the previous one (1) with their bitmaps and per-word rank
+// prefixes, and the pending echo descriptors with theirs
+struct MeshDesc {
+  uint32_t rb[2][kDescWords];
+  uint32_t rp[2][kDescWords];
+  uint32_t eb[kEDesc][kDescWords];
+  uint32_t eall[kDescWords];  // union of the pending echo bitmaps
+  long long et[kEDesc];
+  uint32_t ebig[kEDesc];
+};
+
+__device__ inline long long desc_due(const uint4& d) {
+  return static_cast<long long>((static_cast<uint64_t>(d.y) << 32) | d.x);
+}
+
+// LDS copies of the descriptor bitmaps (reply descriptor h if use[h]; the ne pending echo
+// descriptors) and the reply bitmaps' exclusive rank prefixes per word.  Block-uniform call.
+__device__ inline void mesh_desc_load(const KP& p, MeshDesc& D, uint32_t g, uint32_t ob, uint32_t obp, bool use0,
+                                      bool use1, uint32_t ne) {
+  const uint32_t tid = tidx(), bs = blockDim.x, dw = p.dwords;
+  for (uint32_t k = tid; k < dw; k += bs) {
+    if (use0) D.rb[0][k] = p.rbits[(static_cast<size_t>(ob) * p.NT + g) * dw + k];
+    if (use1) D.rb[1][k] = p.rbits[(static_cast<size_t>(obp) * p.NT + g) * dw + k];
+  }
+  for (uint32_t k = tid; k < ne * dw; k += bs) D.eb[k / dw][k % dw] = p.ebits[static_cast<size_t>(g) * kEDesc * dw + k];
+  if (tid < ne) {
+    const uint4 ed = p.edesc[static_cast<size_t>(g) * kEDesc + tid];
+    D.et[tid] = desc_due(ed);
+    D.ebig[tid] = ed.z;
+  }
+  __syncthreads();
+  if (tid < 64 && (use0 || use1)) {  // wave 0: two words per lane (dw <= 128)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (!(h ? use1 : use0)) continue;
+      const uint32_t k = 2 * tid;
+      const uint32_t a = k < dw ? static_cast<uint32_t>(__popc(D.rb[h][k])) : 0u;
+      const uint32_t b = k + 1 < dw ? static_cast<uint32_t>(__popc(D.rb[h][k + 1])) : 0u;
+      uint32_t in = a + b;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(in, off, 64);
+        if (tid >= static_cast<uint32_t>(off)) in += v;
+      }
+      if (k < dw) D.rp[h][k] = in - a - b;
+      if (k + 1 < dw) D.rp[h][k + 1] = in - b;
+    }
+  }
+  __syncthreads();
+}
+
+// bit le of bitmap row w (LDS)
+__device__ inline bool desc_bit(const uint32_t* w, uint32_t le) { return (w[le >> 5] >> (le & 31u)) & 1u; }
+// rank of in-slot le among the set bits of reply bitmap h
+__device__ inline uint32_t desc_rank(const MeshDesc& D, int h, uint32_t le) {
+  return D.rp[h][le >> 5] + static_cast<uint32_t>(__popc(D.rb[h][le >> 5] & ((1u << (le & 31u)) - 1u)));
+}
+
 template <bool XR, int kMeshU, bool PF>
 __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                    long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ LinkShared L;
+  __shared__ MeshDesc D;
   uint32_t kk;
   if (!list_one(p.act_n[1], kk)) return;
   const uint32_t g = p.act[p.NT + kk];
   const uint32_t tid = tidx();
   const uint32_t n = AT(p.n_ops, g, p.NT);
   const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
-  const bool sl0 = p.eslot && (AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 1u);
-  const bool sl1 = p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u);
+  const uint32_t sf0 = p.eslot ? AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) : 0u;
+  const uint32_t sf1 = p.eslot ? AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) : 0u;
+  const bool sl0 = sf0 & 1u, sl1 = sf1 & 2u;
+  // reply descriptors (k_scan_pbft): live = not sent yet; sd0 / sd1 = due in this window.
+  // Descriptors need the PF variant (the pending echoes are applied to the LDS link words);
+  // the host enables them only with it.
+  const bool dsc = PF && p.desc;
+  if (!PF && p.desc) {
+    if (tid == 0) set_err(p, BCSIM_E_STATE);
+    return;
+  }
+  uint4 rd0 = make_uint4(0, 0, 0, 0), rd1 = make_uint4(0, 0, 0, 0);
+  if (dsc && (sf0 & kSfD)) rd0 = p.rdesc[static_cast<size_t>(ob) * p.NT + g];
+  if (dsc && (sf1 & kSfD1)) rd1 = p.rdesc[static_cast<size_t>(obp) * p.NT + g];
+  const bool dl0 = dsc && (sf0 & kSfD) && desc_due(rd0) >= t_lo;
+  const bool dl1 = dsc && (sf1 & kSfD1) && desc_due(rd1) >= t_lo;
+  const bool sd0 = dl0 && desc_due(rd0) < t_hi, sd1 = dl1 && desc_due(rd1) < t_hi;
+  const uint32_t ne = dsc ? AT(p.en, g, p.NT) : 0u;  // pending echo descriptors
   const uint32_t B = p.n_buckets;
   const uint32_t ib = static_cast<uint32_t>(cell % B);
   const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
@@ -3894,8 +4073,9 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   const bool rx = p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
   const bool rxe = rx && AT(p.eapp, g, p.NT) != t_lo;  // (see link_node)
   // nothing due in the window: no op before t_hi (node_onext is exact unless LLONG_MIN; fixed
-  // app delays only, so no unexpanded jitter broadcast hides behind it), no reply slot, no echo
-  if ((n == 0 || AT(p.node_onext, g, p.NT) >= t_hi) && !sl0 && !sl1 && !rxe) {
+  // app delays only, so no unexpanded jitter broadcast hides behind it), no reply slot or
+  // descriptor, no echo (pending echo descriptors wait for a stage that walks the edges)
+  if ((n == 0 || AT(p.node_onext, g, p.NT) >= t_hi) && !sl0 && !sl1 && !sd0 && !sd1 && !rxe) {
     if (rx && final_win && tid == 0) AT(p.iflag, fidx, static_cast<uint64_t>(B) * p.NT) = 0;
     return;
   }
@@ -3949,9 +4129,46 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   __syncthreads();
   const uint32_t n_bc = L.n_bc;
   if (L.n_list || n_bc > static_cast<uint32_t>(kBcastCap)) {  // not a simple node: the generic kernel
+    // which knows no descriptors: the pending echoes go onto the link words, the live reply
+    // descriptors into reply slots (the slot flags they stand for)
+    if (ne || dl0 || dl1) {
+      mesh_desc_load(p, D, g, ob, obp, dl0, dl1, ne);
+      const uint32_t e0m = AT(p.row, i, p.N + 1), degm = AT(p.row, i + 1, p.N + 1) - e0m;
+      for (uint32_t le = tid; le < degm; le += blockDim.x) {
+        if (ne) {
+          uint64_t* lwp = p.link + edge_loc(p, rep, e0m + le);
+          const uint64_t lw = *lwp;
+          int64_t bu = static_cast<int64_t>(lw >> 16);
+          bool any = false;
+          for (uint32_t d = 0; d < ne; ++d)
+            if (desc_bit(D.eb[d], le)) {
+              bu = (bu > D.et[d] ? bu : D.et[d]) + p.tx_tot[D.ebig[d] ? 1 : 0];
+              any = true;
+            }
+          if (any) {
+            if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+            *lwp = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
+          }
+        }
+        if (dl0 && desc_bit(D.rb[0], le))
+          *eslot_at(p, ob, rep, e0m + le) = make_uint4(rd0.x, rd0.y, rd0.z + desc_rank(D, 0, le), rd0.w);
+        if (dl1 && desc_bit(D.rb[1], le))
+          *eslot_at(p, obp, rep, e0m + le) = make_uint4(rd1.x, rd1.y, rd1.z + desc_rank(D, 1, le), rd1.w);
+      }
+      if (tid == 0) {
+        if (ne) AT(p.en, g, p.NT) = 0;
+        const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
+        if (sf0 & kSfD)  // kSfD0 -> bit 0, kSfD1 -> bit 1 (dead descriptors just go)
+          AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) =
+              static_cast<uint8_t>((sf0 & ~kSfD) | (dl0 ? ((sf0 >> 4) & 3u) : 0u));
+        if (sf1 & kSfD1)
+          AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4) = static_cast<uint8_t>((sf1 & ~kSfD1) | (dl1 ? 2u : 0u));
+      }
+    }
     if (tid == 0) {
       const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
       AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
+      FDBG(L.n_list ? 8 : 9);
     }
     return;
   }
@@ -3985,7 +4202,9 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   const uint32_t bs = blockDim.x;
   // (a node whose broadcasts are not due yet and that has no reply slot or echo to send skips
   // the edges: their link words would be loaded for nothing)
-  const uint32_t deg_w = (n_bc || sl0 || sl1 || rxe) ? deg : 0u;
+  const uint32_t deg_w = (n_bc || sl0 || sl1 || sd0 || sd1 || rxe) ? deg : 0u;
+  const uint32_t ne_w = deg_w ? ne : 0u;  // pending echo descriptors applied by this walk
+  if (sd0 || sd1 || ne_w) mesh_desc_load(p, D, g, ob, obp, sd0, sd1, ne_w);
   const bool xr = XR;  // (a template flag: the one-rank kernel carries no staging registers)
   // PF: the link words of all the node's out-edges in flight at once, parked in LDS (dynamic,
   // deg_max words), so that the edge loop of a pure broadcast has no dependent global load --
@@ -4005,6 +4224,31 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
       for (int q = 0; q < kPF; ++q) {
         const uint32_t k = k0 + q * bs + tid;
         if (k < deg_w) mlw[k] = v[q];
+      }
+    }
+    if (ne_w) {  // the pending echo descriptors, oldest first, onto the parked link words
+      for (uint32_t w = tid; w < p.dwords; w += bs) {
+        uint32_t u = 0;
+        for (uint32_t d = 0; d < ne_w; ++d) u |= D.eb[d][w];
+        D.eall[w] = u;
+      }
+      for (uint32_t le = tid; le < deg_w; le += bs) {
+        uint64_t lw = 0;
+        int64_t bu = 0;
+        bool any = false;
+        for (uint32_t d = 0; d < ne_w; ++d)
+          if (desc_bit(D.eb[d], le)) {
+            if (!any) {
+              lw = mlw[le];
+              bu = static_cast<int64_t>(lw >> 16);
+              any = true;
+            }
+            bu = (bu > D.et[d] ? bu : D.et[d]) + p.tx_tot[D.ebig[d] ? 1 : 0];
+          }
+        if (any) {
+          if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+          mlw[le] = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
+        }
       }
     }
     __syncthreads();
@@ -4036,6 +4280,17 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
       w0[u] = (v && sl0) ? *eslot_at(p, ob, rep, e0 + le) : make_uint4(0, 0, 0, 0);
       w1[u] = (v && sl1) ? *eslot_at(p, obp, rep, e0 + le) : make_uint4(0, 0, 0, 0);
     }
+    // reply descriptors: the edge's reply as a reply-slot word (in-slots of a reply
+    // descriptor and of the cell's reply slots are disjoint: one main record per edge and cell)
+    bool hd0[kMeshU], hd1[kMeshU];
+#pragma unroll
+    for (int u = 0; u < kMeshU; ++u) {
+      const uint32_t le = base + u * bs;
+      hd0[u] = sd0 && le < deg && desc_bit(D.rb[0], le);
+      hd1[u] = sd1 && le < deg && desc_bit(D.rb[1], le);
+      if (hd0[u]) w0[u] = make_uint4(rd0.x, rd0.y, rd0.z + desc_rank(D, 0, le), rd0.w);
+      if (hd1[u]) w1[u] = make_uint4(rd1.x, rd1.y, rd1.z + desc_rank(D, 1, le), rd1.w);
+    }
 #pragma unroll
     for (int u = 0; u < kMeshU; ++u) {
       const uint32_t le = base + u * bs;
@@ -4065,10 +4320,12 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
       // reply slots {due t lo, hi, sub, f0 | f1 << 16} of this arrival cell and the previous one
       const int64_t rt1 = static_cast<int64_t>((static_cast<uint64_t>(w0[u].y) << 32) | w0[u].x);
       const int64_t rt2 = static_cast<int64_t>((static_cast<uint64_t>(w1[u].y) << 32) | w1[u].x);
-      bool hr = sl0 && rt1 >= t_lo && rt1 < t_hi;
-      bool hr2 = sl1 && rt2 >= t_lo && rt2 < t_hi;
+      bool hr = (sl0 || hd0[u]) && rt1 >= t_lo && rt1 < t_hi;
+      bool hr2 = (sl1 || hd1[u]) && rt2 >= t_lo && rt2 < t_hi;
       st_ops += (hr ? 1u : 0u) + (hr2 ? 1u : 0u);
-      if (n_bc == 0 && !he && !hr && !hr2) continue;
+      // pending echo descriptors on this edge: already on its parked link word (PF prefetch)
+      const bool pe = ne_w && desc_bit(D.eall, le);
+      if (n_bc == 0 && !he && !hr && !hr2 && !pe) continue;
       ++st_edges;
       int64_t bu = static_cast<int64_t>(lw[u] >> 16);
       uint32_t lc = static_cast<uint32_t>(lw[u] & 0xFFFFu);
@@ -4237,12 +4494,20 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
     for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x)
       if (L.tflag[k]) set_flag_once(&AT(p.rtile, tb + k, static_cast<uint64_t>(B) * p.R * p.n_tiles));
   }
+  if (tid == 0) {
+    if (ne_w) AT(p.en, g, p.NT) = 0;  // every edge walked: the echo descriptors are applied
+    // a reply descriptor is sent whole (one due instant): its flag goes (a stale flag would keep
+    // k_scan_pbft from taking the echoes of a later window)
+    const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
+    if (sd0) AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) = static_cast<uint8_t>(sf0 & ~kSfD0);
+    if (sd1) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4) = static_cast<uint8_t>(sf1 & ~kSfD1);
+  }
   const unsigned long long t0 = p.wgt ? wg_t0 : 0ull;
   unsigned long long ph[4] = {t0, t0, t0, t0};
   const LinkCounts c8{dropped, sends, n_rec, st_ops, st_edges, st_echo, 0u, 0u};
   // every op due (the broadcasts just sent): nothing to compact, no op to read again
-  link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, n_lists, ovmin, c8, sl1 && final_win, rx && final_win, obp, fidx, t0,
-              ph, n);
+  link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, n_lists, ovmin, c8, (sl1 || sd1) && final_win, rx && final_win, obp,
+              fidx, t0, ph, n);
 }
 
 // ---------------------------------------------------------------------------
@@ -5079,7 +5344,7 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
     const bool sc = has_start || has_stop || node_flagged_w(p, b, g, rep, i, t_hi) || AT(p.node_tnext, g, p.NT) < t_hi;
     // k_link also runs nodes with reply-slot ops of the previous arrival cell due
     const bool lk = sc || AT(p.node_onext, g, p.NT) < t_hi ||
-                    (p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & 2u));
+                    (p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & (2u | kSfD1)));
     fl[j] = static_cast<uint8_t>((sc ? 1u : 0u) | (lk ? 2u : 0u));
     ns += sc ? 1u : 0u;
     nl += lk ? 1u : 0u;
