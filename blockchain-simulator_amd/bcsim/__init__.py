@@ -13,7 +13,7 @@ from . import _abi, partition
 from ._abi import (  # noqa: F401
     PBFT, RAFT, PAXOS, GOSSIP, DELAY_FIXED, DELAY_RANDOM, RNG_GLIBC, RNG_COUNTER,
     TIME_ROUND, TIME_TRUNC, ENC_EXTENDED, ENC_COMPAT, TR, INT64_MAX,
-    QUEUE_INFINITE, QUEUE_DROPTAIL, ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE,
+    QUEUE_INFINITE, QUEUE_DROPTAIL, QUEUE_FQCODEL, ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE,
     Config, TraceRec, Counters, Status, EngineError, default_config,
 )
 

@@ -5,14 +5,14 @@ the sizes against the compiled library.
 """
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 PBFT, RAFT, PAXOS, GOSSIP = 0, 1, 2, 3
 DELAY_FIXED, DELAY_RANDOM = 0, 1
 RNG_GLIBC, RNG_COUNTER = 0, 1
 TIME_ROUND, TIME_TRUNC = 0, 1
 ENC_EXTENDED, ENC_COMPAT = 0, 1
-QUEUE_INFINITE, QUEUE_DROPTAIL = 0, 1
+QUEUE_INFINITE, QUEUE_DROPTAIL, QUEUE_FQCODEL = 0, 1, 2
 ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE = 0, 1, 2
 
 OK = 0
@@ -74,6 +74,14 @@ class Config(C.Structure):
         ("cap_queue_msgs", C.c_uint32),
         ("paxos_decrees", C.c_uint32),
         ("engine_mode", C.c_uint32),
+        ("fq_limit_pkts", C.c_uint32),
+        ("fq_flows", C.c_uint32),
+        ("fq_quantum", C.c_uint32),
+        ("fq_drop_batch", C.c_uint32),
+        ("fq_target_ns", C.c_int64),
+        ("fq_interval_ns", C.c_int64),
+        ("fq_min_bytes", C.c_uint32),
+        ("fq_perturbation", C.c_uint32),
         ("reserved", C.c_uint32 * 2),
     ]
 

@@ -181,7 +181,8 @@ static int validate(const bcsim_config& c) {
   if (c.abi_version != BCSIM_ABI_VERSION) return BCSIM_E_INVAL;
   if (c.protocol > BCSIM_GOSSIP || c.n_nodes < 2 || c.link_rate_bps == 0) return BCSIM_E_INVAL;
   if (c.mtu < 68) return BCSIM_E_INVAL;
-  if (c.queue_model > BCSIM_QUEUE_DROPTAIL) return BCSIM_E_INVAL;
+  if (c.queue_model > BCSIM_QUEUE_FQCODEL) return BCSIM_E_INVAL;
+  if (c.queue_model == BCSIM_QUEUE_FQCODEL && (c.queue_dev_pkts == 0 || c.queue_dev_pkts > 4096)) return BCSIM_E_INVAL;
   if (c.queue_model == BCSIM_QUEUE_DROPTAIL && c.queue_dev_pkts + c.queue_disc_pkts == 0) return BCSIM_E_INVAL;
   if (c.delay_mode == BCSIM_DELAY_RANDOM && c.rng_mode == BCSIM_RNG_GLIBC) {
     // the global glibc stream is consumed at every send in event order; only
@@ -296,7 +297,22 @@ static int setup_device(Sim& s) {
     p.nfr[k] = mt[k]->frames;
     p.tx_full[k] = mt[k]->frames > 1 ? (mt[k]->total - mt[k]->last) / (mt[k]->frames - 1) : mt[k]->total;
   }
-  p.qmodel = c.queue_model == BCSIM_QUEUE_DROPTAIL ? 1u : 0u;
+  p.qmodel = c.queue_model == BCSIM_QUEUE_DROPTAIL ? 1u : c.queue_model == BCSIM_QUEUE_FQCODEL ? 2u : 0u;
+  {  // FQCODEL: ns-3 attribute defaults for 0
+    const uint32_t frag = (c.mtu - 20) & ~7u;
+    const uint32_t bytes[2] = {small, big};
+    for (int k = 0; k < 2; ++k) {
+      p.ip_full[k] = frag + 20;
+      p.ip_last[k] = bytes[k] + 8 - frag * (p.nfr[k] - 1) + 20;
+    }
+    p.fq_limit = c.fq_limit_pkts ? c.fq_limit_pkts : 10240;
+    p.fq_quantum = c.fq_quantum ? c.fq_quantum : c.mtu;
+    p.fq_batch = c.fq_drop_batch ? c.fq_drop_batch : 64;
+    p.fq_min_bytes = c.fq_min_bytes ? c.fq_min_bytes : 1500;
+    p.fq_target_c = static_cast<uint32_t>(static_cast<uint64_t>(c.fq_target_ns > 0 ? c.fq_target_ns : 5000000) >> 10);
+    p.fq_interval_c = static_cast<uint32_t>(static_cast<uint64_t>(c.fq_interval_ns > 0 ? c.fq_interval_ns : 100000000) >> 10);
+    p.fq_devcap = c.queue_dev_pkts;
+  }
   p.qcap_frames = c.queue_dev_pkts + c.queue_disc_pkts;
   p.cap_q = c.cap_queue_msgs ? c.cap_queue_msgs : 256;
   p.pbft_period = fsec_to_ns(c.pbft_timeout_s, tr);
@@ -318,6 +334,12 @@ static int setup_device(Sim& s) {
   for (int64_t v : s.prop) pmin = std::min(pmin, v);
   if (pmin < 0) return BCSIM_E_INVAL;
   s.L = pmin + ms.total;  // lookahead: nothing arrives sooner than this after its send
+  if (p.qmodel == 2) {  // FQCODEL: a message is emitted when its last fragment enters the device
+    int64_t fmin = std::min(ms.last, mb.last);  // queue, at most one frame before it arrives
+    if (mb.frames > 1) fmin = std::min<int64_t>(fmin, p.tx_full[1]);
+    if (ms.frames > 1) fmin = std::min<int64_t>(fmin, p.tx_full[0]);
+    s.L = pmin + fmin;
+  }
   if (s.L <= 0 || s.L >= (1ll << 32)) {
     g_detail = "lookahead out of range";
     return BCSIM_E_UNSUPPORTED;
@@ -407,6 +429,10 @@ static int setup_device(Sim& s) {
     s.sparse = c.engine_mode == BCSIM_ENGINE_SPARSE || (c.engine_mode == BCSIM_ENGINE_AUTO && dense_bytes > 96e9);
   }
   p.sparse = s.sparse ? 1u : 0u;
+  if (s.sparse && p.qmodel == 2) {
+    g_detail = "the FQCODEL queue model needs the dense layout";
+    return BCSIM_E_UNSUPPORTED;
+  }
   p.n_heavy = s.N;
   p.cap_ops_light = p.cap_ops;
   s.bs_scan = static_cast<uint32_t>(std::min<uint64_t>(1024, std::max<uint64_t>(64, next_pow2(s.deg_max + 1))));
@@ -529,7 +555,8 @@ static int setup_device(Sim& s) {
     for (const void* f : {reinterpret_cast<const void*>(k_link<false, false>), reinterpret_cast<const void*>(k_link<false, true>),
                           reinterpret_cast<const void*>(k_link<false, false, true>),
                           reinterpret_cast<const void*>(k_link<false, true, true>),
-                          reinterpret_cast<const void*>(k_link<true, false>), reinterpret_cast<const void*>(k_link<true, true>)})
+                          reinterpret_cast<const void*>(k_link<true, false>), reinterpret_cast<const void*>(k_link<true, true>),
+                          reinterpret_cast<const void*>(k_link<2, false>), reinterpret_cast<const void*>(k_link<2, true>)})
       HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(link_lds_bytes(p))));
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_pbft_tick),
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(s.N)));
@@ -690,8 +717,38 @@ static int setup_device(Sim& s) {
       g_detail = "cap_queue_msgs must be < 65536";
       return BCSIM_E_INVAL;
     }
-    if ((rc = dalloc(s, &p.qmeta, ne)) || (rc = dalloc(s, &p.qring, ne * (p.qmodel ? p.cap_q : 1)))) return rc;
+    if ((rc = dalloc(s, &p.qmeta, ne)) || (rc = dalloc(s, &p.qring, ne * (p.qmodel == 1 ? p.cap_q : 1)))) return rc;
     HIPCHK(hipMemset(p.qmeta, 0, ne * 8));
+  }
+  {  // FQCODEL link queues: header, device-queue ring, packet rings, message table per edge
+    const bool fq = p.qmodel == 2;
+    const size_t ne = fq ? static_cast<size_t>(s.R) * p.E_loc : 1;
+    p.cap_fqm = c.cap_queue_msgs ? std::min<uint32_t>(c.cap_queue_msgs, kFqMaxMsgs) : kFqMaxMsgs;
+    p.cap_fqm = (p.cap_fqm + 31) / 32 * 32;
+    p.cap_fqp = static_cast<uint32_t>(std::min<uint64_t>(p.fq_limit + 1ull, 4096));
+    if (fq && static_cast<double>(ne) * (3.0 * p.cap_fqp + p.cap_fqm) * 16 > 64e9) {
+      g_detail = "FQCODEL link state exceeds 64 GB";
+      return BCSIM_E_UNSUPPORTED;
+    }
+    uint8_t* fqmap = nullptr;
+    if ((rc = dalloc(s, &p.fqh, ne * kFqH)) || (rc = dalloc(s, &p.fqdev, fq ? ne * p.fq_devcap : 1)) ||
+        (rc = dalloc(s, &p.fqpk, fq ? ne * 3 * p.cap_fqp : 1)) || (rc = dalloc(s, &p.fqmsg, fq ? ne * p.cap_fqm : 1)) ||
+        (rc = dalloc(s, &fqmap, fq ? s.E : 1)))
+      return rc;
+    p.fqmap = fqmap;
+    if (fq) {
+      std::vector<uint32_t> h0(kFqH, 0);
+      for (uint32_t f = 0; f < 3; ++f) {
+        h0[f * kFqF + FQ_REC] = 0xFFFFu;  // rec_inv_sqrt = ~0U >> REC_INV_SQRT_SHIFT
+        h0[f * kFqF + FQ_CR] = kInvalid;  // queue-disc class not created yet
+      }
+      std::vector<uint32_t> hall(ne * kFqH);
+      for (size_t k = 0; k < ne; ++k) std::copy(h0.begin(), h0.end(), hall.begin() + k * kFqH);
+      HIPCHK(hipMemcpy(p.fqh, hall.data(), hall.size() * 4, hipMemcpyHostToDevice));
+      const std::vector<uint8_t> map =
+          fq_flow_map(s.N, s.row, s.col, s.rev, c.protocol, c.fq_flows ? c.fq_flows : 1024, c.fq_perturbation);
+      HIPCHK(hipMemcpy(fqmap, map.data(), s.E, hipMemcpyHostToDevice));
+    }
   }
   // k_scan / k_link grids (multiples of 8: one list chunk per XCD).  Dense layout: one
   // workgroup per possible list entry (an inactive node's workgroup exits at once); sparse
@@ -821,6 +878,17 @@ static int setup_device(Sim& s) {
   if (const char* fv = std::getenv("BCSIM_FDBG"); fv && *fv == '1') {  // debug: fast-kernel leave reasons
     if ((rc = dalloc(s, &p.fdbg, 16))) return rc;
     HIPCHK(hipMemset(p.fdbg, 0, 16 * 8));
+  }
+  p.fqlog = nullptr;
+  p.fqlog_n = nullptr;
+  if (const char* fl = std::getenv("BCSIM_FQLOG"); fl && *fl && p.qmodel == 2) {  // debug: FQCODEL link events
+    p.cap_fqlog = 1u << 22;
+    const char* a = std::getenv("BCSIM_FQLOG_T0");
+    const char* b = std::getenv("BCSIM_FQLOG_T1");
+    p.fqlog_t0 = a ? std::atoll(a) : 0;
+    p.fqlog_t1 = b ? std::atoll(b) : LLONG_MAX;
+    if ((rc = dalloc(s, &p.fqlog, 2ull * p.cap_fqlog)) || (rc = dalloc(s, &p.fqlog_n, 1))) return rc;
+    HIPCHK(hipMemset(p.fqlog_n, 0, 4));
   }
   if (const char* wv = std::getenv("BCSIM_WGT"); wv && *wv == '1') {  // debug: k_link per-WG timing
     if ((rc = dalloc(s, &p.wgt, NT * 8)) || (rc = dalloc(s, &p.wgs, NT * 8))) return rc;
@@ -1111,6 +1179,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   } else {
     const size_t ll = link_lds_bytes(s.kp);
     const bool qm = s.kp.qmodel != 0, xr = s.kp.nranks > 1;
+    if (s.kp.qmodel == 2)
+      rc = xr ? launch(s, KS_LINK, (k_link<2, true>), grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw)
+              : launch(s, KS_LINK, (k_link<2, false>), grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw);
+    else
     rc = qm ? (xr ? launch(s, KS_LINK, k_link<true, true>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw)
                   : launch(s, KS_LINK, k_link<true, false>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw))
             : (xr ? launch(s, KS_LINK, k_link<false, true>, grid, dim3(s.bs_link), ll, s.kp_dev, cell, lo, hi, fw)
@@ -1811,6 +1883,18 @@ int bcsim_run(bcsim_sim* h, int64_t t_until_ns) {
   if (s.err) return s.err;
   int rc = bcsim::run(s, t_until_ns);
   if (rc) s.err = rc;
+  if (s.kp.fqlog) {  // debug (BCSIM_FQLOG=<file>): the FQCODEL link events so far
+    uint32_t n = 0;
+    if (hipMemcpy(&n, s.kp.fqlog_n, 4, hipMemcpyDeviceToHost) == hipSuccess) {
+      n = std::min(n, s.kp.cap_fqlog);
+      std::vector<uint4> v(2ull * n);
+      if (n && hipMemcpy(v.data(), s.kp.fqlog, v.size() * 16, hipMemcpyDeviceToHost) != hipSuccess) n = 0;
+      if (FILE* f = std::fopen(std::getenv("BCSIM_FQLOG"), "wb")) {
+        std::fwrite(v.data(), 16, 2ull * n, f);
+        std::fclose(f);
+      }
+    }
+  }
   return rc;
 }
 

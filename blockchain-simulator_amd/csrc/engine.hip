@@ -127,10 +127,29 @@ struct KP {
   // DROPTAIL link queues: per edge a ring of the messages of its busy
   // period, entry = start << 17 | big << 16 | accepted frames; meta = head | n << 16 |
   // frames << 32
-  uint32_t qmodel, qcap_frames, cap_q;
+  uint32_t qmodel, qcap_frames, cap_q;  // qmodel: 0 INFINITE, 1 DROPTAIL, 2 FQCODEL
   uint32_t nfr[2];
   int64_t tx_full[2];
   uint64_t *qring, *qmeta;
+  // FQCODEL link queues, per rank-local edge: a header of kFqH words (three
+  // flows' CoDel + DRR state, new / old flow lists, device-queue ring position, device busy end,
+  // packets in the disc, message-table bitmap), the start times of the device queue's waiting
+  // frames [fq_devcap], three packet rings [3][cap_fqp] {enq lo, enq hi, msg | frame << 16,
+  // IPv4 bytes} and the message table [cap_fqm] {sub, f0 | f1 << 16, f2 | type << 16 | big << 24 |
+  // echo << 25 | lost << 26, fragments left}; fqmap[e] = flow slot per packet class (global edge)
+  uint32_t* fqh;
+  int64_t* fqdev;
+  uint4* fqpk;
+  uint4* fqmsg;
+  const uint8_t* fqmap;
+  uint32_t fq_devcap, cap_fqp, cap_fqm, fq_limit, fq_quantum, fq_batch, fq_min_bytes, fq_target_c, fq_interval_c;
+  uint32_t ip_full[2], ip_last[2];
+  // debug (BCSIM_FQLOG=<file>): every FQCODEL link event with t in [fqlog_t0, fqlog_t1) as two
+  // uint4 {t lo, t hi, edge, kind << 24 | frame}, {msg sub, x lo, x hi, echo} (tools/fq_log.py)
+  uint4* fqlog;
+  uint32_t* fqlog_n;
+  uint32_t cap_fqlog;
+  long long fqlog_t0, fqlog_t1;
   // inbox
   Rec* inbox;            // [B][R][E]  receiver-major (in-slot order)
   uint8_t* rtile;        // [B][R][n_tiles] full mesh: a record for a receiver of this 64-node
@@ -578,6 +597,21 @@ __device__ inline void st_op(Op* q, const Op& o) {
 struct RawOp {
   uint4 a, b;
 };
+// d = c ? s : d, word by word through an opaque lane mask: a plain select of RawOp values between
+// several op sources in divergent code was miscompiled again in the FQCODEL edge loop (a record
+// took its first 16 bytes from one source and the rest from another)
+__device__ inline void raw_sel(RawOp& d, const RawOp& s, bool c) {
+  uint32_t m = 0u - static_cast<uint32_t>(c);
+  asm volatile("" : "+v"(m));
+  d.a.x = (s.a.x & m) | (d.a.x & ~m);
+  d.a.y = (s.a.y & m) | (d.a.y & ~m);
+  d.a.z = (s.a.z & m) | (d.a.z & ~m);
+  d.a.w = (s.a.w & m) | (d.a.w & ~m);
+  d.b.x = (s.b.x & m) | (d.b.x & ~m);
+  d.b.y = (s.b.y & m) | (d.b.y & ~m);
+  d.b.z = (s.b.z & m) | (d.b.z & ~m);
+  d.b.w = (s.b.w & m) | (d.b.w & ~m);
+}
 __device__ inline RawOp raw_zero() { return RawOp{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)}; }
 __device__ inline RawOp ld_raw(const Op* q) {
   const uint4* v = reinterpret_cast<const uint4*>(q);
@@ -3263,6 +3297,344 @@ __device__ inline uint32_t q_admit(const KP& p, uint64_t* ring, uint64_t& meta, 
   return k;
 }
 
+// ---- FQCODEL link queue (oracle/bcsim_oracle.c fq_* restated) ------------
+// One lane owns one directed edge and walks its events in time order (the link's ops in key
+// order, the device-queue wakes in between), so the disc state lives in global memory and is
+// read and written by that lane only.  Words only (no sub-dword struct members: DESIGN §8).
+constexpr uint32_t kFqH = 64, kFqF = 12;
+enum : uint32_t { FQ_HEAD = 0, FQ_N, FQ_BYTES, FQ_FA, FQ_DNEXT, FQ_CNT, FQ_LCNT, FQ_REC, FQ_DROP, FQ_ST, FQ_DEF, FQ_CR };
+enum : uint32_t { FQ_NNEW = 36, FQ_NEWL = 37, FQ_NOLD = 40, FQ_OLDL = 41, FQ_NCR = 44, FQ_STOP = 45, FQ_DH = 46,
+                  FQ_DN = 47, FQ_DEND = 48, FQ_QP = 50, FQ_MBM = 52 };
+constexpr uint32_t kFqMaxMsgs = 128;  // message-table bitmap words FQ_MBM..FQ_MBM+3
+constexpr uint32_t kFqEcho = 1u << 25, kFqLost = 1u << 26;
+
+struct FqLink {
+  uint32_t* h;
+  int64_t* dev;
+  uint4* pk;
+  uint4* msg;
+  uint32_t map, e, src;  // (src: the op source of the current send, debug log only)
+};
+// kinds: 1 enqueue, 2 into the device queue (x = frame start), 3 drop, 4 wake
+__device__ inline void fq_log(const KP& p, const FqLink& L, int64_t t, uint32_t kind, const uint4& pk, int64_t x) {
+  if (!p.fqlog || t < p.fqlog_t0 || t >= p.fqlog_t1) return;
+  const uint32_t pos = atomicAdd(p.fqlog_n, 1u);
+  if (pos >= p.cap_fqlog) return;
+  const uint32_t m = pk.z & 0xFFFFu;
+  p.fqlog[2ull * pos] = make_uint4(static_cast<uint32_t>(t), static_cast<uint32_t>(static_cast<uint64_t>(t) >> 32), L.e,
+                                   (kind << 24) | (pk.z >> 16));
+  p.fqlog[2ull * pos + 1] = make_uint4(kind == 4 ? 0u : L.msg[m].x, static_cast<uint32_t>(x),
+                                       static_cast<uint32_t>(static_cast<uint64_t>(x) >> 32),
+                                       kind == 4 ? 0u : (L.msg[m].z & kFqEcho) ? 1u : 0u);
+}
+struct FqCount {
+  unsigned long long fdrop, lost;
+};
+
+__device__ inline int64_t fq_ld64(const uint32_t* w) {
+  return static_cast<int64_t>((static_cast<uint64_t>(w[1]) << 32) | w[0]);
+}
+__device__ inline void fq_st64(uint32_t* w, int64_t v) {
+  w[0] = static_cast<uint32_t>(v);
+  w[1] = static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32);
+}
+__device__ inline FqLink fq_link(const KP& p, size_t le, uint32_t e) {
+  FqLink L;
+  L.h = p.fqh + le * kFqH;
+  L.dev = p.fqdev + le * p.fq_devcap;
+  L.pk = p.fqpk + le * 3 * p.cap_fqp;
+  L.msg = p.fqmsg + le * p.cap_fqm;
+  L.map = p.fqmap[e];
+  L.e = e;
+  L.src = 0;
+  return L;
+}
+__device__ inline bool fq_pop(const KP& p, FqLink& L, uint32_t f, uint4& out) {
+  uint32_t* F = L.h + f * kFqF;
+  const uint32_t n = F[FQ_N];
+  if (n == 0) return false;
+  const uint32_t hd = F[FQ_HEAD];
+  out = L.pk[f * p.cap_fqp + hd];
+  F[FQ_HEAD] = hd + 1 == p.cap_fqp ? 0u : hd + 1;
+  F[FQ_N] = n - 1;
+  F[FQ_BYTES] -= out.w;
+  L.h[FQ_QP] -= 1;
+  return true;
+}
+__device__ inline void fq_free_msg(FqLink& L, uint32_t m) { L.h[FQ_MBM + (m >> 5)] &= ~(1u << (m & 31u)); }
+// a packet leaves the disc untransmitted (CoDel or overlimit drop): its message is lost
+__device__ inline void fq_drop(const KP& p, FqLink& L, const uint4& pk, FqCount& c, int64_t now) {
+  fq_log(p, L, now, 3, pk, 0);
+  ++c.fdrop;
+  const uint32_t m = pk.z & 0xFFFFu;
+  uint32_t z = L.msg[m].z, left = L.msg[m].w;
+  if (!(z & kFqLost)) {
+    z |= kFqLost;
+    if (!(z & kFqEcho)) ++c.lost;
+  }
+  L.msg[m].z = z;
+  L.msg[m].w = left - 1;
+  if (left == 1) fq_free_msg(L, m);
+}
+// CoDelQueueDisc::OkToDrop (has: a packet was dequeued)
+__device__ inline bool codel_ok(const KP& p, uint32_t* F, bool has, const uint4& pk, int64_t now, uint32_t now_c) {
+  if (!has) {
+    F[FQ_FA] = 0;
+    return false;
+  }
+  const int64_t enq = static_cast<int64_t>((static_cast<uint64_t>(pk.y) << 32) | pk.x);
+  const uint32_t soj = static_cast<uint32_t>(static_cast<uint64_t>(now - enq) >> 10);
+  if (static_cast<int32_t>(soj - p.fq_target_c) < 0 || F[FQ_BYTES] < p.fq_min_bytes) {
+    F[FQ_FA] = 0;
+    return false;
+  }
+  if (F[FQ_FA] == 0) {
+    F[FQ_FA] = now_c + p.fq_interval_c;
+    return false;
+  }
+  return static_cast<int32_t>(now_c - F[FQ_FA]) > 0;
+}
+__device__ inline uint32_t codel_newton(uint32_t rec, uint32_t count) {
+  const uint32_t invsqrt = rec << 16;
+  const uint32_t invsqrt2 = static_cast<uint32_t>((static_cast<uint64_t>(invsqrt) * invsqrt) >> 32);
+  uint64_t val = (3ull << 32) - static_cast<uint64_t>(count) * invsqrt2;
+  val >>= 2;
+  val = (val * invsqrt) >> 31;
+  return static_cast<uint32_t>(val >> 16) & 0xFFFFu;
+}
+__device__ inline uint32_t codel_law(uint32_t t, uint32_t interval, uint32_t rec) {
+  return t + static_cast<uint32_t>((static_cast<uint64_t>(interval) * (rec << 16)) >> 32);
+}
+// CoDelQueueDisc::DoDequeue of flow f
+__device__ inline bool codel_deq(const KP& p, FqLink& L, uint32_t f, int64_t now, uint4& out, FqCount& c) {
+  uint32_t* F = L.h + f * kFqF;
+  uint4 pk;
+  if (!fq_pop(p, L, f, pk)) {
+    F[FQ_DROP] = 0;
+    return false;
+  }
+  const uint32_t now_c = static_cast<uint32_t>(static_cast<uint64_t>(now) >> 10);
+  bool have = true;
+  const bool ok = codel_ok(p, F, true, pk, now, now_c);
+  if (F[FQ_DROP]) {
+    if (!ok) {
+      F[FQ_DROP] = 0;
+    } else if (static_cast<int32_t>(now_c - F[FQ_DNEXT]) >= 0) {
+      while (F[FQ_DROP] && static_cast<int32_t>(now_c - F[FQ_DNEXT]) >= 0) {
+        F[FQ_CNT] += 1;
+        F[FQ_REC] = codel_newton(F[FQ_REC], F[FQ_CNT]);
+        fq_drop(p, L, pk, c, now);
+        have = fq_pop(p, L, f, pk);
+        if (!codel_ok(p, F, have, pk, now, now_c))
+          F[FQ_DROP] = 0;
+        else
+          F[FQ_DNEXT] = codel_law(F[FQ_DNEXT], p.fq_interval_c, F[FQ_REC]);
+      }
+    }
+  } else if (ok) {
+    fq_drop(p, L, pk, c, now);
+    have = fq_pop(p, L, f, pk);
+    (void)codel_ok(p, F, have, pk, now, now_c);
+    F[FQ_DROP] = 1;
+    const int32_t delta = static_cast<int32_t>(F[FQ_CNT] - F[FQ_LCNT]);
+    if (delta > 1 && static_cast<int32_t>((now_c - F[FQ_DNEXT]) - 16u * p.fq_interval_c) < 0) {
+      F[FQ_CNT] = static_cast<uint32_t>(delta);
+      F[FQ_REC] = codel_newton(F[FQ_REC], F[FQ_CNT]);
+    } else {
+      F[FQ_CNT] = 1;
+      F[FQ_REC] = 0xFFFFu;
+    }
+    F[FQ_LCNT] = F[FQ_CNT];
+    F[FQ_DNEXT] = codel_law(now_c, p.fq_interval_c, F[FQ_REC]);
+  }
+  if (have) out = pk;
+  return have;
+}
+__device__ inline void fq_list_pop(uint32_t* h, uint32_t nidx, uint32_t lidx) {
+  const uint32_t n = h[nidx];
+  for (uint32_t k = 1; k < n; ++k) h[lidx + k - 1] = h[lidx + k];
+  h[nidx] = n - 1;
+}
+__device__ inline void fq_list_push(uint32_t* h, uint32_t nidx, uint32_t lidx, uint32_t f) {
+  const uint32_t n = h[nidx];
+  h[lidx + n] = f;
+  h[nidx] = n + 1;
+}
+// FqCoDelQueueDisc::DoDequeue: DRR over the new, then the old flows
+__device__ inline bool fq_deq(const KP& p, FqLink& L, int64_t now, uint4& out, FqCount& c) {
+  uint32_t* h = L.h;
+  for (;;) {
+    int f = -1;
+    while (f < 0 && h[FQ_NNEW]) {
+      const uint32_t q = h[FQ_NEWL];
+      uint32_t* F = h + q * kFqF;
+      if (static_cast<int32_t>(F[FQ_DEF]) <= 0) {
+        F[FQ_DEF] += p.fq_quantum;
+        F[FQ_ST] = 2;
+        fq_list_push(h, FQ_NOLD, FQ_OLDL, q);
+        fq_list_pop(h, FQ_NNEW, FQ_NEWL);
+      } else {
+        f = static_cast<int>(q);
+      }
+    }
+    while (f < 0 && h[FQ_NOLD]) {
+      const uint32_t q = h[FQ_OLDL];
+      uint32_t* F = h + q * kFqF;
+      if (static_cast<int32_t>(F[FQ_DEF]) <= 0) {
+        F[FQ_DEF] += p.fq_quantum;
+        fq_list_pop(h, FQ_NOLD, FQ_OLDL);
+        fq_list_push(h, FQ_NOLD, FQ_OLDL, q);
+      } else {
+        f = static_cast<int>(q);
+      }
+    }
+    if (f < 0) return false;
+    uint32_t* F = h + f * kFqF;
+    if (codel_deq(p, L, static_cast<uint32_t>(f), now, out, c)) {
+      F[FQ_DEF] -= out.w;
+      return true;
+    }
+    if (F[FQ_ST] == 1 && h[FQ_NOLD]) {
+      F[FQ_ST] = 2;
+      fq_list_push(h, FQ_NOLD, FQ_OLDL, static_cast<uint32_t>(f));
+      fq_list_pop(h, FQ_NNEW, FQ_NEWL);
+    } else if (F[FQ_ST] == 1) {
+      F[FQ_ST] = 0;
+      fq_list_pop(h, FQ_NNEW, FQ_NEWL);
+    } else {
+      F[FQ_ST] = 0;
+      fq_list_pop(h, FQ_NOLD, FQ_OLDL);
+    }
+  }
+}
+// device-queue frames that started transmission by `now` no longer wait
+__device__ inline void fq_settle(const KP& p, FqLink& L, int64_t now) {
+  uint32_t dh = L.h[FQ_DH], dn = L.h[FQ_DN];
+  while (dn && L.dev[dh] <= now) {
+    dh = dh + 1 == p.fq_devcap ? 0u : dh + 1;
+    --dn;
+  }
+  L.h[FQ_DH] = dh;
+  L.h[FQ_DN] = dn;
+}
+// a packet from the disc into the device queue; a message whose last fragment this was is
+// delivered (emit(sub, f0|f1, f2|type, big, end of its frame)) unless a fragment was dropped
+template <typename Emit>
+__device__ inline void fq_dev_push(const KP& p, FqLink& L, const uint4& pk, int64_t now, Emit& emit) {
+  const uint32_t m = pk.z & 0xFFFFu, frame = pk.z >> 16;
+  const uint4 me = L.msg[m];
+  const int big = (me.z >> 24) & 1;
+  const int64_t tx = frame + 1 == p.nfr[big] ? p.tx_last[big] : p.tx_full[big];
+  const int64_t dend = fq_ld64(L.h + FQ_DEND);
+  const int64_t start = dend > now ? dend : now;
+  const int64_t end = start + tx;
+  fq_log(p, L, now, 2, pk, start);
+  fq_st64(L.h + FQ_DEND, end);
+  fq_settle(p, L, now);
+  if (start > now) {
+    const uint32_t dh = L.h[FQ_DH], dn = L.h[FQ_DN];
+    uint32_t at = dh + dn;
+    if (at >= p.fq_devcap) at -= p.fq_devcap;
+    L.dev[at] = start;
+    L.h[FQ_DN] = dn + 1;
+    if (dn + 1 == p.fq_devcap) L.h[FQ_STOP] = 1;  // the device queue is full: the disc stops
+  }
+  if (me.w > 1) {
+    L.msg[m].w = me.w - 1;
+    return;
+  }
+  L.msg[m].w = 0;
+  fq_free_msg(L, m);
+  if (!(me.z & (kFqLost | kFqEcho))) emit(me.x, me.y, me.z & 0x00FFFFFFu, big, end);
+}
+// QueueDisc::Run
+template <typename Emit>
+__device__ inline void fq_run(const KP& p, FqLink& L, int64_t now, Emit& emit, FqCount& c) {
+  uint4 pk;
+  while (!L.h[FQ_STOP] && fq_deq(p, L, now, pk, c)) fq_dev_push(p, L, pk, now, emit);
+}
+// the device-queue wakes up to time t (each at its oldest waiting frame's start)
+template <typename Emit>
+__device__ inline void fq_advance(const KP& p, FqLink& L, int64_t t, Emit& emit, FqCount& c) {
+  while (L.h[FQ_STOP]) {
+    const int64_t tw = L.dev[L.h[FQ_DH]];
+    if (tw > t) break;
+    fq_log(p, L, tw, 4, make_uint4(0, 0, 0, 0), L.h[FQ_QP]);
+    fq_settle(p, L, tw);
+    L.h[FQ_STOP] = 0;
+    fq_run(p, L, tw, emit, c);
+  }
+}
+// FqCoDelQueueDisc::FqCoDelDrop: half the fattest flow's bytes (first class on ties)
+__device__ inline void fq_overlimit(const KP& p, FqLink& L, FqCount& c, int64_t now) {
+  uint32_t maxb = 0;
+  int fat = -1;
+  const uint32_t ncr = L.h[FQ_NCR];
+  for (uint32_t r = 0; r < ncr; ++r)
+    for (uint32_t f = 0; f < 3; ++f)
+      if (L.h[f * kFqF + FQ_CR] == r) {
+        if (fat < 0) fat = static_cast<int>(f);
+        if (L.h[f * kFqF + FQ_BYTES] > maxb) {
+          maxb = L.h[f * kFqF + FQ_BYTES];
+          fat = static_cast<int>(f);
+        }
+      }
+  if (fat < 0) return;
+  const uint32_t threshold = maxb >> 1;
+  uint32_t len = 0, count = 0;
+  uint4 pk;
+  do {
+    if (!fq_pop(p, L, static_cast<uint32_t>(fat), pk)) break;
+    fq_drop(p, L, pk, c, now);
+    len += pk.w;
+  } while (++count < p.fq_batch && len < threshold);
+}
+// a message handed to the link at `now`: IPv4 fragments, each enqueued, then QueueDisc::Run
+template <typename Emit>
+__device__ inline void fq_send(const KP& p, FqLink& L, int64_t now, uint32_t sub, uint32_t bz, uint32_t bw24, int big,
+                               bool echo, Emit& emit, FqCount& c) {
+  uint32_t m = kInvalid;
+  for (uint32_t w = 0; w < p.cap_fqm / 32u && m == kInvalid; ++w) {
+    const uint32_t free_bits = ~L.h[FQ_MBM + w];
+    if (free_bits) m = w * 32u + static_cast<uint32_t>(__builtin_ctz(free_bits));
+  }
+  if (m == kInvalid) {
+    set_err(p, BCSIM_E_OVERFLOW);  // more messages in one link's disc than cap_fqm
+    return;
+  }
+  L.h[FQ_MBM + (m >> 5)] |= 1u << (m & 31u);
+  const uint32_t F = p.nfr[big];
+  L.msg[m] = make_uint4(sub, bz, bw24 | (static_cast<uint32_t>(big) << 24) | (echo ? kFqEcho : 0u), F);
+  const uint32_t now_lo = static_cast<uint32_t>(now), now_hi = static_cast<uint32_t>(static_cast<uint64_t>(now) >> 32);
+  for (uint32_t j = 0; j < F; ++j) {
+    const uint32_t cls = j ? 2u : echo ? 1u : 0u;
+    const uint32_t f = (L.map >> (2 * cls)) & 3u;
+    uint32_t* Fh = L.h + f * kFqF;
+    if (Fh[FQ_CR] == kInvalid) Fh[FQ_CR] = L.h[FQ_NCR]++;
+    if (Fh[FQ_ST] == 0) {
+      Fh[FQ_ST] = 1;
+      Fh[FQ_DEF] = p.fq_quantum;
+      fq_list_push(L.h, FQ_NNEW, FQ_NEWL, f);
+    }
+    const uint32_t n = Fh[FQ_N];
+    if (n == p.cap_fqp) {
+      set_err(p, BCSIM_E_OVERFLOW);  // more packets in one flow than cap_fqp
+      return;
+    }
+    uint32_t at = Fh[FQ_HEAD] + n;
+    if (at >= p.cap_fqp) at -= p.cap_fqp;
+    const uint32_t size = j + 1 == F ? p.ip_last[big] : p.ip_full[big];
+    L.pk[f * p.cap_fqp + at] = make_uint4(now_lo, now_hi, m | (j << 16), size);
+    fq_log(p, L, now, 1, L.pk[f * p.cap_fqp + at], f | (L.src << 8));
+    Fh[FQ_N] = n + 1;
+    Fh[FQ_BYTES] += size;
+    const uint32_t qp = L.h[FQ_QP] + 1;
+    L.h[FQ_QP] = qp;
+    if (qp > p.fq_limit) fq_overlimit(p, L, c, now);
+    fq_run(p, L, now, emit, c);
+  }
+}
+
 struct LinkShared {
   uint32_t n_bc, n_keep, n_list;
   uint32_t csum[8];  // block counters (wave sums, LDS atomics)
@@ -3441,10 +3813,10 @@ __device__ __attribute__((always_inline)) inline void link_finish(const KP& p, L
   }
 }
 
-// QM: DROPTAIL queue model; XR: node-partitioned run (records for other ranks).  Both are
-// template flags so the common case (infinite queues, one rank) carries none of their
-// registers through the per-edge loop.
-template <bool QM, bool XR>
+// QM: queue model (0 INFINITE, 1 DROPTAIL, 2 FQCODEL); XR: node-partitioned run (records for
+// other ranks).  Both are template parameters so the common case (infinite queues, one rank)
+// carries none of their registers through the per-edge loop.
+template <int QM, bool XR>
 __device__ __attribute__((always_inline)) inline void link_node(const KP* __restrict__ pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
                           int final_win) {
   const KP& p = *pk;
@@ -3462,7 +3834,9 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   const bool rx = p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
   // the implicit echoes, unless k_scan_pbft applied them in this window
   const bool rxe = rx && AT(p.eapp, g, p.NT) != t_lo;
-  if (n == 0 && !sl && !rxe) {
+  // (FQCODEL: a device-queue wake of a link with packets in its disc is due)
+  const bool fqw = QM == 2 && AT(p.node_onext, g, p.NT) < t_hi;
+  if (n == 0 && !sl && !rxe && !fqw) {
     if (rx && final_win && tidx() == 0) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
     return;
   }
@@ -3626,6 +4000,216 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   long long ovmin = LLONG_MAX;
   const long long cs = cell * p.L;
   const Rec* in_row = p.inbox + inbox_idx(p, ib, rep, e0);  // this node's row
+  if constexpr (QM == 2) {
+    // ---- 2'. FQCODEL: per edge, its ops in key order through the queue disc, the device-queue
+    // wakes in between and up to the window end; records are emitted when a message's last
+    // fragment enters the device queue (oracle fq_*) ----
+    long long fq_wmin = LLONG_MAX;
+    for (uint32_t le = tid; le < deg; le += blockDim.x) {
+      const uint32_t eb = n_list && le ? ecnt[le - 1] : 0u, ee = n_list ? ecnt[le] : 0u;
+      const uint32_t e = e0 + le;
+      const uint32_t s = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e, p.E);
+      uint64_t* lwp = p.link + link_index(p, rep, i, e0, le);
+      const uint64_t lw = *lwp;
+      Rec* ir = const_cast<Rec*>(in_row) + le;
+      Rec r0{};
+      if (rxe) r0 = ld_rec(ir);
+      uint4 w0 = make_uint4(0, 0, 0, 0), w1 = make_uint4(0, 0, 0, 0);
+      if (sl0) w0 = *eslot_at(p, ob, rep, e);
+      if (sl1) w1 = *eslot_at(p, obp, rep, e);
+      bool he = false;
+      RawOp eo = raw_zero();
+      if (rxe) {
+        const long long ta0 = cs + r0.t_off;
+        if (slot_live(r0.flags, cell_tag(p, cell)) && ta0 >= t_lo && ta0 < t_hi && p.echo) {
+          const int bg = (r0.flags & RF_BIG) ? 1 : 0;
+          const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
+          eo = raw_make(ta0, static_cast<uint32_t>(pin + p.tx_last[bg]), s, r0.sub,
+                        static_cast<uint8_t>(OP_ECHO | (bg ? (OPF_BIG << 2) : 0)));
+          he = true;
+          ++st_echo;
+        }
+      }
+      bool hr = false, hr2 = false;
+      RawOp ro = raw_zero(), ro2 = raw_zero();
+      if (sl0) {
+        ro = slot_op(p, w0, i, e);
+        hr = raw_t(ro) >= t_lo && raw_t(ro) < t_hi;
+        if (hr) ++st_ops;
+      }
+      if (sl1) {
+        ro2 = slot_op(p, w1, i, e);
+        hr2 = raw_t(ro2) >= t_lo && raw_t(ro2) < t_hi;
+        if (hr2) ++st_ops;
+      }
+      for (uint32_t a = eb + 1; a < ee; ++a) {  // insertion sort of this edge's ops (few)
+        const uint32_t x = eidx[a];
+        const Op ox = ops[x];
+        uint32_t b2 = a;
+        while (b2 > eb) {
+          const Op& oy = ops[eidx[b2 - 1]];
+          if (!op_key_less(ox, ox.sub, oy, oy.sub)) break;
+          eidx[b2] = eidx[b2 - 1];
+          --b2;
+        }
+        eidx[b2] = x;
+      }
+      ++st_edges;
+      uint32_t lc = static_cast<uint32_t>(lw & 0xFFFFu);
+      const int64_t pr = p.prop_const >= 0 ? p.prop_const : prop[le];
+      const uint32_t slot = p.mesh ? s * (p.N - 1) + (i < s ? i : i - 1) : AT(p.rev, e, p.E);
+      const uint32_t dg = rep * p.N + s;
+      FqLink FL = fq_link(p, eb0 + le, e);
+      FqCount fc{0, 0};
+      // a delivery: the record for the receiver's inbox slot / extras / overflow (as link_node)
+      auto emit = [&](uint32_t sub, uint32_t bz, uint32_t bw24, int big, int64_t end) {
+        const int64_t ta = end + pr;
+        const long long ca = ta / p.L;
+        const long long rel = ca - cell;
+        if (rel < 1) {
+          set_err(p, BCSIM_E_TIE);  // lookahead violated
+          return;
+        }
+        ++n_rec;
+        const uint32_t tof = static_cast<uint32_t>(ta - ca * p.L);
+        const uint32_t w3 = bw24 | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24) |
+            (emit_tag(cell / p.n_buckets, static_cast<uint32_t>(cell % p.n_buckets), ca - cell, p.n_buckets) << 27);
+        Rec r;
+        {
+          const uint4 rv = make_uint4(tof, sub, bz, w3);
+          __builtin_memcpy(&r, &rv, sizeof r);
+        }
+        const bool owner = lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
+        lc = static_cast<uint32_t>(ca) & 0xFFFFu;
+        if (XR) {
+          const uint32_t orank = p.owner[s];
+          if (orank != p.rank) {
+            XRec x;
+            x.r = r;
+            if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+            x.cell = ca;
+            x.slot = slot;
+            x.g = dg;
+            link_stage(p, L, g, B + 1 + orank, x);
+            return;
+          }
+        }
+        if (rel < static_cast<long long>(B)) {
+          const uint32_t bk = static_cast<uint32_t>(ca % B);
+          if (owner) {
+            st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), r);
+            if (p.mesh)
+              set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
+                                static_cast<uint64_t>(B) * p.R * p.n_tiles));
+          } else {
+            XRec x;
+            x.r = r;
+            x.cell = ca;
+            x.slot = slot;
+            x.g = dg;
+            link_stage(p, L, g, bk, x);
+          }
+          if (!(owner && p.mesh)) AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
+          atomicAdd(&L.lcnt[bk], 1u);
+          atomicMin(&L.lmin[bk], tof);
+        } else {
+          XRec x;
+          x.r = r;
+          if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+          x.cell = ca;
+          x.slot = slot;
+          x.g = dg;
+          link_stage(p, L, g, B, x);
+          if (ca < ovmin) ovmin = ca;
+        }
+      };
+      uint32_t a = eb, bi = 0;
+      for (;;) {
+        while (bi < n_bc && (op_flags(L.bco[bi]) & OPF_PAXOS) && le == 0) ++bi;
+        // the earliest of the five sources in key order; the op is assembled word by word
+        // (raw_sel), never by selecting RawOp values
+        int src = -1;
+        RawOp o = raw_zero();
+        uint32_t sub = 0;
+        if (bi < n_bc) {
+          raw_sel(o, ld_raw(&L.bco[bi]), true);
+          sub = raw_sub(o) + ((raw_flags(o) & OPF_PAXOS) ? le - 1 : le);
+          src = 1;
+        }
+        if (a < ee) {
+          const RawOp oa = ld_raw(&ops[eidx[a]]);
+          const bool c = src < 0 || raw_key_less(oa, raw_sub(oa), o, sub);
+          raw_sel(o, oa, c);
+          if (c) {
+            sub = raw_sub(oa);
+            src = 0;
+          }
+        }
+        {
+          const bool c = hr && (src < 0 || raw_key_less(ro, raw_sub(ro), o, sub));
+          raw_sel(o, ro, c);
+          if (c) {
+            sub = raw_sub(ro);
+            src = 2;
+          }
+        }
+        {
+          const bool c = hr2 && (src < 0 || raw_key_less(ro2, raw_sub(ro2), o, sub));
+          raw_sel(o, ro2, c);
+          if (c) {
+            sub = raw_sub(ro2);
+            src = 4;
+          }
+        }
+        {
+          const bool c = he && (src < 0 || raw_key_less(eo, raw_sub(eo), o, sub));
+          raw_sel(o, eo, c);
+          if (c) {
+            sub = raw_sub(eo);
+            src = 3;
+          }
+        }
+        if (src < 0) break;
+        if (src == 0)
+          ++a;
+        else if (src == 1)
+          ++bi;
+        else if (src == 2)
+          hr = false;
+        else if (src == 4)
+          hr2 = false;
+        else
+          he = false;
+        if ((src == 2 || src == 4) && raw_kind(o) == OP_SEND) ++sends;
+        const bool is_echo = src != 1 && raw_kind(o) == OP_ECHO;
+        const int big = (raw_flags(o) & OPF_BIG) ? 1 : 0;
+        const int64_t ot = raw_t(o);
+        fq_advance(p, FL, ot, emit, fc);  // wakes at <= ot come first
+        FL.src = static_cast<uint32_t>(src);
+        fq_send(p, FL, ot, sub, o.b.z, o.b.w & 0x00FFFFFFu, big, is_echo, emit, fc);
+      }
+      fq_advance(p, FL, t_hi - 1, emit, fc);
+      // the next wake with packets waiting in the disc is this node's next link event (a wake
+      // of an empty disc only resets flow states and is applied when the link is next used)
+      if (FL.h[FQ_STOP] && FL.h[FQ_QP]) {
+        const long long tw = FL.dev[FL.h[FQ_DH]];
+        if (tw < fq_wmin) fq_wmin = tw;
+      }
+      fdrop += fc.fdrop;
+      lost += fc.lost;
+      const int64_t bu = fq_ld64(FL.h + FQ_DEND);
+      if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+      *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
+    }
+    if (fq_wmin != LLONG_MAX) atomicMin(&L.omin, fq_wmin);
+    __syncthreads();
+    if (p.wgt && tid == 0) ph[2] = __builtin_amdgcn_s_memrealtime();
+    const LinkCounts lc8{static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends), static_cast<uint32_t>(n_rec),
+                         static_cast<uint32_t>(st_ops),  static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo),
+                         static_cast<uint32_t>(fdrop),   static_cast<uint32_t>(lost)};
+    link_finish(p, L, g, ops, n, t_hi, n_lists, ovmin, lc8, sl1 && final_win, rx && final_win, obp, fidx, wg_t0, ph, n_in);
+    return;
+  } else {
   for (uint32_t le = tid; le < deg; le += blockDim.x) {
     const uint32_t eb = n_list && le ? ecnt[le - 1] : 0u, ee = n_list ? ecnt[le] : 0u;
     const uint32_t e = e0 + le;
@@ -3892,10 +4476,11 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
                        static_cast<uint32_t>(st_ops),  static_cast<uint32_t>(st_edges), static_cast<uint32_t>(st_echo),
                        static_cast<uint32_t>(fdrop),   static_cast<uint32_t>(lost)};
   link_finish(p, L, g, ops, n, t_hi, n_lists, ovmin, lc8, sl1 && final_win, rx && final_win, obp, fidx, wg_t0, ph, n_in);
+  }  // QM != 2
 }
 
 // LOOP: a small grid walks list 3 (the nodes k_gossip_link left over)
-template <bool QM, bool XR, bool LOOP = false>
+template <int QM, bool XR, bool LOOP = false>
 __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                               long long t_hi, int final_win) {
   const KP& p = *pk;

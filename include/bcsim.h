@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define BCSIM_ABI_VERSION 1u
+#define BCSIM_ABI_VERSION 2u
 
 /* ---- enums ---------------------------------------------------------------- */
 /* protocol: replaces the compile-time edit of network-helper.cc:11,17,28 */
@@ -55,8 +55,12 @@ enum { BCSIM_TIME_ROUND = 0, BCSIM_TIME_TRUNC = 1 };
  * (pbft-node.cc:57-63), EXTENDED = same +48 offset without the 8-bit wrap */
 enum { BCSIM_ENC_EXTENDED = 0, BCSIM_ENC_COMPAT = 1 };
 /* Link queue model: INFINITE = unbounded FIFO; DROPTAIL = at most queue_dev_pkts +
- * queue_disc_pkts frames waiting per link, later frames dropped (fragment loss) */
-enum { BCSIM_QUEUE_INFINITE = 0, BCSIM_QUEUE_DROPTAIL = 1 };
+ * queue_disc_pkts frames waiting per link, later frames dropped (fragment loss);
+ * FQCODEL = ns-3 FqCoDelQueueDisc (the newer default root queue disc that
+ * address.Assign installs, blockchain-simulator.cc:41-42) in front of the
+ * queue_dev_pkts device queue with flow control: per-flow CoDel, DRR over the
+ * flows, overlimit drops from the fattest flow */
+enum { BCSIM_QUEUE_INFINITE = 0, BCSIM_QUEUE_DROPTAIL = 1, BCSIM_QUEUE_FQCODEL = 2 };
 enum { BCSIM_ENGINE_AUTO = 0, BCSIM_ENGINE_DENSE = 1, BCSIM_ENGINE_SPARSE = 2 };
 
 /* ---- status codes --------------------------------------------------------- */
@@ -135,6 +139,16 @@ typedef struct bcsim_config {
    * over the active nodes, hub-compact link state (Paxos on the full mesh); AUTO =
    * SPARSE when the dense per-edge state of all replicas exceeds ~96 GB */
   uint32_t engine_mode;        /* BCSIM_ENGINE_AUTO / _DENSE / _SPARSE */
+  /* FQCODEL queue disc (ns-3 FqCoDelQueueDisc / CoDelQueueDisc attributes; 0 = the
+   * ns-3 default in brackets) */
+  uint32_t fq_limit_pkts;      /* MaxSize [10240p] */
+  uint32_t fq_flows;           /* Flows [1024] */
+  uint32_t fq_quantum;         /* Quantum bytes [the device MTU] */
+  uint32_t fq_drop_batch;      /* DropBatchSize [64] */
+  int64_t  fq_target_ns;       /* CoDel Target [5 ms] */
+  int64_t  fq_interval_ns;     /* CoDel Interval [100 ms] */
+  uint32_t fq_min_bytes;       /* CoDel MinBytes [1500] */
+  uint32_t fq_perturbation;    /* Perturbation (hash salt) [0] */
   uint32_t reserved[2];
 } bcsim_config;
 

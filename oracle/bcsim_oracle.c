@@ -32,6 +32,7 @@
 #include "oracle.h"
 
 #include <limits.h>
+#include <stdio.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -173,7 +174,8 @@ static int64_t fsec_ns(float f, int mode) {
 
 /* ------------------------------------------------------------------------ */
 /* Events */
-enum { EV_START = 0, EV_STOP = 1, EV_TIMER = 2, EV_SEND = 3, EV_RECV = 4 };
+enum { EV_START = 0, EV_STOP = 1, EV_TIMER = 2, EV_SEND = 3, EV_RECV = 4,
+       EV_WAKE = 5 /* FQCODEL: a link's device queue has room again (t_sched -2) */ };
 /* timer kinds */
 enum {
   TM_PBFT_BLOCK = 0,
@@ -232,6 +234,45 @@ typedef struct {
   uint64_t frames; /* frames of the entries in the deque */
 } oqueue;
 
+/* FQCODEL link: ns-3 FqCoDelQueueDisc in front of the device queue.
+ * A packet is one IPv4 fragment of a message; flows are the <= 3 distinct flow indices
+ * of the link's traffic classes (first fragments of application sends, first fragments
+ * of echoes, later fragments of either: ports 0). */
+typedef struct {
+  int64_t enq;    /* enqueue time (CoDel timestamp) */
+  uint32_t msg;   /* index into the link's message table */
+  uint32_t size;  /* IPv4 packet bytes (QueueDiscItem::GetSize) */
+  uint32_t frame; /* fragment index */
+} fqpkt;
+typedef struct {
+  fqpkt* a;
+  uint32_t head, n, cap;
+  uint32_t bytes;
+  /* CoDelQueueDisc state (codel time units: ns >> 10) */
+  uint32_t first_above, drop_next, count, last_count;
+  uint16_t rec_inv_sqrt;
+  int dropping;
+  int status;  /* 0 inactive, 1 new, 2 old */
+  int32_t deficit;
+  int created; /* queue-disc class index (creation order), -1 = not created */
+} fqflow;
+typedef struct {
+  omsg m;
+  uint32_t sub, left;
+  int echo, lost, used;
+} fqmsg;
+typedef struct {
+  fqflow f[3];
+  int newl[3], oldl[3], n_new, n_old, n_created;
+  int64_t* dev; /* start times of the waiting device frames (ring) */
+  uint32_t dh, dn;
+  int64_t dev_end;
+  int stopped;
+  uint32_t qpkts;
+  fqmsg* msg;
+  uint32_t nmsg, capmsg;
+} fqlink;
+
 struct bcsim_oracle {
   bcsim_config cfg;
   uint32_t N;
@@ -249,6 +290,15 @@ struct bcsim_oracle {
   uint32_t K;            /* Paxos decrees (>= 1) */
   int64_t* busy;         /* per edge */
   oqueue* q;             /* per edge (DROPTAIL only) */
+  fqlink* fq;            /* per edge (FQCODEL only) */
+  uint8_t* fqmap;        /* per edge: flow slot of class app | echo << 2 | later frags << 4 */
+  uint32_t fq_limit, fq_quantum, fq_flows, fq_batch, fq_min_bytes, fq_devcap;
+  uint32_t fq_target_c, fq_interval_c; /* CoDel units (ns >> 10) */
+  uint32_t ip_full[2], ip_last[2];     /* IPv4 packet bytes of a full / the last fragment */
+  /* debug (ORACLE_FQLOG=<file>): FQCODEL link events, the engine's BCSIM_FQLOG format */
+  uint32_t* flog;
+  size_t nflog, capflog;
+  int64_t flog_t0, flog_t1;
   uint32_t nfr[2];       /* frames per message class (small, big) */
   int64_t tx_full[2];    /* time of a full (non-last) fragment frame */
   oheap heap;
@@ -551,6 +601,516 @@ static int64_t link_xmit(bcsim_oracle* o, uint32_t edge, int big,
   o->busy[edge] = end;
   *ts_last = end - o->tx_last[big];
   return end + o->prop[edge];
+}
+
+/* ------------------------------------------------------------------------ */
+/* FQCODEL.  ns-3 FqCoDelQueueDisc / CoDelQueueDisc restated
+ * (src/traffic-control/model/fq-codel-queue-disc.cc, codel-queue-disc.cc; the
+ * ns-3 version is not recorded, so this is PARITY UNPINNED like the rest of L1):
+ *   classify: Ipv4QueueDiscItem::Hash = Murmur3-32 (seed 0x8BADF00D) of
+ *             src | dst | proto 17 | sport | dport | perturbation (17 bytes, big
+ *             endian; ports 0 for a non-first fragment) mod Flows;
+ *   enqueue:  an inactive flow becomes new with deficit = Quantum; more than
+ *             MaxSize packets -> FqCoDelDrop (half the fattest flow's bytes, at
+ *             most DropBatchSize packets, from its head);
+ *   dequeue:  DRR over new then old flows; each flow is a CoDel queue (Target,
+ *             Interval, MinBytes, Newton-step inverse sqrt control law).
+ * The device queue (queue_dev_pkts) stops the disc when full and wakes it when
+ * its oldest waiting frame starts transmission (flow control); a wake at t runs
+ * before every other event at t. */
+
+/* sender of edge e (sender-major CSR) */
+static uint32_t edge_src(const bcsim_oracle* o, uint32_t e) {
+  uint32_t lo = 0, hi = o->N; /* row[lo] <= e < row[hi] */
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) / 2;
+    if (o->row[mid] <= e)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+/* MurmurHash3_x86_32 (Austin Appleby's public algorithm; ns-3 hash-murmur3.cc) */
+static uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+uint32_t oracle_murmur3_32(const uint8_t* data, uint32_t len, uint32_t seed) {
+  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+  uint32_t h = seed, nb = len / 4;
+  for (uint32_t i = 0; i < nb; ++i) {
+    uint32_t k = (uint32_t)data[4 * i] | ((uint32_t)data[4 * i + 1] << 8) |
+                 ((uint32_t)data[4 * i + 2] << 16) | ((uint32_t)data[4 * i + 3] << 24);
+    k *= c1;
+    k = rotl32(k, 15);
+    k *= c2;
+    h ^= k;
+    h = rotl32(h, 13);
+    h = h * 5 + 0xe6546b64u;
+  }
+  const uint8_t* t = data + 4 * nb;
+  uint32_t k = 0;
+  switch (len & 3) {
+    case 3: k ^= (uint32_t)t[2] << 16; /* fall through */
+    case 2: k ^= (uint32_t)t[1] << 8;  /* fall through */
+    case 1:
+      k ^= t[0];
+      k *= c1;
+      k = rotl32(k, 15);
+      k *= c2;
+      h ^= k;
+  }
+  h ^= len;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+/* Ipv4QueueDiscItem::Hash(perturbation) % flows for one packet class */
+uint32_t oracle_fq_flow(uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport,
+                        uint32_t perturbation, uint32_t flows) {
+  uint8_t b[17];
+  uint32_t w[2] = {src, dst};
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < 4; ++j) b[4 * k + j] = (uint8_t)(w[k] >> (24 - 8 * j));
+  b[8] = 17; /* UDP */
+  b[9] = (uint8_t)(sport >> 8);
+  b[10] = (uint8_t)sport;
+  b[11] = (uint8_t)(dport >> 8);
+  b[12] = (uint8_t)dport;
+  for (int j = 0; j < 4; ++j) b[13 + j] = (uint8_t)(perturbation >> (24 - 8 * j));
+  return oracle_murmur3_32(b, 17, 0x8BADF00Du) % flows;
+}
+
+/* UDP source port of node's client socket for its peer at row position idx: sockets are
+ * created in peer order at StartApplication and take ephemeral ports 49153, 49154, ...
+ * (pbft-node.cc:131-140, raft-node.cc:100-111); Paxos creates socket k for peer k+1
+ * (paxos-node.cc:110-119), so peer 0's replies use a socket made later (49153 + deg). */
+static uint32_t app_port(const bcsim_oracle* o, uint32_t node, uint32_t idx) {
+  uint32_t deg = o->row[node + 1] - o->row[node];
+  if (o->cfg.protocol == BCSIM_PAXOS) return idx >= 1 ? 49153 + idx - 1 : 49153 + deg;
+  return 49153 + idx;
+}
+
+/* per edge: the flow slots of its three packet classes.  Addresses: the k-th link of
+ * the mesh loop (blockchain-simulator.cc:34-51, i outer, j < i inner) gets network
+ * 1.0.0.0 + k*256 (address.NewNetwork), node i .1 and node j .2; a CSR graph numbers its
+ * links the same way (larger endpoint ascending, then smaller). */
+static int fq_build_map(bcsim_oracle* o) {
+  uint32_t E = o->row[o->N];
+  uint32_t* pk = (uint32_t*)malloc((E ? E : 1) * sizeof(uint32_t));
+  if (!pk) return BCSIM_E_NOMEM;
+  uint32_t k = 0;
+  for (uint32_t a = 0; a < o->N; ++a)
+    for (uint32_t e = o->row[a]; e < o->row[a + 1]; ++e)
+      if (o->col[e] < a) {
+        pk[e] = k;
+        pk[o->rev[e]] = k;
+        ++k;
+      }
+  for (uint32_t e = 0; e < E; ++e) {
+    uint32_t s = edge_src(o, e);
+    uint32_t d = o->col[e];
+    uint32_t net = 0x01000000u + (pk[e] << 8);
+    uint32_t src = net + (s > d ? 1u : 2u), dst = net + (d > s ? 1u : 2u);
+    uint32_t pa = app_port(o, s, e - o->row[s]);
+    uint32_t pe = app_port(o, d, o->rev[e] - o->row[d]);
+    uint32_t P = o->cfg.fq_perturbation;
+    uint32_t h[3] = {oracle_fq_flow(src, dst, pa, 7071, P, o->fq_flows),
+                     oracle_fq_flow(src, dst, 7071, pe, P, o->fq_flows),
+                     oracle_fq_flow(src, dst, 0, 0, P, o->fq_flows)};
+    uint32_t slot[3] = {0, 0, 0};
+    slot[1] = h[1] == h[0] ? 0 : 1;
+    slot[2] = h[2] == h[0] ? 0 : h[2] == h[1] ? slot[1] : slot[1] + 1;
+    o->fqmap[e] = (uint8_t)(slot[0] | slot[1] << 2 | slot[2] << 4);
+  }
+  free(pk);
+  return BCSIM_OK;
+}
+
+static void fq_reset(bcsim_oracle* o) {
+  for (uint32_t e = 0; e < o->row[o->N]; ++e) {
+    fqlink* l = &o->fq[e];
+    for (int f = 0; f < 3; ++f) {
+      fqflow* F = &l->f[f];
+      F->head = F->n = 0;
+      F->bytes = 0;
+      F->first_above = F->drop_next = F->count = F->last_count = 0;
+      F->rec_inv_sqrt = (uint16_t)(~0u >> 16);
+      F->dropping = 0;
+      F->status = 0;
+      F->deficit = 0;
+      F->created = -1;
+    }
+    l->n_new = l->n_old = l->n_created = 0;
+    l->dh = l->dn = 0;
+    l->dev_end = 0;
+    l->stopped = 0;
+    l->qpkts = 0;
+    for (uint32_t m = 0; m < l->nmsg; ++m) l->msg[m].used = 0;
+    l->nmsg = 0;
+  }
+}
+
+static void free_fq(bcsim_oracle* o) {
+  if (o->fq && o->row)
+    for (uint32_t e = 0; e < o->row[o->N]; ++e) {
+      for (int f = 0; f < 3; ++f) free(o->fq[e].f[f].a);
+      free(o->fq[e].dev);
+      free(o->fq[e].msg);
+    }
+  free(o->fq);
+  free(o->fqmap);
+  o->fq = NULL;
+  o->fqmap = NULL;
+}
+
+static int codel_before(uint32_t a, uint32_t b) { return (int32_t)(a - b) < 0; }
+static int codel_after(uint32_t a, uint32_t b) { return (int32_t)(a - b) > 0; }
+static int codel_after_eq(uint32_t a, uint32_t b) { return (int32_t)(a - b) >= 0; }
+static uint16_t codel_newton(uint16_t rec, uint32_t count) {
+  uint32_t invsqrt = ((uint32_t)rec) << 16;
+  uint32_t invsqrt2 = (uint32_t)(((uint64_t)invsqrt * invsqrt) >> 32);
+  uint64_t val = (3ull << 32) - ((uint64_t)count * invsqrt2);
+  val >>= 2;
+  val = (val * invsqrt) >> (32 - 2 + 1);
+  return (uint16_t)(val >> 16);
+}
+static uint32_t codel_control_law(uint32_t t, uint32_t interval, uint16_t rec) {
+  return t + (uint32_t)(((uint64_t)interval * ((uint32_t)rec << 16)) >> 32);
+}
+
+static void fq_free_msg(fqlink* l, uint32_t m) {
+  l->msg[m].used = 0;
+  while (l->nmsg && !l->msg[l->nmsg - 1].used) --l->nmsg;
+}
+
+/* kinds: 1 enqueue (x = flow slot), 2 into the device queue (x = frame start), 3 drop, 4 wake
+ * (x = packets in the disc) */
+static void fq_log(bcsim_oracle* o, const fqlink* l, uint32_t kind, const fqpkt* pk, int64_t x) {
+  if (!getenv("ORACLE_FQLOG") || o->now < o->flog_t0 || o->now >= o->flog_t1) return;
+  if (o->nflog == o->capflog) {
+    size_t nc = o->capflog ? 2 * o->capflog : 4096;
+    uint32_t* na = (uint32_t*)realloc(o->flog, nc * 8 * sizeof(uint32_t));
+    if (!na) return;
+    o->flog = na;
+    o->capflog = nc;
+  }
+  uint32_t* r = o->flog + 8 * o->nflog++;
+  uint32_t e = (uint32_t)(l - o->fq);
+  r[0] = (uint32_t)o->now;
+  r[1] = (uint32_t)((uint64_t)o->now >> 32);
+  r[2] = e;
+  r[3] = (kind << 24) | (pk ? pk->frame : 0);
+  r[4] = pk ? l->msg[pk->msg].sub : 0;
+  r[5] = (uint32_t)x;
+  r[6] = (uint32_t)((uint64_t)x >> 32);
+  r[7] = pk ? (uint32_t)l->msg[pk->msg].echo : 0;
+}
+
+/* a packet leaves the disc without transmission (CoDel or overlimit drop) */
+static void fq_drop(bcsim_oracle* o, fqlink* l, const fqpkt* pk) {
+  fq_log(o, l, 3, pk, 0);
+  o->cnt.frames_dropped++;
+  fqmsg* m = &l->msg[pk->msg];
+  if (!m->lost) {
+    m->lost = 1;
+    if (!m->echo) o->cnt.msgs_lost++;
+  }
+  if (--m->left == 0) fq_free_msg(l, pk->msg);
+}
+
+static int fq_pop(fqlink* l, fqflow* F, fqpkt* out) {
+  if (!F->n) return 0;
+  *out = F->a[F->head];
+  F->head = (F->head + 1) % F->cap;
+  --F->n;
+  F->bytes -= out->size;
+  --l->qpkts;
+  return 1;
+}
+
+/* CoDelQueueDisc::OkToDrop */
+static int codel_ok_to_drop(bcsim_oracle* o, fqflow* F, const fqpkt* pk, uint32_t now_c) {
+  if (!pk) {
+    F->first_above = 0;
+    return 0;
+  }
+  uint32_t soj = (uint32_t)((uint64_t)(o->now - pk->enq) >> 10);
+  if (codel_before(soj, o->fq_target_c) || F->bytes < o->fq_min_bytes) {
+    F->first_above = 0;
+    return 0;
+  }
+  if (F->first_above == 0) {
+    F->first_above = now_c + o->fq_interval_c;
+  } else if (codel_after(now_c, F->first_above)) {
+    return 1;
+  }
+  return 0;
+}
+
+/* CoDelQueueDisc::DoDequeue; returns 0 when the flow's queue is (or became) empty */
+static int codel_dequeue(bcsim_oracle* o, fqlink* l, fqflow* F, fqpkt* out) {
+  fqpkt pk;
+  if (!fq_pop(l, F, &pk)) {
+    F->dropping = 0;
+    return 0;
+  }
+  uint32_t now_c = (uint32_t)((uint64_t)o->now >> 10);
+  int have = 1;
+  int ok = codel_ok_to_drop(o, F, &pk, now_c);
+  if (F->dropping) {
+    if (!ok) {
+      F->dropping = 0;
+    } else if (codel_after_eq(now_c, F->drop_next)) {
+      while (F->dropping && codel_after_eq(now_c, F->drop_next)) {
+        ++F->count;
+        F->rec_inv_sqrt = codel_newton(F->rec_inv_sqrt, F->count);
+        fq_drop(o, l, &pk);
+        have = fq_pop(l, F, &pk);
+        if (!codel_ok_to_drop(o, F, have ? &pk : NULL, now_c))
+          F->dropping = 0;
+        else
+          F->drop_next = codel_control_law(F->drop_next, o->fq_interval_c, F->rec_inv_sqrt);
+      }
+    }
+  } else if (ok) {
+    fq_drop(o, l, &pk);
+    have = fq_pop(l, F, &pk);
+    (void)codel_ok_to_drop(o, F, have ? &pk : NULL, now_c);
+    F->dropping = 1;
+    int32_t delta = (int32_t)(F->count - F->last_count);
+    if (delta > 1 && codel_before(now_c - F->drop_next, 16 * o->fq_interval_c)) {
+      F->count = (uint32_t)delta;
+      F->rec_inv_sqrt = codel_newton(F->rec_inv_sqrt, F->count);
+    } else {
+      F->count = 1;
+      F->rec_inv_sqrt = (uint16_t)(~0u >> 16);
+    }
+    F->last_count = F->count;
+    F->drop_next = codel_control_law(now_c, o->fq_interval_c, F->rec_inv_sqrt);
+  }
+  if (have) *out = pk;
+  return have;
+}
+
+static void list_pop_front(int* a, int* n) {
+  for (int k = 1; k < *n; ++k) a[k - 1] = a[k];
+  --*n;
+}
+
+/* FqCoDelQueueDisc::DoDequeue (DRR over new, then old flows) */
+static int fq_dequeue(bcsim_oracle* o, fqlink* l, fqpkt* out) {
+  for (;;) {
+    int f = -1;
+    while (f < 0 && l->n_new) {
+      int c = l->newl[0];
+      if (l->f[c].deficit <= 0) {
+        l->f[c].deficit += (int32_t)o->fq_quantum;
+        l->f[c].status = 2;
+        l->oldl[l->n_old++] = c;
+        list_pop_front(l->newl, &l->n_new);
+      } else {
+        f = c;
+      }
+    }
+    while (f < 0 && l->n_old) {
+      int c = l->oldl[0];
+      if (l->f[c].deficit <= 0) {
+        l->f[c].deficit += (int32_t)o->fq_quantum;
+        list_pop_front(l->oldl, &l->n_old);
+        l->oldl[l->n_old++] = c;
+      } else {
+        f = c;
+      }
+    }
+    if (f < 0) return 0;
+    fqflow* F = &l->f[f];
+    if (codel_dequeue(o, l, F, out)) {
+      F->deficit -= (int32_t)out->size;
+      return 1;
+    }
+    if (F->status == 1 && l->n_old) { /* (a new flow is at the head of the new list) */
+      F->status = 2;
+      l->oldl[l->n_old++] = f;
+      list_pop_front(l->newl, &l->n_new);
+    } else if (F->status == 1) {
+      F->status = 0;
+      list_pop_front(l->newl, &l->n_new);
+    } else {
+      F->status = 0;
+      list_pop_front(l->oldl, &l->n_old);
+    }
+  }
+}
+
+static void fq_schedule_wake(bcsim_oracle* o, uint32_t edge, int64_t t) {
+  oev w;
+  memset(&w, 0, sizeof w);
+  w.t = t;
+  w.ts = -2;
+  w.origin = w.target = edge_src(o, edge);
+  w.kind = EV_WAKE;
+  w.aux = edge;
+  int rc = heap_push(&o->heap, &w);
+  if (rc) set_err(o, rc);
+}
+
+/* frames of the device queue that started transmission by now are no longer waiting */
+static void fq_dev_settle(bcsim_oracle* o, fqlink* l) {
+  while (l->dn && l->dev[l->dh] <= o->now) {
+    l->dh = (l->dh + 1) % o->fq_devcap;
+    --l->dn;
+  }
+}
+
+/* a packet from the disc into the device queue (PointToPointNetDevice::Send) */
+static void fq_dev_push(bcsim_oracle* o, uint32_t edge, fqlink* l, const fqpkt* pk) {
+  fqmsg* m = &l->msg[pk->msg];
+  int big = m->m.big;
+  int64_t tx = pk->frame + 1 == o->nfr[big] ? o->tx_last[big] : o->tx_full[big];
+  int64_t start = l->dev_end > o->now ? l->dev_end : o->now;
+  int64_t end = start + tx;
+  fq_log(o, l, 2, pk, start);
+  l->dev_end = end;
+  fq_dev_settle(o, l);
+  if (start > o->now) {
+    l->dev[(l->dh + l->dn) % o->fq_devcap] = start;
+    ++l->dn;
+    if (l->dn == o->fq_devcap) { /* the queue cannot take another packet: stop the disc */
+      l->stopped = 1;
+      fq_schedule_wake(o, edge, l->dev[l->dh]);
+    }
+  }
+  if (--m->left) return;
+  if (!m->lost && !m->echo) { /* the message's last fragment is on its way: delivery */
+    oev r;
+    memset(&r, 0, sizeof r);
+    r.t = end + o->prop[edge];
+    r.ts = end - o->tx_last[big]; /* t - prop - last-fragment frame time */
+    r.origin = edge_src(o, edge);
+    r.sub = m->sub;
+    r.target = o->col[edge];
+    r.kind = EV_RECV;
+    r.aux = edge;
+    r.m = m->m;
+    int rc = heap_push(&o->heap, &r);
+    if (rc) set_err(o, rc);
+  }
+  fq_free_msg(l, pk->msg);
+}
+
+/* QueueDisc::Run: dequeue into the device while it is not stopped */
+static void fq_run(bcsim_oracle* o, uint32_t edge, fqlink* l) {
+  fqpkt pk;
+  while (!l->stopped && fq_dequeue(o, l, &pk)) fq_dev_push(o, edge, l, &pk);
+}
+
+/* the device queue wakes the disc (its oldest waiting frame starts now) */
+static void fq_wake(bcsim_oracle* o, uint32_t edge) {
+  fqlink* l = &o->fq[edge];
+  fq_log(o, l, 4, NULL, l->qpkts);
+  fq_dev_settle(o, l);
+  l->stopped = 0;
+  fq_run(o, edge, l);
+}
+
+/* FqCoDelQueueDisc::FqCoDelDrop */
+static void fq_overlimit(bcsim_oracle* o, fqlink* l) {
+  uint32_t maxb = 0;
+  int fat = -1; /* the first class (creation order) with the most bytes; class 0 by default */
+  for (int r = 0; r < l->n_created; ++r)
+    for (int f = 0; f < 3; ++f)
+      if (l->f[f].created == r) {
+        if (fat < 0) fat = f;
+        if (l->f[f].bytes > maxb) {
+          maxb = l->f[f].bytes;
+          fat = f;
+        }
+      }
+  if (fat < 0) return;
+  uint32_t threshold = maxb >> 1, len = 0, count = 0;
+  fqpkt pk;
+  do {
+    if (!fq_pop(l, &l->f[fat], &pk)) break;
+    fq_drop(o, l, &pk);
+    len += pk.size;
+  } while (++count < o->fq_batch && len < threshold);
+}
+
+static int fq_push(bcsim_oracle* o, fqflow* F, const fqpkt* pk) {
+  if (F->n == F->cap) {
+    uint32_t nc = F->cap ? 2 * F->cap : 64;
+    fqpkt* na = (fqpkt*)malloc(nc * sizeof(fqpkt));
+    if (!na) return BCSIM_E_NOMEM;
+    for (uint32_t i = 0; i < F->n; ++i) na[i] = F->a[(F->head + i) % F->cap];
+    free(F->a);
+    F->a = na;
+    F->head = 0;
+    F->cap = nc;
+  }
+  F->a[(F->head + F->n) % F->cap] = *pk;
+  ++F->n;
+  F->bytes += pk->size;
+  return BCSIM_OK;
+}
+
+/* a message (application send or echo) handed to the link at o->now: IPv4 fragments
+ * it and hands each fragment to the traffic-control layer (enqueue, then Run) */
+static void fq_send(bcsim_oracle* o, uint32_t edge, const omsg* msg, uint32_t sub, int echo) {
+  fqlink* l = &o->fq[edge];
+  uint32_t mi = 0;
+  while (mi < l->nmsg && l->msg[mi].used) ++mi;
+  if (mi == l->capmsg) {
+    uint32_t nc = l->capmsg ? 2 * l->capmsg : 16;
+    fqmsg* na = (fqmsg*)realloc(l->msg, nc * sizeof(fqmsg));
+    if (!na) {
+      set_err(o, BCSIM_E_NOMEM);
+      return;
+    }
+    for (uint32_t k = l->capmsg; k < nc; ++k) na[k].used = 0;
+    l->msg = na;
+    l->capmsg = nc;
+  }
+  if (mi == l->nmsg) ++l->nmsg;
+  fqmsg* m = &l->msg[mi];
+  m->m = *msg;
+  m->sub = sub;
+  m->echo = echo;
+  m->lost = 0;
+  m->used = 1;
+  int big = msg->big;
+  uint32_t F = o->nfr[big];
+  m->left = F;
+  uint8_t map = o->fqmap[edge];
+  for (uint32_t j = 0; j < F; ++j) {
+    int cls = j ? 2 : echo ? 1 : 0;
+    int f = (map >> (2 * cls)) & 3;
+    fqflow* fl = &l->f[f];
+    fqpkt pk;
+    pk.enq = o->now;
+    pk.msg = mi;
+    pk.size = j + 1 == F ? o->ip_last[big] : o->ip_full[big];
+    pk.frame = j;
+    if (fl->created < 0) fl->created = l->n_created++;
+    if (fl->status == 0) {
+      fl->status = 1;
+      fl->deficit = (int32_t)o->fq_quantum;
+      l->newl[l->n_new++] = f;
+    }
+    int rc = fq_push(o, fl, &pk);
+    if (rc) {
+      set_err(o, rc);
+      return;
+    }
+    fq_log(o, l, 1, &pk, f);
+    ++l->qpkts;
+    if (l->qpkts > o->fq_limit) fq_overlimit(o, l);
+    fq_run(o, edge, l);
+    m = &l->msg[mi]; /* (the table is not reallocated meanwhile; kept for clarity) */
+  }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1043,6 +1603,10 @@ static void exec_event(bcsim_oracle* o, const oev* e) {
         o->cnt.dropped++;
         break;
       }
+      if (o->cfg.queue_model == BCSIM_QUEUE_FQCODEL) { /* delivered when its last fragment leaves the disc */
+        fq_send(o, e->aux, &e->m, e->sub, 0);
+        break;
+      }
       oev r;
       memset(&r, 0, sizeof r);
       int64_t tsl = 0;
@@ -1069,7 +1633,10 @@ static void exec_event(bcsim_oracle* o, const oev* e) {
       o->cnt.delivered_total++;
       if (o->cfg.echo) { /* socket->SendTo(packet, 0, from) :175 */
         int64_t tsl;
-        (void)link_xmit(o, o->rev[e->aux], e->m.big, &tsl);
+        if (o->cfg.queue_model == BCSIM_QUEUE_FQCODEL)
+          fq_send(o, o->rev[e->aux], &e->m, 0, 1);
+        else
+          (void)link_xmit(o, o->rev[e->aux], e->m.big, &tsl);
         o->cnt.echoes++;
       }
       if (o->cfg.protocol == BCSIM_PBFT)
@@ -1082,6 +1649,9 @@ static void exec_event(bcsim_oracle* o, const oev* e) {
         paxos_recv(o, e, i);
       break;
     }
+    case EV_WAKE: /* link-internal: not a protocol event */
+      fq_wake(o, e->aux);
+      break;
   }
 }
 
@@ -1134,6 +1704,7 @@ int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
   if (o->started) return BCSIM_E_STATE;
   uint32_t E = row_ptr[n];
   free_queues(o);
+  free_fq(o);
   free(o->row);
   free(o->col);
   free(o->rev);
@@ -1175,13 +1746,25 @@ int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
       o->rev[e] = hit->e;
     }
   free(t);
+  if (o->cfg.queue_model == BCSIM_QUEUE_FQCODEL) {
+    o->fq = (fqlink*)calloc(E ? E : 1, sizeof(fqlink));
+    o->fqmap = (uint8_t*)calloc(E ? E : 1, 1);
+    if (!o->fq || !o->fqmap) return BCSIM_E_NOMEM;
+    for (uint32_t e = 0; e < E; ++e) {
+      o->fq[e].dev = (int64_t*)malloc(o->fq_devcap * sizeof(int64_t));
+      if (!o->fq[e].dev) return BCSIM_E_NOMEM;
+    }
+    int rc = fq_build_map(o);
+    if (rc) return rc;
+  }
   o->topo_set = 1;
   return BCSIM_OK;
 }
 
 int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
   if (!cfg || !out) return BCSIM_E_INVAL;
-  if (cfg->n_nodes < 2 || cfg->protocol > BCSIM_GOSSIP || cfg->link_rate_bps == 0)
+  if (cfg->n_nodes < 2 || cfg->protocol > BCSIM_GOSSIP || cfg->link_rate_bps == 0 ||
+      cfg->queue_model > BCSIM_QUEUE_FQCODEL)
     return BCSIM_E_INVAL;
   bcsim_oracle* o = (bcsim_oracle*)calloc(1, sizeof(bcsim_oracle));
   if (!o) return BCSIM_E_NOMEM;
@@ -1225,6 +1808,29 @@ int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
                 &o->tx_tot[1], &o->tx_last[1], &o->nfr[1], NULL);
   for (int k = 0; k < 2; ++k) /* full fragment frame: (mtu - 20) & ~7 IP payload + 22 */
     o->tx_full[k] = o->nfr[k] > 1 ? (o->tx_tot[k] - o->tx_last[k]) / (o->nfr[k] - 1) : o->tx_tot[k];
+  { /* IPv4 packet bytes per fragment (QueueDiscItem::GetSize) */
+    uint32_t frag = (o->cfg.mtu - 20) & ~7u, bb[2] = {o->small_bytes, o->big_bytes};
+    for (int k = 0; k < 2; ++k) {
+      o->ip_full[k] = frag + 20;
+      o->ip_last[k] = bb[k] + 8 - frag * (o->nfr[k] - 1) + 20;
+    }
+  }
+  if (o->cfg.queue_model == BCSIM_QUEUE_FQCODEL) { /* ns-3 attribute defaults for 0 */
+    o->fq_limit = o->cfg.fq_limit_pkts ? o->cfg.fq_limit_pkts : 10240;
+    o->fq_flows = o->cfg.fq_flows ? o->cfg.fq_flows : 1024;
+    o->fq_quantum = o->cfg.fq_quantum ? o->cfg.fq_quantum : o->cfg.mtu;
+    o->fq_batch = o->cfg.fq_drop_batch ? o->cfg.fq_drop_batch : 64;
+    o->fq_min_bytes = o->cfg.fq_min_bytes ? o->cfg.fq_min_bytes : 1500;
+    o->fq_target_c = (uint32_t)((uint64_t)(o->cfg.fq_target_ns > 0 ? o->cfg.fq_target_ns : 5000000) >> 10);
+    o->fq_interval_c = (uint32_t)((uint64_t)(o->cfg.fq_interval_ns > 0 ? o->cfg.fq_interval_ns : 100000000) >> 10);
+    o->fq_devcap = o->cfg.queue_dev_pkts;
+    o->flog_t0 = getenv("BCSIM_FQLOG_T0") ? atoll(getenv("BCSIM_FQLOG_T0")) : 0;
+    o->flog_t1 = getenv("BCSIM_FQLOG_T1") ? atoll(getenv("BCSIM_FQLOG_T1")) : INT64_MAX;
+    if (o->fq_devcap == 0) {
+      bcsim_oracle_destroy(o);
+      return BCSIM_E_INVAL;
+    }
+  }
   o->pbft_period = fsec_ns(o->cfg.pbft_timeout_s, mode);
   o->raft_hb = fsec_ns(o->cfg.raft_heartbeat_s, mode);
   for (int k = 0; k < 3; ++k) {
@@ -1288,6 +1894,7 @@ static void reset_replica(bcsim_oracle* o, uint32_t rep) {
     o->q[e].n = 0;
     o->q[e].frames = 0;
   }
+  if (o->fq) fq_reset(o);
   o->heap.n = 0;
   glibc_seed(&o->grng, (uint32_t)(o->cfg.seed + rep));
   o->g_v = 1;
@@ -1355,6 +1962,13 @@ int bcsim_oracle_run(bcsim_oracle* o, int64_t t_until_ns) {
     break;
   }
   o->now = lim;
+  if (getenv("ORACLE_FQLOG")) { /* debug: the FQCODEL link events so far */
+    FILE* f = fopen(getenv("ORACLE_FQLOG"), "wb");
+    if (f) {
+      fwrite(o->flog, 32, o->nflog, f);
+      fclose(f);
+    }
+  }
   return BCSIM_OK;
 }
 
@@ -1410,6 +2024,7 @@ int bcsim_oracle_destroy(bcsim_oracle* o) {
   free(o->gseen);
   free(o->px);
   free_queues(o);
+  free_fq(o);
   free(o->row);
   free(o->col);
   free(o->rev);
@@ -1417,6 +2032,7 @@ int bcsim_oracle_destroy(bcsim_oracle* o) {
   free(o->busy);
   free(o->heap.a);
   free(o->tr);
+  free(o->flog);
   free(o->rep_now);
   free(o);
   return BCSIM_OK;

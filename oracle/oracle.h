@@ -42,6 +42,11 @@ int64_t oracle_tx_ns(uint32_t wire_bytes, uint64_t rate_bps, int mode);
 void    oracle_msg_tx(uint32_t payload, uint32_t mtu, uint64_t rate_bps,
                       int mode, int64_t* tx_total, int64_t* tx_last,
                       uint32_t* n_frames, uint32_t* wire_total);
+/* FQCODEL flow classification: MurmurHash3_x86_32 and
+ * Ipv4QueueDiscItem::Hash(perturbation) % flows */
+uint32_t oracle_murmur3_32(const uint8_t* data, uint32_t len, uint32_t seed);
+uint32_t oracle_fq_flow(uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport,
+                        uint32_t perturbation, uint32_t flows);
 uint32_t oracle_ctr_rand(uint64_t seed, uint32_t replica, uint32_t node,
                          uint64_t k);
 

@@ -110,6 +110,35 @@ def cases():
     }
 
 
+def fq_cases():
+    """FQCODEL queue-disc cases (dense layout only): the saturated 50 KB PBFT
+    links drop by CoDel after ~100 ms above target; a small MaxSize exercises the overlimit
+    drop of the fattest flow, two hash buckets force flow collisions, a short interval a
+    different control-law cadence."""
+    P, R, X, GS = _abi.PBFT, _abi.RAFT, _abi.PAXOS, _abi.GOSSIP
+    F, J, K = _abi.DELAY_FIXED, _abi.DELAY_RANDOM, _abi.RNG_COUNTER
+    Q = _abi.QUEUE_FQCODEL
+    return {
+        "pbft16_fq_100": _cfg(P, 16, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=100, queue_model=Q,
+                              t_end_ns=9_000_000_000),
+        "pbft8_fq_40": _cfg(P, 8, delay_mode=F, app_delay_ns=3_000_000, queue_model=Q),
+        "pbft16_fq_limit64": _cfg(P, 16, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=60, queue_model=Q,
+                                  fq_limit_pkts=64, fq_drop_batch=8, t_end_ns=4_000_000_000),
+        "pbft16_fq_flows2": _cfg(P, 16, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=60, queue_model=Q,
+                                 fq_flows=2, fq_target_ns=2_000_000, fq_interval_ns=30_000_000,
+                                 queue_dev_pkts=30, t_end_ns=4_000_000_000),
+        "pbft12_fq_jitter": _cfg(P, 12, delay_mode=J, rng_mode=K, seed=7, pbft_rounds=40, queue_model=Q),
+        "pbft12_fq_hetero": _cfg(P, 12, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=30, queue_model=Q,
+                                 queue_dev_pkts=40),
+        "gossip64_d4_fq": _cfg(GS, 64, delay_mode=F, app_delay_ns=3_000_000, pbft_rounds=30, stop_ns=-1,
+                               pbft_block_bytes=20000, queue_model=Q, queue_dev_pkts=20, fq_quantum=600),
+        "raft16_fq": _cfg(R, 16, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=4_000_000_000, queue_model=Q,
+                          queue_dev_pkts=10),
+        "paxos32_fq_jitter": _cfg(X, 32, delay_mode=J, rng_mode=K, seed=3, paxos_decrees=3, queue_model=Q,
+                                  queue_dev_pkts=2),
+    }
+
+
 def fullsize_cases():
     """BASELINE configs at full size (too big for the oracle): the bench configurations
     themselves, compared between engine runs (partitioned vs single, tests/test_partition.py)
@@ -125,6 +154,7 @@ def fullsize_cases():
 
 def any_case(name):
     c = cases()
+    c.update(fq_cases())
     return c[name] if name in c else fullsize_cases()[name]
 
 
@@ -137,6 +167,7 @@ TOPOLOGY = {
     "gossip64_d4_droptail": (64, 4, 1),
     "raft48_d6_ctr": (48, 6, 8),
     "gossip64_d4_b2": (64, 4, 1),
+    "gossip64_d4_fq": (64, 4, 1),
 }
 
 
@@ -145,6 +176,7 @@ TOPOLOGY_PROP = {
     "pbft12_hetero_prop": (3_000_000, 700_000),
     "raft24_hetero_prop": (2_500_000, 1_500_000),
     "gossip96_d6_hetero_prop": (3_000_000, 2_000_000),
+    "pbft12_fq_hetero": (3_000_000, 700_000),
 }
 TOPOLOGY["gossip96_d6_hetero_prop"] = (96, 6, 11)
 TOPOLOGY["c5_gossip_r3"] = (65536, 8, 1)

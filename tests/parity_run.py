@@ -1,7 +1,9 @@
 import sys, time, traceback
 import os; R=os.path.dirname(os.path.dirname(os.path.abspath(__file__))); sys.path[:0]=[R, os.path.join(R,'tests'), os.path.join(R,'blockchain-simulator_amd')]
 import oracle, bcsim
-from parity_cases import cases, compare, topology
+from parity_cases import cases as _cases, fq_cases, compare, topology
+def cases():
+    c = _cases(); c.update(fq_cases()); return c
 ok = 0
 sel = sys.argv[1:]
 for name, cfg in sorted(cases().items()):

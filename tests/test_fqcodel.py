@@ -1,0 +1,105 @@
+"""FQCODEL queue disc: ns-3 FqCoDelQueueDisc in front of the
+PointToPointNetDevice queue, the version-dependent default root queue disc that
+`address.Assign` installs (/root/reference/blockchain-simulator.cc:41-42).
+
+CPU: the Murmur3 restatement against the published MurmurHash3_x86_32 vectors; the model is
+FIFO-identical to the INFINITE queue on unsaturated links; message conservation.
+GPU: the HIP engine equals the oracle bit for bit on every FQCODEL case.
+ns-3 itself is absent, so the model beyond the hash is parity unpinned."""
+import ctypes as C
+import copy
+
+import pytest
+
+import oracle
+from bcsim import _abi
+from parity_cases import cases, compare, fq_cases, topology
+
+FQ = fq_cases()
+
+
+def test_murmur3_vectors():
+    lib = oracle.lib()
+    lib.oracle_murmur3_32.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32]
+    lib.oracle_murmur3_32.restype = C.c_uint32
+    # MurmurHash3_x86_32 reference vectors (data, seed, hash)
+    for data, seed, want in [(b"", 0, 0), (b"", 1, 0x514E28B7), (b"", 0xFFFFFFFF, 0x81F16F39),
+                             (b"\0\0\0\0", 0, 0x2362F9DE), (b"aaaa", 0x9747B28C, 0x5A97808A),
+                             (b"Hello, world!", 0x9747B28C, 0x24884CBA),
+                             (b"The quick brown fox jumps over the lazy dog", 0x9747B28C, 0x2FA826CD)]:
+        assert lib.oracle_murmur3_32(data, len(data), seed) == want
+
+
+def test_flow_hash_spreads_classes():
+    """The three packet classes of a link (app / echo first fragments, later fragments) hash to
+    flow indices in [0, Flows); over the n=16 mesh most links keep them apart."""
+    lib = oracle.lib()
+    lib.oracle_fq_flow.argtypes = [C.c_uint32] * 6
+    lib.oracle_fq_flow.restype = C.c_uint32
+    n, k, apart = 16, 0, 0
+    for i in range(1, n):
+        for j in range(i):
+            net = 0x01000000 + (k << 8)
+            a, b = net + 1, net + 2
+            h = {lib.oracle_fq_flow(a, b, 49153 + j, 7071, 0, 1024), lib.oracle_fq_flow(a, b, 7071, 49153 + i - 1, 0, 1024),
+                 lib.oracle_fq_flow(a, b, 0, 0, 0, 1024)}
+            assert all(x < 1024 for x in h)
+            apart += len(h) == 3
+            k += 1
+    assert apart >= k - 3
+    # Flows = 1: one queue per link
+    assert lib.oracle_fq_flow(1, 2, 3, 4, 0, 1) == 0
+
+
+@pytest.mark.parametrize("name", ["pbft16_small_blocks", "raft64_fixed", "paxos32_jitter_ctr", "gossip64_d4_fixed"])
+def test_unsaturated_equals_fifo(name):
+    """Without a standing device-queue backlog the disc never holds a packet across a wake:
+    every message leaves in FIFO order, so the run equals the INFINITE queue."""
+    cfg = cases()[name]
+    fq = copy.copy(cfg)
+    fq.queue_model = _abi.QUEUE_FQCODEL
+    a = oracle.run(cfg, topology=topology(name))
+    b = oracle.run(fq, topology=topology(name))
+    assert b[1]["frames_dropped"] == 0
+    assert compare(a, b) is None
+
+
+@pytest.mark.parametrize("name", sorted(FQ))
+def test_oracle_conservation(name):
+    """Every application send is delivered, lost (a dropped fragment) or still in flight at the
+    end; drops happen on the saturated cases and each lost message dropped >= 1 fragment."""
+    tr, cnt, st = oracle.run(FQ[name], topology=topology(name))[:3]
+    assert st["error"] == 0
+    assert cnt["delivered_total"] + cnt["msgs_lost"] + cnt["dropped"] <= cnt["sends"]
+    assert cnt["msgs_lost"] <= cnt["frames_dropped"]
+    if name.startswith("pbft16") or name.startswith("gossip"):
+        assert cnt["frames_dropped"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(FQ))
+def test_engine_matches_oracle_fqcodel(name, engine_lib):
+    import bcsim
+    cfg = FQ[name]
+    topo = topology(name)
+    ref = oracle.run(cfg, topology=topo)
+    got = bcsim.run(cfg, topology=topo)
+    assert ref[2]["error"] == 0
+    diff = compare(ref, got)
+    assert diff is None, f"{name}: {diff}"
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_fqcodel_partitioned_p2_matches_oracle(engine_lib):
+    """Node-partitioned at P=2 (host transport): the queue disc lives with the sender's edges, so
+    records emitted at a device-queue wake for a receiver on the other rank are shipped like any
+    other; the merged run equals the oracle."""
+    import partition_run
+    names = ["pbft16_fq_100", "pbft12_fq_jitter", "gossip64_d4_fq"]
+    res = partition_run.run(2, names, transport="host", timeout=240)
+    for name in names:
+        merged, err = res[name]
+        assert err is None, f"{name}: {err}"
+        d = compare(oracle.run(FQ[name], topology=topology(name)), merged)
+        assert d is None, f"{name} P=2: {d}"

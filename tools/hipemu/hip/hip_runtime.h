@@ -102,6 +102,12 @@ inline unsigned long long __ballot(int pred) {
   return m;
 }
 inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+inline int __popc(unsigned x) { return __builtin_popcount(x); }
+// lane-exchange / ordering builtins: every lane of the wave must reach them together
+template <typename T>
+inline T __builtin_amdgcn_readlane(T v, int lane) { return __shfl(v, lane); }
+inline void __builtin_amdgcn_wave_barrier() { hipemu_wsync(); }
+#define __builtin_amdgcn_fence(...) std::atomic_thread_fence(std::memory_order_seq_cst)
 inline unsigned long long __builtin_amdgcn_s_memrealtime() {  // 100 MHz
   return static_cast<unsigned long long>(std::chrono::steady_clock::now().time_since_epoch().count() / 10);
 }
@@ -174,6 +180,8 @@ hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t
 hipError_t hipMemset(void*, int, size_t);
 hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t);
 hipError_t hipEventCreate(hipEvent_t*);
+enum { hipEventDisableSystemFence = 0x20000000 };
+inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { return hipEventCreate(e); }
 hipError_t hipEventDestroy(hipEvent_t);
 hipError_t hipEventRecord(hipEvent_t, hipStream_t);
 hipError_t hipEventElapsedTime(float*, hipEvent_t, hipEvent_t);
