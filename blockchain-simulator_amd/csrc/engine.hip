@@ -229,7 +229,7 @@ struct KP {
 
 constexpr int kMaxRanks = 16;
 constexpr uint32_t kDescWords = 128;  // descriptor bitmaps: in-slots of degree <= 4096
-constexpr uint32_t kEDesc = 4;        // pending echo descriptors per node
+constexpr uint32_t kEDesc = 2;        // pending echo descriptors per node (LDS: k_link_mesh keeps 4 WGs/CU)
 // sflag bits of a reply descriptor of the arrival cell (bits 0..3: reply slots due in cell + k)
 constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in this cell / the next
 
@@ -4564,11 +4564,12 @@ __device__ inline void xr_ship(const KP& p, LinkShared& L, uint32_t g, uint32_t 
 // k_link_mesh's view of the node's descriptors (k_scan_pbft): the live reply descriptors of
 // this arrival cell (0) and the previous one (1) with their bitmaps and per-word rank
 // prefixes, and the pending echo descriptors with theirs
+// (2.6 KB: with the 32 KB of parked link words and LinkShared a 256-lane k_link_mesh workgroup
+// stays under 40 KB of LDS, four per CU; a 4.7 KB layout cost 18 % of k_link_mesh time)
 struct MeshDesc {
   uint32_t rb[2][kDescWords];
-  uint32_t rp[2][kDescWords];
+  uint16_t rp[2][kDescWords];  // (ranks < 4096)
   uint32_t eb[kEDesc][kDescWords];
-  uint32_t eall[kDescWords];  // union of the pending echo bitmaps
   long long et[kEDesc];
   uint32_t ebig[kEDesc];
 };
@@ -4606,8 +4607,8 @@ __device__ inline void mesh_desc_load(const KP& p, MeshDesc& D, uint32_t g, uint
         const uint32_t v = __shfl_up(in, off, 64);
         if (tid >= static_cast<uint32_t>(off)) in += v;
       }
-      if (k < dw) D.rp[h][k] = in - a - b;
-      if (k + 1 < dw) D.rp[h][k + 1] = in - b;
+      if (k < dw) D.rp[h][k] = static_cast<uint16_t>(in - a - b);
+      if (k + 1 < dw) D.rp[h][k + 1] = static_cast<uint16_t>(in - b);
     }
   }
   __syncthreads();
@@ -4812,11 +4813,6 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
       }
     }
     if (ne_w) {  // the pending echo descriptors, oldest first, onto the parked link words
-      for (uint32_t w = tid; w < p.dwords; w += bs) {
-        uint32_t u = 0;
-        for (uint32_t d = 0; d < ne_w; ++d) u |= D.eb[d][w];
-        D.eall[w] = u;
-      }
       for (uint32_t le = tid; le < deg_w; le += bs) {
         uint64_t lw = 0;
         int64_t bu = 0;
@@ -4909,7 +4905,8 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
       bool hr2 = (sl1 || hd1[u]) && rt2 >= t_lo && rt2 < t_hi;
       st_ops += (hr ? 1u : 0u) + (hr2 ? 1u : 0u);
       // pending echo descriptors on this edge: already on its parked link word (PF prefetch)
-      const bool pe = ne_w && desc_bit(D.eall, le);
+      bool pe = false;
+      for (uint32_t d = 0; d < ne_w; ++d) pe = pe || desc_bit(D.eb[d], le);
       if (n_bc == 0 && !he && !hr && !hr2 && !pe) continue;
       ++st_edges;
       int64_t bu = static_cast<int64_t>(lw[u] >> 16);
