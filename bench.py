@@ -213,6 +213,9 @@ def main():
                          "pbft-node.cc:66-69) with the counter RNG, instead of the fixed 3 ms")
     ap.add_argument("--mode", choices=("pdes", "replicas"), default="pdes",
                     help="multi-GPU mode (N>1): node-partitioned PDES or independent replicas")
+    ap.add_argument("--pdes1", action="store_true",
+                    help="one GPU with the partition machinery on (a world-1 RCCL group, the per-window "
+                         "control exchange): its cost against the plain single-GPU run")
     args = ap.parse_args()
     if args.nodes <= 0:
         args.nodes = 65536 if args.workload == "gossip" else 4096
@@ -224,10 +227,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
-    if world > 1:
+    if world > 1 or args.pdes1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29561")
+            dist.init_process_group("nccl", rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl")
 
     # HIP-event timing around the k_link class only inside the timed region (an event pair
     # costs a few us of dispatch per launch); the other classes are timed in an extra
@@ -355,7 +363,7 @@ def main():
             "config": {"workload": wl,
                        "nodes": args.nodes, "step": "one 50 ms block interval",
                        "engine": args.engine,
-                       "parallelism": f"{mode}{world}" if world > 1 else "single"},
+                       "parallelism": f"{mode}{world}" if world > 1 or args.pdes1 else "single"},
             "committed_rounds_per_s": rounds / dt,
             "roofline": {"kernel": "k_link (inbox scatter)", "bound": "hbm", "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,

@@ -996,15 +996,14 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     const dim3 gg(static_cast<uint32_t>((static_cast<uint64_t>(s.R) * s.nloc + per_wg - 1) / per_wg));
     // the generic kernel only has work with a timer, START/STOP or extras in the window
     const int loop = lo <= 0 || xa || s.next_timer < hi || (s.cfg.stop_ns >= 0 && s.cfg.stop_ns < hi);
-    if ((rc = launch(s, KS_SCAN, k_gossip_scan, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g, loop)) ||
-        (loop &&
-         (rc = launch(s, KS_SCAN, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), block, lds, s.kp_dev, cell, lo, hi,
-                      cs, fw, xa))))
-      return rc;
-    // the link stage (both kernels) as ONE timed launch of the k_link class
+    // the fused scan + link kernel and the generic kernels after it as ONE timed launch of the
+    // k_link class (it moves every record: the 16 B read, the link word, the 16 B write)
     const bool timed = (kstat_mask() >> KS_LINK) & 1u;
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
-    if ((rc = launch(s, -1, k_gossip_link, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, s.gossip_g)) ||
+    if ((rc = launch(s, -1, k_gossip_cell, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g, loop, fw)) ||
+        (loop &&
+         (rc = launch(s, -1, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), block, lds, s.kp_dev, cell, lo, hi,
+                      cs, fw, xa))) ||
         // (the looped grid may not exceed the workgroups the per-workgroup staging areas
         // were allocated for: xstage / xmeta hold grid_link of them)
         (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(256, s.grid_link)), dim3(s.bs_link),

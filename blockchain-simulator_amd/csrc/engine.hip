@@ -3072,11 +3072,12 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
 //            the same sequence -> GOSSIP_DELIVER trace + one broadcast (sub += deg each)
 // The kernel walks all of this rank's gnodes (no k_active): a node with work in the window
 // (k_active's rule) that is not simple is appended to list 2 for k_scan<.., LOOP>.
-__global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                     long long t_hi, long long cs, int x_active, uint32_t G,
-                                                     int loop) {
+// The dense-gossip scan of one workgroup's node groups; returns true for a lane whose node the
+// generic k_scan must take (appended to list 2).
+__device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP* __restrict__ pk, long long cell,
+                                                                       long long t_lo, long long t_hi, long long cs,
+                                                                       int x_active, uint32_t G, int loop) {
   const KP& p = *pk;
-  BAIL_IF_ERR();
   __shared__ uint32_t s_deliv[BCSIM_MSG_TYPES];
   __shared__ uint32_t s_ev, s_wr, s_nf, s_trbase;
   __shared__ long long s_tmax;
@@ -3233,6 +3234,15 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
     if (s_wr) atomicAdd(&cnt[CNT_WRONG], static_cast<unsigned long long>(s_wr));
     if (s_tmax > LLONG_MIN) atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), s_tmax);
   }
+  return have && !fast;
+}
+
+__global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                     long long t_hi, long long cs, int x_active, uint32_t G,
+                                                     int loop) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  (void)gossip_scan_body(pk, cell, t_lo, t_hi, cs, x_active, G, loop);
 }
 
 // ---------------------------------------------------------------------------
@@ -5102,10 +5112,13 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
 // list; then the ordered compaction of the ops not yet due.  Other nodes of the k_link
 // The kernel walks all of this rank's gnodes: a node with an echo to send or an op due that
 // is not simple is appended to list 3 for k_link<.., LOOP>.
-__global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                     long long t_hi, int final_win, uint32_t G) {
+// The dense-gossip link stage of one workgroup's node groups.  scan_left: this lane's node was
+// left to the generic k_scan in the same window (fused k_gossip_cell), so its link stage waits
+// for the generic k_link after it (list 3).
+__device__ __attribute__((always_inline)) inline void gossip_link_body(const KP* __restrict__ pk, long long cell,
+                                                                       long long t_lo, long long t_hi, int final_win,
+                                                                       uint32_t G, bool scan_left) {
   const KP& p = *pk;
-  BAIL_IF_ERR();
   __shared__ RawOp sop[256];  // due broadcasts of each group in key order (group base + rank)
   __shared__ uint32_t s_c[6];  // sends, records, due ops, edges, echoes, kept
   __shared__ uint8_t s_busy[kMaxBuckets];
@@ -5131,7 +5144,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
   const uint32_t n0 = kl < na ? AT(p.n_ops, g, p.NT) : 0u;
   // nodes link_node would change: an echo to send, or an op due (k_active's rule minus the
   // nodes for which link_node only recomputes an unchanged node_onext)
-  const bool have = rx || (n0 && AT(p.node_onext, g, p.NT) < t_hi);
+  const bool have = rx || (n0 && AT(p.node_onext, g, p.NT) < t_hi) || scan_left;
   const uint32_t n = have ? n0 : 0u;
   const uint32_t e0 = have ? AT(p.row, i, p.N + 1) : 0u;
   const uint32_t deg = have ? AT(p.row, i + 1, p.N + 1) - e0 : 0u;
@@ -5148,7 +5161,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
   }
   const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
   const unsigned long long listed = __ballot(due && !bc) & gmask;
-  const bool fast = have && n <= G && deg <= G && listed == 0;
+  const bool fast = have && n <= G && deg <= G && listed == 0 && !scan_left;
   if (have && !fast && j == 0) {
     const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
     AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
@@ -5320,6 +5333,29 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
     if (s_c[4]) atomicAdd(&ks[KST_ECHO], static_cast<unsigned long long>(s_c[4]));
     if (s_c[5]) atomicAdd(&ks[KST_KEPT], static_cast<unsigned long long>(s_c[5]));
   }
+}
+
+__global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                     long long t_hi, int final_win, uint32_t G) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  gossip_link_body(pk, cell, t_lo, t_hi, final_win, G, false);
+}
+
+// Dense gossip, one kernel per window: each workgroup scans its node groups and then runs their
+// link stage.  A node's link stage needs only the node's own state -- its ops (the ones due now,
+// including those its scan just created when the app delay ends inside the window) and its own
+// inbox row (implicit echoes) -- and writes only records of later cells and its own out-edges,
+// so no other node's scan in this window can affect it.  One launch per window instead of two,
+// and the row is read while still in this CU's cache.
+__global__ __launch_bounds__(256) void k_gossip_cell(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                     long long t_hi, long long cs, int x_active, uint32_t G, int loop,
+                                                     int final_win) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  const bool left = gossip_scan_body(pk, cell, t_lo, t_hi, cs, x_active, G, loop);
+  __syncthreads();  // (the node's new ops, n_ops and node_onext: written by one lane of its group)
+  gossip_link_body(pk, cell, t_lo, t_hi, final_win, G, left);
 }
 
 // ---------------------------------------------------------------------------
