@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end GPU evidence: the GPU test suite, the bench lines of every workload (with the
 # CPU baseline), and the rocprofv3 kernel trace + PMC passes of the headline.
-#   bash tests/gpu_round.sh <tag>      (outputs under gpurun_out/<tag>/)
+#   bash tests/gpu_round.sh <tag> [noprof]     (outputs under gpurun_out/<tag>/)
 set -o pipefail
 tag=${1:-round}
 out=gpurun_out/$tag
@@ -20,5 +20,6 @@ step bench_gossip 240 python bench.py --workload gossip
 step bench_gossip_pdes1 240 python bench.py --workload gossip --pdes1 --no-cpu-baseline
 step bench_paxos 300 python bench.py --workload paxos
 step bench_pbft_jitter 240 python bench.py --jitter
+[ "$2" = "noprof" ] && exit 0
 bash tests/gpu_prof.sh $tag/prof > $out/prof.log 2>&1 || { tail -5 $out/prof.log; exit 1; }
 tail -3 $out/prof.log

@@ -30,6 +30,10 @@ with bcsim.Simulator(c) as s:
         s.run(t)
         cnt, st = s.counters(), s.status()
         ks = s.kernel_stats()
+        if (t // 50_000_000) % 4 == 0:
+            tr = s.trace()
+            com = {r[0] for r in tr if r[6] == _abi.TR["PAXOS_COMMIT"]}
+            print(f"  replicas with a commit: {len(com)} / {R}", flush=True)
         print(f"t={t / 1e6:.0f}ms wall={time.time() - w:.2f}s msgs={cnt['delivered_total']} cells={st['cells']} "
               f"quiescent={st['quiescent']} " + " ".join(f"{k}={v['us'] / 1e3:.1f}ms/{v['launches']}" for k, v in ks.items()),
               flush=True)
