@@ -4768,6 +4768,9 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
     }
     return;
   }
+  // (BCSIM_WGT=1: phase clocks -- classify, descriptors + parked link words, edges, compaction)
+  unsigned long long ph[4] = {wg_t0, wg_t0, wg_t0, wg_t0};
+  if (p.wgt && tid == 0) ph[0] = __builtin_amdgcn_s_memrealtime();
   // the due broadcasts in key order (LDS copies: every lane reads them per edge)
   if (tid < n_bc) L.bco[tid] = ld_op(&ops[L.bc[tid]]);
   __syncthreads();
@@ -4844,6 +4847,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
     }
     __syncthreads();
   }
+  if (p.wgt && tid == 0) ph[1] = __builtin_amdgcn_s_memrealtime();
   // (a wave-uniform trip count: the cross-rank range step after the edges is convergent)
   for (uint32_t b0 = 0; b0 < deg_w; b0 += kMeshU * bs) {
     const uint32_t base = b0 + tid;
@@ -5081,6 +5085,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
     atomicMin(&L.lmin[cb], cmn);
   }
   __syncthreads();
+  if (p.wgt && tid == 0) ph[2] = __builtin_amdgcn_s_memrealtime();
   if (tmap && L.tbk != kInvalid) {  // flush the receiver-tile flags of this sender's records
     const size_t tb = (static_cast<size_t>(L.tbk) * p.R + rep) * p.n_tiles;
     for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x)
@@ -5095,7 +5100,6 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
     if (sd1) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4) = static_cast<uint8_t>(sf1 & ~kSfD1);
   }
   const unsigned long long t0 = p.wgt ? wg_t0 : 0ull;
-  unsigned long long ph[4] = {t0, t0, t0, t0};
   const LinkCounts c8{dropped, sends, n_rec, st_ops, st_edges, st_echo, 0u, 0u};
   // every op due (the broadcasts just sent): nothing to compact, no op to read again
   link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, n_lists, ovmin, c8, (sl1 || sd1) && final_win, rx && final_win, obp,
