@@ -2808,7 +2808,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
             make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), sp,
                        static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m1))) |
                            (static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m2))) << 16));
-      if (due / p.L == cell)
+      if (due < cs + p.L)  // (due >= t >= cs: the arrival cell, without a 64-bit division)
         ++n_slot0;
       else
         ++n_slot1;
@@ -4794,6 +4794,9 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   uint32_t cmn = ~0u;
   const long long cs = cell * p.L;
   const uint32_t N1 = p.N - 1;
+  const uint32_t L32 = static_cast<uint32_t>(p.L);  // (< 2^32: checked on the host)
+  const long long cq_b = cell / B;
+  const uint32_t cr_b = static_cast<uint32_t>(cell % B);
   Rec* in_row = p.inbox + inbox_idx(p, ib, rep, e0);
   const int64_t app = p.app_delay;
   const uint32_t f2r = static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0)));
@@ -4988,16 +4991,29 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
         bu = end;
         if (src == 3) continue;  // the echo only occupies the link
         const int64_t ta = end + pr;
-        const long long ca = ta / p.L;
+        // arrival cell and offset: a 32-bit division of the offset from the cell start (a
+        // record lands at most a ring or so ahead; 64-bit only beyond 2^32 ns)
+        long long ca;
+        uint32_t tof;
+        {
+          const int64_t dtf = ta - cs;
+          if (dtf >= 0 && dtf < (1ll << 32)) {
+            const uint32_t q = static_cast<uint32_t>(dtf) / L32;
+            ca = cell + q;
+            tof = static_cast<uint32_t>(dtf) - q * L32;
+          } else {
+            ca = ta / p.L;
+            tof = static_cast<uint32_t>(ta - ca * p.L);
+          }
+        }
         const long long rel = ca - cell;
         if (rel < 1) {
           set_err(p, BCSIM_E_TIE);  // lookahead violated
           continue;
         }
         ++n_rec;
-        const uint32_t tof = static_cast<uint32_t>(ta - ca * p.L);
         const uint32_t w3 = ow3 | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24) |
-            (emit_tag(cell / p.n_buckets, static_cast<uint32_t>(cell % p.n_buckets), ca - cell, p.n_buckets) << 27);
+            (emit_tag(cq_b, cr_b, rel, B) << 27);
         Rec r;
         {
           const uint4 rv = make_uint4(tof, osub, ow2, w3);
@@ -5025,7 +5041,8 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
           }
         }
         if (rel < static_cast<long long>(B)) {
-          const uint32_t bk = static_cast<uint32_t>(ca % B);
+          uint32_t bk = cr_b + static_cast<uint32_t>(rel);  // (ca % B, rel < B)
+          if (bk >= B) bk -= B;
           if (owner) {
             st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), r);
             uint32_t tb = kInvalid;
