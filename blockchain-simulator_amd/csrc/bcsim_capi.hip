@@ -1486,7 +1486,13 @@ static int zero_tag_buckets(Sim& s, long long a, long long b) {
   }
   for (uint32_t k = 0; k < s.B; ++k)
     if (hit[k]) {
-      HIPCHK(hipMemsetAsync(s.kp.inbox + static_cast<size_t>(k) * per, 0, per * sizeof(Rec), s.stream));
+      {  // (a store kernel: hipMemsetAsync of a 268 MB bucket ran at ~0.2-0.8 TB/s)
+        const uint64_t n16 = per * sizeof(Rec) / 16;
+        const uint32_t nb = static_cast<uint32_t>(std::min<uint64_t>(8192, (n16 + 255) / 256));
+        int rc = launch(s, KS_AUX, k_zero16, dim3(nb), dim3(256), 0, reinterpret_cast<uint4*>(s.kp.inbox + static_cast<size_t>(k) * per),
+                        n16);
+        if (rc) return rc;
+      }
       ++s.tag_zeroes;
       // the latest turn of bucket k in [a, b]
       const long long lastk = b - ((b % s.B - k + s.B) % s.B);

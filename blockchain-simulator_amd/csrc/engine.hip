@@ -6340,6 +6340,14 @@ __global__ void k_draws(const KP* __restrict__ pk, uint32_t) {
   *p.dreq_cnt = 0;
 }
 
+// Zero n16 16-byte words (an inbox bucket for the ring-turn tag invariant): dwordx4 stores,
+// a grid-stride loop over a few thousand workgroups
+__global__ __launch_bounds__(256) void k_zero16(uint4* __restrict__ dst, uint64_t n16) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < n16; k += stride)
+    dst[k] = make_uint4(0, 0, 0, 0);
+}
+
 // global min over node_tnext / node_onext
 // next event time over all nodes: every workgroup reduces a strided share, the last one to
 // finish (threadfence reduction) combines the partial minima
