@@ -61,7 +61,7 @@ struct Sim {
   std::vector<void*> allocs;
   // host mirrors
   Ctl* ctl_h = nullptr;  // pinned
-  uint32_t* act_h = nullptr;  // pinned: the window's active-list lengths (k_scan, k_link)
+  uint32_t* act_h = nullptr;  // pinned: the window's active-list lengths (k_scan, k_link); [4..5] LLONG_MAX
   uint32_t* bcnt_h = nullptr;
   uint32_t* xcnt_h = nullptr;
   void* ctl_d = nullptr;
@@ -107,6 +107,7 @@ struct Sim {
   long long next_cell = 0;     // node-partitioned: the next cell of the whole system, agreed by the
   bool next_known = false;     // last cell's control exchange (no separate all-reduce needed)
   uint64_t ctl_collectives = 0;  // collectives + host syncs of the cell loop (engine counters)
+  uint64_t last_import = 0;      // records k_import placed at the last exchange
   std::vector<int64_t> lead_w; // leader flags packed for the all-reduce
 };
 
@@ -802,7 +803,8 @@ static int setup_device(Sim& s) {
   p.x_cnt = p.bucket_cnt + s.B;
   p.send_cnt = p.x_cnt + s.B;
   HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), ctl_bytes));
-  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.act_h), 16));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.act_h), 32));  // (+ a pinned LLONG_MAX word at [4])
+  *reinterpret_cast<long long*>(s.act_h + 4) = LLONG_MAX;
   s.bcnt_h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.ctl_h) + sizeof(Ctl));
   s.xcnt_h = s.bcnt_h + s.B;
   s.scnt_h = s.xcnt_h + s.B;
@@ -1245,8 +1247,7 @@ static int group_cell(Sim& s, long long cell) {
     // the overflow count as of the last read-back (nothing appends to the list between the
     // end-of-cell read-back and here)
     const uint32_t nov = s.ctl_h->ov_cnt;
-    long long big = LLONG_MAX;
-    HIPCHK(hipMemcpyAsync(s.kp.scal + 1, &big, 8, hipMemcpyHostToDevice, s.stream));
+    HIPCHK(hipMemcpyAsync(s.kp.scal + 1, s.act_h + 4, 8, hipMemcpyHostToDevice, s.stream));  // LLONG_MAX (pinned)
     if (nov) {
       int rc = launch(s, KS_GROUP, k_rebin, dim3((nov + 255) / 256), dim3(256), 0, s.kp_dev, cell, nov);
       if (rc) return rc;
@@ -1377,9 +1378,10 @@ static int exchange(Sim& s, long long cell, int lrc, bool tick) {
                                reinterpret_cast<char*>(s.recvbuf), rb.data())))
     return rc;
   ++s.ctl_collectives;
-  static const long long kNone = LLONG_MAX;
   HIPCHK(hipMemsetAsync(s.kp.send_cnt, 0, 4ull * kMaxRanks, s.stream));
-  HIPCHK(hipMemcpyAsync(s.kp.scal + 4, &kNone, 8, hipMemcpyHostToDevice, s.stream));
+  // (from pinned memory: a pageable source makes the copy a staged, blocking one)
+  HIPCHK(hipMemcpyAsync(s.kp.scal + 4, s.act_h + 4, 8, hipMemcpyHostToDevice, s.stream));
+  s.last_import = n;
   if (n) {
     rc = launch(s, KS_GROUP, k_import, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s.kp_dev, cell,
                 static_cast<const XRec*>(s.recvbuf), static_cast<uint32_t>(n));
@@ -1666,7 +1668,9 @@ static int run(Sim& s, int64_t t_until) {
       // ONE control exchange (segment sizes, next-cell candidates, status, PBFT n_alive), the
       // records for other ranks' nodes, k_import; the next cell is agreed there
       if ((rc = exchange(s, c, lrc, tick))) return rc;
-      lerr = readback(s);  // a failure here rides the next cell's exchange
+      // the bucket counts after k_import (a failure here rides the next cell's exchange); with
+      // nothing imported the end-of-cell read-back before the exchange is still current
+      lerr = s.last_import ? readback(s) : 0;
     } else {
       if (lrc) return lrc;
       if (tick) {

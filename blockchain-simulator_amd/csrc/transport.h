@@ -5,6 +5,8 @@
 //              torch.distributed gloo, several ranks may share one GPU)
 // Included by bcsim_capi.hip after g_detail.
 #pragma once
+#include <algorithm>
+#include <cstring>
 #ifndef HIPEMU
 #include <rccl/rccl.h>
 #endif
@@ -62,9 +64,12 @@ struct RcclXport : Xport {
   uint64_t* d_cnt = nullptr;   // [2][nranks] byte counts
   char* d_host = nullptr;      // alltoallv_host staging (device)
   uint64_t host_cap = 0;
+  int64_t* h_stage = nullptr;  // pinned host staging of the control words and all-reduce values
+                               // (a pageable hipMemcpyAsync is a staged, blocking copy)
 
   ~RcclXport() override {
     if (comm) ncclCommDestroy(comm);
+    if (h_stage) (void)hipHostFree(h_stage);
     if (d_red) (void)hipFree(d_red);
     if (d_cnt) (void)hipFree(d_cnt);
     if (d_host) (void)hipFree(d_host);
@@ -76,13 +81,17 @@ struct RcclXport : Xport {
     NCCLCHK(ncclCommInitRank(&comm, static_cast<int>(n), id, static_cast<int>(r)));
     HIPCHK(hipMalloc(&d_red, kRedMax * sizeof(int64_t)));
     HIPCHK(hipMalloc(&d_cnt, 2ull * n * kCtlWords * sizeof(uint64_t)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h_stage), std::max<size_t>(kRedMax, 2ull * n * kCtlWords) * 8ull, 0));
     return BCSIM_OK;
   }
   int ctl_exchange(hipStream_t st, const int64_t* send, int64_t* recv) override {
-    HIPCHK(hipMemcpyAsync(d_cnt, send, nranks * kCtlWords * 8ull, hipMemcpyHostToDevice, st));
+    const size_t nb = nranks * kCtlWords * 8ull;
+    std::memcpy(h_stage, send, nb);
+    HIPCHK(hipMemcpyAsync(d_cnt, h_stage, nb, hipMemcpyHostToDevice, st));
     NCCLCHK(ncclAllToAll(d_cnt, d_cnt + nranks * kCtlWords, kCtlWords, ncclInt64, comm, st));
-    HIPCHK(hipMemcpyAsync(recv, d_cnt + nranks * kCtlWords, nranks * kCtlWords * 8ull, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_stage + nranks * kCtlWords, d_cnt + nranks * kCtlWords, nb, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    std::memcpy(recv, h_stage + nranks * kCtlWords, nb);
     return BCSIM_OK;
   }
   int sendrecv_dev(hipStream_t st, const char* send_dev, uint64_t stride, const uint64_t* send_bytes, char* recv_dev,
@@ -100,10 +109,12 @@ struct RcclXport : Xport {
   }
   int allreduce_i64(hipStream_t st, int64_t* v, uint32_t n, int op) override {
     if (n > kRedMax) return BCSIM_E_INVAL;
-    HIPCHK(hipMemcpyAsync(d_red, v, n * 8ull, hipMemcpyHostToDevice, st));
+    std::memcpy(h_stage, v, n * 8ull);
+    HIPCHK(hipMemcpyAsync(d_red, h_stage, n * 8ull, hipMemcpyHostToDevice, st));
     NCCLCHK(ncclAllReduce(d_red, d_red, n, ncclInt64, op == 0 ? ncclMin : ncclSum, comm, st));
-    HIPCHK(hipMemcpyAsync(v, d_red, n * 8ull, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_stage, d_red, n * 8ull, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    std::memcpy(v, h_stage, n * 8ull);
     return BCSIM_OK;
   }
   int alltoallv_dev(hipStream_t st, const char* send_dev, uint64_t stride, const uint64_t* send_bytes,
