@@ -347,6 +347,8 @@ static int setup_device(Sim& s) {
   }
   if ((c.protocol == BCSIM_PBFT || c.protocol == BCSIM_GOSSIP) && p.pbft_period <= 0) return BCSIM_E_INVAL;
   p.L = s.L;
+  // ceil(2^64 / L) (L >= 2: the lookahead is at least one frame time)
+  p.L_magic = static_cast<uint64_t>(~0ull / static_cast<uint64_t>(s.L)) + 1ull;
   // delay tables (float seconds -> ns), pbft-node.cc:68, raft-node.cc:65,71, paxos-node.cc:399
   std::vector<int64_t> dpb(3), drf(3), del(150), dpx(50);
   for (int k = 0; k < 3; ++k) {

@@ -53,6 +53,7 @@ struct KP {
   uint32_t protocol, delay_mode, rng_mode, encoding, echo;
   uint32_t deg_max;
   int64_t L;
+  uint64_t L_magic;  // ceil(2^64 / L): x / L for x < 2^32 is the high half of x * L_magic
   int64_t app_delay;
   int64_t tx_tot[2], tx_last[2];
   int64_t pbft_period, raft_hb, raft_prop_delay, stop_ns;
@@ -4998,9 +4999,12 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
         {
           const int64_t dtf = ta - cs;
           if (dtf >= 0 && dtf < (1ll << 32)) {
-            const uint32_t q = static_cast<uint32_t>(dtf) / L32;
+            // floor(x / L) exactly: x * ceil(2^64/L) / 2^64 exceeds x / L by less than x / 2^64
+            // < 1/L (x, L < 2^32), which cannot reach the next integer
+            const uint32_t x = static_cast<uint32_t>(dtf);
+            const uint32_t q = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), p.L_magic));
             ca = cell + q;
-            tof = static_cast<uint32_t>(dtf) - q * L32;
+            tof = x - q * L32;
           } else {
             ca = ta / p.L;
             tof = static_cast<uint32_t>(ta - ca * p.L);
