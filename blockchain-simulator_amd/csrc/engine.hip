@@ -283,6 +283,7 @@ __device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int l
 #else
 #define BAIL_IF_ERR() \
   do {                \
+    (void)p;          \
   } while (0)
 #define TRAIL_AT(pp, g) \
   do {                  \
