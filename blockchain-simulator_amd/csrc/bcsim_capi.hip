@@ -77,6 +77,10 @@ struct Sim {
   bool mesh_link = false;  // full mesh, fixed delay: k_link_mesh first, k_link over list 3
   bool scan_fast = false;  // dense PBFT, fixed delay, reply slots: k_scan_pbft first, k_scan over list 2
   bool mesh_pf = true;     // k_link_mesh parks the node's link words in LDS first (BCSIM_MESH_PF=0: off)
+  // one rank: k_link_mesh<TILE> leaves the simple nodes' edges to k_mesh_tile (BCSIM_MESH_TILE=0: off)
+  // in launches of at least tile_min nodes (BCSIM_TILE_MIN)
+  bool mesh_tile = false;
+  uint32_t tile_min = 1, mesh_epoch = 0;
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -341,13 +345,15 @@ static int setup_device(Sim& s) {
     if (ms.frames > 1) fmin = std::min<int64_t>(fmin, p.tx_full[0]);
     s.L = pmin + fmin;
   }
-  if (s.L <= 0 || s.L >= (1ll << 32)) {
-    g_detail = "lookahead out of range";
+  // (L >= 2: the reciprocal ceil(2^64 / L) below wraps to 0 at L == 1; a 1 ns lookahead means a
+  // zero propagation delay and a 1 ns frame, far outside anything the reference configures)
+  if (s.L < 2 || s.L >= (1ll << 32)) {
+    g_detail = "lookahead out of range (2 ns .. 2^32 ns)";
     return BCSIM_E_UNSUPPORTED;
   }
   if ((c.protocol == BCSIM_PBFT || c.protocol == BCSIM_GOSSIP) && p.pbft_period <= 0) return BCSIM_E_INVAL;
   p.L = s.L;
-  // ceil(2^64 / L) (L >= 2: the lookahead is at least one frame time)
+  // ceil(2^64 / L) (L >= 2, checked above)
   p.L_magic = static_cast<uint64_t>(~0ull / static_cast<uint64_t>(s.L)) + 1ull;
   // delay tables (float seconds -> ns), pbft-node.cc:68, raft-node.cc:65,71, paxos-node.cc:399
   std::vector<int64_t> dpb(3), drf(3), del(150), dpx(50);
@@ -709,6 +715,21 @@ static int setup_device(Sim& s) {
       return rc;
     HIPCHK(hipMemset(p.rdesc, 0xFF, (p.desc ? static_cast<size_t>(kOpRing) * NT : 1) * 16));  // due -1: sent
     HIPCHK(hipMemset(p.en, 0, p.desc ? NT : 1));
+    // the tiled mesh link stage: one rank, the LDS-parked variant of k_link_mesh
+    // as its classify stage, degree <= 4096 (the reply bitmaps' rank prefixes: kRpChunks)
+    {
+      const char* mt = std::getenv("BCSIM_MESH_TILE");
+      s.mesh_tile = s.mesh_link && s.mesh_pf && s.P == 1 && s.deg_max <= 64 * kRpChunks && !(mt && *mt == '0');
+      if (const char* tm = std::getenv("BCSIM_TILE_MIN"); tm && *tm) s.tile_min = static_cast<uint32_t>(std::atoi(tm));
+    }
+    p.n_stiles = (s.N + kTS - 1) / kTS;
+    const size_t njob = s.mesh_tile ? NT : 1;
+    if ((rc = dalloc(s, &p.mjob, njob * 4)) || (rc = dalloc(s, &p.mbc, njob * kMeshBc * 2)) ||
+        (rc = dalloc(s, &p.mrp, njob * 2 * kRpChunks)) ||
+        (rc = dalloc(s, &p.mtile, s.mesh_tile ? static_cast<size_t>(s.R) * p.n_stiles : 1)))
+      return rc;
+    HIPCHK(hipMemset(p.mjob, 0, njob * 4 * 16));  // epoch 0: no job (launch epochs start at 1)
+    HIPCHK(hipMemset(p.mtile, 0, (s.mesh_tile ? static_cast<size_t>(s.R) * p.n_stiles : 1) * 4));
   }
   const size_t n_link = p.hubs ? static_cast<size_t>(s.R) * (static_cast<size_t>(p.hubs) * (s.N - 1) +
                                                               static_cast<size_t>(s.N - p.hubs) * p.hubs)
@@ -1163,17 +1184,31 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     // (node-partitioned: the kernels that stage records for other ranks)
     const dim3 gl(std::min<uint32_t>(256, s.grid_link)), bl(std::min<uint32_t>(1024, 4 * s.bs_link));
     const size_t mlds = static_cast<size_t>(s.deg_max) * 8;  // (the PF variant's link words)
-    if (s.P > 1 ? ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<true, 2, true>, grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw)
-                                   : launch(s, -1, k_link_mesh<true, 2, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw)) ||
-                   (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
-                // (a few nodes -- the leader's block broadcast at a tick -- get 1024-lane workgroups:
-                // the launch is one workgroup's latency)
-                : ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<false, 2, true>, grid, dim3(n_link <= 64 ? 1024 : 256), mlds,
-                                            s.kp_dev, cell, lo, hi, fw)
-                                   : launch(s, -1, k_link_mesh<false, 2, false>, grid, dim3(n_link <= 64 ? 1024 : 256), 0,
-                                            s.kp_dev, cell, lo, hi, fw)) ||
-                   (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw))))
-      return rc;
+    const uint32_t z = 0;
+    if (s.P > 1) {
+      if ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<true, 2, true>, grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw, z)
+                          : launch(s, -1, k_link_mesh<true, 2, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, z)) ||
+          (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
+        return rc;
+    } else if (s.mesh_tile && n_link >= s.tile_min) {
+      // the simple nodes' edges by 32 x 64 (sender x receiver) tiles; a launch
+      // epoch tells this launch's jobs from stale ones
+      const uint32_t ep = ++s.mesh_epoch == 0 ? ++s.mesh_epoch : s.mesh_epoch;
+      const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
+      if ((rc = launch(s, -1, (k_link_mesh<false, 2, true, true>), grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw, ep)) ||
+          (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(256), 0, s.kp_dev, cell, lo, hi, ep)) ||
+          (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
+        return rc;
+    } else {
+      // (a few nodes -- the leader's block broadcast at a tick -- get 1024-lane workgroups:
+      // the launch is one workgroup's latency)
+      if ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<false, 2, true>, grid, dim3(n_link <= 64 ? 1024 : 256), mlds,
+                                   s.kp_dev, cell, lo, hi, fw, z)
+                          : launch(s, -1, k_link_mesh<false, 2, false>, grid, dim3(n_link <= 64 ? 1024 : 256), 0,
+                                   s.kp_dev, cell, lo, hi, fw, z)) ||
+          (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
+        return rc;
+    }
     if (timed) {
       if ((rc = ev_end(s))) return rc;
     } else {
@@ -1613,6 +1648,18 @@ static int run(Sim& s, int64_t t_until) {
     const long long hi = std::min<long long>(ce, lim);
     if (lo >= hi) {  // nothing left before the limit inside this cell
       if (lim != INT64_MAX) s.t_done = std::max<int64_t>(s.t_done, lim);
+      // (node-partitioned: the exchange already agreed on this cell, so every rank is here; a
+      // failure carried out of the last window leaves with every rank, as at the exit above)
+      if (s.xp) {
+        int64_t cv[2] = {LLONG_MAX, carried};
+        if ((rc = s.xp->allreduce_i64(s.stream, cv, 2, 0))) return rc;
+        ++s.ctl_collectives;
+        if (carried) return carried;
+        if (cv[1] < 0) {
+          g_detail = "another rank of the partition failed";
+          return BCSIM_E_PEER;
+        }
+      }
       break;
     }
     int lrc = carried;  // this rank's status of the cell

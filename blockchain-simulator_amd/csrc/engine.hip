@@ -122,6 +122,15 @@ struct KP {
   uint4* edesc;           // [NT][kEDesc] {t lo, t hi, big, 0}
   uint32_t* ebits;        // [NT][kEDesc][dwords]
   uint8_t* en;            // [NT] pending echo descriptors
+  // full-mesh tiled link stage (k_mesh_tile): the job k_link_mesh<TILE> leaves per
+  // gnode -- {epoch, flags, ne | n_bc << 8, 0}, the two reply descriptors, the pending echo times --
+  // its due broadcasts in key order (RawOp words), the reply bitmaps' rank prefixes per 64-slot
+  // chunk, and per (replica, 32-sender tile) the epoch of the last launch that left a job in it
+  uint4* mjob;            // [NT][4]
+  uint4* mbc;             // [NT][kMeshBc][2]
+  uint16_t* mrp;          // [NT][2][kRpChunks]
+  uint32_t* mtile;        // [R][n_stiles]
+  uint32_t n_stiles;
   int64_t prop_const;    // propagation delay of every edge, or -1 (per-edge array)
   // links
   uint64_t* link;  // per edge: busy_until << 16 | (arrival cell of the last record & 0xFFFF)
@@ -233,6 +242,10 @@ constexpr uint32_t kDescWords = 128;  // descriptor bitmaps: in-slots of degree 
 constexpr uint32_t kEDesc = 2;        // pending echo descriptors per node (LDS: k_link_mesh keeps 4 WGs/CU)
 // sflag bits of a reply descriptor of the arrival cell (bits 0..3: reply slots due in cell + k)
 constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in this cell / the next
+// tiled mesh link stage: due broadcasts per job, senders x receivers per tile, 64-slot chunks
+constexpr uint32_t kMeshBc = 2, kTS = 32, kTR = 64, kRpChunks = kDescWords / 2;
+// job flags (mjob[g][0].y)
+constexpr uint32_t kJSl0 = 1u, kJSl1 = 2u, kJSd0 = 4u, kJSd1 = 8u, kJRxe = 16u, kJBig0 = 32u, kJBig1 = 64u;
 
 
 // ---------------------------------------------------------------------------
@@ -3255,6 +3268,7 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
 // a cell beyond the ring to the overflow list).
 constexpr int kBcastCap = 64;  // due broadcasts per node per cell
 constexpr int kTile = 64;        // receiver tile of the full-mesh tile flags (rtile)
+static_assert(kTile == static_cast<int>(kTR), "k_mesh_tile: one receiver tile per workgroup");
 constexpr int kMaxTiles = 1024;  // 64-node tiles (N <= 65536)
 constexpr int kMaxBuckets = 64;
 
@@ -4633,9 +4647,13 @@ __device__ inline uint32_t desc_rank(const MeshDesc& D, int h, uint32_t le) {
   return D.rp[h][le >> 5] + static_cast<uint32_t>(__popc(D.rb[h][le >> 5] & ((1u << (le & 31u)) - 1u)));
 }
 
-template <bool XR, int kMeshU, bool PF>
+// TILE (one rank): a node whose due broadcasts fit a job (<= kMeshBc) leaves its edges to
+// k_mesh_tile -- the job (due broadcasts in key order, reply / echo descriptors, flags) and the
+// node's own bookkeeping (op compaction, counters, slot and descriptor flags) are done here,
+// the per-edge FIFO and the records there, 32 senders x 64 receivers per workgroup.
+template <bool XR, int kMeshU, bool PF, bool TILE = false>
 __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                   long long t_hi, int final_win) {
+                                                   long long t_hi, int final_win, uint32_t epoch) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ LinkShared L;
@@ -4788,6 +4806,67 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
     }
   }
   __syncthreads();
+
+  if (TILE && n_bc <= kMeshBc) {
+    // the edges go to k_mesh_tile: the job, then this node's own bookkeeping
+    const bool any = n_bc || sl0 || sl1 || sd0 || sd1 || rxe;
+    const uint32_t ne_j = any ? ne : 0u;  // pending echo descriptors: applied by the tile
+    if (any) {
+      const size_t jb = static_cast<size_t>(g) * kMeshBc * 2;
+      if (tid < 2 * n_bc) p.mbc[jb + tid] = reinterpret_cast<const uint4*>(&L.bco[tid >> 1])[tid & 1u];
+      // rank prefixes of the live reply bitmaps per 64-slot chunk (wave 0, a chunk per lane)
+      if (tid < 64 && (sd0 || sd1)) {
+        const uint32_t dw = p.dwords;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (!(h ? sd1 : sd0)) continue;
+          const uint32_t* rb = p.rbits + (static_cast<size_t>(h ? obp : ob) * p.NT + g) * dw;
+          const uint32_t k = 2 * tid;
+          const uint32_t c = (k < dw ? static_cast<uint32_t>(__popc(rb[k])) : 0u) +
+                             (k + 1 < dw ? static_cast<uint32_t>(__popc(rb[k + 1])) : 0u);
+          uint32_t in = c;
+#pragma unroll
+          for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(in, off, 64);
+            if (tid >= static_cast<uint32_t>(off)) in += v;
+          }
+          if (tid < kRpChunks) p.mrp[(static_cast<size_t>(g) * 2 + h) * kRpChunks + tid] = static_cast<uint16_t>(in - c);
+        }
+      }
+      if (tid == 0) {
+        uint32_t fl = (sl0 ? kJSl0 : 0u) | (sl1 ? kJSl1 : 0u) | (sd0 ? kJSd0 : 0u) | (sd1 ? kJSd1 : 0u) | (rxe ? kJRxe : 0u);
+        uint4 q3 = make_uint4(0, 0, 0, 0);
+        if (ne_j) {
+          const uint4 ed0 = p.edesc[static_cast<size_t>(g) * kEDesc];
+          q3.x = ed0.x;
+          q3.y = ed0.y;
+          if (ed0.z) fl |= kJBig0;
+          if (ne_j > 1) {
+            const uint4 ed1 = p.edesc[static_cast<size_t>(g) * kEDesc + 1];
+            q3.z = ed1.x;
+            q3.w = ed1.y;
+            if (ed1.z) fl |= kJBig1;
+          }
+        }
+        uint4* J = p.mjob + static_cast<size_t>(g) * 4;
+        J[1] = rd0;
+        J[2] = rd1;
+        J[3] = q3;
+        J[0] = make_uint4(epoch, fl, ne_j | (n_bc << 8), 0u);
+        p.mtile[static_cast<size_t>(rep) * p.n_stiles + i / kTS] = epoch;
+      }
+    }
+    if (tid == 0) {  // (as after the edge walk below)
+      if (ne_j) AT(p.en, g, p.NT) = 0;
+      const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
+      if (sd0) AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) = static_cast<uint8_t>(sf0 & ~kSfD0);
+      if (sd1) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4) = static_cast<uint8_t>(sf1 & ~kSfD1);
+    }
+    const LinkCounts c8{dropped, sends, 0u, st_ops, 0u, 0u, 0u, 0u};
+    link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, n_lists, LLONG_MAX, c8, (sl1 || sd1) && final_win,
+                rx && final_win, obp, fidx, p.wgt ? wg_t0 : 0ull, ph, n);
+    return;
+  }
 
   // ---- per out-edge: merge broadcasts / reply slots / implicit echo in key order, FIFO, emit ----
   uint32_t n_rec = 0, st_edges = 0, st_echo = 0;
@@ -5126,6 +5205,370 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   // every op due (the broadcasts just sent): nothing to compact, no op to read again
   link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, n_lists, ovmin, c8, (sl1 || sd1) && final_win, rx && final_win, obp,
               fidx, t0, ph, n);
+}
+
+// ---------------------------------------------------------------------------
+// k_mesh_tile (full mesh, one rank, fixed app delay, infinite queues): the edge walk of the
+// jobs k_link_mesh<TILE> left, for a tile of 32 senders x 64 receivers per workgroup.  The same
+// per-edge work as k_link_mesh's edge loop (the pending echo descriptors onto the link word, then
+// the due broadcasts, reply slots / descriptors and implicit echo merged in key order through
+// the FIFO, pbft-node.cc:349-368 fan-out, :175 echo), but the memory side is coalesced both
+// ways: a wave walks one sender's 64 out-edges to the tile's receivers (link words, own inbox
+// row and reply slots are 64 consecutive words of the sender's row), and the records are
+// transposed in LDS and written receiver by receiver -- 32 consecutive in-slots (512 B) of each
+// receiver's row instead of 64 scattered 16-byte stores 64 KB apart.  A record that is not the
+// edge's first slot record of the launch is stored directly; extras / overflow records are
+// appended to their lists with one atomic each (rare: the heavy waves are one record per edge).
+struct TileShared {
+  uint4 rec[kTR * kTS];     // slot records, receiver-major, sender index swizzled (tsw)
+  uint8_t rbk[kTR * kTS];   // their buckets (0xFF: none)
+  uint4 job[kTS][4];
+  uint4 bc[kTS][kMeshBc * 2];
+  uint32_t lcnt[kMaxBuckets];
+  uint32_t lmin[kMaxBuckets];
+  uint32_t csum[8];
+  unsigned long long bkm;   // buckets holding slot records of this tile
+  long long ovmin;
+};
+// (receiver, sender) -> LDS index: the sender index XOR the receiver's low bits, so that a wave
+// writing one sender's 64 receivers and a wave reading two receivers' 32 senders both spread
+// over the banks
+__device__ inline uint32_t tsw(uint32_t s, uint32_t i) { return s * kTS + (i ^ (s & (kTS - 1u))); }
+
+// an extras (list < B) or overflow (list == B) record, appended directly (see link_stage)
+__device__ inline void tile_append(const KP& p, uint32_t list, const XRec& x) {
+  if (list == p.n_buckets) {
+    const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+    if (pos >= p.cap_ov) {
+      set_err(p, BCSIM_E_OVERFLOW);
+      return;
+    }
+    AT(p.ov, pos, p.cap_ov) = x;
+  } else {
+    const uint32_t pos = atomicAdd(&p.x_cnt[list], 1u);
+    if (pos >= p.cap_x) {
+      set_err(p, BCSIM_E_OVERFLOW);
+      return;
+    }
+    AT(p.xbuf, static_cast<size_t>(list) * p.cap_x + pos, p.cap_xbuf) = x;
+  }
+}
+
+// rank of out-edge le among the set bits of a reply bitmap: the chunk prefix (k_link_mesh<TILE>)
+// plus the bits of le's 64-slot chunk below it
+__device__ inline uint32_t tile_rank(const KP& p, uint32_t g, int h, uint32_t ob, uint32_t le, bool& bit) {
+  const uint32_t* rb = p.rbits + (static_cast<size_t>(ob) * p.NT + g) * p.dwords;
+  const uint32_t c = le >> 6, w0 = 2 * c;
+  const uint32_t lo = rb[w0], hi = w0 + 1 < p.dwords ? rb[w0 + 1] : 0u;
+  const uint32_t b = le & 63u;
+  bit = ((b < 32 ? lo >> b : hi >> (b - 32)) & 1u) != 0;
+  const uint32_t below = b < 32 ? static_cast<uint32_t>(__popc(lo & ((1u << b) - 1u)))
+                                : static_cast<uint32_t>(__popc(lo)) + static_cast<uint32_t>(__popc(hi & ((1u << (b - 32)) - 1u)));
+  return p.mrp[(static_cast<size_t>(g) * 2 + h) * kRpChunks + c] + below;
+}
+
+__global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
+                                                   uint32_t epoch) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ TileShared T;
+  const uint32_t nrt = p.n_tiles, nst = p.n_stiles;
+  const uint32_t rep = blockIdx.x / (nst * nrt), rem = blockIdx.x % (nst * nrt);
+  const uint32_t st = rem / nrt, rt = rem % nrt;
+  if (p.mtile[static_cast<size_t>(rep) * nst + st] != epoch) return;  // no job among these senders
+  const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
+  const uint32_t N = p.N, N1 = N - 1, B = p.n_buckets;
+  const uint32_t i0 = st * kTS, s0 = rt * kTR;
+  if (tid < kTS * 4) {
+    const uint32_t i = i0 + (tid >> 2);
+    T.job[tid >> 2][tid & 3u] =
+        i < N ? p.mjob[(static_cast<size_t>(rep) * N + i) * 4 + (tid & 3u)] : make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t k = tid; k < kTR * kTS / 4; k += blockDim.x) reinterpret_cast<uint32_t*>(T.rbk)[k] = 0xFFFFFFFFu;
+  for (uint32_t k = tid; k < B; k += blockDim.x) {
+    T.lcnt[k] = 0;
+    T.lmin[k] = ~0u;
+  }
+  if (tid < 8) T.csum[tid] = 0;
+  if (tid == 0) {
+    T.bkm = 0ull;
+    T.ovmin = LLONG_MAX;
+  }
+  __syncthreads();
+  if (tid < kTS * kMeshBc * 2) {
+    const uint32_t il = tid / (kMeshBc * 2), w = tid % (kMeshBc * 2);
+    const uint4 J = T.job[il][0];
+    if (J.x == epoch && (w >> 1) < ((J.z >> 8) & 0xFFu))
+      T.bc[il][w] = p.mbc[(static_cast<size_t>(rep) * N + i0 + il) * kMeshBc * 2 + w];
+  }
+  __syncthreads();
+
+  const uint32_t ib = static_cast<uint32_t>(cell % B);
+  const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
+  const long long cs = cell * p.L;
+  const uint32_t L32 = static_cast<uint32_t>(p.L);
+  const long long cq_b = cell / B;
+  const uint32_t cr_b = static_cast<uint32_t>(cell % B);
+  const uint32_t tag = cell_tag(p, cell);
+  const int64_t app = p.app_delay;
+  const uint32_t w3r = static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0))) | (kPbPrepareRes << 16);
+  const uint32_t s = s0 + lane;
+  uint32_t n_rec = 0, st_edges = 0, st_echo = 0, st_ops = 0, sends = 0;
+  unsigned long long bkm = 0ull;
+  long long ovmin = LLONG_MAX;
+  uint32_t cb = kInvalid, cbn = 0, cmn = ~0u;
+#pragma unroll 1
+  for (uint32_t il = wv; il < kTS; il += nwv) {
+    const uint4 J = T.job[il][0];
+    if (J.x != epoch) continue;  // (wave-uniform)
+    const uint32_t i = i0 + il;
+    const uint32_t g = rep * N + i;
+    const uint32_t fl = J.y, ne = J.z & 0xFFu, n_bc = (J.z >> 8) & 0xFFu;
+    const bool sl0 = fl & kJSl0, sl1 = fl & kJSl1, sd0 = fl & kJSd0, sd1 = fl & kJSd1, rxe = fl & kJRxe;
+    const bool v = s < N && s != i;
+    const uint32_t le = s < i ? s : s - 1;
+    const uint32_t e = i * N1 + (v ? le : 0u);
+    // the edge's loads together
+    uint64_t* lwp = p.link + edge_loc(p, rep, e);
+    const uint64_t lw0 = v ? *lwp : 0ull;
+    const uint4 r0 = (v && rxe) ? *reinterpret_cast<const uint4*>(p.inbox + inbox_idx(p, ib, rep, e)) : make_uint4(0, 0, 0, 0);
+    uint4 w0 = (v && sl0) ? *eslot_at(p, ob, rep, e) : make_uint4(0, 0, 0, 0);
+    uint4 w1 = (v && sl1) ? *eslot_at(p, obp, rep, e) : make_uint4(0, 0, 0, 0);
+    bool hd0 = false, hd1 = false;
+    if (v && sd0) {
+      const uint32_t rk = tile_rank(p, g, 0, ob, le, hd0);
+      if (hd0) w0 = make_uint4(T.job[il][1].x, T.job[il][1].y, T.job[il][1].z + rk, T.job[il][1].w);
+    }
+    if (v && sd1) {
+      const uint32_t rk = tile_rank(p, g, 1, obp, le, hd1);
+      if (hd1) w1 = make_uint4(T.job[il][2].x, T.job[il][2].y, T.job[il][2].z + rk, T.job[il][2].w);
+    }
+    if (!v) continue;
+    // pending echo descriptors, oldest first, onto the link word
+    int64_t bu = static_cast<int64_t>(lw0 >> 16);
+    uint32_t lc = static_cast<uint32_t>(lw0 & 0xFFFFu);
+    bool pe = false;
+    for (uint32_t d = 0; d < ne; ++d) {
+      const uint32_t* eb = p.ebits + (static_cast<size_t>(g) * kEDesc + d) * p.dwords;
+      if ((eb[le >> 5] >> (le & 31u)) & 1u) {
+        const uint4 q3 = T.job[il][3];
+        const int64_t et = static_cast<int64_t>(d ? ((static_cast<uint64_t>(q3.w) << 32) | q3.z)
+                                                  : ((static_cast<uint64_t>(q3.y) << 32) | q3.x));
+        bu = (bu > et ? bu : et) + p.tx_tot[(fl & (d ? kJBig1 : kJBig0)) ? 1 : 0];
+        pe = true;
+      }
+    }
+    // implicit echo of in-slot le
+    bool he = false;
+    int64_t et = 0;
+    uint32_t edt = 0, esub = 0;
+    int ebig = 0;
+    if (rxe) {
+      const uint32_t rfl = r0.w >> 24;
+      const long long ta0 = cs + r0.x;
+      if (slot_live(rfl, tag) && ta0 >= t_lo && ta0 < t_hi && p.echo) {
+        ebig = (rfl & RF_BIG) ? 1 : 0;
+        const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
+        et = ta0;
+        edt = static_cast<uint32_t>(pin + p.tx_last[ebig]);
+        esub = r0.y;
+        he = true;
+        ++st_echo;
+      }
+    }
+    const int64_t rt1 = static_cast<int64_t>((static_cast<uint64_t>(w0.y) << 32) | w0.x);
+    const int64_t rt2 = static_cast<int64_t>((static_cast<uint64_t>(w1.y) << 32) | w1.x);
+    bool hr = (sl0 || hd0) && rt1 >= t_lo && rt1 < t_hi;
+    bool hr2 = (sl1 || hd1) && rt2 >= t_lo && rt2 < t_hi;
+    st_ops += (hr ? 1u : 0u) + (hr2 ? 1u : 0u);
+    if (n_bc == 0 && !he && !hr && !hr2 && !pe) continue;
+    ++st_edges;
+    const int64_t pr = p.prop_const >= 0 ? p.prop_const : p.prop[e];
+    const uint32_t slot = s * N1 + (i < s ? i : i - 1);
+    const uint32_t dg = rep * N + s;
+    bool in_lds = false;
+    uint32_t bi = 0;
+    for (;;) {
+      while (bi < n_bc && ((T.bc[il][2 * bi + 1].w >> 26) & OPF_PAXOS) && le == 0) ++bi;
+      // the earliest source: 1 broadcast, 2 / 4 reply slots, 3 echo
+      int src = 0;
+      int64_t ot = 0;
+      uint32_t odt = 0, oor = 0, osub = 0, ow2 = 0, ow3 = 0;
+      int big = 0;
+      if (bi < n_bc) {
+        const uint4 a = T.bc[il][2 * bi], bw = T.bc[il][2 * bi + 1];
+        ot = static_cast<int64_t>((static_cast<uint64_t>(a.y) << 32) | a.x);
+        odt = a.z;
+        oor = a.w;
+        osub = bw.x + (((bw.w >> 26) & OPF_PAXOS) ? le - 1 : le);
+        ow2 = bw.z;
+        ow3 = bw.w & 0x00FFFFFFu;
+        big = ((bw.w >> 26) & OPF_BIG) ? 1 : 0;
+        src = 1;
+      }
+      if (hr && (src == 0 || kless(rt1, static_cast<uint32_t>(app), i, w0.z, ot, odt, oor, osub))) {
+        ot = rt1;
+        odt = static_cast<uint32_t>(app);
+        oor = i;
+        osub = w0.z;
+        ow2 = w0.w;
+        ow3 = w3r;
+        big = 0;
+        src = 2;
+      }
+      if (hr2 && (src == 0 || kless(rt2, static_cast<uint32_t>(app), i, w1.z, ot, odt, oor, osub))) {
+        ot = rt2;
+        odt = static_cast<uint32_t>(app);
+        oor = i;
+        osub = w1.z;
+        ow2 = w1.w;
+        ow3 = w3r;
+        big = 0;
+        src = 4;
+      }
+      if (he && (src == 0 || kless(et, edt, s, esub, ot, odt, oor, osub))) {
+        ot = et;
+        big = ebig;
+        src = 3;
+      }
+      if (src == 0) break;
+      if (src == 1)
+        ++bi;
+      else if (src == 2)
+        hr = false;
+      else if (src == 4)
+        hr2 = false;
+      else
+        he = false;
+      if (src == 2 || src == 4) ++sends;
+      const int64_t start = bu > ot ? bu : ot;
+      const int64_t end = start + p.tx_tot[big];
+      bu = end;
+      if (src == 3) continue;  // the echo only occupies the link
+      const int64_t ta = end + pr;
+      long long ca;
+      uint32_t tof;
+      {
+        const int64_t dtf = ta - cs;
+        if (dtf >= 0 && dtf < (1ll << 32)) {  // (floor by the reciprocal, see k_link_mesh)
+          const uint32_t x = static_cast<uint32_t>(dtf);
+          const uint32_t q = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), p.L_magic));
+          ca = cell + q;
+          tof = x - q * L32;
+        } else {
+          ca = ta / p.L;
+          tof = static_cast<uint32_t>(ta - ca * p.L);
+        }
+      }
+      const long long rel = ca - cell;
+      if (rel < 1) {
+        set_err(p, BCSIM_E_TIE);  // lookahead violated
+        continue;
+      }
+      ++n_rec;
+      const uint32_t w3 = ow3 | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24) |
+                          (emit_tag(cq_b, cr_b, rel, B) << 27);
+      const uint4 rv = make_uint4(tof, osub, ow2, w3);
+      const bool owner = lc != (static_cast<uint32_t>(ca) & 0xFFFFu);
+      lc = static_cast<uint32_t>(ca) & 0xFFFFu;
+      if (rel < static_cast<long long>(B)) {
+        uint32_t bk = cr_b + static_cast<uint32_t>(rel);
+        if (bk >= B) bk -= B;
+        if (owner) {
+          if (!in_lds) {  // the edge's first slot record: through the LDS transpose
+            const uint32_t q = tsw(lane, il);
+            T.rec[q] = rv;
+            T.rbk[q] = static_cast<uint8_t>(bk);
+            bkm |= 1ull << bk;
+            in_lds = true;
+          } else {
+            *reinterpret_cast<uint4*>(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox)) = rv;
+            set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
+                              static_cast<uint64_t>(B) * p.R * p.n_tiles));
+          }
+        } else {
+          XRec x;
+          __builtin_memcpy(&x.r, &rv, sizeof rv);
+          x.cell = ca;
+          x.slot = slot;
+          x.g = dg;
+          tile_append(p, bk, x);
+          AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
+        }
+        if (bk != cb) {
+          if (cbn) {
+            atomicAdd(&T.lcnt[cb], cbn);
+            atomicMin(&T.lmin[cb], cmn);
+          }
+          cb = bk;
+          cbn = 0;
+          cmn = ~0u;
+        }
+        ++cbn;
+        if (tof < cmn) cmn = tof;
+      } else {
+        XRec x;
+        __builtin_memcpy(&x.r, &rv, sizeof rv);
+        if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+        x.cell = ca;
+        x.slot = slot;
+        x.g = dg;
+        tile_append(p, B, x);
+        if (ca < ovmin) ovmin = ca;
+      }
+    }
+    if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+    *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
+  }
+  if (cbn) {
+    atomicAdd(&T.lcnt[cb], cbn);
+    atomicMin(&T.lmin[cb], cmn);
+  }
+  // buckets and counters: wave reductions, LDS atomics
+  for (int d = 32; d > 0; d >>= 1) {
+    bkm |= static_cast<unsigned long long>(__shfl_xor(bkm, d, 64));
+    ovmin = min(ovmin, static_cast<long long>(__shfl_xor(ovmin, d, 64)));
+  }
+  {
+    const uint32_t c5[5] = {sends, n_rec, st_ops, st_edges, st_echo};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint32_t ws = wave_sum(c5[k]);
+      if (lane == 0 && ws) atomicAdd(&T.csum[k], ws);
+    }
+  }
+  if (lane == 0) {
+    if (bkm) atomicOr(&T.bkm, bkm);
+    if (ovmin != LLONG_MAX) atomicMin(&T.ovmin, ovmin);
+  }
+  __syncthreads();
+  // the transposed slot records: each receiver's 32 in-slots of this sender tile in one run
+  for (uint32_t x = tid; x < kTR * kTS; x += blockDim.x) {
+    const uint32_t sl = x / kTS, il = x % kTS;
+    const uint32_t q = tsw(sl, il);
+    const uint32_t bk = T.rbk[q];
+    if (bk == 0xFFu) continue;
+    const uint32_t sr = s0 + sl, i = i0 + il;
+    const uint32_t slot = sr * N1 + (i < sr ? i : i - 1);
+    *reinterpret_cast<uint4*>(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox)) = T.rec[q];
+  }
+  if (tid < B && ((T.bkm >> tid) & 1ull))  // receiver-tile flags of the buckets written
+    set_flag_once(&AT(p.rtile, (static_cast<size_t>(tid) * p.R + rep) * p.n_tiles + rt,
+                      static_cast<uint64_t>(B) * p.R * p.n_tiles));
+  for (uint32_t k = tid; k < B; k += blockDim.x)
+    if (T.lcnt[k]) {
+      mark_busy(&p.bucket_cnt[k]);
+      bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + T.lmin[k]);
+    }
+  if (tid == 0) {
+    unsigned long long* cnt = cnt_stripe(p, rep);
+    if (T.csum[0]) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(T.csum[0]));
+    if (T.csum[1]) atomicAdd(&kst_stripe(p)[KST_REC], static_cast<unsigned long long>(T.csum[1]));
+    if (T.csum[2]) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(T.csum[2]));
+    if (T.csum[3]) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(T.csum[3]));
+    if (T.csum[4]) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(T.csum[4]));
+    if (T.ovmin != LLONG_MAX) atomicMin(&p.scal[1], T.ovmin);
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -103,6 +103,7 @@ inline unsigned long long __ballot(int pred) {
 }
 inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
 inline int __popc(unsigned x) { return __builtin_popcount(x); }
+inline unsigned long long __umul64hi(unsigned long long a, unsigned long long b) { return static_cast<unsigned long long>((static_cast<unsigned __int128>(a) * b) >> 64); }
 // lane-exchange / ordering builtins: every lane of the wave must reach them together
 template <typename T>
 inline T __builtin_amdgcn_readlane(T v, int lane) { return __shfl(v, lane); }
