@@ -81,6 +81,14 @@ struct Sim {
   // in launches of at least tile_min nodes (BCSIM_TILE_MIN)
   bool mesh_tile = false;
   uint32_t tile_min = 1, mesh_epoch = 0;
+  // the list-2 overlap (BCSIM_L2_OVERLAP=0: off): k_scan_pbft's leftover nodes are scanned and
+  // linked by the generic kernels on stream2 (parameter block kp_dev2: list 2, its own staging
+  // area) while stream runs everyone else's link stage; joined before the link class ends
+  bool l2_overlap = false;
+  uint32_t win_epoch = 0, l2_pending = 0;
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  KP* kp_dev2 = nullptr;
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -114,6 +122,8 @@ struct Sim {
   uint64_t last_import = 0;      // records k_import placed at the last exchange
   std::vector<int64_t> lead_w; // leader flags packed for the all-reduce
 };
+
+static bool sync_each();
 
 static std::string trail_dump(const Sim& s) {
   std::string out;
@@ -656,7 +666,9 @@ static int setup_device(Sim& s) {
       (rc = dalloc(s, &p.n_ops, NT)))
     return rc;
   if (!s.sparse && p.cap_eidx < p.cap_ops) {  // k_link index area of nodes with > cap_eidx due ops
-    if ((rc = dalloc(s, &p.eidx_g, static_cast<size_t>(s.R) * s.N * p.cap_ops))) return rc;
+    // (per workgroup; the looped grids of the list-2 overlap use rows [kLoopGrid, 2 kLoopGrid))
+    const size_t rows = std::max<size_t>(static_cast<size_t>(s.R) * s.N, 2 * kLoopGrid);
+    if ((rc = dalloc(s, &p.eidx_g, rows * p.cap_ops))) return rc;
   } else {
     p.eidx_g = nullptr;
   }
@@ -730,6 +742,14 @@ static int setup_device(Sim& s) {
       return rc;
     HIPCHK(hipMemset(p.mjob, 0, njob * 4 * 16));  // epoch 0: no job (launch epochs start at 1)
     HIPCHK(hipMemset(p.mtile, 0, (s.mesh_tile ? static_cast<size_t>(s.R) * p.n_stiles : 1) * 4));
+    {
+      const char* lo = std::getenv("BCSIM_L2_OVERLAP");
+      const bool dbg = std::getenv("BCSIM_FDBG") || std::getenv("BCSIM_WGT") || sync_each();
+      s.l2_overlap = s.mesh_tile && s.scan_fast && !dbg && !(lo && *lo == '0');
+    }
+    if ((rc = dalloc(s, &p.l2mark, s.l2_overlap ? NT : 1))) return rc;
+    HIPCHK(hipMemset(p.l2mark, 0, (s.l2_overlap ? NT : 1) * 4));
+    p.loop_list = 3;
   }
   const size_t n_link = p.hubs ? static_cast<size_t>(s.R) * (static_cast<size_t>(p.hubs) * (s.N - 1) +
                                                               static_cast<size_t>(s.N - p.hubs) * p.hubs)
@@ -786,8 +806,8 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &p.bmin, s.B))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
       (rc = dalloc(s, &p.xbuf, p.cap_xbuf)) || (rc = dalloc(s, &p.xgrp, p.cap_x)) ||
-      (rc = dalloc(s, &p.xstage, static_cast<size_t>(s.grid_link) * p.cap_stage)) ||
-      (rc = dalloc(s, &p.xmeta, static_cast<size_t>(s.grid_link) * p.cap_stage)) ||
+      (rc = dalloc(s, &p.xstage, (static_cast<size_t>(s.grid_link) + (s.l2_overlap ? kLoopGrid : 0)) * p.cap_stage)) ||
+      (rc = dalloc(s, &p.xmeta, (static_cast<size_t>(s.grid_link) + (s.l2_overlap ? kLoopGrid : 0)) * p.cap_stage)) ||
       (rc = dalloc(s, &p.ov, p.cap_ov)))
     return rc;
   // active lists of k_scan / k_link (k_active; emptied by k_next / k_pbft_tick)
@@ -937,6 +957,18 @@ static int setup_device(Sim& s) {
   HIPCHK(hipDeviceSynchronize());
   if ((rc = dalloc(s, &s.kp_dev, 1))) return rc;
   HIPCHK(hipMemcpy(s.kp_dev, &s.kp, sizeof(KP), hipMemcpyHostToDevice));
+  if (s.l2_overlap) {  // the second stream's link stage: list 2, staging rows past the first grids
+    KP k2 = s.kp;
+    k2.loop_list = 2;
+    k2.xstage += static_cast<size_t>(s.grid_link) * p.cap_stage;
+    k2.xmeta += static_cast<size_t>(s.grid_link) * p.cap_stage;
+    if (k2.eidx_g) k2.eidx_g += static_cast<size_t>(kLoopGrid) * p.cap_ops;
+    if ((rc = dalloc(s, &s.kp_dev2, 1))) return rc;
+    HIPCHK(hipMemcpy(s.kp_dev2, &k2, sizeof(KP), hipMemcpyHostToDevice));
+    HIPCHK(hipStreamCreateWithFlags(&s.stream2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_fork, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPCHK(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming | hipEventDisableSystemFence));
+  }
   if (!s.sparse && s.P == 1 && c.protocol == BCSIM_PBFT) {
     KP kb = s.kp;
     kb.cap_arr = 2 * s.kp.cap_arr;
@@ -1080,13 +1112,21 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   else if (s.scan_fast && !(lo <= 0 && 0 < hi) && !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi)) {
     // PBFT heavy waves: one pass over each row in registers; the nodes it leaves (list 2) to
     // the generic kernel -- a small looped grid, with the doubled staging window if there is one
-    rc = launch(s, KS_SCAN, k_scan_pbft, grid, dim3(kFastLanes), 0, s.kp_dev, cell, lo, hi, cs, xa);
+    const uint32_t wep = s.l2_overlap ? (++s.win_epoch == 0 ? ++s.win_epoch : s.win_epoch) : 0u;
+    rc = launch(s, KS_SCAN, k_scan_pbft, grid, dim3(kFastLanes), 0, s.kp_dev, cell, lo, hi, cs, xa, wep);
+    if (!rc && wep) {  // fork: list 2 is scanned (and linked, below) on the second stream
+      HIPCHK(hipEventRecord(s.ev_fork, s.stream));
+      HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_fork, 0));
+      std::swap(s.stream, s.stream2);
+      s.l2_pending = wep;
+    }
     if (!rc)
       rc = s.kp_dev_big
-               ? launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false, true>), dim3(std::min<uint32_t>(grid.x, 256)), dim3(1024),
+               ? launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false, true>), dim3(std::min<uint32_t>(grid.x, kLoopGrid)), dim3(1024),
                         s.lds_big, s.kp_dev_big, cell, lo, hi, cs, fw, xa)
                : launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false, true>), dim3(std::min<uint32_t>(grid.x, 512)), block, lds,
                         s.kp_dev, cell, lo, hi, cs, fw, xa);
+    if (wep) std::swap(s.stream, s.stream2);
   } else if (s.sparse && s.cfg.protocol == BCSIM_PAXOS && s.paxos_fast) {
     // sparse Paxos: one lane per node takes the acceptors' request windows; the generic
     // kernel walks the rest (list 2)
@@ -1158,6 +1198,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     }
   }
   grid = dim3(s.sparse ? s.grid_link : (n_link + 7) / 8 * 8);
+  if (grid.x == 0 && s.l2_pending) grid = dim3(8);  // (list 2 is in list 1; the join below must run anyway)
   if (grid.x == 0)
     rc = BCSIM_OK;
   else if (s.sparse && s.paxos_fast && s.kp.qmodel == 0 && s.P == 1) {
@@ -1182,12 +1223,23 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
     // (list 3 holds a few nodes, the leader's cells among them: wide workgroups)
     // (node-partitioned: the kernels that stage records for other ranks)
-    const dim3 gl(std::min<uint32_t>(256, s.grid_link)), bl(std::min<uint32_t>(1024, 4 * s.bs_link));
+    const dim3 gl(std::min<uint32_t>(kLoopGrid, s.grid_link)), bl(std::min<uint32_t>(1024, 4 * s.bs_link));
     const size_t mlds = static_cast<size_t>(s.deg_max) * 8;  // (the PF variant's link words)
-    const uint32_t z = 0;
+    const uint32_t z = 0, wep = s.l2_pending;
+    if (wep) {  // list 2's link stage on the second stream, after its scan there
+      std::swap(s.stream, s.stream2);
+      // (the generic link stage knows no descriptors: flush them first, as k_link_mesh does for the
+      // nodes it hands on)
+      rc = s.kp.desc ? launch(s, -1, k_desc_flush, dim3(std::min<uint32_t>(64, s.grid_link)), dim3(256), 0, s.kp_dev, cell, lo)
+                     : BCSIM_OK;
+      if (!rc) rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev2, cell, lo, hi, fw);
+      std::swap(s.stream, s.stream2);
+      if (rc) return rc;
+      HIPCHK(hipEventRecord(s.ev_join, s.stream2));
+    }
     if (s.P > 1) {
-      if ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<true, 2, true>, grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw, z)
-                          : launch(s, -1, k_link_mesh<true, 2, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, z)) ||
+      if ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<true, 2, true>, grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw, z, z)
+                          : launch(s, -1, k_link_mesh<true, 2, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, z, z)) ||
           (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
     } else if (s.mesh_tile && n_link >= s.tile_min) {
@@ -1195,7 +1247,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       // epoch tells this launch's jobs from stale ones
       const uint32_t ep = ++s.mesh_epoch == 0 ? ++s.mesh_epoch : s.mesh_epoch;
       const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
-      if ((rc = launch(s, -1, (k_link_mesh<false, 2, true, true>), grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw, ep)) ||
+      if ((rc = launch(s, -1, (k_link_mesh<false, 2, true, true>), grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
           (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(256), 0, s.kp_dev, cell, lo, hi, ep)) ||
           (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
@@ -1203,11 +1255,15 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       // (a few nodes -- the leader's block broadcast at a tick -- get 1024-lane workgroups:
       // the launch is one workgroup's latency)
       if ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<false, 2, true>, grid, dim3(n_link <= 64 ? 1024 : 256), mlds,
-                                   s.kp_dev, cell, lo, hi, fw, z)
+                                   s.kp_dev, cell, lo, hi, fw, z, wep)
                           : launch(s, -1, k_link_mesh<false, 2, false>, grid, dim3(n_link <= 64 ? 1024 : 256), 0,
-                                   s.kp_dev, cell, lo, hi, fw, z)) ||
+                                   s.kp_dev, cell, lo, hi, fw, z, wep)) ||
           (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
+    }
+    if (wep) {  // join (inside the timed k_link class: it ends when both streams are done)
+      HIPCHK(hipStreamWaitEvent(s.stream, s.ev_join, 0));
+      s.l2_pending = 0;
     }
     if (timed) {
       if ((rc = ev_end(s))) return rc;
@@ -1834,6 +1890,9 @@ static void destroy(Sim* s) {
   }
   if (s->ctl_h) (void)hipHostFree(s->ctl_h);
   if (s->stream) (void)hipStreamDestroy(s->stream);
+  if (s->stream2) (void)hipStreamDestroy(s->stream2);
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
   delete s->xp;
   delete s;
 }

@@ -131,6 +131,12 @@ struct KP {
   uint16_t* mrp;          // [NT][2][kRpChunks]
   uint32_t* mtile;        // [R][n_stiles]
   uint32_t n_stiles;
+  // list-2 overlap: k_scan_pbft stamps the nodes it leaves to the generic kernels
+  // with the window's epoch; their scan and link stage run on a second stream beside the other
+  // nodes' link stage, which skips them.  loop_list: the list k_link<.., LOOP> walks (3; 2 in
+  // the second stream's parameter block)
+  uint32_t* l2mark;       // [NT]
+  uint32_t loop_list;
   int64_t prop_const;    // propagation delay of every edge, or -1 (per-edge array)
   // links
   uint64_t* link;  // per edge: busy_until << 16 | (arrival cell of the last record & 0xFFFF)
@@ -244,6 +250,7 @@ constexpr uint32_t kEDesc = 2;        // pending echo descriptors per node (LDS:
 constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in this cell / the next
 // tiled mesh link stage: due broadcasts per job, senders x receivers per tile, 64-slot chunks
 constexpr uint32_t kMeshBc = 2, kTS = 32, kTR = 64, kRpChunks = kDescWords / 2;
+constexpr uint32_t kLoopGrid = 256;  // workgroups of the looped generic grids (lists 2, 3) at most
 // job flags (mjob[g][0].y)
 constexpr uint32_t kJSl0 = 1u, kJSl1 = 2u, kJSd0 = 4u, kJSd1 = 8u, kJRxe = 16u, kJBig0 = 32u, kJBig1 = 64u;
 
@@ -2505,7 +2512,7 @@ __device__ inline uint32_t fast_key_find(const FastShared& F, uint32_t key) {
     if (p.wgs && tid == 0) p.wgs[8ull * g + (k)] = __builtin_amdgcn_s_memrealtime();       \
   } while (0)
 __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                   long long t_hi, long long cs, int x_active) {
+                                                   long long t_hi, long long cs, int x_active, uint32_t wep) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ FastShared F;
@@ -2527,6 +2534,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
       !p.impl || !p.eslot || p.delay_mode != BCSIM_DELAY_FIXED) {
     if (tid == 0) {
       AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+      if (wep) AT(p.l2mark, g, p.NT) = wep;
       FDBG(!flag ? 0 : has_ss ? 1 : timer ? 2 : xn ? 3 : (deg > kFastLanes * kFastRPL || deg > p.cap_arr) ? 4 : 5);
     }
     return;
@@ -2671,6 +2679,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   if (F.bad || F.kmin != F.kmax) {
     if (tid == 0) {
       AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+      if (wep) AT(p.l2mark, g, p.NT) = wep;
       FDBG(F.bad ? 6 : 7);
     }
     return;
@@ -4512,8 +4521,9 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (LOOP) {
-    for (ListRange lr = list_range(p.act_n[3]); lr.k < lr.end; lr.k += lr.step) {
-      link_node<QM, XR>(pk, p.act[3ull * p.NT + lr.k], cell, t_lo, t_hi, final_win);
+    const uint32_t ll = p.loop_list;
+    for (ListRange lr = list_range(p.act_n[ll]); lr.k < lr.end; lr.k += lr.step) {
+      link_node<QM, XR>(pk, p.act[static_cast<size_t>(ll) * p.NT + lr.k], cell, t_lo, t_hi, final_win);
       __syncthreads();
     }
     return;
@@ -4647,13 +4657,78 @@ __device__ inline uint32_t desc_rank(const MeshDesc& D, int h, uint32_t le) {
   return D.rp[h][le >> 5] + static_cast<uint32_t>(__popc(D.rb[h][le >> 5] & ((1u << (le & 31u)) - 1u)));
 }
 
+// A node leaving the descriptor-aware kernels for the generic ones (which know no descriptors):
+// its pending echo descriptors go onto the link words, its live reply descriptors into reply
+// slots (the slot flags they stand for).  Block-uniform call.
+__device__ inline void mesh_desc_flush(const KP& p, MeshDesc& D, uint32_t g, uint32_t ob, uint32_t obp, uint32_t sf0,
+                                       uint32_t sf1, const uint4& rd0, const uint4& rd1, bool dl0, bool dl1, uint32_t ne) {
+  const uint32_t tid = tidx();
+  const uint32_t rep = g / p.N, i = g % p.N;
+  mesh_desc_load(p, D, g, ob, obp, dl0, dl1, ne);
+  const uint32_t e0m = AT(p.row, i, p.N + 1), degm = AT(p.row, i + 1, p.N + 1) - e0m;
+  for (uint32_t le = tid; le < degm; le += blockDim.x) {
+    if (ne) {
+      uint64_t* lwp = p.link + edge_loc(p, rep, e0m + le);
+      const uint64_t lw = *lwp;
+      int64_t bu = static_cast<int64_t>(lw >> 16);
+      bool any = false;
+      for (uint32_t d = 0; d < ne; ++d)
+        if (desc_bit(D.eb[d], le)) {
+          bu = (bu > D.et[d] ? bu : D.et[d]) + p.tx_tot[D.ebig[d] ? 1 : 0];
+          any = true;
+        }
+      if (any) {
+        if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
+        *lwp = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
+      }
+    }
+    if (dl0 && desc_bit(D.rb[0], le))
+      *eslot_at(p, ob, rep, e0m + le) = make_uint4(rd0.x, rd0.y, rd0.z + desc_rank(D, 0, le), rd0.w);
+    if (dl1 && desc_bit(D.rb[1], le))
+      *eslot_at(p, obp, rep, e0m + le) = make_uint4(rd1.x, rd1.y, rd1.z + desc_rank(D, 1, le), rd1.w);
+  }
+  if (tid == 0) {
+    if (ne) AT(p.en, g, p.NT) = 0;
+    const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
+    if (sf0 & kSfD)  // kSfD0 -> bit 0, kSfD1 -> bit 1 (dead descriptors just go)
+      AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) =
+          static_cast<uint8_t>((sf0 & ~kSfD) | (dl0 ? ((sf0 >> 4) & 3u) : 0u));
+    if (sf1 & kSfD1)
+      AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4) = static_cast<uint8_t>((sf1 & ~kSfD1) | (dl1 ? 2u : 0u));
+  }
+}
+
+// The list-2 overlap's descriptor flush (second stream, after the generic scan of list 2 and
+// before its generic link stage): mesh_desc_flush for every node of the list with pending echo
+// or live reply descriptors, as k_link_mesh does for the nodes it hands to the generic kernel.
+__global__ __launch_bounds__(256) void k_desc_flush(const KP* __restrict__ pk, long long cell, long long t_lo) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ MeshDesc D;
+  const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
+  const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
+  for (ListRange lr = list_range(p.act_n[2]); lr.k < lr.end; lr.k += lr.step) {
+    const uint32_t g = p.act[2ull * p.NT + lr.k];
+    const uint32_t sf0 = AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4);
+    const uint32_t sf1 = AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4);
+    uint4 rd0 = make_uint4(0, 0, 0, 0), rd1 = make_uint4(0, 0, 0, 0);
+    if (sf0 & kSfD) rd0 = p.rdesc[static_cast<size_t>(ob) * p.NT + g];
+    if (sf1 & kSfD1) rd1 = p.rdesc[static_cast<size_t>(obp) * p.NT + g];
+    const bool dl0 = (sf0 & kSfD) && desc_due(rd0) >= t_lo;
+    const bool dl1 = (sf1 & kSfD1) && desc_due(rd1) >= t_lo;
+    const uint32_t ne = AT(p.en, g, p.NT);
+    if (ne || dl0 || dl1) mesh_desc_flush(p, D, g, ob, obp, sf0, sf1, rd0, rd1, dl0, dl1, ne);
+    __syncthreads();
+  }
+}
+
 // TILE (one rank): a node whose due broadcasts fit a job (<= kMeshBc) leaves its edges to
 // k_mesh_tile -- the job (due broadcasts in key order, reply / echo descriptors, flags) and the
 // node's own bookkeeping (op compaction, counters, slot and descriptor flags) are done here,
 // the per-edge FIFO and the records there, 32 senders x 64 receivers per workgroup.
 template <bool XR, int kMeshU, bool PF, bool TILE = false>
 __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                   long long t_hi, int final_win, uint32_t epoch) {
+                                                   long long t_hi, int final_win, uint32_t epoch, uint32_t wep) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ LinkShared L;
@@ -4661,6 +4736,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   uint32_t kk;
   if (!list_one(p.act_n[1], kk)) return;
   const uint32_t g = p.act[p.NT + kk];
+  if (wep && AT(p.l2mark, g, p.NT) == wep) return;  // left to the generic kernels (second stream)
   const uint32_t tid = tidx();
   const uint32_t n = AT(p.n_ops, g, p.NT);
   const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
@@ -4747,40 +4823,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   if (L.n_list || n_bc > static_cast<uint32_t>(kBcastCap)) {  // not a simple node: the generic kernel
     // which knows no descriptors: the pending echoes go onto the link words, the live reply
     // descriptors into reply slots (the slot flags they stand for)
-    if (ne || dl0 || dl1) {
-      mesh_desc_load(p, D, g, ob, obp, dl0, dl1, ne);
-      const uint32_t e0m = AT(p.row, i, p.N + 1), degm = AT(p.row, i + 1, p.N + 1) - e0m;
-      for (uint32_t le = tid; le < degm; le += blockDim.x) {
-        if (ne) {
-          uint64_t* lwp = p.link + edge_loc(p, rep, e0m + le);
-          const uint64_t lw = *lwp;
-          int64_t bu = static_cast<int64_t>(lw >> 16);
-          bool any = false;
-          for (uint32_t d = 0; d < ne; ++d)
-            if (desc_bit(D.eb[d], le)) {
-              bu = (bu > D.et[d] ? bu : D.et[d]) + p.tx_tot[D.ebig[d] ? 1 : 0];
-              any = true;
-            }
-          if (any) {
-            if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
-            *lwp = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
-          }
-        }
-        if (dl0 && desc_bit(D.rb[0], le))
-          *eslot_at(p, ob, rep, e0m + le) = make_uint4(rd0.x, rd0.y, rd0.z + desc_rank(D, 0, le), rd0.w);
-        if (dl1 && desc_bit(D.rb[1], le))
-          *eslot_at(p, obp, rep, e0m + le) = make_uint4(rd1.x, rd1.y, rd1.z + desc_rank(D, 1, le), rd1.w);
-      }
-      if (tid == 0) {
-        if (ne) AT(p.en, g, p.NT) = 0;
-        const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
-        if (sf0 & kSfD)  // kSfD0 -> bit 0, kSfD1 -> bit 1 (dead descriptors just go)
-          AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) =
-              static_cast<uint8_t>((sf0 & ~kSfD) | (dl0 ? ((sf0 >> 4) & 3u) : 0u));
-        if (sf1 & kSfD1)
-          AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4) = static_cast<uint8_t>((sf1 & ~kSfD1) | (dl1 ? 2u : 0u));
-      }
-    }
+    if (ne || dl0 || dl1) mesh_desc_flush(p, D, g, ob, obp, sf0, sf1, rd0, rd1, dl0, dl1, ne);
     if (tid == 0) {
       const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
       AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;

@@ -181,10 +181,11 @@ hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t
 hipError_t hipMemset(void*, int, size_t);
 hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t);
 hipError_t hipEventCreate(hipEvent_t*);
-enum { hipEventDisableSystemFence = 0x20000000 };
+enum { hipEventDisableSystemFence = 0x20000000, hipEventDisableTiming = 0x2 };
 inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { return hipEventCreate(e); }
 hipError_t hipEventDestroy(hipEvent_t);
 hipError_t hipEventRecord(hipEvent_t, hipStream_t);
+inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }  // (streams run in issue order)
 hipError_t hipEventElapsedTime(float*, hipEvent_t, hipEvent_t);
 hipError_t hipGetLastError();
 hipError_t hipFuncSetAttribute(const void*, hipFuncAttribute, int);
