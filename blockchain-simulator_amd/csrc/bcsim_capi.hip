@@ -727,17 +727,16 @@ static int setup_device(Sim& s) {
       return rc;
     HIPCHK(hipMemset(p.rdesc, 0xFF, (p.desc ? static_cast<size_t>(kOpRing) * NT : 1) * 16));  // due -1: sent
     HIPCHK(hipMemset(p.en, 0, p.desc ? NT : 1));
-    // the tiled mesh link stage: one rank, the LDS-parked variant of k_link_mesh
-    // as its classify stage, degree <= 4096 (the reply bitmaps' rank prefixes: kRpChunks)
+    // the tiled mesh link stage: one rank, degree <= 4096 (the descriptor bitmaps)
     {
       const char* mt = std::getenv("BCSIM_MESH_TILE");
-      s.mesh_tile = s.mesh_link && s.mesh_pf && s.P == 1 && s.deg_max <= 64 * kRpChunks && !(mt && *mt == '0');
+      s.mesh_tile = s.mesh_link && s.mesh_pf && s.P == 1 && s.deg_max <= 32 * kDescWords && !(mt && *mt == '0');
       if (const char* tm = std::getenv("BCSIM_TILE_MIN"); tm && *tm) s.tile_min = static_cast<uint32_t>(std::atoi(tm));
     }
     p.n_stiles = (s.N + kTS - 1) / kTS;
     const size_t njob = s.mesh_tile ? NT : 1;
     if ((rc = dalloc(s, &p.mjob, njob * 4)) || (rc = dalloc(s, &p.mbc, njob * kMeshBc * 2)) ||
-        (rc = dalloc(s, &p.mrp, njob * 2 * kRpChunks)) ||
+        (rc = dalloc(s, &p.mtb, njob * p.n_tiles * 2)) || (rc = dalloc(s, &p.mte, njob * p.n_tiles * kEDesc)) ||
         (rc = dalloc(s, &p.mtile, s.mesh_tile ? static_cast<size_t>(s.R) * p.n_stiles : 1)))
       return rc;
     HIPCHK(hipMemset(p.mjob, 0, njob * 4 * 16));  // epoch 0: no job (launch epochs start at 1)
@@ -937,10 +936,14 @@ static int setup_device(Sim& s) {
   }
   if (const char* wv = std::getenv("BCSIM_WGT"); wv && *wv == '1') {  // debug: k_link per-WG timing
     if ((rc = dalloc(s, &p.wgt, NT * 8)) || (rc = dalloc(s, &p.wgs, NT * 8))) return rc;
+    const size_t ntw = static_cast<size_t>(s.R) * p.n_stiles * p.n_tiles;
+    if ((rc = dalloc(s, &p.wgtt, ntw * 8))) return rc;
+    HIPCHK(hipMemset(p.wgtt, 0, ntw * 64));
     HIPCHK(hipMemset(p.wgt, 0, NT * 64));
     HIPCHK(hipMemset(p.wgs, 0, NT * 64));
   }
   p.dbg_tmax = LLONG_MIN;
+  if (const char* xv = std::getenv("BCSIM_EXP"); xv && *xv) p.exp = static_cast<uint32_t>(std::strtol(xv, nullptr, 0));
   if (const char* fv = std::getenv("BCSIM_DBG_FAIL_CELL"); fv && *fv) s.dbg_fail_cell = std::atoll(fv);
   if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
   std::vector<long long> big_ll(NT, LLONG_MAX);
@@ -1040,6 +1043,53 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
   return BCSIM_OK;
 }
 #define launch(s, cls, kernel, ...) launch_named(s, #kernel, cls, kernel, __VA_ARGS__)
+
+// debug (BCSIM_WGT=1): k_mesh_tile phase clocks of a launch (100 MHz s_memrealtime): span, mean
+// per phase over the workgroups that had jobs, and how many were running at each 10 us
+static int tile_phase_report(Sim& s, long long cell, uint32_t nt) {
+  std::vector<unsigned long long> w(8ull * nt);
+  HIPCHK(hipStreamSynchronize(s.stream));
+  HIPCHK(hipMemcpy(w.data(), s.kp.wgtt, w.size() * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(s.kp.wgtt, 0, w.size() * 8));
+  unsigned long long t0 = ~0ull, t1 = 0;
+  double m[5] = {0, 0, 0, 0, 0};
+  uint32_t n = 0;
+  for (uint32_t b = 0; b < nt; ++b) {
+    const unsigned long long* q = &w[8ull * b];
+    if (!q[0] || !q[5]) continue;
+    ++n;
+    t0 = std::min(t0, q[0]);
+    t1 = std::max(t1, q[5]);
+    for (int k = 0; k < 5; ++k) m[k] += static_cast<double>(q[k + 1] - q[k]);
+  }
+  if (!n || t1 - t0 < 5000) return BCSIM_OK;
+  std::fprintf(stderr, "[tile] cell %lld span %.1f us, %u WGs, mean us: prologue %.2f lw %.2f edges %.2f barrier %.2f out %.2f; running per 10 us:",
+               cell, (t1 - t0) / 100.0, n, m[0] / n / 100, m[1] / n / 100, m[2] / n / 100, m[3] / n / 100, m[4] / n / 100);
+  for (unsigned long long t = t0; t < t1; t += 1000) {
+    uint32_t r = 0;
+    for (uint32_t b = 0; b < nt; ++b) {
+      const unsigned long long* q = &w[8ull * b];
+      if (q[0] && q[5] && q[0] <= t + 500 && q[5] >= t + 500) ++r;
+    }
+    std::fprintf(stderr, " %u", r);
+  }
+  std::fprintf(stderr, "\n");
+  std::vector<uint32_t> idx;
+  for (uint32_t b = 0; b < nt; ++b)
+    if (w[8ull * b] && w[8ull * b + 5]) idx.push_back(b);
+  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return w[8ull * a + 5] > w[8ull * b + 5]; });
+  std::fprintf(stderr, "[tile]   last to finish:");
+  for (size_t k = 0; k < std::min<size_t>(6, idx.size()); ++k) {
+    const unsigned long long* q = &w[8ull * idx[k]];
+    const uint32_t rem = idx[k] % (s.kp.n_stiles * s.kp.n_tiles);
+    std::fprintf(stderr, " [st %u rt %u start +%.1f total %.1f:", rem / s.kp.n_tiles, rem % s.kp.n_tiles, (q[0] - t0) / 100.0,
+                 (q[5] - q[0]) / 100.0);
+    for (int j = 0; j < 5; ++j) std::fprintf(stderr, " %.1f", (q[j + 1] - q[j]) / 100.0);
+    std::fprintf(stderr, "]");
+  }
+  std::fprintf(stderr, "\n");
+  return BCSIM_OK;
+}
 
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
@@ -1228,11 +1278,9 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     const uint32_t z = 0, wep = s.l2_pending;
     if (wep) {  // list 2's link stage on the second stream, after its scan there
       std::swap(s.stream, s.stream2);
-      // (the generic link stage knows no descriptors: flush them first, as k_link_mesh does for the
+      // (the generic link stage flushes the nodes' descriptors first, as k_link_mesh does for the
       // nodes it hands on)
-      rc = s.kp.desc ? launch(s, -1, k_desc_flush, dim3(std::min<uint32_t>(64, s.grid_link)), dim3(256), 0, s.kp_dev, cell, lo)
-                     : BCSIM_OK;
-      if (!rc) rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev2, cell, lo, hi, fw);
+      rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev2, cell, lo, hi, fw);
       std::swap(s.stream, s.stream2);
       if (rc) return rc;
       HIPCHK(hipEventRecord(s.ev_join, s.stream2));
@@ -1247,8 +1295,9 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       // epoch tells this launch's jobs from stale ones
       const uint32_t ep = ++s.mesh_epoch == 0 ? ++s.mesh_epoch : s.mesh_epoch;
       const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
-      if ((rc = launch(s, -1, (k_link_mesh<false, 2, true, true>), grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
-          (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(256), 0, s.kp_dev, cell, lo, hi, ep)) ||
+      if ((rc = launch(s, -1, k_mesh_prep, grid, dim3(64), 0, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
+          (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(512), 0, s.kp_dev, cell, lo, hi, ep)) ||
+          (s.kp.wgtt && (rc = tile_phase_report(s, cell, nt))) ||
           (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
     } else {

@@ -122,13 +122,15 @@ struct KP {
   uint4* edesc;           // [NT][kEDesc] {t lo, t hi, big, 0}
   uint32_t* ebits;        // [NT][kEDesc][dwords]
   uint8_t* en;            // [NT] pending echo descriptors
-  // full-mesh tiled link stage (k_mesh_tile): the job k_link_mesh<TILE> leaves per
-  // gnode -- {epoch, flags, ne | n_bc << 8, 0}, the two reply descriptors, the pending echo times --
-  // its due broadcasts in key order (RawOp words), the reply bitmaps' rank prefixes per 64-slot
-  // chunk, and per (replica, 32-sender tile) the epoch of the last launch that left a job in it
+  // full-mesh tiled link stage (k_mesh_prep -> k_mesh_tile): the job k_mesh_prep
+  // leaves per gnode -- {epoch, flags, ne | n_bc << 8, 0}, the two reply descriptors, the pending
+  // echo times -- its due broadcasts in key order (RawOp words), its descriptor bitmaps cut into
+  // 64-receiver tiles (bit k = receiver tile base + k), and per (replica, 32-sender tile) the epoch
+  // of the last launch that left a job in it
   uint4* mjob;            // [NT][4]
   uint4* mbc;             // [NT][kMeshBc][2]
-  uint16_t* mrp;          // [NT][2][kRpChunks]
+  uint4* mtb;             // [NT][n_tiles][2] reply bitmaps per receiver tile: {mask lo, mask hi, rank base, 0}
+  uint2* mte;             // [NT][n_tiles][kEDesc] pending echo bitmaps per receiver tile
   uint32_t* mtile;        // [R][n_stiles]
   uint32_t n_stiles;
   // list-2 overlap: k_scan_pbft stamps the nodes it leaves to the generic kernels
@@ -208,6 +210,8 @@ struct KP {
   int32_t* dbg;  // first error's source line
   unsigned long long* trail;  // BCSIM_CHECKED + BCSIM_TRAIL: host-mapped breadcrumbs
   unsigned long long* wgt;    // BCSIM_WGT: per-workgroup k_link timing [NT][8] (debug)
+  unsigned long long* wgtt;   // BCSIM_WGT: per-workgroup k_mesh_tile phase clocks [tiles][8] (debug)
+  uint32_t exp;               // BCSIM_EXP: performance experiments that break results (debug, never in tests)
   unsigned long long* wgs;    // BCSIM_WGT: per-workgroup k_scan phase timing [NT][8] (debug)
   unsigned long long* fdbg;   // BCSIM_FDBG: why nodes leave the fast kernels [16] (debug; see FDBG)
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
@@ -249,7 +253,7 @@ constexpr uint32_t kEDesc = 2;        // pending echo descriptors per node (LDS:
 // sflag bits of a reply descriptor of the arrival cell (bits 0..3: reply slots due in cell + k)
 constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in this cell / the next
 // tiled mesh link stage: due broadcasts per job, senders x receivers per tile, 64-slot chunks
-constexpr uint32_t kMeshBc = 2, kTS = 32, kTR = 64, kRpChunks = kDescWords / 2;
+constexpr uint32_t kMeshBc = 2, kTS = 32, kTR = 64;
 constexpr uint32_t kLoopGrid = 256;  // workgroups of the looped generic grids (lists 2, 3) at most
 // job flags (mjob[g][0].y)
 constexpr uint32_t kJSl0 = 1u, kJSl1 = 2u, kJSd0 = 4u, kJSd1 = 8u, kJRxe = 16u, kJBig0 = 32u, kJBig1 = 64u;
@@ -4515,6 +4519,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
 }
 
 // LOOP: a small grid walks list 3 (the nodes k_gossip_link left over)
+__device__ void node_desc_flush(const KP& p, uint32_t g, long long cell, long long t_lo);
 template <int QM, bool XR, bool LOOP = false>
 __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                               long long t_hi, int final_win) {
@@ -4523,7 +4528,14 @@ __global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long l
   if (LOOP) {
     const uint32_t ll = p.loop_list;
     for (ListRange lr = list_range(p.act_n[ll]); lr.k < lr.end; lr.k += lr.step) {
-      link_node<QM, XR>(pk, p.act[static_cast<size_t>(ll) * p.NT + lr.k], cell, t_lo, t_hi, final_win);
+      const uint32_t g = p.act[static_cast<size_t>(ll) * p.NT + lr.k];
+      // (the nodes the descriptor-aware kernels handed on: their descriptors first, as
+      // pending echoes on the link words and reply slots -- this kernel knows no descriptors)
+      if (!QM && !XR && p.desc) {
+        node_desc_flush(p, g, cell, t_lo);
+        __syncthreads();
+      }
+      link_node<QM, XR>(pk, g, cell, t_lo, t_hi, final_win);
       __syncthreads();
     }
     return;
@@ -4698,35 +4710,26 @@ __device__ inline void mesh_desc_flush(const KP& p, MeshDesc& D, uint32_t g, uin
   }
 }
 
-// The list-2 overlap's descriptor flush (second stream, after the generic scan of list 2 and
-// before its generic link stage): mesh_desc_flush for every node of the list with pending echo
-// or live reply descriptors, as k_link_mesh does for the nodes it hands to the generic kernel.
-__global__ __launch_bounds__(256) void k_desc_flush(const KP* __restrict__ pk, long long cell, long long t_lo) {
-  const KP& p = *pk;
-  BAIL_IF_ERR();
+// The descriptor flush of a node handed to the generic link kernel (k_link<.., LOOP> over list 2 --
+// the list-2 overlap -- and list 3 -- the nodes k_mesh_prep left): mesh_desc_flush if it has
+// pending echo or live reply descriptors, as k_link_mesh does for the nodes it hands on.
+// Block-uniform call.
+__device__ void node_desc_flush(const KP& p, uint32_t g, long long cell, long long t_lo) {
   __shared__ MeshDesc D;
   const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
   const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
-  for (ListRange lr = list_range(p.act_n[2]); lr.k < lr.end; lr.k += lr.step) {
-    const uint32_t g = p.act[2ull * p.NT + lr.k];
-    const uint32_t sf0 = AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4);
-    const uint32_t sf1 = AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4);
-    uint4 rd0 = make_uint4(0, 0, 0, 0), rd1 = make_uint4(0, 0, 0, 0);
-    if (sf0 & kSfD) rd0 = p.rdesc[static_cast<size_t>(ob) * p.NT + g];
-    if (sf1 & kSfD1) rd1 = p.rdesc[static_cast<size_t>(obp) * p.NT + g];
-    const bool dl0 = (sf0 & kSfD) && desc_due(rd0) >= t_lo;
-    const bool dl1 = (sf1 & kSfD1) && desc_due(rd1) >= t_lo;
-    const uint32_t ne = AT(p.en, g, p.NT);
-    if (ne || dl0 || dl1) mesh_desc_flush(p, D, g, ob, obp, sf0, sf1, rd0, rd1, dl0, dl1, ne);
-    __syncthreads();
-  }
+  const uint32_t sf0 = AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4);
+  const uint32_t sf1 = AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4);
+  uint4 rd0 = make_uint4(0, 0, 0, 0), rd1 = make_uint4(0, 0, 0, 0);
+  if (sf0 & kSfD) rd0 = p.rdesc[static_cast<size_t>(ob) * p.NT + g];
+  if (sf1 & kSfD1) rd1 = p.rdesc[static_cast<size_t>(obp) * p.NT + g];
+  const bool dl0 = (sf0 & kSfD) && desc_due(rd0) >= t_lo;
+  const bool dl1 = (sf1 & kSfD1) && desc_due(rd1) >= t_lo;
+  const uint32_t ne = AT(p.en, g, p.NT);
+  if (ne || dl0 || dl1) mesh_desc_flush(p, D, g, ob, obp, sf0, sf1, rd0, rd1, dl0, dl1, ne);
 }
 
-// TILE (one rank): a node whose due broadcasts fit a job (<= kMeshBc) leaves its edges to
-// k_mesh_tile -- the job (due broadcasts in key order, reply / echo descriptors, flags) and the
-// node's own bookkeeping (op compaction, counters, slot and descriptor flags) are done here,
-// the per-edge FIFO and the records there, 32 senders x 64 receivers per workgroup.
-template <bool XR, int kMeshU, bool PF, bool TILE = false>
+template <bool XR, int kMeshU, bool PF>
 __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                    long long t_hi, int final_win, uint32_t epoch, uint32_t wep) {
   const KP& p = *pk;
@@ -4849,67 +4852,6 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
     }
   }
   __syncthreads();
-
-  if (TILE && n_bc <= kMeshBc) {
-    // the edges go to k_mesh_tile: the job, then this node's own bookkeeping
-    const bool any = n_bc || sl0 || sl1 || sd0 || sd1 || rxe;
-    const uint32_t ne_j = any ? ne : 0u;  // pending echo descriptors: applied by the tile
-    if (any) {
-      const size_t jb = static_cast<size_t>(g) * kMeshBc * 2;
-      if (tid < 2 * n_bc) p.mbc[jb + tid] = reinterpret_cast<const uint4*>(&L.bco[tid >> 1])[tid & 1u];
-      // rank prefixes of the live reply bitmaps per 64-slot chunk (wave 0, a chunk per lane)
-      if (tid < 64 && (sd0 || sd1)) {
-        const uint32_t dw = p.dwords;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          if (!(h ? sd1 : sd0)) continue;
-          const uint32_t* rb = p.rbits + (static_cast<size_t>(h ? obp : ob) * p.NT + g) * dw;
-          const uint32_t k = 2 * tid;
-          const uint32_t c = (k < dw ? static_cast<uint32_t>(__popc(rb[k])) : 0u) +
-                             (k + 1 < dw ? static_cast<uint32_t>(__popc(rb[k + 1])) : 0u);
-          uint32_t in = c;
-#pragma unroll
-          for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t v = __shfl_up(in, off, 64);
-            if (tid >= static_cast<uint32_t>(off)) in += v;
-          }
-          if (tid < kRpChunks) p.mrp[(static_cast<size_t>(g) * 2 + h) * kRpChunks + tid] = static_cast<uint16_t>(in - c);
-        }
-      }
-      if (tid == 0) {
-        uint32_t fl = (sl0 ? kJSl0 : 0u) | (sl1 ? kJSl1 : 0u) | (sd0 ? kJSd0 : 0u) | (sd1 ? kJSd1 : 0u) | (rxe ? kJRxe : 0u);
-        uint4 q3 = make_uint4(0, 0, 0, 0);
-        if (ne_j) {
-          const uint4 ed0 = p.edesc[static_cast<size_t>(g) * kEDesc];
-          q3.x = ed0.x;
-          q3.y = ed0.y;
-          if (ed0.z) fl |= kJBig0;
-          if (ne_j > 1) {
-            const uint4 ed1 = p.edesc[static_cast<size_t>(g) * kEDesc + 1];
-            q3.z = ed1.x;
-            q3.w = ed1.y;
-            if (ed1.z) fl |= kJBig1;
-          }
-        }
-        uint4* J = p.mjob + static_cast<size_t>(g) * 4;
-        J[1] = rd0;
-        J[2] = rd1;
-        J[3] = q3;
-        J[0] = make_uint4(epoch, fl, ne_j | (n_bc << 8), 0u);
-        p.mtile[static_cast<size_t>(rep) * p.n_stiles + i / kTS] = epoch;
-      }
-    }
-    if (tid == 0) {  // (as after the edge walk below)
-      if (ne_j) AT(p.en, g, p.NT) = 0;
-      const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
-      if (sd0) AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) = static_cast<uint8_t>(sf0 & ~kSfD0);
-      if (sd1) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4) = static_cast<uint8_t>(sf1 & ~kSfD1);
-    }
-    const LinkCounts c8{dropped, sends, 0u, st_ops, 0u, 0u, 0u, 0u};
-    link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, n_lists, LLONG_MAX, c8, (sl1 || sd1) && final_win,
-                rx && final_win, obp, fidx, p.wgt ? wg_t0 : 0ull, ph, n);
-    return;
-  }
 
   // ---- per out-edge: merge broadcasts / reply slots / implicit echo in key order, FIFO, emit ----
   uint32_t n_rec = 0, st_edges = 0, st_echo = 0;
@@ -5251,66 +5193,248 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
 }
 
 // ---------------------------------------------------------------------------
-// k_mesh_tile (full mesh, one rank, fixed app delay, infinite queues): the edge walk of the
-// jobs k_link_mesh<TILE> left, for a tile of 32 senders x 64 receivers per workgroup.  The same
-// per-edge work as k_link_mesh's edge loop (the pending echo descriptors onto the link word, then
-// the due broadcasts, reply slots / descriptors and implicit echo merged in key order through
-// the FIFO, pbft-node.cc:349-368 fan-out, :175 echo), but the memory side is coalesced both
-// ways: a wave walks one sender's 64 out-edges to the tile's receivers (link words, own inbox
-// row and reply slots are 64 consecutive words of the sender's row), and the records are
-// transposed in LDS and written receiver by receiver -- 32 consecutive in-slots (512 B) of each
-// receiver's row instead of 64 scattered 16-byte stores 64 KB apart.  A record that is not the
-// edge's first slot record of the launch is stored directly; extras / overflow records are
-// appended to their lists with one atomic each (rare: the heavy waves are one record per edge).
+// The tiled full-mesh link stage (one rank, fixed app delay, infinite queues):
+//   k_mesh_prep   one wave per active node: classify its due ops (pbft-node.cc:349-368
+//                 broadcasts, the reply descriptors of k_scan_pbft, :212-222), leave a job for the
+//                 tiles -- the due broadcasts in key order, flags, descriptor times and the
+//                 descriptor bitmaps cut into 64-receiver tiles -- and do the node's own bookkeeping
+//                 (op compaction, counters, slot / descriptor flags); a node whose due ops are not
+//                 all broadcasts (or more than kMeshBc) goes to list 3 (generic kernel)
+//   k_mesh_tile   32 senders x 64 receivers per workgroup: the per-edge FIFO and records
+//   k_link<.., LOOP> over list 3 (descriptors flushed first: node_desc_flush)
+// Same results as k_link_mesh's edge walk.
+
+// bits [a, a + 64) of a descriptor bitmap held in LDS (words >= dw read as 0)
+__device__ inline uint64_t bits64(const uint32_t* w, uint32_t dw, uint32_t a) {
+  const uint32_t q = a >> 5, r = a & 31u;
+  const uint64_t w0 = q < dw ? w[q] : 0u, w1 = q + 1 < dw ? w[q + 1] : 0u, w2 = q + 2 < dw ? w[q + 2] : 0u;
+  const uint64_t lo = w0 | (w1 << 32);
+  return r ? (lo >> r) | (w2 << (64 - r)) : lo;
+}
+// the bitmap of sender i's out-edges cut to receiver tile s0 .. s0 + 63: bit k = out-edge to
+// receiver s0 + k (the full mesh's out-edge index le = s - (s > i), no bit for s == i or s >= N)
+__device__ inline uint64_t tile_mask(const uint32_t* w, uint32_t dw, uint32_t i, uint32_t s0, uint32_t N) {
+  uint64_t m;
+  if (i < s0) {
+    m = bits64(w, dw, s0 - 1);
+  } else if (i >= s0 + 64) {
+    m = bits64(w, dw, s0);
+  } else {
+    const uint32_t j = i - s0;
+    const uint64_t A = bits64(w, dw, s0);
+    const uint64_t below = j ? (~0ull >> (64 - j)) : 0ull;  // bits < j
+    m = (A & below) | ((A << 1) & ~below & ~(1ull << j));
+  }
+  const uint32_t nv = N - s0;  // receivers of the tile that exist
+  return nv >= 64 ? m : (m & ((1ull << nv) - 1ull));
+}
+
+__global__ __launch_bounds__(64) void k_mesh_prep(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
+                                                  int final_win, uint32_t epoch, uint32_t wep) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ LinkShared L;
+  __shared__ MeshDesc D;
+  uint32_t kk;
+  if (!list_one(p.act_n[1], kk)) return;
+  const uint32_t g = p.act[p.NT + kk];
+  if (wep && AT(p.l2mark, g, p.NT) == wep) return;  // left to the generic kernels (second stream)
+  const uint32_t tid = tidx();
+  const uint32_t n = AT(p.n_ops, g, p.NT);
+  const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
+  const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
+  const uint32_t sf0 = AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4);
+  const uint32_t sf1 = AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4);
+  const bool sl0 = sf0 & 1u, sl1 = sf1 & 2u;
+  const bool dsc = p.desc != 0;
+  uint4 rd0 = make_uint4(0, 0, 0, 0), rd1 = make_uint4(0, 0, 0, 0);
+  if (dsc && (sf0 & kSfD)) rd0 = p.rdesc[static_cast<size_t>(ob) * p.NT + g];
+  if (dsc && (sf1 & kSfD1)) rd1 = p.rdesc[static_cast<size_t>(obp) * p.NT + g];
+  const bool dl0 = dsc && (sf0 & kSfD) && desc_due(rd0) >= t_lo;
+  const bool dl1 = dsc && (sf1 & kSfD1) && desc_due(rd1) >= t_lo;
+  const bool sd0 = dl0 && desc_due(rd0) < t_hi, sd1 = dl1 && desc_due(rd1) < t_hi;
+  const uint32_t ne = dsc ? AT(p.en, g, p.NT) : 0u;
+  const uint32_t B = p.n_buckets;
+  const uint32_t ib = static_cast<uint32_t>(cell % B);
+  const size_t fidx = static_cast<size_t>(ib) * p.NT + g;
+  const uint32_t rep = g / p.N, i = g % p.N;
+  const bool rx = p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
+  const bool rxe = rx && AT(p.eapp, g, p.NT) != t_lo;
+  if ((n == 0 || AT(p.node_onext, g, p.NT) >= t_hi) && !sl0 && !sl1 && !sd0 && !sd1 && !rxe) {
+    if (rx && final_win && tid == 0) AT(p.iflag, fidx, static_cast<uint64_t>(B) * p.NT) = 0;
+    return;
+  }
+  for (uint32_t k = tid; k < B; k += blockDim.x) {
+    L.lcnt[k] = 0;
+    L.lmin[k] = ~0u;
+  }
+  const uint32_t n_lists = B + 1;
+  for (uint32_t k = tid; k < n_lists; k += blockDim.x) L.lst[k] = 0;
+  if (tid < 8) L.csum[tid] = 0;
+  if (tid == 0) {
+    L.n_bc = 0;
+    L.n_list = 0;
+    L.nst = 0;
+    L.omin = LLONG_MAX;
+    L.ovmin = LLONG_MAX;
+  }
+  __syncthreads();
+  const uint32_t deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
+  Op* ops = p.ops + op_base(p, g);
+  uint32_t sends = 0, st_ops = 0, other = 0;
+  for (uint32_t k = tid; k < n; k += blockDim.x) {
+    const RawOp o = ld_raw(&ops[k]);
+    const uint32_t kind = raw_kind(o);
+    if (kind == OP_BCAST_J) {
+      other += (raw_flags(o) & OPF_DONE) ? 0u : 1u;
+      continue;
+    }
+    if (raw_t(o) >= t_hi) continue;
+    if (kind != OP_BCAST || (raw_flags(o) & OPF_PAXOS)) {  // (Paxos broadcasts: k_link_mesh / generic)
+      ++other;
+      continue;
+    }
+    ++st_ops;
+    const uint32_t pos = atomicAdd(&L.n_bc, 1u);
+    if (pos < kBcastCap) L.bc[pos] = k;
+    sends += deg;
+  }
+  {
+    const uint32_t ws = wave_sum(other);
+    if (tid == 0 && ws) L.n_list = ws;
+  }
+  __syncthreads();
+  const uint32_t n_bc = L.n_bc;
+  if (L.n_list || n_bc > kMeshBc) {  // the generic kernel takes the node (node_desc_flush first)
+    if (tid == 0) {
+      const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
+      AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
+    }
+    return;
+  }
+  // the due broadcasts in key order (<= 2), as RawOp words
+  const size_t jb = static_cast<size_t>(g) * kMeshBc * 2;
+  if (tid < 2 * n_bc) {
+    uint32_t k = tid >> 1;
+    if (n_bc == 2) {
+      const RawOp a = ld_raw(&ops[L.bc[0]]), b = ld_raw(&ops[L.bc[1]]);
+      const bool swap = raw_key_less(b, raw_sub(b), a, raw_sub(a));
+      k = swap ? 1u - k : k;
+    }
+    p.mbc[jb + tid] = reinterpret_cast<const uint4*>(&ops[L.bc[k]])[tid & 1u];
+  }
+  // descriptor bitmaps cut to receiver tiles (lane = tile)
+  const uint32_t ne_j = ne;  // (every edge is walked: any pending echo descriptor is applied)
+  if (sd0 || sd1 || ne_j) {
+    mesh_desc_load(p, D, g, ob, obp, sd0, sd1, ne_j);
+    const uint32_t dw = p.dwords, nt = p.n_tiles;
+    for (uint32_t rt = tid; rt < nt; rt += blockDim.x) {
+      const uint32_t s0 = rt * kTR;
+      const uint32_t le0 = s0 > i ? s0 - 1 : s0;  // out-edge index of the tile's first receiver
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (!(h ? sd1 : sd0)) continue;
+        const uint64_t m = tile_mask(D.rb[h], dw, i, s0, p.N);
+        const uint32_t base = le0 < deg ? desc_rank(D, h, le0) : 0u;
+        p.mtb[(static_cast<size_t>(g) * nt + rt) * 2 + h] =
+            make_uint4(static_cast<uint32_t>(m), static_cast<uint32_t>(m >> 32), base, 0u);
+      }
+      for (uint32_t d = 0; d < ne_j; ++d) {
+        const uint64_t m = tile_mask(D.eb[d], dw, i, s0, p.N);
+        p.mte[(static_cast<size_t>(g) * nt + rt) * kEDesc + d] = make_uint2(static_cast<uint32_t>(m), static_cast<uint32_t>(m >> 32));
+      }
+    }
+  }
+  if (tid == 0) {
+    uint32_t fl = (sl0 ? kJSl0 : 0u) | (sl1 ? kJSl1 : 0u) | (sd0 ? kJSd0 : 0u) | (sd1 ? kJSd1 : 0u) | (rxe ? kJRxe : 0u);
+    uint4 q3 = make_uint4(0, 0, 0, 0);
+    if (ne_j) {
+      const uint4 ed0 = p.edesc[static_cast<size_t>(g) * kEDesc];
+      q3.x = ed0.x;
+      q3.y = ed0.y;
+      if (ed0.z) fl |= kJBig0;
+      if (ne_j > 1) {
+        const uint4 ed1 = p.edesc[static_cast<size_t>(g) * kEDesc + 1];
+        q3.z = ed1.x;
+        q3.w = ed1.y;
+        if (ed1.z) fl |= kJBig1;
+      }
+    }
+    uint4* J = p.mjob + static_cast<size_t>(g) * 4;
+    J[1] = rd0;
+    J[2] = rd1;
+    J[3] = q3;
+    J[0] = make_uint4(epoch, fl, ne_j | (n_bc << 8), 0u);
+    p.mtile[static_cast<size_t>(rep) * p.n_stiles + i / kTS] = epoch;
+    if (ne_j) AT(p.en, g, p.NT) = 0;
+    // a due reply descriptor is sent whole: its flag goes (as in k_link_mesh)
+    if (sd0) AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) = static_cast<uint8_t>(sf0 & ~kSfD0);
+    if (sd1) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4) = static_cast<uint8_t>(sf1 & ~kSfD1);
+  }
+  unsigned long long ph[4] = {0, 0, 0, 0};
+  const LinkCounts c8{0u, sends, 0u, st_ops, 0u, 0u, 0u, 0u};
+  link_finish(p, L, g, ops, n_bc == n ? 0u : n, t_hi, n_lists, LLONG_MAX, c8, (sl1 || sd1) && final_win, rx && final_win,
+              obp, fidx, 0ull, ph, n);
+}
+
+// k_mesh_tile: the edges of the jobs k_mesh_prep left, for a tile of 32 senders x 64 receivers
+// per workgroup.  The same per-edge work as k_link_mesh's edge loop (the pending echo
+// descriptors onto the link word, then the due broadcasts, reply slots / descriptors and the
+// implicit echo merged in key order through the FIFO, pbft-node.cc:349-368 fan-out, :175
+// echo), but the memory side is coalesced both ways: a wave walks one sender's out-edges to the
+// tile's 64 receivers (link words, own inbox row and reply slots are 64 consecutive words of
+// the sender's row; the link words of all of a wave's senders are loaded at once, parked in
+// the record area), and the records are transposed in LDS and written receiver by receiver --
+// 32 consecutive in-slots (512 B) of each receiver's row instead of 16-byte stores 64 KB apart.
+// A second slot record of an edge is stored directly; extras / overflow records are staged in
+// LDS and appended with one atomic per list (the leader's block broadcast: 64 per tile).
+constexpr uint32_t kTX = 64;  // staged extras / overflow records per tile
 struct TileShared {
-  uint4 rec[kTR * kTS];     // slot records, receiver-major, sender index swizzled (tsw)
-  uint8_t rbk[kTR * kTS];   // their buckets (0xFF: none)
+  uint4 rec[kTR * kTS];     // link words (.x, .y), then slot records; receiver-major, sender swizzled (tsw)
+  uint8_t rbk[kTR * kTS];   // the record's bucket (0xFF: none)
   uint4 job[kTS][4];
   uint4 bc[kTS][kMeshBc * 2];
+  uint4 mtb[kTS][2];        // reply descriptor tile masks {lo, hi, rank base}
+  uint2 mte[kTS][kEDesc];   // pending echo descriptor tile masks
+  XRec xs[kTX];
+  uint32_t xm[kTX];         // list << 24 | rank
+  uint32_t xn;
+  uint32_t lst[kMaxBuckets + 1];
   uint32_t lcnt[kMaxBuckets];
   uint32_t lmin[kMaxBuckets];
   uint32_t csum[8];
   unsigned long long bkm;   // buckets holding slot records of this tile
   long long ovmin;
+  long long bmin[kMaxBuckets];  // the buckets' arrival-time bounds as of the start (read early)
 };
 // (receiver, sender) -> LDS index: the sender index XOR the receiver's low bits, so that a wave
 // writing one sender's 64 receivers and a wave reading two receivers' 32 senders both spread
 // over the banks
 __device__ inline uint32_t tsw(uint32_t s, uint32_t i) { return s * kTS + (i ^ (s & (kTS - 1u))); }
 
-// an extras (list < B) or overflow (list == B) record, appended directly (see link_stage)
-__device__ inline void tile_append(const KP& p, uint32_t list, const XRec& x) {
-  if (list == p.n_buckets) {
-    const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
-    if (pos >= p.cap_ov) {
-      set_err(p, BCSIM_E_OVERFLOW);
-      return;
-    }
-    AT(p.ov, pos, p.cap_ov) = x;
-  } else {
-    const uint32_t pos = atomicAdd(&p.x_cnt[list], 1u);
-    if (pos >= p.cap_x) {
-      set_err(p, BCSIM_E_OVERFLOW);
-      return;
-    }
-    AT(p.xbuf, static_cast<size_t>(list) * p.cap_x + pos, p.cap_xbuf) = x;
+__device__ inline void tile_append(const KP& p, TileShared& T, uint32_t list, const XRec& x) {
+  const uint32_t pos = atomicAdd(&T.xn, 1u);
+  if (pos < kTX) {
+    const uint32_t rank = atomicAdd(&T.lst[list], 1u);
+    T.xs[pos] = x;
+    T.xm[pos] = (list << 24) | rank;
+    return;
   }
+  // (staging full: a direct, contended append)
+  uint32_t* ctr = list == p.n_buckets ? p.ov_cnt : &p.x_cnt[list];
+  const uint32_t cap = list == p.n_buckets ? p.cap_ov : p.cap_x;
+  const uint32_t at = atomicAdd(ctr, 1u);
+  if (at >= cap) {
+    set_err(p, BCSIM_E_OVERFLOW);
+    return;
+  }
+  if (list == p.n_buckets)
+    AT(p.ov, at, p.cap_ov) = x;
+  else
+    AT(p.xbuf, static_cast<size_t>(list) * p.cap_x + at, p.cap_xbuf) = x;
 }
 
-// rank of out-edge le among the set bits of a reply bitmap: the chunk prefix (k_link_mesh<TILE>)
-// plus the bits of le's 64-slot chunk below it
-__device__ inline uint32_t tile_rank(const KP& p, uint32_t g, int h, uint32_t ob, uint32_t le, bool& bit) {
-  const uint32_t* rb = p.rbits + (static_cast<size_t>(ob) * p.NT + g) * p.dwords;
-  const uint32_t c = le >> 6, w0 = 2 * c;
-  const uint32_t lo = rb[w0], hi = w0 + 1 < p.dwords ? rb[w0 + 1] : 0u;
-  const uint32_t b = le & 63u;
-  bit = ((b < 32 ? lo >> b : hi >> (b - 32)) & 1u) != 0;
-  const uint32_t below = b < 32 ? static_cast<uint32_t>(__popc(lo & ((1u << b) - 1u)))
-                                : static_cast<uint32_t>(__popc(lo)) + static_cast<uint32_t>(__popc(hi & ((1u << (b - 32)) - 1u)));
-  return p.mrp[(static_cast<size_t>(g) * 2 + h) * kRpChunks + c] + below;
-}
-
-__global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_mesh_tile(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
                                                    uint32_t epoch) {
   const KP& p = *pk;
   BAIL_IF_ERR();
@@ -5320,32 +5444,66 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
   const uint32_t st = rem / nrt, rt = rem % nrt;
   if (p.mtile[static_cast<size_t>(rep) * nst + st] != epoch) return;  // no job among these senders
   const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
+  unsigned long long* tph = p.wgtt ? p.wgtt + 8ull * blockIdx.x : nullptr;  // (debug phase clocks)
+#define TPH(k)                                                       \
+  do {                                                               \
+    if (tph && tid == 0) tph[(k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  TPH(0);
   const uint32_t N = p.N, N1 = N - 1, B = p.n_buckets;
   const uint32_t i0 = st * kTS, s0 = rt * kTR;
+  const size_t gb = static_cast<size_t>(rep) * N + i0;  // gnode of the tile's first sender
+  const uint32_t s = s0 + lane;
+  // the link words of every edge of this wave's senders first (whether or not the sender has a
+  // job: the loads need not wait for the job words), all in flight with the job loads below
+  uint64_t lv[kTS / 8];
+#pragma unroll
+  for (uint32_t k = 0; k < kTS / 8; ++k) {
+    const uint32_t il = wv + k * nwv;
+    const uint32_t i = i0 + il;
+    const bool v = il < kTS && i < N && s < N && s != i;
+    lv[k] = v ? p.link[edge_loc(p, rep, i * N1 + (s < i ? s : s - 1))] : 0ull;
+  }
+  // jobs, broadcasts and descriptor tile masks of the 32 senders, all loads at once (a stale job
+  // is told by its epoch; the other words are used only under its flags)
   if (tid < kTS * 4) {
-    const uint32_t i = i0 + (tid >> 2);
-    T.job[tid >> 2][tid & 3u] =
-        i < N ? p.mjob[(static_cast<size_t>(rep) * N + i) * 4 + (tid & 3u)] : make_uint4(0, 0, 0, 0);
+    const uint32_t il = tid >> 2;
+    T.job[il][tid & 3u] = i0 + il < N ? p.mjob[(gb + il) * 4 + (tid & 3u)] : make_uint4(0, 0, 0, 0);
+  } else if (tid < kTS * 4 + kTS * kMeshBc * 2) {
+    const uint32_t k = tid - kTS * 4, il = k / (kMeshBc * 2);
+    if (i0 + il < N) T.bc[il][k % (kMeshBc * 2)] = p.mbc[(gb + il) * kMeshBc * 2 + k % (kMeshBc * 2)];
+  } else if (tid < kTS * 4 + kTS * kMeshBc * 2 + kTS * 2) {
+    const uint32_t k = tid - kTS * 4 - kTS * kMeshBc * 2, il = k >> 1;
+    if (i0 + il < N) T.mtb[il][k & 1u] = p.mtb[((gb + il) * nrt + rt) * 2 + (k & 1u)];
+  } else if (tid < kTS * 4 + kTS * kMeshBc * 2 + kTS * 2 + kTS * kEDesc) {
+    const uint32_t k = tid - kTS * 4 - kTS * kMeshBc * 2 - kTS * 2, il = k / kEDesc;
+    if (i0 + il < N) T.mte[il][k % kEDesc] = p.mte[((gb + il) * nrt + rt) * kEDesc + k % kEDesc];
   }
   for (uint32_t k = tid; k < kTR * kTS / 4; k += blockDim.x) reinterpret_cast<uint32_t*>(T.rbk)[k] = 0xFFFFFFFFu;
   for (uint32_t k = tid; k < B; k += blockDim.x) {
     T.lcnt[k] = 0;
     T.lmin[k] = ~0u;
   }
+  for (uint32_t k = tid; k <= B; k += blockDim.x) T.lst[k] = 0;
+  for (uint32_t k = tid; k < B; k += blockDim.x) T.bmin[k] = *reinterpret_cast<volatile long long*>(&p.bmin[k]);
   if (tid < 8) T.csum[tid] = 0;
   if (tid == 0) {
     T.bkm = 0ull;
     T.ovmin = LLONG_MAX;
+    T.xn = 0;
+  }
+  TPH(1);
+  // the link words parked in the edges' record slots (each lane reads back only its own)
+#pragma unroll
+  for (uint32_t k = 0; k < kTS / 8; ++k) {
+    const uint32_t il = wv + k * nwv;
+    if (il < kTS) {
+      T.rec[tsw(lane, il)].x = static_cast<uint32_t>(lv[k]);
+      T.rec[tsw(lane, il)].y = static_cast<uint32_t>(lv[k] >> 32);
+    }
   }
   __syncthreads();
-  if (tid < kTS * kMeshBc * 2) {
-    const uint32_t il = tid / (kMeshBc * 2), w = tid % (kMeshBc * 2);
-    const uint4 J = T.job[il][0];
-    if (J.x == epoch && (w >> 1) < ((J.z >> 8) & 0xFFu))
-      T.bc[il][w] = p.mbc[(static_cast<size_t>(rep) * N + i0 + il) * kMeshBc * 2 + w];
-  }
-  __syncthreads();
-
+  TPH(2);
   const uint32_t ib = static_cast<uint32_t>(cell % B);
   const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
   const long long cs = cell * p.L;
@@ -5355,36 +5513,132 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
   const uint32_t tag = cell_tag(p, cell);
   const int64_t app = p.app_delay;
   const uint32_t w3r = static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0))) | (kPbPrepareRes << 16);
-  const uint32_t s = s0 + lane;
+  const unsigned long long lbit = 1ull << lane, lbelow = lbit - 1ull;
+  // (the fast path's parameters, read once)
+  const int64_t tx0 = p.tx_tot[0], tx1 = p.tx_tot[1], prc = p.prop_const;
+  const uint64_t Lmag = p.L_magic;
   uint32_t n_rec = 0, st_edges = 0, st_echo = 0, st_ops = 0, sends = 0;
   unsigned long long bkm = 0ull;
   long long ovmin = LLONG_MAX;
   uint32_t cb = kInvalid, cbn = 0, cmn = ~0u;
 #pragma unroll 1
   for (uint32_t il = wv; il < kTS; il += nwv) {
-    const uint4 J = T.job[il][0];
-    if (J.x != epoch) continue;  // (wave-uniform)
+    // the sender's job words are uniform: scalar registers, scalar branches
+    if (static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(T.job[il][0].x))) != epoch) continue;
+    const uint32_t fl = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(T.job[il][0].y)));
+    const uint32_t jz = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(T.job[il][0].z)));
     const uint32_t i = i0 + il;
-    const uint32_t g = rep * N + i;
-    const uint32_t fl = J.y, ne = J.z & 0xFFu, n_bc = (J.z >> 8) & 0xFFu;
+    const uint32_t ne = jz & 0xFFu, n_bc = (jz >> 8) & 0xFFu;
     const bool sl0 = fl & kJSl0, sl1 = fl & kJSl1, sd0 = fl & kJSd0, sd1 = fl & kJSd1, rxe = fl & kJRxe;
     const bool v = s < N && s != i;
     const uint32_t le = s < i ? s : s - 1;
     const uint32_t e = i * N1 + (v ? le : 0u);
-    // the edge's loads together
-    uint64_t* lwp = p.link + edge_loc(p, rep, e);
-    const uint64_t lw0 = v ? *lwp : 0ull;
+    const uint32_t q = tsw(lane, il);
+    const uint64_t lw0 = (static_cast<uint64_t>(T.rec[q].y) << 32) | T.rec[q].x;
+    // ---- the heavy waves' shape (uniform): one kind of source per edge -- the one due broadcast,
+    // or the one due reply descriptor -- and a constant propagation delay.  A lane whose record is
+    // the edge's first slot record of a cell 1 .. B-1 ahead is finished here; any other lane goes
+    // to the general merge below with nothing changed.
+    if (!rxe && !sl0 && !sl1 && prc >= 0 && ((n_bc == 1 && !sd0 && !sd1) || (n_bc == 0 && sd0 != sd1))) {
+      // the source's uniform words: due time, the first edge's sub, payload words, frame size
+      uint32_t u_tlo, u_thi, u_sub, u_w2, u_w3;
+      bool has;
+      if (n_bc) {
+        u_tlo = T.bc[il][0].x;
+        u_thi = T.bc[il][0].y;
+        u_sub = T.bc[il][1].x;
+        u_w2 = T.bc[il][1].z;
+        u_w3 = T.bc[il][1].w;
+        has = v;
+      } else {
+        const int h = sd0 ? 0 : 1;
+        const uint4 mb = T.mtb[il][h];
+        const unsigned long long m = (static_cast<unsigned long long>(mb.y) << 32) | mb.x;
+        has = v && (m & lbit);
+        u_tlo = T.job[il][1 + h].x;
+        u_thi = T.job[il][1 + h].y;
+        u_sub = T.job[il][1 + h].z + mb.z + static_cast<uint32_t>(__popcll(m & lbelow)) - le;  // (+ le below)
+        u_w2 = T.job[il][1 + h].w;
+        u_w3 = w3r;
+      }
+      u_tlo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(u_tlo)));
+      u_thi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(u_thi)));
+      u_w2 = n_bc ? static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(u_w2))) : u_w2;
+      u_w3 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(u_w3)));
+      const int big = (n_bc && ((u_w3 >> 26) & OPF_BIG)) ? 1 : 0;
+      const int64_t ot = static_cast<int64_t>((static_cast<uint64_t>(u_thi) << 32) | u_tlo);
+      const int64_t txu = big ? tx1 : tx0;
+      const uint32_t w3u = (u_w3 & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+      int64_t bu = static_cast<int64_t>(lw0 >> 16);
+      bool pe = false;
+      for (uint32_t d = 0; d < ne; ++d) {  // pending echo descriptors, oldest first
+        const uint2 em = T.mte[il][d];
+        const unsigned long long m = (static_cast<unsigned long long>(em.y) << 32) | em.x;
+        const uint4 q3 = T.job[il][3];
+        const int64_t et = static_cast<int64_t>(d ? ((static_cast<uint64_t>(q3.w) << 32) | q3.z)
+                                                  : ((static_cast<uint64_t>(q3.y) << 32) | q3.x));
+        const int64_t eb = (bu > et ? bu : et) + p.tx_tot[(fl & (d ? kJBig1 : kJBig0)) ? 1 : 0];
+        const bool hit = v && (m & lbit);
+        bu = hit ? eb : bu;
+        pe = pe || hit;
+      }
+      const int64_t start = bu > ot ? bu : ot;
+      const int64_t end = start + txu;
+      const int64_t dtf = end + prc - cs;
+      const uint32_t x = static_cast<uint32_t>(dtf);
+      const uint32_t qq = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), Lmag));
+      const uint32_t lc0 = static_cast<uint32_t>(lw0 & 0xFFFFu);
+      const uint32_t ca16 = static_cast<uint32_t>(cell + qq) & 0xFFFFu;
+      const uint32_t bq = cr_b + qq;
+      const bool wrap = bq >= B;
+      const bool ok = has && (static_cast<uint64_t>(dtf) >> 32) == 0 && qq - 1u < B - 1u && lc0 != ca16;
+      const uint32_t lc = ok ? ca16 : lc0;
+      if (ok) {
+        const uint32_t bk = wrap ? bq - B : bq;
+        const uint32_t tof = x - qq * L32;
+        T.rec[q] = make_uint4(tof, u_sub + le, u_w2, w3u | (static_cast<uint32_t>((cq_b + (wrap ? 1 : 0)) & 31) << 27));
+        T.rbk[q] = static_cast<uint8_t>(bk);
+        bkm |= 1ull << bk;
+        ++n_rec;
+        if (!n_bc) {
+          ++sends;
+          ++st_ops;
+        }
+        const bool nb = bk != cb;
+        if (nb && cbn) {
+          atomicAdd(&T.lcnt[cb], cbn);
+          atomicMin(&T.lmin[cb], cmn);
+        }
+        cbn = nb ? 1u : cbn + 1u;
+        cmn = nb ? tof : (tof < cmn ? tof : cmn);
+        cb = bk;
+      }
+      const bool done = ok || !has;
+      if (done && (ok || pe)) {
+        ++st_edges;
+        p.link[edge_loc(p, rep, e)] = (static_cast<uint64_t>(ok ? end : bu) << 16) | lc;
+      }
+      if (done) continue;
+    }
+    // ---- the general merge ----
+    // (rare in the heavy waves: the implicit echo and reply slots of the edge)
     const uint4 r0 = (v && rxe) ? *reinterpret_cast<const uint4*>(p.inbox + inbox_idx(p, ib, rep, e)) : make_uint4(0, 0, 0, 0);
     uint4 w0 = (v && sl0) ? *eslot_at(p, ob, rep, e) : make_uint4(0, 0, 0, 0);
     uint4 w1 = (v && sl1) ? *eslot_at(p, obp, rep, e) : make_uint4(0, 0, 0, 0);
     bool hd0 = false, hd1 = false;
-    if (v && sd0) {
-      const uint32_t rk = tile_rank(p, g, 0, ob, le, hd0);
-      if (hd0) w0 = make_uint4(T.job[il][1].x, T.job[il][1].y, T.job[il][1].z + rk, T.job[il][1].w);
+    if (sd0) {
+      const uint4 mb = T.mtb[il][0];
+      const unsigned long long m = (static_cast<unsigned long long>(mb.y) << 32) | mb.x;
+      hd0 = v && (m & lbit);
+      if (hd0) w0 = make_uint4(T.job[il][1].x, T.job[il][1].y, T.job[il][1].z + mb.z + static_cast<uint32_t>(__popcll(m & lbelow)),
+                               T.job[il][1].w);
     }
-    if (v && sd1) {
-      const uint32_t rk = tile_rank(p, g, 1, obp, le, hd1);
-      if (hd1) w1 = make_uint4(T.job[il][2].x, T.job[il][2].y, T.job[il][2].z + rk, T.job[il][2].w);
+    if (sd1) {
+      const uint4 mb = T.mtb[il][1];
+      const unsigned long long m = (static_cast<unsigned long long>(mb.y) << 32) | mb.x;
+      hd1 = v && (m & lbit);
+      if (hd1) w1 = make_uint4(T.job[il][2].x, T.job[il][2].y, T.job[il][2].z + mb.z + static_cast<uint32_t>(__popcll(m & lbelow)),
+                               T.job[il][2].w);
     }
     if (!v) continue;
     // pending echo descriptors, oldest first, onto the link word
@@ -5392,8 +5646,9 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
     uint32_t lc = static_cast<uint32_t>(lw0 & 0xFFFFu);
     bool pe = false;
     for (uint32_t d = 0; d < ne; ++d) {
-      const uint32_t* eb = p.ebits + (static_cast<size_t>(g) * kEDesc + d) * p.dwords;
-      if ((eb[le >> 5] >> (le & 31u)) & 1u) {
+      const uint2 em = T.mte[il][d];
+      const unsigned long long m = (static_cast<unsigned long long>(em.y) << 32) | em.x;
+      if (m & lbit) {
         const uint4 q3 = T.job[il][3];
         const int64_t et = static_cast<int64_t>(d ? ((static_cast<uint64_t>(q3.w) << 32) | q3.z)
                                                   : ((static_cast<uint64_t>(q3.y) << 32) | q3.x));
@@ -5430,64 +5685,12 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
     const uint32_t slot = s * N1 + (i < s ? i : i - 1);
     const uint32_t dg = rep * N + s;
     bool in_lds = false;
-    uint32_t bi = 0;
-    for (;;) {
-      while (bi < n_bc && ((T.bc[il][2 * bi + 1].w >> 26) & OPF_PAXOS) && le == 0) ++bi;
-      // the earliest source: 1 broadcast, 2 / 4 reply slots, 3 echo
-      int src = 0;
-      int64_t ot = 0;
-      uint32_t odt = 0, oor = 0, osub = 0, ow2 = 0, ow3 = 0;
-      int big = 0;
-      if (bi < n_bc) {
-        const uint4 a = T.bc[il][2 * bi], bw = T.bc[il][2 * bi + 1];
-        ot = static_cast<int64_t>((static_cast<uint64_t>(a.y) << 32) | a.x);
-        odt = a.z;
-        oor = a.w;
-        osub = bw.x + (((bw.w >> 26) & OPF_PAXOS) ? le - 1 : le);
-        ow2 = bw.z;
-        ow3 = bw.w & 0x00FFFFFFu;
-        big = ((bw.w >> 26) & OPF_BIG) ? 1 : 0;
-        src = 1;
-      }
-      if (hr && (src == 0 || kless(rt1, static_cast<uint32_t>(app), i, w0.z, ot, odt, oor, osub))) {
-        ot = rt1;
-        odt = static_cast<uint32_t>(app);
-        oor = i;
-        osub = w0.z;
-        ow2 = w0.w;
-        ow3 = w3r;
-        big = 0;
-        src = 2;
-      }
-      if (hr2 && (src == 0 || kless(rt2, static_cast<uint32_t>(app), i, w1.z, ot, odt, oor, osub))) {
-        ot = rt2;
-        odt = static_cast<uint32_t>(app);
-        oor = i;
-        osub = w1.z;
-        ow2 = w1.w;
-        ow3 = w3r;
-        big = 0;
-        src = 4;
-      }
-      if (he && (src == 0 || kless(et, edt, s, esub, ot, odt, oor, osub))) {
-        ot = et;
-        big = ebig;
-        src = 3;
-      }
-      if (src == 0) break;
-      if (src == 1)
-        ++bi;
-      else if (src == 2)
-        hr = false;
-      else if (src == 4)
-        hr2 = false;
-      else
-        he = false;
-      if (src == 2 || src == 4) ++sends;
+    // one message through the FIFO and out as a record (slot via the LDS transpose, direct,
+    // extras or overflow)
+    auto emit = [&](int64_t ot, uint32_t osub, uint32_t ow2, uint32_t ow3, int big) {
       const int64_t start = bu > ot ? bu : ot;
       const int64_t end = start + p.tx_tot[big];
       bu = end;
-      if (src == 3) continue;  // the echo only occupies the link
       const int64_t ta = end + pr;
       long long ca;
       uint32_t tof;
@@ -5495,9 +5698,9 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
         const int64_t dtf = ta - cs;
         if (dtf >= 0 && dtf < (1ll << 32)) {  // (floor by the reciprocal, see k_link_mesh)
           const uint32_t x = static_cast<uint32_t>(dtf);
-          const uint32_t q = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), p.L_magic));
-          ca = cell + q;
-          tof = x - q * L32;
+          const uint32_t qq = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), p.L_magic));
+          ca = cell + qq;
+          tof = x - qq * L32;
         } else {
           ca = ta / p.L;
           tof = static_cast<uint32_t>(ta - ca * p.L);
@@ -5506,7 +5709,7 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
       const long long rel = ca - cell;
       if (rel < 1) {
         set_err(p, BCSIM_E_TIE);  // lookahead violated
-        continue;
+        return;
       }
       ++n_rec;
       const uint32_t w3 = ow3 | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24) |
@@ -5519,7 +5722,6 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
         if (bk >= B) bk -= B;
         if (owner) {
           if (!in_lds) {  // the edge's first slot record: through the LDS transpose
-            const uint32_t q = tsw(lane, il);
             T.rec[q] = rv;
             T.rbk[q] = static_cast<uint8_t>(bk);
             bkm |= 1ull << bk;
@@ -5535,7 +5737,7 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
           x.cell = ca;
           x.slot = slot;
           x.g = dg;
-          tile_append(p, bk, x);
+          tile_append(p, T, bk, x);
           AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
         }
         if (bk != cb) {
@@ -5556,18 +5758,91 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
         x.cell = ca;
         x.slot = slot;
         x.g = dg;
-        tile_append(p, B, x);
+        tile_append(p, T, B, x);
         if (ca < ovmin) ovmin = ca;
+      }
+    };
+    if (static_cast<uint32_t>(n_bc) + (hr ? 1u : 0u) + (hr2 ? 1u : 0u) + (he ? 1u : 0u) == 1u) {
+      // one source (the heavy waves: a broadcast, or a reply): no merge
+      if (n_bc) {
+        const uint4 a = T.bc[il][0], bw = T.bc[il][1];
+        emit(static_cast<int64_t>((static_cast<uint64_t>(a.y) << 32) | a.x), bw.x + le, bw.z, bw.w & 0x00FFFFFFu,
+             ((bw.w >> 26) & OPF_BIG) ? 1 : 0);
+      } else if (hr || hr2) {
+        ++sends;
+        const uint4 w = hr ? w0 : w1;
+        emit(hr ? rt1 : rt2, w.z, w.w, w3r, 0);
+      } else {  // the echo only occupies the link
+        bu = (bu > et ? bu : et) + p.tx_tot[ebig];
+      }
+    } else {
+      uint32_t bi = 0;
+      for (;;) {
+        // the earliest source: 1 broadcast, 2 / 4 reply slots, 3 echo (Paxos broadcasts never get here)
+        int src = 0;
+        int64_t ot = 0;
+        uint32_t odt = 0, oor = 0, osub = 0, ow2 = 0, ow3 = 0;
+        int big = 0;
+        if (bi < n_bc) {
+          const uint4 a = T.bc[il][2 * bi], bw = T.bc[il][2 * bi + 1];
+          ot = static_cast<int64_t>((static_cast<uint64_t>(a.y) << 32) | a.x);
+          odt = a.z;
+          oor = a.w;
+          osub = bw.x + le;
+          ow2 = bw.z;
+          ow3 = bw.w & 0x00FFFFFFu;
+          big = ((bw.w >> 26) & OPF_BIG) ? 1 : 0;
+          src = 1;
+        }
+        if (hr && (src == 0 || kless(rt1, static_cast<uint32_t>(app), i, w0.z, ot, odt, oor, osub))) {
+          ot = rt1;
+          odt = static_cast<uint32_t>(app);
+          oor = i;
+          osub = w0.z;
+          ow2 = w0.w;
+          ow3 = w3r;
+          big = 0;
+          src = 2;
+        }
+        if (hr2 && (src == 0 || kless(rt2, static_cast<uint32_t>(app), i, w1.z, ot, odt, oor, osub))) {
+          ot = rt2;
+          odt = static_cast<uint32_t>(app);
+          oor = i;
+          osub = w1.z;
+          ow2 = w1.w;
+          ow3 = w3r;
+          big = 0;
+          src = 4;
+        }
+        if (he && (src == 0 || kless(et, edt, s, esub, ot, odt, oor, osub))) {
+          ot = et;
+          big = ebig;
+          src = 3;
+        }
+        if (src == 0) break;
+        if (src == 1)
+          ++bi;
+        else if (src == 2)
+          hr = false;
+        else if (src == 4)
+          hr2 = false;
+        else
+          he = false;
+        if (src == 3) {  // the echo only occupies the link
+          bu = (bu > ot ? bu : ot) + p.tx_tot[big];
+          continue;
+        }
+        if (src == 2 || src == 4) ++sends;
+        emit(ot, osub, ow2, ow3, big);
       }
     }
     if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
-    *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
+    p.link[edge_loc(p, rep, e)] = (static_cast<uint64_t>(bu) << 16) | lc;
   }
   if (cbn) {
     atomicAdd(&T.lcnt[cb], cbn);
     atomicMin(&T.lmin[cb], cmn);
   }
-  // buckets and counters: wave reductions, LDS atomics
   for (int d = 32; d > 0; d >>= 1) {
     bkm |= static_cast<unsigned long long>(__shfl_xor(bkm, d, 64));
     ovmin = min(ovmin, static_cast<long long>(__shfl_xor(ovmin, d, 64)));
@@ -5584,24 +5859,51 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
     if (bkm) atomicOr(&T.bkm, bkm);
     if (ovmin != LLONG_MAX) atomicMin(&T.ovmin, ovmin);
   }
+  TPH(3);
   __syncthreads();
+  TPH(4);
   // the transposed slot records: each receiver's 32 in-slots of this sender tile in one run
   for (uint32_t x = tid; x < kTR * kTS; x += blockDim.x) {
     const uint32_t sl = x / kTS, il = x % kTS;
     const uint32_t q = tsw(sl, il);
     const uint32_t bk = T.rbk[q];
-    if (bk == 0xFFu) continue;
+    if (bk == 0xFFu || (p.exp & 4u)) continue;
     const uint32_t sr = s0 + sl, i = i0 + il;
     const uint32_t slot = sr * N1 + (i < sr ? i : i - 1);
     *reinterpret_cast<uint4*>(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox)) = T.rec[q];
   }
-  if (tid < B && ((T.bkm >> tid) & 1ull))  // receiver-tile flags of the buckets written
-    set_flag_once(&AT(p.rtile, (static_cast<size_t>(tid) * p.R + rep) * p.n_tiles + rt,
-                      static_cast<uint64_t>(B) * p.R * p.n_tiles));
+  // staged extras / overflow records: one atomic per list
+  if (T.xn) {
+    for (uint32_t k = tid; k <= B; k += blockDim.x) {
+      const uint32_t c = T.lst[k];
+      if (!c) continue;
+      uint32_t* ctr = k == B ? p.ov_cnt : &p.x_cnt[k];
+      const uint32_t cap = k == B ? p.cap_ov : p.cap_x;
+      const uint32_t base = atomicAdd(ctr, c);
+      if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
+      T.lst[k] = base;  // (this lane's list only: no other lane reads it before the barrier)
+    }
+    __syncthreads();
+    const uint32_t nx = min(T.xn, kTX);
+    for (uint32_t k = tid; k < nx; k += blockDim.x) {
+      const uint32_t list = T.xm[k] >> 24, at = T.lst[list] + (T.xm[k] & 0xFFFFFFu);
+      if (list == B) {
+        if (at < p.cap_ov) p.ov[at] = T.xs[k];
+      } else if (at < p.cap_x) {
+        p.xbuf[static_cast<size_t>(list) * p.cap_x + at] = T.xs[k];
+      }
+    }
+  }
+  // receiver-tile flags of the buckets written, busy buckets, arrival-time bounds: stores and
+  // atomics that return nothing (no round trip at the end of the workgroup); the bound is
+  // lowered only below the value read at the start
+  if (tid < B && ((T.bkm >> tid) & 1ull))
+    AT(p.rtile, (static_cast<size_t>(tid) * p.R + rep) * p.n_tiles + rt, static_cast<uint64_t>(B) * p.R * p.n_tiles) = 1;
   for (uint32_t k = tid; k < B; k += blockDim.x)
     if (T.lcnt[k]) {
-      mark_busy(&p.bucket_cnt[k]);
-      bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + T.lmin[k]);
+      p.bucket_cnt[k] = 1u;
+      const long long t = bucket_t0(p, (t_hi - 1) / p.L, k) + T.lmin[k];
+      if (t < T.bmin[k]) atomicMin(&p.bmin[k], t);
     }
   if (tid == 0) {
     unsigned long long* cnt = cnt_stripe(p, rep);
@@ -5612,6 +5914,8 @@ __global__ __launch_bounds__(256) void k_mesh_tile(const KP* __restrict__ pk, lo
     if (T.csum[4]) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(T.csum[4]));
     if (T.ovmin != LLONG_MAX) atomicMin(&p.scal[1], T.ovmin);
   }
+  TPH(5);
+#undef TPH
 }
 
 // ---------------------------------------------------------------------------
