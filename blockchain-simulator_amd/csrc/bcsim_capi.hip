@@ -158,7 +158,7 @@ static int dalloc(Sim& s, T** p, size_t count) {
     return BCSIM_E_NOMEM;
   }
   s.allocs.push_back(q);
-  *p = static_cast<T*>(q);
+  *p = (T*)q  /* (device pass: T may carry address space 1) */;
   return BCSIM_OK;
 }
 
@@ -382,10 +382,10 @@ static int setup_device(Sim& s) {
   std::copy(del.begin(), del.end(), tab.begin() + 8);
   std::copy(dpx.begin(), dpx.end(), tab.begin() + 160);
   HIPCHK(hipMemcpy(tables, tab.data(), 256 * sizeof(int64_t), hipMemcpyHostToDevice));
-  p.pbft_delay = tables;
-  p.raft_delay = tables + 4;
-  p.raft_elec = tables + 8;
-  p.paxos_delay = tables + 160;
+  p.pbft_delay = (decltype(p.pbft_delay))(tables);
+  p.raft_delay = (decltype(p.raft_delay))(tables + 4);
+  p.raft_elec = (decltype(p.raft_elec))(tables + 8);
+  p.paxos_delay = (decltype(p.paxos_delay))(tables + 160);
   p.jit_delay = (c.protocol == BCSIM_PBFT || c.protocol == BCSIM_GOSSIP) ? p.pbft_delay : c.protocol == BCSIM_RAFT ? p.raft_delay : p.paxos_delay;
   p.jit_mod = c.protocol == BCSIM_PAXOS ? 50 : 3;
   const int64_t* tab_jit = tab.data() + (p.jit_delay - tables);
@@ -411,11 +411,11 @@ static int setup_device(Sim& s) {
   HIPCHK(hipMemcpy(rev, s.rev.data(), static_cast<size_t>(s.E) * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(prop, s.prop.data(), static_cast<size_t>(s.E) * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(prop_in, pin.data(), static_cast<size_t>(s.E) * 8, hipMemcpyHostToDevice));
-  p.row = row;
-  p.col = col;
-  p.rev = rev;
-  p.prop = prop;
-  p.prop_in = prop_in;
+  p.row = (decltype(p.row))(row);
+  p.col = (decltype(p.col))(col);
+  p.rev = (decltype(p.rev))(rev);
+  p.prop = (decltype(p.prop))(prop);
+  p.prop_in = (decltype(p.prop_in))(prop_in);
   p.prop_const = s.E ? s.prop[0] : 0;  // uniform links: k_link skips the per-edge loads
   for (uint32_t e = 1; e < s.E && p.prop_const >= 0; ++e)
     if (s.prop[e] != s.prop[0]) p.prop_const = -1;
@@ -608,7 +608,7 @@ static int setup_device(Sim& s) {
     uint16_t* own_d = nullptr;
     if ((rc = dalloc(s, &own_d, s.N))) return rc;
     HIPCHK(hipMemcpy(own_d, own.data(), s.N * 2ull, hipMemcpyHostToDevice));
-    p.owner = own_d;
+    p.owner = (decltype(p.owner))(own_d);
     // per destination rank: at most one record per (local sender, remote
     // receiver) edge per cell, plus second records and broadcasts
     const uint64_t cs = std::max<uint64_t>(65536, 2ull * s.R * s.nloc * std::min<uint64_t>(s.deg_max, s.N) + 4096);
@@ -621,8 +621,8 @@ static int setup_device(Sim& s) {
       return rc;
     HIPCHK(hipMemset(la, 0, NT + 8));
     HIPCHK(hipMemset(ll, 0, NT + 8));
-    p.lead_all = la;
-    p.lead_loc = ll;
+    p.lead_all = (decltype(p.lead_all))(la);
+    p.lead_loc = (decltype(p.lead_loc))(ll);
     s.lead_w.assign((NT + 7) / 8, 0);
   }
 
@@ -642,17 +642,17 @@ static int setup_device(Sim& s) {
   int32_t* ibuf = nullptr;
   const size_t nint = 14;
   if ((rc = dalloc(s, &ibuf, NT * nint))) return rc;
-  p.is_leader = ibuf;
-  p.has_voted = ibuf + NT;
-  p.m_value = ibuf + 2 * NT;
-  p.vote_s = ibuf + 3 * NT;
-  p.vote_f = ibuf + 4 * NT;
-  p.acv = ibuf + 5 * NT;
-  p.blockNum = ibuf + 6 * NT;
-  p.round = ibuf + 7 * NT;
-  p.decree = ibuf + 8 * NT;
-  p.ticket = ibuf + 11 * NT;
-  p.proposal = ibuf + 13 * NT;
+  p.is_leader = (decltype(p.is_leader))(ibuf);
+  p.has_voted = (decltype(p.has_voted))(ibuf + NT);
+  p.m_value = (decltype(p.m_value))(ibuf + 2 * NT);
+  p.vote_s = (decltype(p.vote_s))(ibuf + 3 * NT);
+  p.vote_f = (decltype(p.vote_f))(ibuf + 4 * NT);
+  p.acv = (decltype(p.acv))(ibuf + 5 * NT);
+  p.blockNum = (decltype(p.blockNum))(ibuf + 6 * NT);
+  p.round = (decltype(p.round))(ibuf + 7 * NT);
+  p.decree = (decltype(p.decree))(ibuf + 8 * NT);
+  p.ticket = (decltype(p.ticket))(ibuf + 11 * NT);
+  p.proposal = (decltype(p.proposal))(ibuf + 13 * NT);
   p.K = c.paxos_decrees ? c.paxos_decrees : 1;
   {  // Paxos acceptor state per decree (START initialises it)
     const size_t npx = c.protocol == BCSIM_PAXOS ? static_cast<size_t>(NT) * p.K * 4 : 4;
@@ -778,7 +778,7 @@ static int setup_device(Sim& s) {
         (rc = dalloc(s, &p.fqpk, fq ? ne * 3 * p.cap_fqp : 1)) || (rc = dalloc(s, &p.fqmsg, fq ? ne * p.cap_fqm : 1)) ||
         (rc = dalloc(s, &fqmap, fq ? s.E : 1)))
       return rc;
-    p.fqmap = fqmap;
+    p.fqmap = (decltype(p.fqmap))(fqmap);
     if (fq) {
       std::vector<uint32_t> h0(kFqH, 0);
       for (uint32_t f = 0; f < 3; ++f) {
@@ -832,16 +832,16 @@ static int setup_device(Sim& s) {
   if ((rc = dalloc(s, &ctl, ctl_bytes))) return rc;
   s.ctl_d = ctl;
   Ctl* cd = reinterpret_cast<Ctl*>(ctl);
-  p.err = &cd->err;
-  p.dbg = &cd->dbg;
-  p.trace_cnt = &cd->trace_cnt;
-  p.vlog_cnt = &cd->vlog_cnt;
-  p.dreq_cnt = &cd->dreq_cnt;
-  p.ov_cnt = &cd->ov_cnt;
-  p.scal = cd->scal;
+  p.err = (decltype(p.err))(&cd->err);
+  p.dbg = (decltype(p.dbg))(&cd->dbg);
+  p.trace_cnt = (decltype(p.trace_cnt))(&cd->trace_cnt);
+  p.vlog_cnt = (decltype(p.vlog_cnt))(&cd->vlog_cnt);
+  p.dreq_cnt = (decltype(p.dreq_cnt))(&cd->dreq_cnt);
+  p.ov_cnt = (decltype(p.ov_cnt))(&cd->ov_cnt);
+  p.scal = (decltype(p.scal))(cd->scal);
   if ((rc = dalloc(s, &p.nxt_part, 2 * kNextBlocks)) || (rc = dalloc(s, &p.nxt_done, 1))) return rc;
   HIPCHK(hipMemset(p.nxt_done, 0, 4));
-  p.bucket_cnt = reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl));
+  p.bucket_cnt = (decltype(p.bucket_cnt))(reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl)));
   p.x_cnt = p.bucket_cnt + s.B;
   p.send_cnt = p.x_cnt + s.B;
   HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), ctl_bytes));
@@ -858,7 +858,7 @@ static int setup_device(Sim& s) {
   int32_t* gl = nullptr;
   if ((rc = dalloc(s, &gl, static_cast<size_t>(s.R) * p.glibc_len)) || (rc = dalloc(s, &p.glibc_pos, s.R)))
     return rc;
-  p.glibc = gl;
+  p.glibc = (decltype(p.glibc))(gl);
   p.cap_glibc = static_cast<uint64_t>(s.R) * p.glibc_len;
   if (need_glibc) {
     if (s.R > 64) return BCSIM_E_UNSUPPORTED;
@@ -1296,7 +1296,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       const uint32_t ep = ++s.mesh_epoch == 0 ? ++s.mesh_epoch : s.mesh_epoch;
       const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
       if ((rc = launch(s, -1, k_mesh_prep, grid, dim3(64), 0, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
-          (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(512), 0, s.kp_dev, cell, lo, hi, ep)) ||
+          (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(kTileThreads), 0, s.kp_dev, cell, lo, hi, ep)) ||
           (s.kp.wgtt && (rc = tile_phase_report(s, cell, nt))) ||
           (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
@@ -1593,7 +1593,7 @@ static int sync_leaders(Sim& s) {
     if ((rc = s.xp->allreduce_i64(s.stream, s.lead_w.data() + k, n, 1))) return rc;
     ++s.ctl_collectives;
   }
-  HIPCHK(hipMemcpyAsync(const_cast<uint8_t*>(s.kp.lead_all), s.lead_w.data(), s.NT, hipMemcpyHostToDevice, s.stream));
+  HIPCHK(hipMemcpyAsync((void*)s.kp.lead_all, s.lead_w.data(), s.NT, hipMemcpyHostToDevice, s.stream));
   return BCSIM_OK;
 }
 

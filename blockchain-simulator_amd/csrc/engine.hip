@@ -45,7 +45,10 @@
 namespace bcsim {
 
 // ---------------------------------------------------------------------------
-// kernel parameter block (device-resident, one per simulation)
+// kernel parameter block (device-resident, one per simulation).  Its arrays are global memory;
+// device code reaches them through gbl() (below), so that accesses compile to global_*
+// instructions instead of flat_* ones.
+#define GP(T) T*
 constexpr uint32_t kKstStripes = 64;
 constexpr uint32_t kNextBlocks = 64;  // k_next workgroups at most  // kstat[kKstStripes][8]: per-workgroup stripes, summed on the host
 struct KP {
@@ -60,38 +63,57 @@ struct KP {
   uint32_t pbft_rounds, pbft_seq_cap, pbft_view_change, raft_blocks;
   uint32_t raft_prop_rounds, paxos_proposers;
   uint64_t seed;
-  int64_t *pbft_delay, *raft_delay, *raft_elec, *paxos_delay;
-  int64_t* jit_delay;  // the running protocol's getRandomDelay table
+  GP(int64_t) pbft_delay;
+  GP(int64_t) raft_delay;
+  GP(int64_t) raft_elec;
+  GP(int64_t) paxos_delay;
+  GP(int64_t) jit_delay;  // the running protocol's getRandomDelay table
   uint32_t jit_mod;
   // topology (per replica, shared)
-  const uint32_t *row, *col, *rev;
-  const int64_t* prop;     // per edge (sender-major)
-  const int64_t* prop_in;  // per in-slot q: prop[rev[q]]
+  GP(const uint32_t) row;
+  GP(const uint32_t) col;
+  GP(const uint32_t) rev;
+  GP(const int64_t) prop;     // per edge (sender-major)
+  GP(const int64_t) prop_in;  // per in-slot q: prop[rev[q]]
   // common node state
-  uint32_t* sub;
-  uint64_t* draws;
+  GP(uint32_t) sub;
+  GP(uint64_t) draws;
   // PBFT
-  int32_t *leader, *block_num;
-  uint8_t* tick_alive;
-  uint32_t* tick_sub;
-  int32_t *tx_val, *tx_pv, *tx_cv;
-  int32_t *g_n, *g_nround;  // per replica
+  GP(int32_t) leader;
+  GP(int32_t) block_num;
+  GP(uint8_t) tick_alive;
+  GP(uint32_t) tick_sub;
+  GP(int32_t) tx_val;
+  GP(int32_t) tx_pv;
+  GP(int32_t) tx_cv;
+  GP(int32_t) g_n;  // per replica
+  GP(int32_t) g_nround;
   // Raft / Paxos
-  int32_t *is_leader, *has_voted, *m_value, *vote_s, *vote_f, *acv, *blockNum, *round;
-  uint32_t *next_election, *next_heartbeat;
-  int32_t *ticket, *proposal, *decree;
-  int32_t* px;   // Paxos acceptor state [NT][K][4]: t_max, command, t_store, isCommit (per decree)
+  GP(int32_t) is_leader;
+  GP(int32_t) has_voted;
+  GP(int32_t) m_value;
+  GP(int32_t) vote_s;
+  GP(int32_t) vote_f;
+  GP(int32_t) acv;
+  GP(int32_t) blockNum;
+  GP(int32_t) round;
+  GP(uint32_t) next_election;
+  GP(uint32_t) next_heartbeat;
+  GP(int32_t) ticket;
+  GP(int32_t) proposal;
+  GP(int32_t) decree;
+  GP(int32_t) px;   // Paxos acceptor state [NT][K][4]: t_max, command, t_store, isCommit (per decree)
   uint32_t K;    // Paxos decrees (>= 1)
   // Gossip (BCSIM_GOSSIP): first-receipt flag per (gnode, sequence); origin tick count in round[]
-  uint8_t* gseen;
+  GP(uint8_t) gseen;
   // timers / ops
-  TimerEnt* timers;
+  GP(TimerEnt) timers;
   uint32_t cap_timers;
-  Op* ops;
-  uint32_t* n_ops;
+  GP(Op) ops;
+  GP(uint32_t) n_ops;
   uint32_t cap_ops;
   uint32_t cap_eidx;  // k_link LDS index capacity for listed due ops
-  uint32_t* eidx_g;   // [grid][cap_ops] k_link index area of a node with more (nullptr: cap_eidx == cap_ops)
+  GP(uint32_t) eidx_g;   // [grid][cap_ops] k_link index area of a node with more (nullptr: cap_eidx == cap_ops)
   // per-edge reply slots: ring of kOpRing cells, one slot per
   // (replica, edge) for a unicast reply (PBFT PREPARE_RES) of the edge's main
   // inbox record.  A slot op is live while t >= the current window start;
@@ -101,8 +123,8 @@ struct KP {
   // (no read-before-write); entry = {due t lo, due t hi, sub, f0 | f1 << 16} of the PBFT
   // PREPARE_RES (type, f2 = '0', dt = app delay, origin = node are implied).  Only with
   // fixed app delays < L (due cell <= arrival cell + 1).
-  uint4* eslot;          // [kOpRing][R][E]
-  uint8_t* sflag;        // [kOpRing][NT] bit k: replies of this arrival cell due in arrival cell + k
+  GP(uint4) eslot;          // [kOpRing][R][E]
+  GP(uint8_t) sflag;        // [kOpRing][NT] bit k: replies of this arrival cell due in arrival cell + k
   uint64_t cap_eslot;
   // implicit echoes: k_link echoes a node's main inbox records itself (the
   // in-slot index is the reverse out-edge) and releases the slots; k_scan
@@ -110,116 +132,120 @@ struct KP {
   uint32_t impl;
   // window stamp per gnode: k_scan_pbft applied the implicit echoes of the window starting at
   // eapp[g] itself (the link kernels skip them); LLONG_MIN = never
-  long long* eapp;
+  GP(long long) eapp;
   // PBFT heavy-wave descriptors (k_scan_pbft -> k_link_mesh): a PREPARE wave's
   // replies as ONE descriptor {due, first sub, payload} + the bitmap of in-slots that replied
   // (sub + rank), and the waves' echoes as pending {t, big} + bitmap, applied by the node's next
   // link stage that walks its edges (k_link_mesh: the link words are loaded there anyway)
   uint32_t desc;          // enabled: dense full mesh with k_link_mesh as the link stage
   uint32_t dwords;        // bitmap words per descriptor: ceil(deg_max / 32) <= kDescWords
-  uint4* rdesc;           // [kOpRing][NT] {due lo, due hi, sub, f0 | f1 << 16} of the arrival cell
-  uint32_t* rbits;        // [kOpRing][NT][dwords]
-  uint4* edesc;           // [NT][kEDesc] {t lo, t hi, big, 0}
-  uint32_t* ebits;        // [NT][kEDesc][dwords]
-  uint8_t* en;            // [NT] pending echo descriptors
+  GP(uint4) rdesc;           // [kOpRing][NT] {due lo, due hi, sub, f0 | f1 << 16} of the arrival cell
+  GP(uint32_t) rbits;        // [kOpRing][NT][dwords]
+  GP(uint4) edesc;           // [NT][kEDesc] {t lo, t hi, big, 0}
+  GP(uint32_t) ebits;        // [NT][kEDesc][dwords]
+  GP(uint8_t) en;            // [NT] pending echo descriptors
   // full-mesh tiled link stage (k_mesh_prep -> k_mesh_tile): the job k_mesh_prep
   // leaves per gnode -- {epoch, flags, ne | n_bc << 8, 0}, the two reply descriptors, the pending
   // echo times -- its due broadcasts in key order (RawOp words), its descriptor bitmaps cut into
   // 64-receiver tiles (bit k = receiver tile base + k), and per (replica, 32-sender tile) the epoch
   // of the last launch that left a job in it
-  uint4* mjob;            // [NT][4]
-  uint4* mbc;             // [NT][kMeshBc][2]
-  uint4* mtb;             // [NT][n_tiles][2] reply bitmaps per receiver tile: {mask lo, mask hi, rank base, 0}
-  uint2* mte;             // [NT][n_tiles][kEDesc] pending echo bitmaps per receiver tile
-  uint32_t* mtile;        // [R][n_stiles]
+  GP(uint4) mjob;            // [NT][4]
+  GP(uint4) mbc;             // [NT][kMeshBc][2]
+  GP(uint4) mtb;             // [NT][n_tiles][2] reply bitmaps per receiver tile: {mask lo, mask hi, rank base, 0}
+  GP(uint2) mte;             // [NT][n_tiles][kEDesc] pending echo bitmaps per receiver tile
+  GP(uint32_t) mtile;        // [R][n_stiles]
   uint32_t n_stiles;
   // list-2 overlap: k_scan_pbft stamps the nodes it leaves to the generic kernels
   // with the window's epoch; their scan and link stage run on a second stream beside the other
   // nodes' link stage, which skips them.  loop_list: the list k_link<.., LOOP> walks (3; 2 in
   // the second stream's parameter block)
-  uint32_t* l2mark;       // [NT]
+  GP(uint32_t) l2mark;       // [NT]
   uint32_t loop_list;
   int64_t prop_const;    // propagation delay of every edge, or -1 (per-edge array)
   // links
-  uint64_t* link;  // per edge: busy_until << 16 | (arrival cell of the last record & 0xFFFF)
+  GP(uint64_t) link;  // per edge: busy_until << 16 | (arrival cell of the last record & 0xFFFF)
   // DROPTAIL link queues: per edge a ring of the messages of its busy
   // period, entry = start << 17 | big << 16 | accepted frames; meta = head | n << 16 |
   // frames << 32
   uint32_t qmodel, qcap_frames, cap_q;  // qmodel: 0 INFINITE, 1 DROPTAIL, 2 FQCODEL
   uint32_t nfr[2];
   int64_t tx_full[2];
-  uint64_t *qring, *qmeta;
+  GP(uint64_t) qring;
+  GP(uint64_t) qmeta;
   // FQCODEL link queues, per rank-local edge: a header of kFqH words (three
   // flows' CoDel + DRR state, new / old flow lists, device-queue ring position, device busy end,
   // packets in the disc, message-table bitmap), the start times of the device queue's waiting
   // frames [fq_devcap], three packet rings [3][cap_fqp] {enq lo, enq hi, msg | frame << 16,
   // IPv4 bytes} and the message table [cap_fqm] {sub, f0 | f1 << 16, f2 | type << 16 | big << 24 |
   // echo << 25 | lost << 26, fragments left}; fqmap[e] = flow slot per packet class (global edge)
-  uint32_t* fqh;
-  int64_t* fqdev;
-  uint4* fqpk;
-  uint4* fqmsg;
-  const uint8_t* fqmap;
+  GP(uint32_t) fqh;
+  GP(int64_t) fqdev;
+  GP(uint4) fqpk;
+  GP(uint4) fqmsg;
+  GP(const uint8_t) fqmap;
   uint32_t fq_devcap, cap_fqp, cap_fqm, fq_limit, fq_quantum, fq_batch, fq_min_bytes, fq_target_c, fq_interval_c;
   uint32_t ip_full[2], ip_last[2];
   // debug (BCSIM_FQLOG=<file>): every FQCODEL link event with t in [fqlog_t0, fqlog_t1) as two
   // uint4 {t lo, t hi, edge, kind << 24 | frame}, {msg sub, x lo, x hi, echo} (tools/fq_log.py)
-  uint4* fqlog;
-  uint32_t* fqlog_n;
+  GP(uint4) fqlog;
+  GP(uint32_t) fqlog_n;
   uint32_t cap_fqlog;
   long long fqlog_t0, fqlog_t1;
   // inbox
-  Rec* inbox;            // [B][R][E]  receiver-major (in-slot order)
-  uint8_t* rtile;        // [B][R][n_tiles] full mesh: a record for a receiver of this 64-node
+  GP(Rec) inbox;            // [B][R][E]  receiver-major (in-slot order)
+  GP(uint8_t) rtile;        // [B][R][n_tiles] full mesh: a record for a receiver of this 64-node
                          // tile sits in the bucket (senders set one byte per tile, not one per node)
   uint32_t mesh, n_tiles;  // full-mesh topology (arithmetic peers / in-slots)
-  uint8_t* iflag;        // [B][NT] node has records in the bucket
-  long long* bmin;       // [B] lower bound of the arrival times of the bucket's records (LLONG_MAX: none):
+  GP(uint8_t) iflag;        // [B][NT] node has records in the bucket
+  GP(long long) bmin;       // [B] lower bound of the arrival times of the bucket's records (LLONG_MAX: none):
                          // a window that ends before it skips the flagged rows (node_flagged_w)
-  uint32_t* bucket_cnt;  // [B] nonzero = the bucket holds records (slots + extras); see mark_busy
-  uint32_t* x_cnt;       // [B] extras in the bucket
+  GP(uint32_t) bucket_cnt;  // [B] nonzero = the bucket holds records (slots + extras); see mark_busy
+  GP(uint32_t) x_cnt;       // [B] extras in the bucket
   uint32_t n_buckets;
-  XRec* xbuf;            // [B][cap_x]
+  GP(XRec) xbuf;            // [B][cap_x]
   uint32_t cap_x;
-  XRec* xgrp;            // extras of the current cell grouped by receiver
-  XRec* xstage;          // [NT][cap_stage] k_link staging of extras / overflow records
-  uint32_t* xmeta;       // [NT][cap_stage] (list << 24) | rank within the list
+  GP(XRec) xgrp;            // extras of the current cell grouped by receiver
+  GP(XRec) xstage;          // [NT][cap_stage] k_link staging of extras / overflow records
+  GP(uint32_t) xmeta;       // [NT][cap_stage] (list << 24) | rank within the list
   uint32_t cap_stage;
-  XRec* ov;
-  uint32_t* ov_cnt;
+  GP(XRec) ov;
+  GP(uint32_t) ov_cnt;
   uint32_t cap_ov;
-  uint32_t *seg_cnt, *seg_off, *cursor;
+  GP(uint32_t) seg_cnt;
+  GP(uint32_t) seg_off;
+  GP(uint32_t) cursor;
   uint32_t cap_arr;  // LDS staging capacity of k_scan (power of two, <= 4096)
   // outputs
-  bcsim_trace_rec* trace;
-  uint32_t* trace_cnt;
+  GP(bcsim_trace_rec) trace;
+  GP(uint32_t) trace_cnt;
   uint32_t cap_trace;
-  VLog* vlog;
-  uint32_t* vlog_cnt;
+  GP(VLog) vlog;
+  GP(uint32_t) vlog_cnt;
   uint32_t cap_vlog;
-  DrawReq* dreq;
-  uint32_t* dreq_cnt;
+  GP(DrawReq) dreq;
+  GP(uint32_t) dreq_cnt;
   uint32_t cap_dreq;
-  const int32_t* glibc;
+  GP(const int32_t) glibc;
   uint32_t glibc_len;
-  uint32_t* glibc_pos;  // per replica
-  unsigned long long* counters;  // R * CNT_N
+  GP(uint32_t) glibc_pos;  // per replica
+  GP(unsigned long long) counters;  // R * CNT_N
   uint32_t cnt_stripes;  // counters[cnt_stripes][R][CNT_N]: workgroup b adds to stripe b % cnt_stripes
-  unsigned long long* kstat;     // link / scan algorithmic counters (KST_*)
-  int32_t* err;
-  int32_t* dbg;  // first error's source line
-  unsigned long long* trail;  // BCSIM_CHECKED + BCSIM_TRAIL: host-mapped breadcrumbs
-  unsigned long long* wgt;    // BCSIM_WGT: per-workgroup k_link timing [NT][8] (debug)
-  unsigned long long* wgtt;   // BCSIM_WGT: per-workgroup k_mesh_tile phase clocks [tiles][8] (debug)
+  GP(unsigned long long) kstat;     // link / scan algorithmic counters (KST_*)
+  GP(int32_t) err;
+  GP(int32_t) dbg;  // first error's source line
+  GP(unsigned long long) trail;  // BCSIM_CHECKED + BCSIM_TRAIL: host-mapped breadcrumbs
+  GP(unsigned long long) wgt;    // BCSIM_WGT: per-workgroup k_link timing [NT][8] (debug)
+  GP(unsigned long long) wgtt;   // BCSIM_WGT: per-workgroup k_mesh_tile phase clocks [tiles][8] (debug)
   uint32_t exp;               // BCSIM_EXP: performance experiments that break results (debug, never in tests)
-  unsigned long long* wgs;    // BCSIM_WGT: per-workgroup k_scan phase timing [NT][8] (debug)
-  unsigned long long* fdbg;   // BCSIM_FDBG: why nodes leave the fast kernels [16] (debug; see FDBG)
+  GP(unsigned long long) wgs;    // BCSIM_WGT: per-workgroup k_scan phase timing [NT][8] (debug)
+  GP(unsigned long long) fdbg;   // BCSIM_FDBG: why nodes leave the fast kernels [16] (debug; see FDBG)
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
-  long long *node_tnext, *node_onext;
-  long long* scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks, [3] next timer,
+  GP(long long) node_tnext;
+  GP(long long) node_onext;
+  GP(long long) scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks, [3] next timer,
                     // [4] earliest arrival cell shipped to another rank (node-partitioned)
-  long long* nxt_part;  // [kNextBlocks] k_next per-workgroup minima
-  uint32_t* nxt_done;   // k_next workgroups finished (the last one reduces and resets it)
+  GP(long long) nxt_part;  // [kNextBlocks] k_next per-workgroup minima
+  GP(uint32_t) nxt_done;   // k_next workgroups finished (the last one reduces and resets it)
   // node partition (multi-GPU PDES): this rank owns nodes
   // [nlo, nlo + nloc) of every replica; records for other ranks' receivers
   // are staged in sendbuf and exchanged once per cell
@@ -228,20 +254,20 @@ struct KP {
   // edges in the rows of this rank's nodes, [e_lo, e_lo + E_loc) of every replica
   uint32_t e_lo;
   uint64_t E_loc;
-  const uint16_t* owner;    // [N] rank owning node i
-  XRec* sendbuf;            // [nranks][cap_send]
-  uint32_t* send_cnt;       // [nranks] (control block)
+  GP(const uint16_t) owner;    // [N] rank owning node i
+  GP(XRec) sendbuf;            // [nranks][cap_send]
+  GP(uint32_t) send_cnt;       // [nranks] (control block)
   uint32_t cap_send;
-  const uint8_t* lead_all;  // [R][N] PBFT leader flags gathered from all ranks
-  uint8_t* lead_loc;        // [R][N] this rank's leader flags (k_lead)
+  GP(const uint8_t) lead_all;  // [R][N] PBFT leader flags gathered from all ranks
+  GP(uint8_t) lead_loc;        // [R][N] this rank's leader flags (k_lead)
   // sparse mode: no per-edge inbox slots (every record goes through
   // the bucket lists), launches over compact lists of active gnodes, hub-compact link
   // state (hubs > 0: only edges with an endpoint < hubs carry traffic)
   uint32_t sparse, hubs;
   uint32_t cap_ops_light, n_heavy;  // nodes < n_heavy hold cap_ops pending ops, others cap_ops_light
-  uint32_t* act;    // [4][NT] gnodes of the window: k_scan list, k_link list, and (dense gossip)
+  GP(uint32_t) act;    // [4][NT] gnodes of the window: k_scan list, k_link list, and (dense gossip)
                     // the nodes k_gossip_scan / k_gossip_link leave to the generic kernels
-  uint32_t* act_n;  // [4] their lengths
+  GP(uint32_t) act_n;  // [4] their lengths
   // debug (BCSIM_DBG_EVENTS=<t_max ns>): Raft/Paxos/gossip serial handlers emit one
   // trace record of kind 90 + event class per handled event with t < dbg_tmax
   long long dbg_tmax;
@@ -253,7 +279,8 @@ constexpr uint32_t kEDesc = 2;        // pending echo descriptors per node (LDS:
 // sflag bits of a reply descriptor of the arrival cell (bits 0..3: reply slots due in cell + k)
 constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in this cell / the next
 // tiled mesh link stage: due broadcasts per job, senders x receivers per tile, 64-slot chunks
-constexpr uint32_t kMeshBc = 2, kTS = 32, kTR = 64;
+constexpr uint32_t kMeshBc = 2, kTS = 16, kTR = 64;
+constexpr uint32_t kTileThreads = kTS * 16;  // four senders per wave
 constexpr uint32_t kLoopGrid = 256;  // workgroups of the looped generic grids (lists 2, 3) at most
 // job flags (mjob[g][0].y)
 constexpr uint32_t kJSl0 = 1u, kJSl1 = 2u, kJSd0 = 4u, kJSd1 = 8u, kJRxe = 16u, kJBig0 = 32u, kJBig1 = 64u;
@@ -261,10 +288,83 @@ constexpr uint32_t kJSl0 = 1u, kJSl1 = 2u, kJSd0 = 4u, kJSd1 = 8u, kJRxe = 16u, 
 
 // ---------------------------------------------------------------------------
 // device helpers
+// A KP array pointer as a global-memory (address space 1) pointer: accesses through it compile
+// to global_* instructions.  Through a plain pointer loaded from the parameter block the
+// compiler emits flat_* accesses, and a flat access may alias LDS, so it drains all outstanding
+// memory operations (s_waitcnt vmcnt(0)) before the next LDS access -- which serialised the LDS
+// phases of the tile and scan kernels behind their global stores.  (The round trip cast back to
+// a generic pointer is folded away: the access must go through the G<T> pointer itself.)
+#ifdef __HIP_DEVICE_COMPILE__
+template <typename T>
+using G = __attribute__((address_space(1))) T;
+#else
+template <typename T>
+using G = T;  // (host pass: the device functions are parsed, not compiled)
+#endif
+template <typename T>
+__device__ __forceinline__ G<T>* gbl(T* q) {
+  return (G<T>*)q;
+}
+// 16-byte global load / store through an address-space-1 pointer (native vector type: the HIP
+// vector class has no address-space-qualified copy operations)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gld4(const void* q) {
+  const u32x4 v = *(const G<u32x4>*)q;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <typename T, typename V>
+__device__ __forceinline__ void gadd(T* q, V v) {  // a global atomic add whose result is not used
+  __hip_atomic_fetch_add(gbl(q), static_cast<T>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T, typename V>
+__device__ __forceinline__ T gadd_r(T* q, V v) {  // ... whose result is used
+  return __hip_atomic_fetch_add(gbl(q), static_cast<T>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T, typename V>
+__device__ __forceinline__ void gmin(T* q, V v) {  // global atomic min (result not used)
+  __hip_atomic_fetch_min(gbl(q), static_cast<T>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gst4(void* q, const uint4& w) {
+  u32x4 v;
+  v.x = w.x;
+  v.y = w.y;
+  v.z = w.z;
+  v.w = w.w;
+  *(G<u32x4>*)q = v;
+}
+// whole-struct copies to / from global memory (AT() yields address-space-1 lvalues; the structs'
+// own copy operations are for generic ones): 16-byte pieces when the size allows, else words
+template <typename T>
+__device__ __forceinline__ void gput(G<T>& d, const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "gput: word-sized structs");
+  if constexpr (sizeof(T) % 16 == 0) {
+    for (size_t k = 0; k < sizeof(T) / 16; ++k)
+      ((G<u32x4>*)&d)[k] = reinterpret_cast<const u32x4*>(&v)[k];
+  } else {
+    for (size_t k = 0; k < sizeof(T) / 4; ++k) ((G<uint32_t>*)&d)[k] = reinterpret_cast<const uint32_t*>(&v)[k];
+  }
+}
+template <typename T>
+__device__ __forceinline__ T gget(const G<T>& s) {
+  static_assert(sizeof(T) % 4 == 0, "gget: word-sized structs");
+  T v;
+  if constexpr (sizeof(T) % 16 == 0) {
+    for (size_t k = 0; k < sizeof(T) / 16; ++k) reinterpret_cast<u32x4*>(&v)[k] = ((const G<u32x4>*)&s)[k];
+  } else {
+    for (size_t k = 0; k < sizeof(T) / 4; ++k) reinterpret_cast<uint32_t*>(&v)[k] = ((const G<uint32_t>*)&s)[k];
+  }
+  return v;
+}
+
 // First error wins; its source line goes to p.dbg so the host can name the
 // exact capacity or invariant that failed (bcsim_last_error_detail).
 __device__ inline void set_err_(const KP& p, int32_t code, int line) {
-  if (atomicCAS(p.err, 0, code) == 0) atomicCAS(p.dbg, 0, line);
+  int32_t z = 0;
+  if (__hip_atomic_compare_exchange_strong(gbl(p.err), &z, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)) {
+    z = 0;
+    __hip_atomic_compare_exchange_strong(gbl(p.dbg), &z, line, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 // The code and line are materialised by volatile asm INSIDE the (cold) error branch: as plain
 // constants, loop-invariant code motion hoisted every call site's pair out of the per-arrival
@@ -283,7 +383,7 @@ __device__ inline void set_err_(const KP& p, int32_t code, int line) {
 // recorded (source line in p.dbg, BCSIM_E_OVERFLOW in p.err) and the wave
 // stops instead of faulting the GPU.
 template <typename T>
-__device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int line) {
+__device__ inline G<T>& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int line) {
 #ifdef BCSIM_CHECKED
   if (idx >= cap) {
     atomicCAS(p.dbg, 0, line);
@@ -291,7 +391,7 @@ __device__ inline T& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, int l
     __builtin_amdgcn_endpgm();  // stop this wave: no access through garbage
   }
 #endif
-  return base[idx];
+  return gbl(base)[idx];
 }
 #ifdef BCSIM_CHECKED
 #define BAIL_IF_ERR() \
@@ -344,7 +444,8 @@ __device__ inline bool node_flagged_w(const KP& p, uint32_t b, uint32_t g, uint3
 }
 // lower the bucket's arrival-time bound (read first: most writers find it already lower)
 __device__ inline void bmin_lower(const KP& p, uint32_t b, long long t) {
-  if (t < *reinterpret_cast<volatile long long*>(&p.bmin[b])) atomicMin(&p.bmin[b], t);
+  if (t < *reinterpret_cast<volatile G<long long>*>(gbl(p.bmin) + b))
+    __hip_atomic_fetch_min(gbl(p.bmin) + b, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // start time of the cell that bucket k holds, seen from cell `cell` (records are emitted
 // 1 .. B-1 cells ahead)
@@ -355,7 +456,7 @@ __device__ inline long long bucket_t0(const KP& p, long long cell, uint32_t k) {
 }
 // set-once byte flag (many writers of the same byte: read first, store only if clear)
 __device__ inline void set_flag_once(uint8_t* f) {
-  if (*reinterpret_cast<volatile uint8_t*>(f) == 0) *f = 1;
+  if (*reinterpret_cast<volatile G<uint8_t>*>(gbl(f)) == 0) *gbl(f) = 1;
 }
 
 // blockIdx -> gnode of this rank's partition (XCD-contiguous ranges)
@@ -521,8 +622,8 @@ __device__ inline unsigned long long* cnt_stripe(const KP& p, uint32_t rep) {
 __device__ inline unsigned long long* kst_stripe(const KP& p) { return p.kstat + 8 * (blockIdx.x & (kKstStripes - 1)); }
 // bucket_cnt is only tested for nonzero: workgroups set it once instead of all adding to it
 __device__ inline void mark_busy(uint32_t* w) {
-  if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    __hip_atomic_store(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__hip_atomic_load(gbl(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    __hip_atomic_store(gbl(w), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // trace record at a reserved position (emit_trace reserves one; gossip reserves a window's worth)
@@ -548,11 +649,11 @@ __device__ inline void put_trace(const KP& p, uint32_t pos, const Key& k, uint32
 
 __device__ inline void emit_trace(const KP& p, const Key& k, uint32_t rep, uint32_t node, uint32_t kind,
                                   int32_t a, int32_t b, int32_t c) {
-  put_trace(p, atomicAdd(p.trace_cnt, 1u), k, rep, node, kind, a, b, c);
+  put_trace(p, gadd_r(p.trace_cnt, 1u), k, rep, node, kind, a, b, c);
 }
 
 __device__ inline void emit_vlog(const KP& p, const Key& k, uint32_t rep, uint32_t node, int32_t v) {
-  const uint32_t pos = atomicAdd(p.vlog_cnt, 1u);
+  const uint32_t pos = gadd_r(p.vlog_cnt, 1u);
   if (pos >= p.cap_vlog) {
     set_err(p, BCSIM_E_OVERFLOW);
     return;
@@ -573,7 +674,7 @@ __device__ inline void emit_vlog(const KP& p, const Key& k, uint32_t rep, uint32
 // one 16-byte memory access per record (the compiler otherwise splits the
 // mixed-width struct into byte / short / dwordx3 pieces)
 __device__ inline Rec ld_rec(const Rec* p) {
-  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  const uint4 v = gld4(p);
   Rec r;
   __builtin_memcpy(&r, &v, sizeof r);
   return r;
@@ -581,9 +682,9 @@ __device__ inline Rec ld_rec(const Rec* p) {
 __device__ inline void st_rec(Rec* p, const Rec& r) {
   uint4 v;
   __builtin_memcpy(&v, &r, sizeof v);
-  *reinterpret_cast<uint4*>(p) = v;
+  gst4(p, v);
 }
-__device__ inline void clr_rec(Rec* p) { *reinterpret_cast<uint4*>(p) = make_uint4(0, 0, 0, 0); }
+__device__ inline void clr_rec(Rec* p) { gst4(p, make_uint4(0, 0, 0, 0)); }
 // Inbox-slot records carry a ring-turn tag in flags bits 3-7: (arrival cell / B) mod 32.  A slot
 // is live for cell c only with the tag of c, so a delivered record needs no clear: it goes stale
 // when the bucket comes round again, and the host zeroes a bucket once every 32 turns
@@ -603,7 +704,7 @@ __device__ inline uint32_t emit_tag(long long cq, uint32_t cr, long long rel, ui
 // 32-byte ops as two dwordx4 accesses
 __device__ inline Op ld_op(const Op* q) {
   const uint4* v = reinterpret_cast<const uint4*>(q);
-  const uint4 a = v[0], b = v[1];
+  const uint4 a = gld4(v), b = gld4(v + 1);
   Op o;
   __builtin_memcpy(&o, &a, 16);
   __builtin_memcpy(reinterpret_cast<char*>(&o) + 16, &b, 16);
@@ -614,8 +715,8 @@ __device__ inline void st_op(Op* q, const Op& o) {
   __builtin_memcpy(&a, &o, 16);
   __builtin_memcpy(&b, reinterpret_cast<const char*>(&o) + 16, 16);
   uint4* v = reinterpret_cast<uint4*>(q);
-  v[0] = a;
-  v[1] = b;
+  gst4(v, a);
+  gst4(v + 1, b);
 }
 
 // An Op as its two raw dwordx4 words: a = {t lo, t hi, dt, origin}, b = {sub, edge,
@@ -641,7 +742,7 @@ __device__ inline void raw_sel(RawOp& d, const RawOp& s, bool c) {
 __device__ inline RawOp raw_zero() { return RawOp{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)}; }
 __device__ inline RawOp ld_raw(const Op* q) {
   const uint4* v = reinterpret_cast<const uint4*>(q);
-  return RawOp{v[0], v[1]};
+  return RawOp{gld4(v), gld4(v + 1)};
 }
 __device__ inline int64_t raw_t(const RawOp& o) {
   return static_cast<int64_t>((static_cast<uint64_t>(o.a.y) << 32) | o.a.x);
@@ -816,7 +917,7 @@ __global__ void k_xcount(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
     const int ld = __ffsll(static_cast<long long>(rem)) - 1;
     const uint32_t gl = __shfl(g, ld, 64);
     const unsigned long long same = __ballot(v && g == gl);
-    if (lane == static_cast<uint32_t>(ld)) atomicAdd(&AT(p.seg_cnt, gl, p.NT), static_cast<uint32_t>(__popcll(same)));
+    if (lane == static_cast<uint32_t>(ld)) __hip_atomic_fetch_add(&AT(p.seg_cnt, gl, p.NT), static_cast<uint32_t>(__popcll(same)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     rem &= ~same;
   }
 }
@@ -954,7 +1055,7 @@ __global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
     const unsigned long long same = __ballot(v && x.g == gl);
     uint32_t base = 0;
     if (lane == static_cast<uint32_t>(ld))
-      base = AT(p.seg_off, gl, p.NT + 1) + atomicAdd(&AT(p.cursor, gl, p.NT), static_cast<uint32_t>(__popcll(same)));
+      base = AT(p.seg_off, gl, p.NT + 1) + __hip_atomic_fetch_add(&AT(p.cursor, gl, p.NT), static_cast<uint32_t>(__popcll(same)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     base = __shfl(base, ld, 64);
     if (v && x.g == gl) pos = base + static_cast<uint32_t>(__popcll(same & ((1ull << lane) - 1ull)));
     rem &= ~same;
@@ -1011,7 +1112,7 @@ __global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long l
   if (tidx() == 0) {
     long long m = wmin[0];
     for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) m = wmin[w] < m ? wmin[w] : m;
-    if (m != LLONG_MAX) atomicMin(&p.scal[1], m);
+    if (m != LLONG_MAX) gmin(&p.scal[1], m);
   }
 }
 
@@ -1130,7 +1231,7 @@ __device__ void raft_arm_election(Ctx& c, RaftState& s) {  // getElectionTimeout
     s.next_election = ctx_timer(c, TM_RAFT_ELECTION, AT(p.raft_elec, r % 150, 150));
   } else {
     s.next_election = ctx_timer(c, TM_RAFT_ELECTION, 0, true);
-    const uint32_t pos = atomicAdd(p.dreq_cnt, 1u);
+    const uint32_t pos = gadd_r(p.dreq_cnt, 1u);
     if (pos >= p.cap_dreq) {
       set_err(p, BCSIM_E_OVERFLOW);
       return;
@@ -2035,7 +2136,7 @@ __device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint3
   }
   __syncthreads();
   // one trace reservation per window for all its first receipts (no per-record global atomic)
-  if (tid == 0) S.tr_pos = S.tr_n ? atomicAdd(p.trace_cnt, S.tr_n) : 0u;
+  if (tid == 0) S.tr_pos = S.tr_n ? gadd_r(p.trace_cnt, S.tr_n) : 0u;
   for (uint32_t r = tid; r < n; r += blockDim.x)
     if (acls[r])
       AT(p.gseen, static_cast<size_t>(g) * p.pbft_seq_cap + rec_of(rs, asec[r]).f0,
@@ -2508,7 +2609,7 @@ __device__ inline uint32_t fast_key_find(const FastShared& F, uint32_t key) {
 // k_link_mesh (8 listed ops, 9 too many broadcasts) for the generic kernels
 #define FDBG(k)                                             \
   do {                                                      \
-    if (p.fdbg) atomicAdd(&p.fdbg[(k)], 1ull);              \
+    if (p.fdbg) gadd_r(&p.fdbg[(k)], 1ull);              \
   } while (0)
 // BCSIM_WGT=1 (debug): per-workgroup phase clock of k_scan_pbft, same slots as scan_node's SPH
 #define FPH(k)                                                                              \
@@ -2537,7 +2638,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   if (!flag || has_ss || timer || xn || deg > kFastLanes * kFastRPL || deg > p.cap_arr || blockDim.x != kFastLanes ||
       !p.impl || !p.eslot || p.delay_mode != BCSIM_DELAY_FIXED) {
     if (tid == 0) {
-      AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+      AT(p.act, 2ull * p.NT + gadd_r(&p.act_n[2], 1u), 4ull * p.NT) = g;
       if (wep) AT(p.l2mark, g, p.NT) = wep;
       FDBG(!flag ? 0 : has_ss ? 1 : timer ? 2 : xn ? 3 : (deg > kFastLanes * kFastRPL || deg > p.cap_arr) ? 4 : 5);
     }
@@ -2567,7 +2668,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
 #pragma unroll
   for (uint32_t j = 0; j < kFastRPL; ++j) {  // the whole row in flight at once
     const uint32_t k = j * kFastLanes + tid;
-    rv[j] = k < deg ? *reinterpret_cast<const uint4*>(slots + k) : make_uint4(0, 0, 0, 0);
+    rv[j] = k < deg ? gld4(slots + k) : make_uint4(0, 0, 0, 0);
   }
   // ... and the link words of its out-edges with it (LDS; used by the echo pass at the end)
   if (echo_dir) {
@@ -2576,7 +2677,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
 #pragma unroll
     for (uint32_t j = 0; j < kFastRPL; ++j) {
       const uint32_t k = j * kFastLanes + tid;
-      lv[j] = k < deg ? lrow[k] : 0ull;
+      lv[j] = k < deg ? gbl(lrow)[k] : 0ull;
     }
 #pragma unroll
     for (uint32_t j = 0; j < kFastRPL; ++j) F.lw[j * kFastLanes + tid] = lv[j];
@@ -2682,7 +2783,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   // anything else the generic path must take -- nothing has been written
   if (F.bad || F.kmin != F.kmax) {
     if (tid == 0) {
-      AT(p.act, 2ull * p.NT + atomicAdd(&p.act_n[2], 1u), 4ull * p.NT) = g;
+      AT(p.act, 2ull * p.NT + gadd_r(&p.act_n[2], 1u), 4ull * p.NT) = g;
       if (wep) AT(p.l2mark, g, p.NT) = wep;
       FDBG(F.bad ? 6 : 7);
     }
@@ -2783,7 +2884,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   if (p.desc && tot.x == tot.w && tot.x != 0 && F.fmin == F.fmax) {
     rdesc_on = !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & kSfD);
     if (!rdesc_on) {
-      const uint4 od = p.rdesc[static_cast<size_t>(cell % kOpRing) * p.NT + g];
+      const uint4 od = gld4(p.rdesc + static_cast<size_t>(cell % kOpRing) * p.NT + g);
       rdesc_on = static_cast<long long>((static_cast<uint64_t>(od.y) << 32) | od.x) < t_lo;
     }
   }
@@ -2832,10 +2933,10 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
       const int64_t due = t + app;
       const uint64_t ut = static_cast<uint64_t>(due);
       if (!rdesc_on)
-        *eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q) =
-            make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), sp,
-                       static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m1))) |
-                           (static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m2))) << 16));
+        gst4(eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q),
+             make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), sp,
+                        static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m1))) |
+                            (static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m2))) << 16)));
       if (due < cs + p.L)  // (due >= t >= cs: the arrival cell, without a 64-bit division)
         ++n_slot0;
       else
@@ -2871,7 +2972,7 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
       const int64_t bu0 = static_cast<int64_t>(lw >> 16);
       const int64_t bu = (bu0 > t ? bu0 : t) + p.tx_tot[((r.w >> 24) & RF_BIG) ? 1 : 0];
       if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
-      lrow[j * kFastLanes + tid] = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
+      gbl(lrow)[j * kFastLanes + tid] = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
     }
   }
   if (rdesc_on || echo_desc) {  // descriptor bitmaps: bit k = in-slot k holds an arrival
@@ -2883,8 +2984,8 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
       const uint32_t w0 = j * (kFastLanes / 32) + wv * 2 + lane;
       if (lane < 2 && w0 < p.dwords) {
         const uint32_t word = static_cast<uint32_t>(mv >> (32 * lane));
-        if (rdesc_on) rb[w0] = word;
-        if (echo_desc) eb[w0] = word;
+        if (rdesc_on) gbl(rb)[w0] = word;
+        if (echo_desc) gbl(eb)[w0] = word;
       }
     }
   }
@@ -2917,8 +3018,8 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
     uint8_t& f = AT(p.sflag, (cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT);
     if (rdesc_on) {  // kSfD0 / kSfD1: the descriptor's replies are due in this cell / the next
       const uint64_t ud = static_cast<uint64_t>(cs + static_cast<long long>(F.kmax >> 32) + app);
-      p.rdesc[static_cast<size_t>(cell % kOpRing) * p.NT + g] =
-          make_uint4(static_cast<uint32_t>(ud), static_cast<uint32_t>(ud >> 32), sub0, F.fmin);
+      gst4(p.rdesc + static_cast<size_t>(cell % kOpRing) * p.NT + g,
+           make_uint4(static_cast<uint32_t>(ud), static_cast<uint32_t>(ud >> 32), sub0, F.fmin));
       f = static_cast<uint8_t>((f & ~kSfD) | (sm << 4));
     } else {
       f = static_cast<uint8_t>(f | sm);
@@ -2936,26 +3037,26 @@ __global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, lo
   FPH(7);
   if (echo_desc) {
     const uint64_t ut = static_cast<uint64_t>(cs + static_cast<long long>(F.kmax >> 32));
-    p.edesc[static_cast<size_t>(g) * kEDesc + ne0] = make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32),
-                                                                F.bigs == 1u ? 1u : 0u, 0u);
+    gst4(p.edesc + static_cast<size_t>(g) * kEDesc + ne0,
+         make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), F.bigs == 1u ? 1u : 0u, 0u));
     AT(p.en, g, p.NT) = static_cast<uint8_t>(ne0 + 1);
   }
   if (echo_dir || echo_desc) {
     AT(p.eapp, g, p.NT) = t_lo;
-    if (tot.w) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(tot.w));
+    if (tot.w) gadd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(tot.w));
   }
   unsigned long long* cnt = cnt_stripe(p, rep);
   const uint32_t type_of[4] = {PB_PRE_PREPARE, PB_PREPARE, PB_COMMIT, PB_PREPARE_RES};
   for (int t4 = 0; t4 < 4; ++t4)
-    if (F.tcount[t4]) atomicAdd(&cnt[CNT_DELIV + type_of[t4]], static_cast<unsigned long long>(F.tcount[t4]));
+    if (F.tcount[t4]) gadd(&cnt[CNT_DELIV + type_of[t4]], static_cast<unsigned long long>(F.tcount[t4]));
   const unsigned long long n = tot.w;
   if (n) {
-    atomicAdd(&cnt[CNT_DELIV_TOTAL], n);
-    if (p.echo) atomicAdd(&cnt[CNT_ECHOES], n);
-    atomicAdd(&kst_stripe(p)[KST_DELIV], n);
-    atomicAdd(&cnt[CNT_EVENTS], n);
+    gadd(&cnt[CNT_DELIV_TOTAL], n);
+    if (p.echo) gadd(&cnt[CNT_ECHOES], n);
+    gadd(&kst_stripe(p)[KST_DELIV], n);
+    gadd(&cnt[CNT_EVENTS], n);
     // every arrival is at one instant: t = cs + t_off of any of them
-    atomicMax(reinterpret_cast<long long*>(&cnt[CNT_TLAST]), cs + static_cast<long long>(F.kmax >> 32));
+    __hip_atomic_fetch_max(gbl(reinterpret_cast<long long*>(&cnt[CNT_TLAST])), cs + static_cast<long long>(F.kmax >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -3015,7 +3116,7 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
       if (nops + 2 * cnt > ocap) fast = false;  // the generic path raises the overflow
     }
     if (!fast) {
-      const uint32_t pos = atomicAdd(&p.act_n[2], 1u);
+      const uint32_t pos = gadd_r(&p.act_n[2], 1u);
       AT(p.act, 2ull * p.NT + pos, 4ull * p.NT) = g;
       continue;
     }
@@ -3138,7 +3239,7 @@ __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP*
     // (loop == 0: the host skips k_scan<.., LOOP> -- no timer, START, STOP or extras can be
     // due in the window -- so no node may be left over)
     if (!loop) set_err(p, BCSIM_E_TIE);
-    const uint32_t pos = atomicAdd(&p.act_n[2], 1u);
+    const uint32_t pos = gadd_r(&p.act_n[2], 1u);
     AT(p.act, 2ull * p.NT + pos, 3ull * p.NT) = g;
   }
   // this lane's in-slot
@@ -3215,7 +3316,7 @@ __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP*
     draws0 = AT(p.draws, g, p.NT);
   }
   __syncthreads();
-  if (tid == 0) s_trbase = s_nf ? atomicAdd(p.trace_cnt, s_nf) : 0u;
+  if (tid == 0) s_trbase = s_nf ? gadd_r(p.trace_cnt, s_nf) : 0u;
   __syncthreads();
   if (nf) {
     const uint32_t ocap = op_cap(p, g);
@@ -3357,7 +3458,7 @@ struct FqLink {
 // kinds: 1 enqueue, 2 into the device queue (x = frame start), 3 drop, 4 wake
 __device__ inline void fq_log(const KP& p, const FqLink& L, int64_t t, uint32_t kind, const uint4& pk, int64_t x) {
   if (!p.fqlog || t < p.fqlog_t0 || t >= p.fqlog_t1) return;
-  const uint32_t pos = atomicAdd(p.fqlog_n, 1u);
+  const uint32_t pos = gadd_r(p.fqlog_n, 1u);
   if (pos >= p.cap_fqlog) return;
   const uint32_t m = pk.z & 0xFFFFu;
   p.fqlog[2ull * pos] = make_uint4(static_cast<uint32_t>(t), static_cast<uint32_t>(static_cast<uint64_t>(t) >> 32), L.e,
@@ -3705,22 +3806,22 @@ __device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32
   }
   if (list > p.n_buckets) {  // another rank's receiver
     const uint32_t r = list - p.n_buckets - 1;
-    atomicMin(&p.scal[4], static_cast<long long>(static_cast<uint64_t>(x.cell) & ((1ull << 48) - 1)));
-    const uint32_t pos = atomicAdd(&p.send_cnt[r], 1u);
+    gmin(&p.scal[4], static_cast<long long>(static_cast<uint64_t>(x.cell) & ((1ull << 48) - 1)));
+    const uint32_t pos = gadd_r(&p.send_cnt[r], 1u);
     if (pos >= p.cap_send) {
       set_err(p, BCSIM_E_OVERFLOW);
       return;
     }
     p.sendbuf[static_cast<size_t>(r) * p.cap_send + pos] = x;
   } else if (list == p.n_buckets) {
-    const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+    const uint32_t pos = gadd_r(p.ov_cnt, 1u);
     if (pos >= p.cap_ov) {
       set_err(p, BCSIM_E_OVERFLOW);
       return;
     }
     AT(p.ov, pos, p.cap_ov) = x;
   } else {
-    const uint32_t pos = atomicAdd(&p.x_cnt[list], 1u);
+    const uint32_t pos = gadd_r(&p.x_cnt[list], 1u);
     if (pos >= p.cap_x) {
       set_err(p, BCSIM_E_OVERFLOW);
       return;
@@ -3806,7 +3907,7 @@ __device__ __attribute__((always_inline)) inline void link_finish(const KP& p, L
   }
   if (n_lists > B + 1) {
     for (int d = 32; d > 0; d >>= 1) xmin = min(xmin, static_cast<long long>(__shfl_xor(xmin, d, 64)));
-    if ((tid & 63u) == 0 && xmin != LLONG_MAX) atomicMin(&p.scal[4], xmin);
+    if ((tid & 63u) == 0 && xmin != LLONG_MAX) gmin(&p.scal[4], xmin);
   }
   // ---- 5. counters: wave sums, LDS atomics, one global atomic per workgroup ----
   {
@@ -3842,7 +3943,7 @@ __device__ __attribute__((always_inline)) inline void link_finish(const KP& p, L
     p.wgt[8ull * g + 6] = ph[3];
   }
   if (tid == 0) {
-    if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
+    if (L.ovmin != LLONG_MAX) gmin(&p.scal[1], L.ovmin);
     // the previous arrival cell's replies are all consumed now
     if (clr_slots) AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) = 0;
     if (clr_rx) AT(p.iflag, fidx, static_cast<uint64_t>(p.n_buckets) * p.NT) = 0;
@@ -4828,7 +4929,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
     // descriptors into reply slots (the slot flags they stand for)
     if (ne || dl0 || dl1) mesh_desc_flush(p, D, g, ob, obp, sf0, sf1, rd0, rd1, dl0, dl1, ne);
     if (tid == 0) {
-      const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
+      const uint32_t pos = gadd_r(&p.act_n[3], 1u);
       AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
       FDBG(L.n_list ? 8 : 9);
     }
@@ -5307,7 +5408,7 @@ __global__ __launch_bounds__(64) void k_mesh_prep(const KP* __restrict__ pk, lon
   const uint32_t n_bc = L.n_bc;
   if (L.n_list || n_bc > kMeshBc) {  // the generic kernel takes the node (node_desc_flush first)
     if (tid == 0) {
-      const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
+      const uint32_t pos = gadd_r(&p.act_n[3], 1u);
       AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
     }
     return;
@@ -5406,6 +5507,7 @@ struct TileShared {
   unsigned long long bkm;   // buckets holding slot records of this tile
   long long ovmin;
   long long bmin[kMaxBuckets];  // the buckets' arrival-time bounds as of the start (read early)
+  uint64_t lwo[kTS][kTR];       // updated link words (0: unchanged), written out after the walk
 };
 // (receiver, sender) -> LDS index: the sender index XOR the receiver's low bits, so that a wave
 // writing one sender's 64 receivers and a wave reading two receivers' 32 senders both spread
@@ -5423,18 +5525,18 @@ __device__ inline void tile_append(const KP& p, TileShared& T, uint32_t list, co
   // (staging full: a direct, contended append)
   uint32_t* ctr = list == p.n_buckets ? p.ov_cnt : &p.x_cnt[list];
   const uint32_t cap = list == p.n_buckets ? p.cap_ov : p.cap_x;
-  const uint32_t at = atomicAdd(ctr, 1u);
+  const uint32_t at = gadd_r(ctr, 1u);
   if (at >= cap) {
     set_err(p, BCSIM_E_OVERFLOW);
     return;
   }
-  if (list == p.n_buckets)
-    AT(p.ov, at, p.cap_ov) = x;
-  else
-    AT(p.xbuf, static_cast<size_t>(list) * p.cap_x + at, p.cap_xbuf) = x;
+  uint4* dst = reinterpret_cast<uint4*>(list == p.n_buckets ? p.ov + at : p.xbuf + static_cast<size_t>(list) * p.cap_x + at);
+  const uint4* src = reinterpret_cast<const uint4*>(&x);
+  gst4(dst, src[0]);
+  gst4(dst + 1, src[1]);
 }
 
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_mesh_tile(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
+__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_mesh_tile(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
                                                    uint32_t epoch) {
   const KP& p = *pk;
   BAIL_IF_ERR();
@@ -5442,9 +5544,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const uint32_t nrt = p.n_tiles, nst = p.n_stiles;
   const uint32_t rep = blockIdx.x / (nst * nrt), rem = blockIdx.x % (nst * nrt);
   const uint32_t st = rem / nrt, rt = rem % nrt;
-  if (p.mtile[static_cast<size_t>(rep) * nst + st] != epoch) return;  // no job among these senders
+  if (gbl(p.mtile)[static_cast<size_t>(rep) * nst + st] != epoch) return;  // no job among these senders
   const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
-  unsigned long long* tph = p.wgtt ? p.wgtt + 8ull * blockIdx.x : nullptr;  // (debug phase clocks)
+  G<unsigned long long>* tph = p.wgtt ? gbl(p.wgtt) + 8ull * blockIdx.x : nullptr;  // (debug phase clocks)
 #define TPH(k)                                                       \
   do {                                                               \
     if (tph && tid == 0) tph[(k)] = __builtin_amdgcn_s_memrealtime(); \
@@ -5456,36 +5558,40 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   const uint32_t s = s0 + lane;
   // the link words of every edge of this wave's senders first (whether or not the sender has a
   // job: the loads need not wait for the job words), all in flight with the job loads below
-  uint64_t lv[kTS / 8];
+  uint64_t lv[4];
 #pragma unroll
-  for (uint32_t k = 0; k < kTS / 8; ++k) {
+  for (uint32_t k = 0; k < 4; ++k) {
     const uint32_t il = wv + k * nwv;
     const uint32_t i = i0 + il;
     const bool v = il < kTS && i < N && s < N && s != i;
-    lv[k] = v ? p.link[edge_loc(p, rep, i * N1 + (s < i ? s : s - 1))] : 0ull;
+    lv[k] = v ? gbl(p.link)[edge_loc(p, rep, i * N1 + (s < i ? s : s - 1))] : 0ull;
   }
   // jobs, broadcasts and descriptor tile masks of the 32 senders, all loads at once (a stale job
   // is told by its epoch; the other words are used only under its flags)
   if (tid < kTS * 4) {
     const uint32_t il = tid >> 2;
-    T.job[il][tid & 3u] = i0 + il < N ? p.mjob[(gb + il) * 4 + (tid & 3u)] : make_uint4(0, 0, 0, 0);
+    T.job[il][tid & 3u] = i0 + il < N ? gld4(p.mjob + (gb + il) * 4 + (tid & 3u)) : make_uint4(0, 0, 0, 0);
   } else if (tid < kTS * 4 + kTS * kMeshBc * 2) {
     const uint32_t k = tid - kTS * 4, il = k / (kMeshBc * 2);
-    if (i0 + il < N) T.bc[il][k % (kMeshBc * 2)] = p.mbc[(gb + il) * kMeshBc * 2 + k % (kMeshBc * 2)];
+    if (i0 + il < N) T.bc[il][k % (kMeshBc * 2)] = gld4(p.mbc + (gb + il) * kMeshBc * 2 + k % (kMeshBc * 2));
   } else if (tid < kTS * 4 + kTS * kMeshBc * 2 + kTS * 2) {
     const uint32_t k = tid - kTS * 4 - kTS * kMeshBc * 2, il = k >> 1;
-    if (i0 + il < N) T.mtb[il][k & 1u] = p.mtb[((gb + il) * nrt + rt) * 2 + (k & 1u)];
+    if (i0 + il < N) T.mtb[il][k & 1u] = gld4(p.mtb + ((gb + il) * nrt + rt) * 2 + (k & 1u));
   } else if (tid < kTS * 4 + kTS * kMeshBc * 2 + kTS * 2 + kTS * kEDesc) {
     const uint32_t k = tid - kTS * 4 - kTS * kMeshBc * 2 - kTS * 2, il = k / kEDesc;
-    if (i0 + il < N) T.mte[il][k % kEDesc] = p.mte[((gb + il) * nrt + rt) * kEDesc + k % kEDesc];
+    if (i0 + il < N) {
+      const uint64_t m = gbl(reinterpret_cast<uint64_t*>(p.mte))[((gb + il) * nrt + rt) * kEDesc + k % kEDesc];
+      T.mte[il][k % kEDesc] = make_uint2(static_cast<uint32_t>(m), static_cast<uint32_t>(m >> 32));
+    }
   }
   for (uint32_t k = tid; k < kTR * kTS / 4; k += blockDim.x) reinterpret_cast<uint32_t*>(T.rbk)[k] = 0xFFFFFFFFu;
+  for (uint32_t k = tid; k < kTR * kTS; k += blockDim.x) (&T.lwo[0][0])[k] = 0ull;
   for (uint32_t k = tid; k < B; k += blockDim.x) {
     T.lcnt[k] = 0;
     T.lmin[k] = ~0u;
   }
   for (uint32_t k = tid; k <= B; k += blockDim.x) T.lst[k] = 0;
-  for (uint32_t k = tid; k < B; k += blockDim.x) T.bmin[k] = *reinterpret_cast<volatile long long*>(&p.bmin[k]);
+  for (uint32_t k = tid; k < B; k += blockDim.x) T.bmin[k] = *reinterpret_cast<volatile G<long long>*>(&gbl(p.bmin)[k]);
   if (tid < 8) T.csum[tid] = 0;
   if (tid == 0) {
     T.bkm = 0ull;
@@ -5495,7 +5601,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   TPH(1);
   // the link words parked in the edges' record slots (each lane reads back only its own)
 #pragma unroll
-  for (uint32_t k = 0; k < kTS / 8; ++k) {
+  for (uint32_t k = 0; k < 4; ++k) {
     const uint32_t il = wv + k * nwv;
     if (il < kTS) {
       T.rec[tsw(lane, il)].x = static_cast<uint32_t>(lv[k]);
@@ -5616,15 +5722,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       const bool done = ok || !has;
       if (done && (ok || pe)) {
         ++st_edges;
-        p.link[edge_loc(p, rep, e)] = (static_cast<uint64_t>(ok ? end : bu) << 16) | lc;
+        T.lwo[il][lane] = (static_cast<uint64_t>(ok ? end : bu) << 16) | lc;
       }
       if (done) continue;
     }
     // ---- the general merge ----
     // (rare in the heavy waves: the implicit echo and reply slots of the edge)
-    const uint4 r0 = (v && rxe) ? *reinterpret_cast<const uint4*>(p.inbox + inbox_idx(p, ib, rep, e)) : make_uint4(0, 0, 0, 0);
-    uint4 w0 = (v && sl0) ? *eslot_at(p, ob, rep, e) : make_uint4(0, 0, 0, 0);
-    uint4 w1 = (v && sl1) ? *eslot_at(p, obp, rep, e) : make_uint4(0, 0, 0, 0);
+    const uint4 r0 = (v && rxe) ? gld4(p.inbox + inbox_idx(p, ib, rep, e)) : make_uint4(0, 0, 0, 0);
+    uint4 w0 = (v && sl0) ? gld4(eslot_at(p, ob, rep, e)) : make_uint4(0, 0, 0, 0);
+    uint4 w1 = (v && sl1) ? gld4(eslot_at(p, obp, rep, e)) : make_uint4(0, 0, 0, 0);
     bool hd0 = false, hd1 = false;
     if (sd0) {
       const uint4 mb = T.mtb[il][0];
@@ -5666,7 +5772,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       const long long ta0 = cs + r0.x;
       if (slot_live(rfl, tag) && ta0 >= t_lo && ta0 < t_hi && p.echo) {
         ebig = (rfl & RF_BIG) ? 1 : 0;
-        const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
+        const int64_t pin = p.prop_const >= 0 ? p.prop_const : gbl(p.prop_in)[e];
         et = ta0;
         edt = static_cast<uint32_t>(pin + p.tx_last[ebig]);
         esub = r0.y;
@@ -5681,7 +5787,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     st_ops += (hr ? 1u : 0u) + (hr2 ? 1u : 0u);
     if (n_bc == 0 && !he && !hr && !hr2 && !pe) continue;
     ++st_edges;
-    const int64_t pr = p.prop_const >= 0 ? p.prop_const : p.prop[e];
+    const int64_t pr = p.prop_const >= 0 ? p.prop_const : gbl(p.prop)[e];
     const uint32_t slot = s * N1 + (i < s ? i : i - 1);
     const uint32_t dg = rep * N + s;
     bool in_lds = false;
@@ -5727,7 +5833,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
             bkm |= 1ull << bk;
             in_lds = true;
           } else {
-            *reinterpret_cast<uint4*>(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox)) = rv;
+            gst4(p.inbox + inbox_idx(p, bk, rep, slot), rv);
             set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
                               static_cast<uint64_t>(B) * p.R * p.n_tiles));
           }
@@ -5738,7 +5844,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
           x.slot = slot;
           x.g = dg;
           tile_append(p, T, bk, x);
-          AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT) = 1;
+          gbl(p.iflag)[static_cast<size_t>(bk) * p.NT + dg] = 1;
         }
         if (bk != cb) {
           if (cbn) {
@@ -5837,7 +5943,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       }
     }
     if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
-    p.link[edge_loc(p, rep, e)] = (static_cast<uint64_t>(bu) << 16) | lc;
+    T.lwo[il][lane] = (static_cast<uint64_t>(bu) << 16) | lc;
   }
   if (cbn) {
     atomicAdd(&T.lcnt[cb], cbn);
@@ -5862,7 +5968,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   TPH(3);
   __syncthreads();
   TPH(4);
-  // the transposed slot records: each receiver's 32 in-slots of this sender tile in one run
+  // the link words, sender-major (one sender's 64 out-edges per wave-instruction)
+  for (uint32_t x = tid; x < kTR * kTS; x += blockDim.x) {
+    const uint32_t il = x / kTR, sl = x % kTR;
+    const uint64_t w = T.lwo[il][sl];
+    if (!w) continue;
+    const uint32_t i = i0 + il, sr = s0 + sl;
+    gbl(p.link)[edge_loc(p, rep, i * N1 + (sr < i ? sr : sr - 1))] = w;
+  }
+  // the transposed slot records: each receiver's in-slots of this sender tile in one run
   for (uint32_t x = tid; x < kTR * kTS; x += blockDim.x) {
     const uint32_t sl = x / kTS, il = x % kTS;
     const uint32_t q = tsw(sl, il);
@@ -5870,7 +5984,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     if (bk == 0xFFu || (p.exp & 4u)) continue;
     const uint32_t sr = s0 + sl, i = i0 + il;
     const uint32_t slot = sr * N1 + (i < sr ? i : i - 1);
-    *reinterpret_cast<uint4*>(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox)) = T.rec[q];
+    gst4(p.inbox + inbox_idx(p, bk, rep, slot), T.rec[q]);
   }
   // staged extras / overflow records: one atomic per list
   if (T.xn) {
@@ -5879,7 +5993,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
       if (!c) continue;
       uint32_t* ctr = k == B ? p.ov_cnt : &p.x_cnt[k];
       const uint32_t cap = k == B ? p.cap_ov : p.cap_x;
-      const uint32_t base = atomicAdd(ctr, c);
+      const uint32_t base = gadd_r(ctr, c);
       if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
       T.lst[k] = base;  // (this lane's list only: no other lane reads it before the barrier)
     }
@@ -5888,9 +6002,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     for (uint32_t k = tid; k < nx; k += blockDim.x) {
       const uint32_t list = T.xm[k] >> 24, at = T.lst[list] + (T.xm[k] & 0xFFFFFFu);
       if (list == B) {
-        if (at < p.cap_ov) p.ov[at] = T.xs[k];
+        if (at < p.cap_ov) {
+          const uint4* src = reinterpret_cast<const uint4*>(&T.xs[k]);
+          uint4* dst = reinterpret_cast<uint4*>(p.ov + at);
+          gst4(dst, src[0]);
+          gst4(dst + 1, src[1]);
+        }
       } else if (at < p.cap_x) {
-        p.xbuf[static_cast<size_t>(list) * p.cap_x + at] = T.xs[k];
+        const uint4* src = reinterpret_cast<const uint4*>(&T.xs[k]);
+        uint4* dst = reinterpret_cast<uint4*>(p.xbuf + static_cast<size_t>(list) * p.cap_x + at);
+        gst4(dst, src[0]);
+        gst4(dst + 1, src[1]);
       }
     }
   }
@@ -5898,21 +6020,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   // atomics that return nothing (no round trip at the end of the workgroup); the bound is
   // lowered only below the value read at the start
   if (tid < B && ((T.bkm >> tid) & 1ull))
-    AT(p.rtile, (static_cast<size_t>(tid) * p.R + rep) * p.n_tiles + rt, static_cast<uint64_t>(B) * p.R * p.n_tiles) = 1;
+    gbl(p.rtile)[(static_cast<size_t>(tid) * p.R + rep) * p.n_tiles + rt] = 1;
   for (uint32_t k = tid; k < B; k += blockDim.x)
     if (T.lcnt[k]) {
-      p.bucket_cnt[k] = 1u;
+      gbl(p.bucket_cnt)[k] = 1u;
       const long long t = bucket_t0(p, (t_hi - 1) / p.L, k) + T.lmin[k];
-      if (t < T.bmin[k]) atomicMin(&p.bmin[k], t);
+      if (t < T.bmin[k]) __hip_atomic_fetch_min(gbl(p.bmin) + k, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   if (tid == 0) {
     unsigned long long* cnt = cnt_stripe(p, rep);
-    if (T.csum[0]) atomicAdd(&cnt[CNT_SENDS], static_cast<unsigned long long>(T.csum[0]));
-    if (T.csum[1]) atomicAdd(&kst_stripe(p)[KST_REC], static_cast<unsigned long long>(T.csum[1]));
-    if (T.csum[2]) atomicAdd(&kst_stripe(p)[KST_OPS], static_cast<unsigned long long>(T.csum[2]));
-    if (T.csum[3]) atomicAdd(&kst_stripe(p)[KST_EDGES], static_cast<unsigned long long>(T.csum[3]));
-    if (T.csum[4]) atomicAdd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(T.csum[4]));
-    if (T.ovmin != LLONG_MAX) atomicMin(&p.scal[1], T.ovmin);
+    unsigned long long* ks = kst_stripe(p);
+    if (T.csum[0]) gadd(&cnt[CNT_SENDS], static_cast<unsigned long long>(T.csum[0]));
+    if (T.csum[1]) gadd(&ks[KST_REC], static_cast<unsigned long long>(T.csum[1]));
+    if (T.csum[2]) gadd(&ks[KST_OPS], static_cast<unsigned long long>(T.csum[2]));
+    if (T.csum[3]) gadd(&ks[KST_EDGES], static_cast<unsigned long long>(T.csum[3]));
+    if (T.csum[4]) gadd(&ks[KST_ECHO], static_cast<unsigned long long>(T.csum[4]));
+    if (T.ovmin != LLONG_MAX) __hip_atomic_fetch_min(gbl(p.scal) + 1, T.ovmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   TPH(5);
 #undef TPH
@@ -5979,7 +6102,7 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
   const unsigned long long listed = __ballot(due && !bc) & gmask;
   const bool fast = have && n <= G && deg <= G && listed == 0 && !scan_left;
   if (have && !fast && j == 0) {
-    const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
+    const uint32_t pos = gadd_r(&p.act_n[3], 1u);
     AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
   }
   // key-order rank of this lane's due broadcast; the group's broadcasts to LDS in that order
@@ -6079,7 +6202,7 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
           if (owner) {
             st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), xr.r);
           } else {
-            const uint32_t pos = atomicAdd(&p.x_cnt[bk], 1u);
+            const uint32_t pos = gadd_r(&p.x_cnt[bk], 1u);
             if (pos >= p.cap_x)
               set_err(p, BCSIM_E_OVERFLOW);
             else
@@ -6090,12 +6213,12 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
           atomicMin(&s_bmin[bk], static_cast<long long>(ta));
         } else {
           if (owner) xr.r.flags = static_cast<uint8_t>(xr.r.flags | RF_OWNER);
-          const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+          const uint32_t pos = gadd_r(p.ov_cnt, 1u);
           if (pos >= p.cap_ov)
             set_err(p, BCSIM_E_OVERFLOW);
           else
             AT(p.ov, pos, p.cap_ov) = xr;
-          atomicMin(&p.scal[1], static_cast<long long>(ca));
+          gmin(&p.scal[1], static_cast<long long>(ca));
         }
       }
       if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
@@ -6497,7 +6620,7 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
       p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
     }
   }
-  if (xmin != LLONG_MAX) atomicMin(&p.scal[4], xmin);
+  if (xmin != LLONG_MAX) gmin(&p.scal[4], xmin);
   // ---- 5. counters ----
   uint4 t1, t2;
   (void)block_scan4(make_uint4(static_cast<uint32_t>(dropped), static_cast<uint32_t>(sends),
@@ -6521,7 +6644,7 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
       bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + L.lmin[k]);
     }
   if (tid == 0) {
-    if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
+    if (L.ovmin != LLONG_MAX) gmin(&p.scal[1], L.ovmin);
     AT(p.n_ops, g, p.NT) = L.n_keep;
     AT(p.node_onext, g, p.NT) = L.omin;
     atomicAdd(&kst_stripe(p)[KST_KEPT], static_cast<unsigned long long>(L.n_keep));
@@ -6589,7 +6712,7 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
       if (raw_t(o) < t_hi) due |= 1u << c;
     }
     if (kl < na && !fast) {
-      const uint32_t pos = atomicAdd(&p.act_n[3], 1u);
+      const uint32_t pos = gadd_r(&p.act_n[3], 1u);
       AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
     }
     uint32_t c_rec = 0, c_ops = 0, c_edges = 0, c_echo = 0, c_sends = 0;
@@ -6733,7 +6856,7 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
       bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + L.lmin[k]);
     }
     if (tid == 0) {
-      if (L.ovmin != LLONG_MAX) atomicMin(&p.scal[1], L.ovmin);
+      if (L.ovmin != LLONG_MAX) gmin(&p.scal[1], L.ovmin);
       unsigned long long* ks = kst_stripe(p);
       if (s_c[0]) atomicAdd(&ks[KST_REC], static_cast<unsigned long long>(s_c[0]));
       if (s_c[1]) atomicAdd(&ks[KST_OPS], static_cast<unsigned long long>(s_c[1]));
@@ -6791,8 +6914,8 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
   }
   __syncthreads();
   if (tid == 0) {
-    s_base[0] = s_n[0] ? atomicAdd(&p.act_n[0], s_n[0]) : 0u;
-    s_base[1] = s_n[1] ? atomicAdd(&p.act_n[1], s_n[1]) : 0u;
+    s_base[0] = s_n[0] ? gadd_r(&p.act_n[0], s_n[0]) : 0u;
+    s_base[1] = s_n[1] ? gadd_r(&p.act_n[1], s_n[1]) : 0u;
   }
   __syncthreads();
   uint32_t ps = s_base[0], pl = s_base[1];
@@ -6823,7 +6946,7 @@ __device__ inline void import_one(const KP& p, long long g_cur, XRec x, uint32_t
     if (owner) {
       st_rec(&AT(p.inbox, inbox_idx(p, b, rep, x.slot), p.cap_inbox), x.r);
     } else {
-      const uint32_t pos = atomicAdd(&p.x_cnt[b], 1u);
+      const uint32_t pos = gadd_r(&p.x_cnt[b], 1u);
       if (pos < p.cap_x)
         AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
       else
@@ -6833,7 +6956,7 @@ __device__ inline void import_one(const KP& p, long long g_cur, XRec x, uint32_t
     bmin_lower(p, b, x.cell * p.L + static_cast<long long>(x.r.t_off));
     atomicAdd(&lb[b], 1u);
   } else {
-    const uint32_t pos = atomicAdd(p.ov_cnt, 1u);
+    const uint32_t pos = gadd_r(p.ov_cnt, 1u);
     if (pos < p.cap_ov)
       AT(p.ov, pos, p.cap_ov) = x;
     else
@@ -6887,7 +7010,7 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
   __syncthreads();
   for (uint32_t q = tidx(); q < B; q += blockDim.x)
     if (lb[q]) mark_busy(&p.bucket_cnt[q]);
-  if (tidx() == 0 && ovmin_s != LLONG_MAX) atomicMin(&p.scal[1], ovmin_s);
+  if (tidx() == 0 && ovmin_s != LLONG_MAX) gmin(&p.scal[1], ovmin_s);
 }
 
 // k_lead (multi-GPU, PBFT): this rank's "ticking leader" flags for k_pbft_tick
@@ -7203,7 +7326,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     __hip_atomic_store(&p.nxt_part[blockIdx.x], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&p.nxt_part[kNextBlocks + blockIdx.x], mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __threadfence();
-    last = atomicAdd(p.nxt_done, 1u) == nb - 1;
+    last = gadd_r(p.nxt_done, 1u) == nb - 1;
   }
   if (!__shfl(static_cast<int>(last), 0, 64)) return;
   __threadfence();
