@@ -70,6 +70,7 @@ struct Sim {
   int x_active = 0;            // extras of the grouped cell are in xgrp
   uint32_t bs_scan = 64, bs_link = 64;
   long long dbg_fail_cell = -1;  // test hook (BCSIM_DBG_FAIL_CELL): this rank fails at that cell
+  long long dbg_fail_import = -1;  // test hook (BCSIM_DBG_FAIL_IMPORT): ... after that cell's exchange
   bool sparse = false;
   uint32_t grid_scan = 0, grid_link = 0;  // k_scan / k_link workgroups (walking the active lists)
   uint32_t gossip_g = 0;  // dense gossip: lanes per node of k_gossip_scan (0 = generic k_scan only)
@@ -945,6 +946,7 @@ static int setup_device(Sim& s) {
   p.dbg_tmax = LLONG_MIN;
   if (const char* xv = std::getenv("BCSIM_EXP"); xv && *xv) p.exp = static_cast<uint32_t>(std::strtol(xv, nullptr, 0));
   if (const char* fv = std::getenv("BCSIM_DBG_FAIL_CELL"); fv && *fv) s.dbg_fail_cell = std::atoll(fv);
+  if (const char* fv = std::getenv("BCSIM_DBG_FAIL_IMPORT"); fv && *fv) s.dbg_fail_import = std::atoll(fv);
   if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -1825,6 +1827,10 @@ static int run(Sim& s, int64_t t_until) {
       // the bucket counts after k_import (a failure here rides the next cell's exchange); with
       // nothing imported the end-of-cell read-back before the exchange is still current
       lerr = s.last_import ? readback(s) : 0;
+      if (!lerr && s.dbg_fail_import >= 0 && static_cast<long long>(s.cells) > s.dbg_fail_import) {
+        g_detail = "injected failure after the exchange (BCSIM_DBG_FAIL_IMPORT)";  // test hook
+        lerr = BCSIM_E_OVERFLOW;
+      }
     } else {
       if (lrc) return lrc;
       if (tick) {

@@ -307,7 +307,11 @@ __device__ __forceinline__ G<T>* gbl(T* q) {
 }
 // 16-byte global load / store through an address-space-1 pointer (native vector type: the HIP
 // vector class has no address-space-qualified copy operations)
+#ifdef HIPEMU
+typedef uint4 u32x4;  // (debug host emulator, tools/hipemu)
+#else
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#endif
 __device__ __forceinline__ uint4 gld4(const void* q) {
   const u32x4 v = *(const G<u32x4>*)q;
   return make_uint4(v.x, v.y, v.z, v.w);

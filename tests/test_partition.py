@@ -137,14 +137,16 @@ def test_partitioned_n512_matches_oracle(engine_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("name", ["c4_bench_r4", "c5_gossip_r3"])
-def test_partitioned_fullsize_equals_single(name, engine_lib):
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("name,world", [("c4_bench_r4", 2), ("c5_gossip_r3", 2), ("c4_bench_r4", 4), ("c4_bench_r4", 8),
+                                        ("c5_gossip_r3", 4)])
+def test_partitioned_fullsize_equals_single(name, world, engine_lib):
     """SURVEY.md §4 item 4 at BASELINE size: the bench configurations themselves --
     C4 PBFT n=4096 (50 KB blocks, glibc lottery on, 4 rounds; blockchain-simulator.cc:34-51
     mesh) and C5 gossip n=65536 on the random 8-regular graph (3 rounds, echoes on) --
-    node-partitioned over 2 ranks sharing the GPU (host transport) give merged traces and
-    counters identical to the single-process run, bit for bit."""
+    node-partitioned over 2, 4 and 8 ranks sharing the GPU (host transport; BASELINE configs[3]
+    "1/2/4/8 MI355X node-partitioned PDES") give merged traces and counters identical to the
+    single-process run, bit for bit."""
     import bcsim
     import partition_run
     from parity_cases import any_case
@@ -152,11 +154,11 @@ def test_partitioned_fullsize_equals_single(name, engine_lib):
     single = bcsim.run(any_case(name), topology=topo)
     assert single[2]["error"] == 0 and single[2]["quiescent"]
     assert single[1]["delivered_total"] > 0
-    merged, err = partition_run.run(2, [name], transport="host", timeout=540)[name]
+    merged, err = partition_run.run(world, [name], transport="host", timeout=840)[name]
     assert err is None, err
     d = compare(single, merged)
-    assert d is None, f"{name} world=2: {d}"
-    if name.startswith("c4"):
+    assert d is None, f"{name} world={world}: {d}"
+    if name.startswith("c4") and world == 2:
         # broadcast de-dup (k_link_mesh xr_ship -> k_import): about half the 16.8 M records of
         # a heavy cell cross ranks, shipped as range records of up to 64 edges, so the volume
         # is far below one 32-byte record per cross-rank delivery
@@ -206,12 +208,12 @@ def test_rccl_transport_world1(engine_lib):
         assert d is None, f"{name}: {d}"
 
 
-def _fail_worker(rank, world, port, fail_rank, q):
+def _fail_worker(rank, world, port, fail_rank, q, fail_cell="3", t_until=None, hook="BCSIM_DBG_FAIL_CELL"):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [repo, os.path.join(repo, "tests"), os.path.join(repo, "blockchain-simulator_amd")]
     if rank == fail_rank:
-        os.environ["BCSIM_DBG_FAIL_CELL"] = "3"  # this rank alone fails at its 4th cell
+        os.environ[hook] = fail_cell  # this rank alone fails at that cell
     import torch.distributed as dist
     import bcsim
     from parity_cases import cases
@@ -221,7 +223,10 @@ def _fail_worker(rank, world, port, fail_rank, q):
     try:
         with bcsim.Simulator(cases()["pbft16_fixed_100"]) as s:
             s.set_partition(dist, transport="host")
-            s.run()
+            if t_until is None:
+                s.run()
+            else:
+                s.run(t_until)
     except bcsim.EngineError as e:
         code = e.code
     q.put((rank, code))
@@ -239,6 +244,29 @@ def test_one_rank_failure_stops_every_rank(engine_lib):
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_fail_worker, args=(r, world, port, fail_rank, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res[fail_rank] == -4  # BCSIM_E_OVERFLOW (injected)
+    assert res[1 - fail_rank] == -11  # BCSIM_E_PEER
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_failure_in_last_partial_window_stops_every_rank(engine_lib):
+    """A failure found after the exchange of the last window of a run() whose end is not a cell
+    boundary (here: rank 1 fails after the exchange of the first window -- BCSIM_DBG_FAIL_IMPORT,
+    as a k_import overflow found by the read-back would -- and the limit cuts that window at half
+    a cell) is not lost: it is carried into the next iteration, which finds nothing left before
+    the limit (bcsim_capi.hip run(), the lo >= hi exit), and every rank leaves with it."""
+    world, fail_rank = 2, 1
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    t_half = 1_500_000  # half of the C1 lookahead cell (3 ms + one 34-byte frame)
+    ps = [ctx.Process(target=_fail_worker, args=(r, world, port, fail_rank, q, "0", t_half, "BCSIM_DBG_FAIL_IMPORT")) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=180) for _ in ps)

@@ -39,6 +39,10 @@ struct uint4 {
   unsigned x, y, z, w;
 };
 inline uint4 make_uint4(unsigned a, unsigned b, unsigned c, unsigned d) { return uint4{a, b, c, d}; }
+struct uint2 {
+  unsigned x, y;
+};
+inline uint2 make_uint2(unsigned a, unsigned b) { return uint2{a, b}; }
 extern thread_local hipemu_ctx hipemu_t;
 #define threadIdx (hipemu_t.tid)
 #define blockIdx (hipemu_t.bid)
@@ -107,6 +111,8 @@ inline unsigned long long __umul64hi(unsigned long long a, unsigned long long b)
 // lane-exchange / ordering builtins: every lane of the wave must reach them together
 template <typename T>
 inline T __builtin_amdgcn_readlane(T v, int lane) { return __shfl(v, lane); }
+// (the engine reads only wave-uniform values this way)
+inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
 inline void __builtin_amdgcn_wave_barrier() { hipemu_wsync(); }
 #define __builtin_amdgcn_fence(...) std::atomic_thread_fence(std::memory_order_seq_cst)
 inline unsigned long long __builtin_amdgcn_s_memrealtime() {  // 100 MHz
@@ -152,6 +158,26 @@ inline void __hip_atomic_store(T* p, U v, int, int) { __atomic_store_n(p, static
 template <typename T>
 inline T __hip_atomic_load(T* p, int, int) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 #define __HIP_MEMORY_SCOPE_AGENT 1
+template <typename T, typename U>
+inline T __hip_atomic_fetch_add(T* p, U v, int, int) { return __atomic_fetch_add(p, static_cast<T>(v), __ATOMIC_RELAXED); }
+template <typename T, typename U>
+inline T __hip_atomic_fetch_min(T* p, U v, int, int) {
+  T o = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (static_cast<T>(v) < o && !__atomic_compare_exchange_n(p, &o, static_cast<T>(v), false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
+  return o;
+}
+template <typename T, typename U>
+inline T __hip_atomic_fetch_max(T* p, U v, int, int) {
+  T o = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (static_cast<T>(v) > o && !__atomic_compare_exchange_n(p, &o, static_cast<T>(v), false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
+  return o;
+}
+template <typename T, typename U>
+inline bool __hip_atomic_compare_exchange_strong(T* p, T* expected, U desired, int, int, int) {
+  return __atomic_compare_exchange_n(p, expected, static_cast<T>(desired), false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+}
 #define __HIP_MEMORY_SCOPE_WORKGROUP 2
 inline void __threadfence() { std::atomic_thread_fence(std::memory_order_seq_cst); }
 
