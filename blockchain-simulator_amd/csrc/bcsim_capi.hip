@@ -774,12 +774,16 @@ static int setup_device(Sim& s) {
       g_detail = "FQCODEL link state exceeds 64 GB";
       return BCSIM_E_UNSUPPORTED;
     }
-    uint8_t* fqmap = nullptr;
+    uint32_t* fqlnk = nullptr;
+    const size_t nt = fq ? s.NT : 1;
     if ((rc = dalloc(s, &p.fqh, ne * kFqH)) || (rc = dalloc(s, &p.fqdev, fq ? ne * p.fq_devcap : 1)) ||
         (rc = dalloc(s, &p.fqpk, fq ? ne * 3 * p.cap_fqp : 1)) || (rc = dalloc(s, &p.fqmsg, fq ? ne * p.cap_fqm : 1)) ||
-        (rc = dalloc(s, &fqmap, fq ? s.E : 1)))
+        (rc = dalloc(s, &fqlnk, fq ? s.E : 1)) || (rc = dalloc(s, &p.fqport, ne)) || (rc = dalloc(s, &p.fqpeer, ne)) ||
+        (rc = dalloc(s, &p.fqkey, ne)) || (rc = dalloc(s, &p.fqnport, nt)) || (rc = dalloc(s, &p.fqphant, nt)))
       return rc;
-    p.fqmap = (decltype(p.fqmap))(fqmap);
+    p.fqlnk = (decltype(p.fqlnk))(fqlnk);
+    p.fq_flows = c.fq_flows ? c.fq_flows : 1024;
+    p.fq_pert = c.fq_perturbation;
     if (fq) {
       std::vector<uint32_t> h0(kFqH, 0);
       for (uint32_t f = 0; f < 3; ++f) {
@@ -789,9 +793,14 @@ static int setup_device(Sim& s) {
       std::vector<uint32_t> hall(ne * kFqH);
       for (size_t k = 0; k < ne; ++k) std::copy(h0.begin(), h0.end(), hall.begin() + k * kFqH);
       HIPCHK(hipMemcpy(p.fqh, hall.data(), hall.size() * 4, hipMemcpyHostToDevice));
-      const std::vector<uint8_t> map =
-          fq_flow_map(s.N, s.row, s.col, s.rev, c.protocol, c.fq_flows ? c.fq_flows : 1024, c.fq_perturbation);
-      HIPCHK(hipMemcpy(fqmap, map.data(), s.E, hipMemcpyHostToDevice));
+      const std::vector<uint32_t> lnk = fq_link_numbers(s.N, s.row, s.col, s.rev);
+      HIPCHK(hipMemcpy(fqlnk, lnk.data(), s.E * 4, hipMemcpyHostToDevice));
+      // sockets unbound (port 0), no first-send keys pending (all ones)
+      HIPCHK(hipMemset(p.fqport, 0, ne * 4));
+      HIPCHK(hipMemset(p.fqpeer, 0, ne * 4));
+      HIPCHK(hipMemset(p.fqkey, 0xFF, ne * 16));
+      HIPCHK(hipMemset(p.fqnport, 0, nt * 4));
+      HIPCHK(hipMemset(p.fqphant, 0, nt * 4));
     }
   }
   // k_scan / k_link grids (multiples of 8: one list chunk per XCD).  Dense layout: one
@@ -1157,10 +1166,25 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
             : launch(s, KS_SCAN, k_scan<P, false>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa))
   if (grid.x == 0)
     rc = BCSIM_OK;  // no node has work in the window
-  else if (s.kp_dev_big && !s.sparse && s.P == 1 && grid.x <= s.few_scan)
-    // a few nodes (the leader's cells): the doubled staging window, a 1024-lane workgroup each
-    rc = launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false>), grid, dim3(1024), s.lds_big, s.kp_dev_big, cell, lo, hi, cs, fw,
-                xa);
+  else if (s.kp_dev_big && !s.sparse && s.P == 1 && grid.x <= s.few_scan) {
+    // a few nodes (the leader's cells): the doubled staging window, a 1024-lane workgroup each.
+    // With the list-2 overlap they are scanned and linked on the second stream, beside the
+    // other nodes' link stage (which skips them)
+    const uint32_t wep = s.l2_overlap && s.mesh_link ? (++s.win_epoch == 0 ? ++s.win_epoch : s.win_epoch) : 0u;
+    if (wep) {
+      rc = launch(s, -1, k_l2_take, dim3(1), dim3(256), 0, s.kp_dev, wep);
+      if (!rc) {
+        HIPCHK(hipEventRecord(s.ev_fork, s.stream));
+        HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_fork, 0));
+        std::swap(s.stream, s.stream2);
+        s.l2_pending = wep;
+      }
+    }
+    if (!rc)
+      rc = launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false>), grid, dim3(1024), s.lds_big, s.kp_dev_big, cell, lo, hi, cs, fw,
+                  xa);
+    if (wep) std::swap(s.stream, s.stream2);
+  }
   else if (s.scan_fast && !(lo <= 0 && 0 < hi) && !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi)) {
     // PBFT heavy waves: one pass over each row in registers; the nodes it leaves (list 2) to
     // the generic kernel -- a small looped grid, with the doubled staging window if there is one

@@ -177,12 +177,23 @@ struct KP {
   // packets in the disc, message-table bitmap), the start times of the device queue's waiting
   // frames [fq_devcap], three packet rings [3][cap_fqp] {enq lo, enq hi, msg | frame << 16,
   // IPv4 bytes} and the message table [cap_fqm] {sub, f0 | f1 << 16, f2 | type << 16 | big << 24 |
-  // echo << 25 | lost << 26, fragments left}; fqmap[e] = flow slot per packet class (global edge)
+  // echo << 25 | lost << 26, fragments left}.  Flow classification (oracle fq_bind /
+  // fq_class_slot): fqlnk[e] = the link's number in the mesh loop (global edge), fqport = the
+  // UDP port of the edge's client socket (0 until its first send binds it), fqpeer = the port of
+  // the reverse edge's socket (the echo class's destination port), fqnport[g] = sockets the
+  // node bound so far, fqphant[g] = Paxos's *end() socket bound, fqkey = a window's first-send
+  // keys {t lo, t hi, dt, sub} (binding order scratch)
   GP(uint32_t) fqh;
   GP(int64_t) fqdev;
   GP(uint4) fqpk;
   GP(uint4) fqmsg;
-  GP(const uint8_t) fqmap;
+  GP(const uint32_t) fqlnk;
+  GP(uint32_t) fqport;
+  GP(uint32_t) fqpeer;
+  GP(uint32_t) fqnport;
+  GP(uint32_t) fqphant;
+  GP(uint4) fqkey;
+  uint32_t fq_flows, fq_pert;
   uint32_t fq_devcap, cap_fqp, cap_fqm, fq_limit, fq_quantum, fq_batch, fq_min_bytes, fq_target_c, fq_interval_c;
   uint32_t ip_full[2], ip_last[2];
   // debug (BCSIM_FQLOG=<file>): every FQCODEL link event with t in [fqlog_t0, fqlog_t1) as two
@@ -279,7 +290,13 @@ constexpr uint32_t kEDesc = 2;        // pending echo descriptors per node (LDS:
 // sflag bits of a reply descriptor of the arrival cell (bits 0..3: reply slots due in cell + k)
 constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in this cell / the next
 // tiled mesh link stage: due broadcasts per job, senders x receivers per tile, 64-slot chunks
-constexpr uint32_t kMeshBc = 2, kTS = 16, kTR = 64;
+#ifndef BCSIM_TILE_TS
+#define BCSIM_TILE_TS 16
+#endif
+#ifndef BCSIM_TILE_DEFER
+#define BCSIM_TILE_DEFER 1  // link words through LDS, written after the walk (0: in the walk)
+#endif
+constexpr uint32_t kMeshBc = 2, kTS = BCSIM_TILE_TS, kTR = 64;
 constexpr uint32_t kTileThreads = kTS * 16;  // four senders per wave
 constexpr uint32_t kLoopGrid = 256;  // workgroups of the looped generic grids (lists 2, 3) at most
 // job flags (mjob[g][0].y)
@@ -528,6 +545,19 @@ struct Key {
   int64_t t, ts;
   uint32_t origin, sub;
 };
+// d = c ? s : d word by word through an opaque lane mask: the scan loop's choice of the next
+// event among arrival / timers / start / stop, written as struct assignments, was miscompiled
+// once the global-address accesses changed the schedule (a timer's t and ts with an arrival's
+// origin and sub: raft64_fixed), as RawOp selects were before (raw_sel)
+__device__ inline void key_sel(Key& d, const Key& s, bool c) {
+  uint32_t m = 0u - static_cast<uint32_t>(c);
+  asm volatile("" : "+v"(m));
+  const uint64_t m2 = (static_cast<uint64_t>(m) << 32) | m;
+  d.t = static_cast<int64_t>((static_cast<uint64_t>(s.t) & m2) | (static_cast<uint64_t>(d.t) & ~m2));
+  d.ts = static_cast<int64_t>((static_cast<uint64_t>(s.ts) & m2) | (static_cast<uint64_t>(d.ts) & ~m2));
+  d.origin = (s.origin & m) | (d.origin & ~m);
+  d.sub = (s.sub & m) | (d.sub & ~m);
+}
 __device__ inline bool key_less(const Key& a, const Key& b) {
   if (a.t != b.t) return a.t < b.t;
   if (a.ts != b.ts) return a.ts < b.ts;
@@ -722,6 +752,15 @@ __device__ inline void st_op(Op* q, const Op& o) {
   gst4(v, a);
   gst4(v + 1, b);
 }
+// (the LDS copies of ops: plain pointers -- ld_op / st_op / ld_raw are for global memory only)
+__device__ inline void st_op_lds(Op* q, const Op& o) {
+  uint4 a, b;
+  __builtin_memcpy(&a, &o, 16);
+  __builtin_memcpy(&b, reinterpret_cast<const char*>(&o) + 16, 16);
+  uint4* v = reinterpret_cast<uint4*>(q);
+  v[0] = a;
+  v[1] = b;
+}
 
 // An Op as its two raw dwordx4 words: a = {t lo, t hi, dt, origin}, b = {sub, edge,
 // f0 | f1 << 16, f2 | type << 16 | kind_flags << 24} (the Op layout above).
@@ -747,6 +786,10 @@ __device__ inline RawOp raw_zero() { return RawOp{make_uint4(0, 0, 0, 0), make_u
 __device__ inline RawOp ld_raw(const Op* q) {
   const uint4* v = reinterpret_cast<const uint4*>(q);
   return RawOp{gld4(v), gld4(v + 1)};
+}
+__device__ inline RawOp ld_raw_lds(const Op* q) {
+  const uint4* v = reinterpret_cast<const uint4*>(q);
+  return RawOp{v[0], v[1]};
 }
 __device__ inline int64_t raw_t(const RawOp& o) {
   return static_cast<int64_t>((static_cast<uint64_t>(o.a.y) << 32) | o.a.x);
@@ -1498,6 +1541,7 @@ constexpr uint32_t kTypeMask = 0xFFu << kTypeShift;
 constexpr uint32_t kIdxMask = (1u << kTypeShift) - 1u;
 __device__ inline uint32_t cls_type(uint32_t w) { return (w & kTypeMask) >> kTypeShift; }
 
+constexpr uint32_t kSortKeys = 32;  // sort_window's counting sort: distinct keys
 struct ScanShared {
   uint32_t wcnt[kMaxWaves];
   uint4 wsum[kMaxWaves];
@@ -1518,6 +1562,10 @@ struct ScanShared {
   uint32_t ocnt[kOpRing];  // reply-slot ops written, by due cell - cell
   uint32_t tr_n, tr_pos;   // gossip: first receipts of the window, next reserved trace position
   unsigned long long ph[8];  // BCSIM_WGT phase clock (debug)
+  // sort_window's counting sort: the distinct keys (ascending once sorted), per-key bases
+  unsigned long long sk[kSortKeys];
+  uint32_t skb[kSortKeys];
+  uint32_t snk, sbad;
 };
 #define SPH(k)                                                         \
   do {                                                                 \
@@ -1672,8 +1720,126 @@ __device__ inline bool sec_less(uint64_t ka, uint32_t sa, uint64_t kb, uint32_t 
   return ka < kb || (ka == kb && sa < sb);
 }
 
-// Sort (akey, asec) pairs of [0, n) unless already ordered.
-__device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec) {
+// Counting sort of the staged main-row arrivals [0, n) by key when they carry at most kSortKeys
+// distinct keys (the heavy waves: a few broadcast instants), stable in staging order, which is
+// the slot order (asec ascending) -- the order sec_less gives equal keys.  Positions: the key's
+// base + the same-key arrivals of earlier 64-arrival segments (a per-(segment, key) count table
+// in `tab`, prefix-summed by one wave per key) + the rank inside the segment (a ballot).  Three
+// barriers and O(n) work instead of the bitonic network's O(n log^2 n) with ~90 barriers (the
+// PBFT leader's 8K-arrival windows: ~100 us in one workgroup).  false: not applicable, nothing
+// written.
+__device__ bool sort_window_count(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec, uint32_t* tab,
+                                  uint32_t cap) {
+  const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
+  const uint32_t iters = (n + blockDim.x - 1) / blockDim.x;
+  if (iters * nwv * kSortKeys > cap) return false;
+  if (tid < kSortKeys) S.sk[tid] = ~0ull;
+  if (tid == 0) S.sbad = 0;
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += blockDim.x) {  // the distinct keys (CAS insert, read first)
+    const unsigned long long k = akey[r];
+    bool done = false;
+    for (uint32_t q = 0; q < kSortKeys && !done; ++q) {
+      const unsigned long long t = __hip_atomic_load(&S.sk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (t == k) done = true;
+      else if (t == ~0ull) done = atomicCAS(&S.sk[q], ~0ull, k) == ~0ull || S.sk[q] == k;
+    }
+    if (!done) S.sbad = 1;
+  }
+  __syncthreads();
+  if (S.sbad) return false;  // (uniform)
+  if (tid == 0) {  // sort the few keys
+    uint32_t nk = 0;
+    while (nk < kSortKeys && S.sk[nk] != ~0ull) ++nk;
+    for (uint32_t a = 1; a < nk; ++a) {
+      const unsigned long long x = S.sk[a];
+      uint32_t b = a;
+      while (b > 0 && S.sk[b - 1] > x) {
+        S.sk[b] = S.sk[b - 1];
+        --b;
+      }
+      S.sk[b] = x;
+    }
+    S.snk = nk;
+  }
+  __syncthreads();
+  const uint32_t nk = S.snk;
+  const uint32_t nseg = iters * nwv;  // segment s = it * nwv + wv: 64 consecutive arrivals
+  const uint64_t lt = (1ull << lane) - 1ull;
+  // each arrival: its key index and rank in the segment (into its own akey word: the key itself
+  // is S.sk[index]); per (segment, key) counts into tab
+  for (uint32_t it = 0; it < iters; ++it) {
+    const uint32_t r = it * blockDim.x + tid;
+    const bool v = r < n;
+    uint32_t d = 0;
+    if (v) {
+      const unsigned long long k = akey[r];
+      for (uint32_t q = 0; q < nk; ++q)
+        if (S.sk[q] == k) d = q;
+    }
+    uint32_t rk = 0, cl = 0;
+    for (uint32_t q = 0; q < nk; ++q) {
+      const uint64_t m = __ballot(v && d == q);
+      if (v && d == q) rk = static_cast<uint32_t>(__popcll(m & lt));
+      if (lane == q) cl = static_cast<uint32_t>(__popcll(m));
+    }
+    if (lane < nk) tab[(it * nwv + wv) * kSortKeys + lane] = cl;
+    if (v) akey[r] = d | (rk << 8);
+  }
+  __syncthreads();
+  // per key: exclusive prefix over the segments (one wave per key, 64 segments per step)
+  for (uint32_t q = wv; q < nk; q += nwv) {
+    uint32_t run = 0;
+    for (uint32_t s0 = 0; s0 < nseg; s0 += 64) {
+      const uint32_t sg = s0 + lane;
+      const uint32_t c = sg < nseg ? tab[sg * kSortKeys + q] : 0u;
+      uint32_t inc = c;
+      for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+      }
+      if (sg < nseg) tab[sg * kSortKeys + q] = run + inc - c;
+      run += static_cast<uint32_t>(__shfl(inc, 63, 64));
+    }
+    if (lane == 0) S.skb[q] = run;  // (the key's total for now)
+  }
+  __syncthreads();
+  if (tid == 0) {  // key bases in key order
+    uint32_t b = 0;
+    for (uint32_t q = 0; q < nk; ++q) {
+      const uint32_t c = S.skb[q];
+      S.skb[q] = b;
+      b += c;
+    }
+  }
+  __syncthreads();
+  // final position | sec << 32 into the arrival's own akey word, then the scatter of the secs,
+  // then the keys by runs
+  for (uint32_t it = 0; it < iters; ++it) {
+    const uint32_t r = it * blockDim.x + tid;
+    if (r >= n) continue;
+    const uint32_t dr = static_cast<uint32_t>(akey[r]), d = dr & 0xFFu;
+    const uint32_t pos = S.skb[d] + tab[(it * nwv + wv) * kSortKeys + d] + (dr >> 8);
+    akey[r] = pos | (static_cast<uint64_t>(asec[r]) << 32);
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += blockDim.x) {
+    const uint64_t w = akey[r];
+    asec[static_cast<uint32_t>(w)] = static_cast<uint32_t>(w >> 32);
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += blockDim.x) {
+    uint32_t d = 0;
+    for (uint32_t q = 1; q < nk; ++q)
+      if (S.skb[q] <= r) d = q;
+    akey[r] = S.sk[d];
+  }
+  __syncthreads();
+  return true;
+}
+
+// Sort (akey, asec) pairs of [0, n) unless already ordered (tab: cap words of scratch).
+__device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec, uint32_t* tab, uint32_t cap) {
   const uint32_t tid = tidx();
   if (tid == 0) S.unsorted = 0;
   __syncthreads();
@@ -1683,6 +1849,7 @@ __device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t*
   if (__ballot(bad) && (tid & 63) == 0) S.unsorted = 1;
   __syncthreads();
   if (!S.unsorted) return;
+  if (n == S.n_main && sort_window_count(S, n, akey, asec, tab, cap)) return;
   uint32_t P2 = 2;
   while (P2 < n) P2 <<= 1;
   for (uint32_t k = n + tid; k < P2; k += blockDim.x) {
@@ -2270,7 +2437,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
     }
     const uint32_t n_main = S.n_main;
     SPH(1);
-    sort_window(S, n, akey, asec);
+    sort_window(S, n, akey, asec, acls, cap);
     SPH(2);
 
     const RecSrc rsrc{slots, xs};
@@ -2304,25 +2471,24 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
           const TimerEnt& te = tm[k];
           if (!te.alive || te.pending_draw || te.t >= wb || te.t < t_lo) continue;
           const Key kk{te.t, te.ts, i, te.sub};
-          if (which < 0 || key_less(kk, best)) {
-            best = kk;
+          const bool cb = which < 0 || key_less(kk, best);
+          key_sel(best, kk, cb);
+          if (cb) {
             which = 1;
             tsel = static_cast<int>(k);
           }
         }
         if (start_pending && 0 < wb) {
           const Key kk{0, -1, i, 0};
-          if (which < 0 || key_less(kk, best)) {
-            best = kk;
-            which = 2;
-          }
+          const bool cb = which < 0 || key_less(kk, best);
+          key_sel(best, kk, cb);
+          if (cb) which = 2;
         }
         if (stop_pending && p.stop_ns < wb) {
           const Key kk{p.stop_ns, -1, i, 1};
-          if (which < 0 || key_less(kk, best)) {
-            best = kk;
-            which = 3;
-          }
+          const bool cb = which < 0 || key_less(kk, best);
+          key_sel(best, kk, cb);
+          if (cb) which = 3;
         }
         TRAIL(c);
         if (which < 0) break;
@@ -3452,12 +3618,20 @@ enum : uint32_t { FQ_NNEW = 36, FQ_NEWL = 37, FQ_NOLD = 40, FQ_OLDL = 41, FQ_NCR
 constexpr uint32_t kFqMaxMsgs = 128;  // message-table bitmap words FQ_MBM..FQ_MBM+3
 constexpr uint32_t kFqEcho = 1u << 25, kFqLost = 1u << 26;
 
+// header words past the message bitmap: the packet classes' bound flows (slot of class c in
+// bits 2c..2c+1, bound bit 8 + c) and their flow indices
+constexpr uint32_t FQ_MAP = 56, FQ_HSH = 57;
+// a FQCODEL record shipped to another rank carries its socket's port - 49152 in cell bits 48-61
+constexpr int kXPortShift = 48;
+static_assert(FQ_MBM + kFqMaxMsgs / 32 <= FQ_MAP && FQ_HSH + 3 <= kFqH, "FQCODEL header layout");
 struct FqLink {
   uint32_t* h;
   int64_t* dev;
   uint4* pk;
   uint4* msg;
-  uint32_t map, e, src;  // (src: the op source of the current send, debug log only)
+  uint32_t e, src;  // (src: the op source of the current send, debug log only)
+  uint32_t ia, ib;  // the link's sender / receiver IPv4 addresses
+  uint32_t pa, pe;  // client port of this edge's socket / of the reverse edge's (0: not bound)
 };
 // kinds: 1 enqueue, 2 into the device queue (x = frame start), 3 drop, 4 wake
 __device__ inline void fq_log(const KP& p, const FqLink& L, int64_t t, uint32_t kind, const uint4& pk, int64_t x) {
@@ -3482,16 +3656,73 @@ __device__ inline void fq_st64(uint32_t* w, int64_t v) {
   w[0] = static_cast<uint32_t>(v);
   w[1] = static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32);
 }
-__device__ inline FqLink fq_link(const KP& p, size_t le, uint32_t e) {
+// edge e = (i -> j) at rank-local index le.  Addresses: the k-th link of the mesh loop
+// (blockchain-simulator.cc:34-51) is network 1.0.0.0 + k*256, its larger endpoint .1
+__device__ inline FqLink fq_link(const KP& p, size_t le, uint32_t e, uint32_t i, uint32_t j) {
   FqLink L;
   L.h = p.fqh + le * kFqH;
   L.dev = p.fqdev + le * p.fq_devcap;
   L.pk = p.fqpk + le * 3 * p.cap_fqp;
   L.msg = p.fqmsg + le * p.cap_fqm;
-  L.map = p.fqmap[e];
   L.e = e;
   L.src = 0;
+  const uint32_t net = 0x01000000u + (p.fqlnk[e] << 8);
+  L.ia = net + (i > j ? 1u : 2u);
+  L.ib = net + (j > i ? 1u : 2u);
+  L.pa = p.fqport[le];
+  L.pe = p.fqpeer[le];
   return L;
+}
+// Ipv4QueueDiscItem::Hash: Murmur3-32 (seed 0x8BADF00D) of src | dst | proto 17 | sport |
+// dport | perturbation, big endian (17 bytes; oracle_fq_flow)
+__device__ inline uint32_t fq_hash(uint32_t src, uint32_t dst, uint32_t sp, uint32_t dp, uint32_t pert) {
+  auto bs = [](uint32_t x) { return __builtin_bswap32(x); };
+  auto mix = [](uint32_t h, uint32_t k) {
+    k *= 0xcc9e2d51u;
+    k = (k << 15) | (k >> 17);
+    k *= 0x1b873593u;
+    h ^= k;
+    h = (h << 13) | (h >> 19);
+    return h * 5u + 0xe6546b64u;
+  };
+  // bytes: src(4) dst(4) | 17 sp_hi sp_lo dp_hi | dp_lo pert(3 high bytes) | pert low byte
+  const uint32_t w2 = 17u | ((sp >> 8) & 0xFFu) << 8 | (sp & 0xFFu) << 16 | ((dp >> 8) & 0xFFu) << 24;
+  const uint32_t w3 = (dp & 0xFFu) | ((pert >> 24) & 0xFFu) << 8 | ((pert >> 16) & 0xFFu) << 16 | ((pert >> 8) & 0xFFu) << 24;
+  uint32_t h = 0x8BADF00Du;
+  h = mix(h, bs(src));
+  h = mix(h, bs(dst));
+  h = mix(h, w2);
+  h = mix(h, w3);
+  uint32_t k = pert & 0xFFu;  // tail byte
+  k *= 0xcc9e2d51u;
+  k = (k << 15) | (k >> 17);
+  k *= 0x1b873593u;
+  h ^= k;
+  h ^= 17u;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  return h ^ (h >> 16);
+}
+// the flow slot of packet class cls (0 app, 1 echo first fragment, 2 later fragment), bound at
+// the class's first packet: the slot of an already bound class with the same flow index, else
+// slot cls (oracle fq_class_slot)
+__device__ inline uint32_t fq_class_slot(const KP& p, FqLink& L, uint32_t cls) {
+  const uint32_t m = L.h[FQ_MAP];
+  if (m & (0x100u << cls)) return (m >> (2 * cls)) & 3u;
+  const uint32_t sp = cls == 0 ? L.pa : cls == 1 ? 7071u : 0u, dp = cls == 0 ? 7071u : cls == 1 ? L.pe : 0u;
+  if (cls < 2 && (sp | dp) == 7071u) set_err(p, BCSIM_E_STATE);  // a send from an unbound socket
+  const uint32_t h = fq_hash(L.ia, L.ib, sp, dp, p.fq_pert) % p.fq_flows;
+  uint32_t slot = cls;
+  for (uint32_t c = 0; c < 3; ++c)
+    if ((m & (0x100u << c)) && L.h[FQ_HSH + c] == h) {
+      slot = (m >> (2 * c)) & 3u;
+      break;
+    }
+  L.h[FQ_HSH + cls] = h;
+  L.h[FQ_MAP] = m | (0x100u << cls) | (slot << (2 * cls));
+  return slot;
 }
 __device__ inline bool fq_pop(const KP& p, FqLink& L, uint32_t f, uint4& out) {
   uint32_t* F = L.h + f * kFqF;
@@ -3752,7 +3983,7 @@ __device__ inline void fq_send(const KP& p, FqLink& L, int64_t now, uint32_t sub
   const uint32_t now_lo = static_cast<uint32_t>(now), now_hi = static_cast<uint32_t>(static_cast<uint64_t>(now) >> 32);
   for (uint32_t j = 0; j < F; ++j) {
     const uint32_t cls = j ? 2u : echo ? 1u : 0u;
-    const uint32_t f = (L.map >> (2 * cls)) & 3u;
+    const uint32_t f = fq_class_slot(p, L, cls);
     uint32_t* Fh = L.h + f * kFqF;
     if (Fh[FQ_CR] == kInvalid) Fh[FQ_CR] = L.h[FQ_NCR]++;
     if (Fh[FQ_ST] == 0) {
@@ -3794,6 +4025,10 @@ struct LinkShared {
   long long omin, ovmin;
   uint8_t tflag[kMaxTiles];  // full mesh: receiver tiles this sender wrote in this launch
   uint32_t tbk;              // (the bucket of those records; one per launch in practice)
+  // FQCODEL socket binding: this window's unbound sockets that send, the Paxos *end()
+  // socket's first send (fqph: it has one) and its key
+  uint32_t fqc, fqph, fqph_dt, fqph_sub;
+  long long fqph_t;
 };
 
 // Stage one extras / overflow record of k_link (list = bucket, or B for the
@@ -4065,6 +4300,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     L.omin = LLONG_MAX;
     L.ovmin = LLONG_MAX;
     L.tbk = kInvalid;
+    L.fqc = 0;
   }
   __syncthreads();
   unsigned long long dropped = 0, sends = 0, st_ops = 0;
@@ -4108,10 +4344,10 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       const Op ox = L.bco[a];
       uint32_t b2 = a;
       while (b2 > 0 && op_key_less(ox, ox.sub, L.bco[b2 - 1], L.bco[b2 - 1].sub)) {
-        st_op(&L.bco[b2], L.bco[b2 - 1]);
+        st_op_lds(&L.bco[b2], L.bco[b2 - 1]);
         --b2;
       }
-      st_op(&L.bco[b2], ox);
+      st_op_lds(&L.bco[b2], ox);
     }
   }
   // listed due ops (unicast / echo) grouped by edge: counting sort over the out-edges.
@@ -4138,6 +4374,130 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   }
   __syncthreads();
 
+  if constexpr (QM == 2) {
+    // ---- 1'. FQCODEL: a client socket binds -- takes the node's next ephemeral port -- at its
+    // first send (oracle fq_bind).  The unbound sockets sending in this window are ranked by
+    // the event key (t, t - dt, sub) of their first send; a rare pass (nothing after a node's
+    // sockets have all sent once), so the rank is a plain count over the node's edges ----
+    auto key_less = [](int64_t ta, uint32_t da, uint32_t sa, int64_t tb, uint32_t db, uint32_t sb) {
+      if (ta != tb) return ta < tb;
+      if (da != db) return da > db;
+      return sa < sb;
+    };
+    const uint32_t pbase = AT(p.fqnport, g, p.NT);
+    uint32_t my_c = 0;
+    for (uint32_t le = tid; le < deg; le += blockDim.x) {
+      const size_t x = eb0 + le;
+      if (p.fqport[x]) continue;
+      bool have = false;
+      int64_t bt = 0;
+      uint32_t bd = 0, bsb = 0;
+      auto consider = [&](int64_t t, uint32_t d, uint32_t sb) {
+        if (!have || key_less(t, d, sb, bt, bd, bsb)) {
+          have = true;
+          bt = t;
+          bd = d;
+          bsb = sb;
+        }
+      };
+      const uint32_t eb = n_list && le ? ecnt[le - 1] : 0u, ee = n_list ? ecnt[le] : 0u;
+      for (uint32_t a = eb; a < ee; ++a) {
+        const Op& o = ops[eidx[a]];
+        if (op_kind(o) != OP_ECHO) consider(o.t, o.dt, o.sub);
+      }
+      for (uint32_t bi = 0; bi < n_bc; ++bi) {  // (key order: the first one that reaches le)
+        const bool px = (op_flags(L.bco[bi]) & OPF_PAXOS) != 0;
+        if (px && le == 0) continue;
+        consider(L.bco[bi].t, L.bco[bi].dt, L.bco[bi].sub + (px ? le - 1 : le));
+        break;
+      }
+      const uint32_t e = e0 + le;
+      if (sl0) {
+        const RawOp r = slot_op(p, *eslot_at(p, ob, rep, e), i, e);
+        if (raw_t(r) >= t_lo && raw_t(r) < t_hi && raw_kind(r) != OP_ECHO) consider(raw_t(r), raw_dt(r), raw_sub(r));
+      }
+      if (sl1) {
+        const RawOp r = slot_op(p, *eslot_at(p, obp, rep, e), i, e);
+        if (raw_t(r) >= t_lo && raw_t(r) < t_hi && raw_kind(r) != OP_ECHO) consider(raw_t(r), raw_dt(r), raw_sub(r));
+      }
+      const uint64_t ut = static_cast<uint64_t>(bt);
+      p.fqkey[x] = have ? make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), bd, bsb)
+                        : make_uint4(~0u, ~0u, ~0u, ~0u);
+      my_c += have ? 1u : 0u;
+    }
+    {
+      const uint32_t ws = wave_sum(my_c);
+      if ((tid & 63u) == 0 && ws) atomicAdd(&L.fqc, ws);
+    }
+    if (tid == 0) {  // Paxos's *end() socket (its sends carry no edge)
+      L.fqph = 0;
+      if (p.protocol == BCSIM_PAXOS && !AT(p.fqphant, g, p.NT)) {
+        bool have = false;
+        int64_t bt = 0;
+        uint32_t bd = 0, bsb = 0;
+        auto consider = [&](int64_t t, uint32_t d, uint32_t sb) {
+          if (!have || key_less(t, d, sb, bt, bd, bsb)) {
+            have = true;
+            bt = t;
+            bd = d;
+            bsb = sb;
+          }
+        };
+        for (uint32_t k = 0; k < n; ++k) {
+          const Op& o = ops[k];
+          if (op_kind(o) == OP_SEND && o.edge == kInvalid && o.t < t_hi) consider(o.t, o.dt, o.sub);
+        }
+        for (uint32_t bi = 0; bi < n_bc; ++bi)
+          if (op_flags(L.bco[bi]) & OPF_PAXOS) {
+            consider(L.bco[bi].t, L.bco[bi].dt, L.bco[bi].sub + deg - 1);
+            break;
+          }
+        if (have) {
+          L.fqph = 1;
+          L.fqph_t = bt;
+          L.fqph_dt = bd;
+          L.fqph_sub = bsb;
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t nc = L.fqc + L.fqph;
+    if (nc) {
+      if (pbase + nc > 16383u && tid == 0) set_err(p, BCSIM_E_UNSUPPORTED);  // ephemeral ports used up
+      for (uint32_t le = tid; le < deg; le += blockDim.x) {
+        const size_t x = eb0 + le;
+        const uint4 kv = p.fqkey[x];
+        if ((kv.x & kv.y) == ~0u) continue;
+        const int64_t t = static_cast<int64_t>((static_cast<uint64_t>(kv.y) << 32) | kv.x);
+        uint32_t rank = 0;
+        for (uint32_t q = 0; q < deg; ++q) {
+          const uint4 o = p.fqkey[eb0 + q];
+          if ((o.x & o.y) == ~0u) continue;
+          rank += key_less(static_cast<int64_t>((static_cast<uint64_t>(o.y) << 32) | o.x), o.z, o.w, t, kv.z, kv.w) ? 1u : 0u;
+        }
+        if (L.fqph && key_less(L.fqph_t, L.fqph_dt, L.fqph_sub, t, kv.z, kv.w)) ++rank;
+        const uint32_t port = 49153u + pbase + rank;
+        p.fqport[x] = port;
+        // the echo class of the reverse edge sends to this port: its copy at the receiver (a
+        // receiver on another rank learns it from the shipped records, k_import)
+        const uint32_t j = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e0 + le, p.E);
+        if (!XR || p.owner[j] == p.rank) {
+          const uint32_t slot = p.mesh ? j * (p.N - 1) + (i < j ? i : i - 1) : AT(p.rev, e0 + le, p.E);
+          p.fqpeer[edge_loc(p, rep, slot)] = port;
+        }
+      }
+      __syncthreads();
+      for (uint32_t le = tid; le < deg; le += blockDim.x) {
+        const size_t x = eb0 + le;
+        const uint4 kv = p.fqkey[x];
+        if ((kv.x & kv.y) != ~0u) p.fqkey[x] = make_uint4(~0u, ~0u, ~0u, ~0u);
+      }
+      if (tid == 0) {
+        AT(p.fqnport, g, p.NT) = pbase + nc;
+        if (L.fqph) AT(p.fqphant, g, p.NT) = 1u;
+      }
+    }
+  }
   if (p.wgt && tid == 0) ph[1] = __builtin_amdgcn_s_memrealtime();
   // ---- 2. per edge: sort its ops by key, merge with broadcasts, FIFO, emit ----
   unsigned long long n_rec = 0, st_edges = 0, st_echo = 0, fdrop = 0, lost = 0;
@@ -4203,7 +4563,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       const int64_t pr = p.prop_const >= 0 ? p.prop_const : prop[le];
       const uint32_t slot = p.mesh ? s * (p.N - 1) + (i < s ? i : i - 1) : AT(p.rev, e, p.E);
       const uint32_t dg = rep * p.N + s;
-      FqLink FL = fq_link(p, eb0 + le, e);
+      FqLink FL = fq_link(p, eb0 + le, e, i, s);
       FqCount fc{0, 0};
       // a delivery: the record for the receiver's inbox slot / extras / overflow (as link_node)
       auto emit = [&](uint32_t sub, uint32_t bz, uint32_t bw24, int big, int64_t end) {
@@ -4227,11 +4587,11 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
         lc = static_cast<uint32_t>(ca) & 0xFFFFu;
         if (XR) {
           const uint32_t orank = p.owner[s];
-          if (orank != p.rank) {
+          if (orank != p.rank) {  // (with the sending socket's port for the receiver's echo class)
             XRec x;
             x.r = r;
             if (owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
-            x.cell = ca;
+            x.cell = ca | (static_cast<long long>(FL.pa - 49152u) << kXPortShift);
             x.slot = slot;
             x.g = dg;
             link_stage(p, L, g, B + 1 + orank, x);
@@ -4276,7 +4636,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
         RawOp o = raw_zero();
         uint32_t sub = 0;
         if (bi < n_bc) {
-          raw_sel(o, ld_raw(&L.bco[bi]), true);
+          raw_sel(o, ld_raw_lds(&L.bco[bi]), true);
           sub = raw_sub(o) + ((raw_flags(o) & OPF_PAXOS) ? le - 1 : le);
           src = 1;
         }
@@ -4454,7 +4814,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       RawOp o = raw_zero();
       uint32_t sub = 0;
       if (bi < n_bc) {
-        o = ld_raw(&L.bco[bi]);
+        o = ld_raw_lds(&L.bco[bi]);
         sub = raw_sub(o) + ((raw_flags(o) & OPF_PAXOS) ? le - 1 : le);
         src = 1;
       }
@@ -4950,10 +5310,10 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
       const Op ox = L.bco[a];
       uint32_t b2 = a;
       while (b2 > 0 && op_key_less(ox, ox.sub, L.bco[b2 - 1], L.bco[b2 - 1].sub)) {
-        st_op(&L.bco[b2], L.bco[b2 - 1]);
+        st_op_lds(&L.bco[b2], L.bco[b2 - 1]);
         --b2;
       }
-      st_op(&L.bco[b2], ox);
+      st_op_lds(&L.bco[b2], ox);
     }
   }
   __syncthreads();
@@ -5511,7 +5871,7 @@ struct TileShared {
   unsigned long long bkm;   // buckets holding slot records of this tile
   long long ovmin;
   long long bmin[kMaxBuckets];  // the buckets' arrival-time bounds as of the start (read early)
-  uint64_t lwo[kTS][kTR];       // updated link words (0: unchanged), written out after the walk
+  uint64_t lwo[BCSIM_TILE_DEFER ? kTS : 1][kTR];  // updated link words (0: unchanged), written out after the walk
 };
 // (receiver, sender) -> LDS index: the sender index XOR the receiver's low bits, so that a wave
 // writing one sender's 64 receivers and a wave reading two receivers' 32 senders both spread
@@ -5589,7 +5949,8 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
     }
   }
   for (uint32_t k = tid; k < kTR * kTS / 4; k += blockDim.x) reinterpret_cast<uint32_t*>(T.rbk)[k] = 0xFFFFFFFFu;
-  for (uint32_t k = tid; k < kTR * kTS; k += blockDim.x) (&T.lwo[0][0])[k] = 0ull;
+  if (BCSIM_TILE_DEFER)
+    for (uint32_t k = tid; k < kTR * kTS; k += blockDim.x) (&T.lwo[0][0])[k] = 0ull;
   for (uint32_t k = tid; k < B; k += blockDim.x) {
     T.lcnt[k] = 0;
     T.lmin[k] = ~0u;
@@ -5726,7 +6087,11 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
       const bool done = ok || !has;
       if (done && (ok || pe)) {
         ++st_edges;
-        T.lwo[il][lane] = (static_cast<uint64_t>(ok ? end : bu) << 16) | lc;
+        const uint64_t nw = (static_cast<uint64_t>(ok ? end : bu) << 16) | lc;
+        if (BCSIM_TILE_DEFER)
+          T.lwo[BCSIM_TILE_DEFER ? il : 0][lane] = nw;
+        else
+          gbl(p.link)[edge_loc(p, rep, e)] = nw;
       }
       if (done) continue;
     }
@@ -5947,7 +6312,10 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
       }
     }
     if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
-    T.lwo[il][lane] = (static_cast<uint64_t>(bu) << 16) | lc;
+    if (BCSIM_TILE_DEFER)
+      T.lwo[BCSIM_TILE_DEFER ? il : 0][lane] = (static_cast<uint64_t>(bu) << 16) | lc;
+    else
+      gbl(p.link)[edge_loc(p, rep, e)] = (static_cast<uint64_t>(bu) << 16) | lc;
   }
   if (cbn) {
     atomicAdd(&T.lcnt[cb], cbn);
@@ -5973,9 +6341,9 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
   __syncthreads();
   TPH(4);
   // the link words, sender-major (one sender's 64 out-edges per wave-instruction)
-  for (uint32_t x = tid; x < kTR * kTS; x += blockDim.x) {
+  for (uint32_t x = tid; BCSIM_TILE_DEFER && x < kTR * kTS; x += blockDim.x) {
     const uint32_t il = x / kTR, sl = x % kTR;
-    const uint64_t w = T.lwo[il][sl];
+    const uint64_t w = T.lwo[BCSIM_TILE_DEFER ? il : 0][sl];
     if (!w) continue;
     const uint32_t i = i0 + il, sr = s0 + sl;
     gbl(p.link)[edge_loc(p, rep, i * N1 + (sr < i ? sr : sr - 1))] = w;
@@ -6974,6 +7342,21 @@ __device__ inline void import_one(const KP& p, long long g_cur, XRec x, uint32_t
 // ring -> overflow); a range record (xr_ship) is expanded here into its per-edge records
 // (receiver s, its in-slot and sub + k follow from the sender and the first receiver).
 // g_cur = the cell just processed.
+// k_l2_take (list-2 overlap of a few-node scan window, PBFT full mesh): the window's scan list
+// (the leader's cells: a handful of nodes) becomes list 2 -- scanned and linked on the second
+// stream -- and its nodes are stamped so that the other nodes' link stage skips them
+__global__ __launch_bounds__(256) void k_l2_take(const KP* __restrict__ pk, uint32_t wep) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  const uint32_t n = p.act_n[0];
+  for (uint32_t k = blockIdx.x * blockDim.x + tidx(); k < n; k += gridDim.x * blockDim.x) {
+    const uint32_t g = AT(p.act, k, 4ull * p.NT);
+    AT(p.act, 2ull * p.NT + k, 4ull * p.NT) = g;
+    AT(p.l2mark, g, p.NT) = wep;
+  }
+  if (blockIdx.x == 0 && tidx() == 0) p.act_n[2] = n;
+}
+
 __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long long g_cur, const XRec* __restrict__ rx,
                                                 uint32_t n) {
   const KP& p = *pk;
@@ -7007,6 +7390,11 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
         }
       }
     } else {
+      if (p.qmodel == 2) {  // FQCODEL: the sender's client port, for this receiver's echo class
+        const uint32_t po = static_cast<uint32_t>((cw >> kXPortShift) & 0x3FFFu);
+        if (po) p.fqpeer[edge_loc(p, x.g / p.N, x.slot)] = 49152u + po;
+        x.cell = static_cast<long long>(cw & ((1ull << kXPortShift) - 1));
+      }
       import_one(p, g_cur, x, lb, ovmin);
     }
   }

@@ -87,70 +87,14 @@ std::vector<int32_t> glibc_stream(uint32_t seed, size_t n) {
 }
 
 // MurmurHash3_x86_32 (public algorithm; ns-3 Hash32 = Murmur3 with seed 0x8BADF00D)
-static uint32_t murmur3(const uint8_t* d, uint32_t len, uint32_t h) {
-  auto rot = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
-  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
-  uint32_t i = 0;
-  for (; i + 4 <= len; i += 4) {
-    uint32_t k = d[i] | (d[i + 1] << 8) | (d[i + 2] << 16) | (static_cast<uint32_t>(d[i + 3]) << 24);
-    h ^= rot(k * c1, 15) * c2;
-    h = rot(h, 13) * 5 + 0xe6546b64u;
-  }
+std::vector<uint32_t> fq_link_numbers(uint32_t N, const std::vector<uint32_t>& row, const std::vector<uint32_t>& col,
+                                      const std::vector<uint32_t>& rev) {
+  std::vector<uint32_t> link(row[N]);
   uint32_t k = 0;
-  for (uint32_t j = len & 3; j > 0; --j) k |= static_cast<uint32_t>(d[i + j - 1]) << (8 * (j - 1));
-  if (len & 3) h ^= rot(k * c1, 15) * c2;
-  h ^= len;
-  h = (h ^ (h >> 16)) * 0x85ebca6bu;
-  h = (h ^ (h >> 13)) * 0xc2b2ae35u;
-  return h ^ (h >> 16);
-}
-
-std::vector<uint8_t> fq_flow_map(uint32_t N, const std::vector<uint32_t>& row, const std::vector<uint32_t>& col,
-                                 const std::vector<uint32_t>& rev, uint32_t protocol, uint32_t flows,
-                                 uint32_t perturbation) {
-  const uint32_t E = row[N];
-  std::vector<uint32_t> link(E), src(E);
-  uint32_t k = 0;  // the mesh loop's link order (blockchain-simulator.cc:34-51): larger endpoint, then smaller
   for (uint32_t a = 0; a < N; ++a)
-    for (uint32_t e = row[a]; e < row[a + 1]; ++e) {
-      src[e] = a;
+    for (uint32_t e = row[a]; e < row[a + 1]; ++e)
       if (col[e] < a) link[e] = link[rev[e]] = k++;
-    }
-  // client socket k of a node takes ephemeral port 49153 + k, sockets in peer order; Paxos's
-  // socket k serves peer k + 1 and peer 0 gets a later one (paxos-node.cc:110-119)
-  auto port = [&](uint32_t node, uint32_t idx) -> uint32_t {
-    const uint32_t deg = row[node + 1] - row[node];
-    if (protocol == BCSIM_PAXOS) return idx ? 49152 + idx : 49153 + deg;
-    return 49153 + idx;
-  };
-  auto flow = [&](uint32_t s, uint32_t d, uint32_t sp, uint32_t dp) {
-    uint8_t b[17];
-    const uint32_t w[5] = {s, d, 0, 0, perturbation};
-    for (int j = 0; j < 4; ++j) {
-      b[j] = static_cast<uint8_t>(w[0] >> (24 - 8 * j));
-      b[4 + j] = static_cast<uint8_t>(w[1] >> (24 - 8 * j));
-      b[13 + j] = static_cast<uint8_t>(w[4] >> (24 - 8 * j));
-    }
-    b[8] = 17;
-    b[9] = static_cast<uint8_t>(sp >> 8);
-    b[10] = static_cast<uint8_t>(sp);
-    b[11] = static_cast<uint8_t>(dp >> 8);
-    b[12] = static_cast<uint8_t>(dp);
-    return murmur3(b, 17, 0x8BADF00Du) % flows;
-  };
-  std::vector<uint8_t> map(E);
-  for (uint32_t e = 0; e < E; ++e) {
-    const uint32_t s = src[e], d = col[e];
-    const uint32_t net = 0x01000000u + (link[e] << 8);  // 1.0.0.0/24, NewNetwork per link
-    const uint32_t ia = net + (s > d ? 1u : 2u), ib = net + (d > s ? 1u : 2u);  // node i of the loop is .1
-    const uint32_t hA = flow(ia, ib, port(s, e - row[s]), 7071);
-    const uint32_t hE = flow(ia, ib, 7071, port(d, rev[e] - row[d]));
-    const uint32_t hF = flow(ia, ib, 0, 0);
-    const uint32_t sE = hE == hA ? 0u : 1u;
-    const uint32_t sF = hF == hA ? 0u : hF == hE ? sE : sE + 1u;
-    map[e] = static_cast<uint8_t>(sE << 2 | sF << 4);
-  }
-  return map;
+  return link;
 }
 
 }  // namespace bcsim

@@ -36,13 +36,11 @@ MsgTx message_tx(uint32_t payload, uint32_t mtu, uint64_t rate_bps,
 // feedback generator, r[i] = r[i-3] + r[i-31], 310 discarded outputs).
 std::vector<int32_t> glibc_stream(uint32_t seed, size_t n);
 
-// FQCODEL: per directed edge the flow slots (0..2) of its three packet
-// classes -- application first fragments | echo first fragments << 2 | later fragments << 4 --
-// from ns-3's Ipv4QueueDiscItem::Hash (Murmur3-32 of the 5-tuple) modulo `flows`, with the
-// reference's addressing (one 1.0.k.0/24 network per link of the mesh loop) and ports
-// (7071, ephemeral client ports in peer order).  CSR rows ascending, rev = reverse edges.
-std::vector<uint8_t> fq_flow_map(uint32_t N, const std::vector<uint32_t>& row, const std::vector<uint32_t>& col,
-                                 const std::vector<uint32_t>& rev, uint32_t protocol, uint32_t flows,
-                                 uint32_t perturbation);
+// FQCODEL: per directed edge the number of its link in the reference's mesh
+// loop (blockchain-simulator.cc:34-51: larger endpoint ascending, then smaller), which names the
+// link's 1.0.k.0/24 network.  CSR rows ascending, rev = reverse edges.  The flow of each packet
+// class is bound on the device when the class first reaches the disc (engine fq_class_slot).
+std::vector<uint32_t> fq_link_numbers(uint32_t N, const std::vector<uint32_t>& row, const std::vector<uint32_t>& col,
+                                      const std::vector<uint32_t>& rev);
 
 }  // namespace bcsim

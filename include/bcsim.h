@@ -59,7 +59,8 @@ enum { BCSIM_ENC_EXTENDED = 0, BCSIM_ENC_COMPAT = 1 };
  * FQCODEL = ns-3 FqCoDelQueueDisc (the newer default root queue disc that
  * address.Assign installs, blockchain-simulator.cc:41-42) in front of the
  * queue_dev_pkts device queue with flow control: per-flow CoDel, DRR over the
- * flows, overlimit drops from the fattest flow */
+ * flows, overlimit drops from the fattest flow; flows are the 5-tuple hash with
+ * each client socket's ephemeral port bound at its first send */
 enum { BCSIM_QUEUE_INFINITE = 0, BCSIM_QUEUE_DROPTAIL = 1, BCSIM_QUEUE_FQCODEL = 2 };
 enum { BCSIM_ENGINE_AUTO = 0, BCSIM_ENGINE_DENSE = 1, BCSIM_ENGINE_SPARSE = 2 };
 

@@ -271,6 +271,10 @@ typedef struct {
   uint32_t qpkts;
   fqmsg* msg;
   uint32_t nmsg, capmsg;
+  /* flow of each packet class (app / echo first fragments, later fragments), bound when the
+   * class first reaches the disc: its slot and Murmur3 flow index (fq_class_slot) */
+  uint32_t cslot[3], chash[3];
+  int cbound[3];
 } fqlink;
 
 struct bcsim_oracle {
@@ -291,7 +295,10 @@ struct bcsim_oracle {
   int64_t* busy;         /* per edge */
   oqueue* q;             /* per edge (DROPTAIL only) */
   fqlink* fq;            /* per edge (FQCODEL only) */
-  uint8_t* fqmap;        /* per edge: flow slot of class app | echo << 2 | later frags << 4 */
+  uint32_t* fqlnk;       /* per edge: its link's number in the mesh loop (the /24 network) */
+  uint32_t* fqport;      /* per edge: UDP port of the sender's client socket, 0 = not bound yet */
+  uint32_t* fqnport;     /* per node: client sockets bound so far (ephemeral ports 49153, ...) */
+  uint8_t* fqphant;      /* per node: the Paxos *end() socket is bound */
   uint32_t fq_limit, fq_quantum, fq_flows, fq_batch, fq_min_bytes, fq_devcap;
   uint32_t fq_target_c, fq_interval_c; /* CoDel units (ns >> 10) */
   uint32_t ip_full[2], ip_last[2];     /* IPv4 packet bytes of a full / the last fragment */
@@ -684,50 +691,72 @@ uint32_t oracle_fq_flow(uint32_t src, uint32_t dst, uint32_t sport, uint32_t dpo
   return oracle_murmur3_32(b, 17, 0x8BADF00Du) % flows;
 }
 
-/* UDP source port of node's client socket for its peer at row position idx: sockets are
- * created in peer order at StartApplication and take ephemeral ports 49153, 49154, ...
- * (pbft-node.cc:131-140, raft-node.cc:100-111); Paxos creates socket k for peer k+1
- * (paxos-node.cc:110-119), so peer 0's replies use a socket made later (49153 + deg). */
-static uint32_t app_port(const bcsim_oracle* o, uint32_t node, uint32_t idx) {
-  uint32_t deg = o->row[node + 1] - o->row[node];
-  if (o->cfg.protocol == BCSIM_PAXOS) return idx >= 1 ? 49153 + idx - 1 : 49153 + deg;
-  return 49153 + idx;
-}
-
-/* per edge: the flow slots of its three packet classes.  Addresses: the k-th link of
- * the mesh loop (blockchain-simulator.cc:34-51, i outer, j < i inner) gets network
- * 1.0.0.0 + k*256 (address.NewNetwork), node i .1 and node j .2; a CSR graph numbers its
- * links the same way (larger endpoint ascending, then smaller). */
-static int fq_build_map(bcsim_oracle* o) {
-  uint32_t E = o->row[o->N];
-  uint32_t* pk = (uint32_t*)malloc((E ? E : 1) * sizeof(uint32_t));
-  if (!pk) return BCSIM_E_NOMEM;
+/* The k-th link of the mesh loop (blockchain-simulator.cc:34-51, i outer, j < i inner) gets
+ * network 1.0.0.0 + k*256 (address.NewNetwork), node i .1 and node j .2; a CSR graph numbers
+ * its links the same way (larger endpoint ascending, then smaller). */
+static void fq_build_links(bcsim_oracle* o) {
   uint32_t k = 0;
   for (uint32_t a = 0; a < o->N; ++a)
     for (uint32_t e = o->row[a]; e < o->row[a + 1]; ++e)
       if (o->col[e] < a) {
-        pk[e] = k;
-        pk[o->rev[e]] = k;
+        o->fqlnk[e] = k;
+        o->fqlnk[o->rev[e]] = k;
         ++k;
       }
-  for (uint32_t e = 0; e < E; ++e) {
-    uint32_t s = edge_src(o, e);
-    uint32_t d = o->col[e];
-    uint32_t net = 0x01000000u + (pk[e] << 8);
-    uint32_t src = net + (s > d ? 1u : 2u), dst = net + (d > s ? 1u : 2u);
-    uint32_t pa = app_port(o, s, e - o->row[s]);
-    uint32_t pe = app_port(o, d, o->rev[e] - o->row[d]);
-    uint32_t P = o->cfg.fq_perturbation;
-    uint32_t h[3] = {oracle_fq_flow(src, dst, pa, 7071, P, o->fq_flows),
-                     oracle_fq_flow(src, dst, 7071, pe, P, o->fq_flows),
-                     oracle_fq_flow(src, dst, 0, 0, P, o->fq_flows)};
-    uint32_t slot[3] = {0, 0, 0};
-    slot[1] = h[1] == h[0] ? 0 : 1;
-    slot[2] = h[2] == h[0] ? 0 : h[2] == h[1] ? slot[1] : slot[1] + 1;
-    o->fqmap[e] = (uint8_t)(slot[0] | slot[1] << 2 | slot[2] << 4);
+}
+
+/* Client sockets are created and Connect()ed in peer order at StartApplication
+ * (pbft-node.cc:131-140, raft-node.cc:100-111, paxos-node.cc:110-119), but ns-3's
+ * UdpSocketImpl::Connect only records the default peer: the socket binds -- takes the node's
+ * next ephemeral port, 49153, 49154, ... (Ipv4EndPointDemux::AllocateEphemeralPort) -- in
+ * DoSend, at its FIRST SendPacket.  Ports therefore follow the order of first sends, i.e. the
+ * event order of the node's SendPacket events.  edge = UINT32_MAX is Paxos's *end() socket
+ * (paxos-node.cc:481-493): it binds too, then the datagram finds no route. */
+static void fq_bind(bcsim_oracle* o, uint32_t node, uint32_t edge) {
+  if (edge == UINT32_MAX) {
+    if (o->fqphant[node]) return;
+    o->fqphant[node] = 1;
+  } else if (o->fqport[edge]) {
+    return;
   }
-  free(pk);
-  return BCSIM_OK;
+  uint32_t port = 49153 + o->fqnport[node]++;
+  if (port > 65535) { /* the 16383 ephemeral ports are used up (the reference's Bind fails) */
+    set_err(o, BCSIM_E_UNSUPPORTED);
+    return;
+  }
+  if (edge != UINT32_MAX) o->fqport[edge] = port;
+}
+
+/* the flow slot of packet class cls (0 app, 1 echo first fragment, 2 later fragment) on edge:
+ * bound at the class's first packet -- it shares the slot of an already bound class with the
+ * same flow index (hash collision), else takes slot cls.  App packets travel from the
+ * sender's client port to 7071, echoes from 7071 to the receiver's client port for the
+ * sender (the reverse edge's), later fragments carry no ports. */
+static uint32_t fq_class_slot(bcsim_oracle* o, uint32_t edge, fqlink* l, int cls) {
+  if (l->cbound[cls]) return l->cslot[cls];
+  uint32_t s = edge_src(o, edge), d = o->col[edge];
+  uint32_t net = 0x01000000u + (o->fqlnk[edge] << 8);
+  uint32_t src = net + (s > d ? 1u : 2u), dst = net + (d > s ? 1u : 2u);
+  uint32_t sp = 0, dp = 0;
+  if (cls == 0) {
+    sp = o->fqport[edge];
+    dp = 7071;
+  } else if (cls == 1) {
+    sp = 7071;
+    dp = o->fqport[o->rev[edge]];
+  }
+  if (cls < 2 && (sp | dp) == 7071) set_err(o, BCSIM_E_STATE); /* a send from an unbound socket */
+  uint32_t h = oracle_fq_flow(src, dst, sp, dp, o->cfg.fq_perturbation, o->fq_flows);
+  uint32_t slot = (uint32_t)cls;
+  for (int c = 0; c < 3; ++c)
+    if (l->cbound[c] && l->chash[c] == h) {
+      slot = l->cslot[c];
+      break;
+    }
+  l->cbound[cls] = 1;
+  l->chash[cls] = h;
+  l->cslot[cls] = slot;
+  return slot;
 }
 
 static void fq_reset(bcsim_oracle* o) {
@@ -751,7 +780,11 @@ static void fq_reset(bcsim_oracle* o) {
     l->qpkts = 0;
     for (uint32_t m = 0; m < l->nmsg; ++m) l->msg[m].used = 0;
     l->nmsg = 0;
+    for (int c = 0; c < 3; ++c) l->cbound[c] = 0;
   }
+  memset(o->fqport, 0, (size_t)o->row[o->N] * sizeof(uint32_t));
+  memset(o->fqnport, 0, (size_t)o->N * sizeof(uint32_t));
+  memset(o->fqphant, 0, o->N);
 }
 
 static void free_fq(bcsim_oracle* o) {
@@ -762,9 +795,13 @@ static void free_fq(bcsim_oracle* o) {
       free(o->fq[e].msg);
     }
   free(o->fq);
-  free(o->fqmap);
+  free(o->fqlnk);
+  free(o->fqport);
+  free(o->fqnport);
+  free(o->fqphant);
   o->fq = NULL;
-  o->fqmap = NULL;
+  o->fqlnk = o->fqport = o->fqnport = NULL;
+  o->fqphant = NULL;
 }
 
 static int codel_before(uint32_t a, uint32_t b) { return (int32_t)(a - b) < 0; }
@@ -1084,10 +1121,9 @@ static void fq_send(bcsim_oracle* o, uint32_t edge, const omsg* msg, uint32_t su
   int big = msg->big;
   uint32_t F = o->nfr[big];
   m->left = F;
-  uint8_t map = o->fqmap[edge];
   for (uint32_t j = 0; j < F; ++j) {
     int cls = j ? 2 : echo ? 1 : 0;
-    int f = (map >> (2 * cls)) & 3;
+    int f = (int)fq_class_slot(o, edge, l, cls);
     fqflow* fl = &l->f[f];
     fqpkt pk;
     pk.enq = o->now;
@@ -1599,6 +1635,7 @@ static void exec_event(bcsim_oracle* o, const oev* e) {
       break;
     case EV_SEND: { /* SendPacket :323-325 -> socket->Send -> p2p device */
       o->cnt.sends++;
+      if (o->cfg.queue_model == BCSIM_QUEUE_FQCODEL) fq_bind(o, i, e->aux);
       if (e->aux == UINT32_MAX) {
         o->cnt.dropped++;
         break;
@@ -1748,14 +1785,16 @@ int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
   free(t);
   if (o->cfg.queue_model == BCSIM_QUEUE_FQCODEL) {
     o->fq = (fqlink*)calloc(E ? E : 1, sizeof(fqlink));
-    o->fqmap = (uint8_t*)calloc(E ? E : 1, 1);
-    if (!o->fq || !o->fqmap) return BCSIM_E_NOMEM;
+    o->fqlnk = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
+    o->fqport = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
+    o->fqnport = (uint32_t*)calloc(o->N, sizeof(uint32_t));
+    o->fqphant = (uint8_t*)calloc(o->N, 1);
+    if (!o->fq || !o->fqlnk || !o->fqport || !o->fqnport || !o->fqphant) return BCSIM_E_NOMEM;
     for (uint32_t e = 0; e < E; ++e) {
       o->fq[e].dev = (int64_t*)malloc(o->fq_devcap * sizeof(int64_t));
       if (!o->fq[e].dev) return BCSIM_E_NOMEM;
     }
-    int rc = fq_build_map(o);
-    if (rc) return rc;
+    fq_build_links(o);
   }
   o->topo_set = 1;
   return BCSIM_OK;
@@ -2011,6 +2050,14 @@ int bcsim_oracle_read_status(bcsim_oracle* o, bcsim_status* out) {
   out->quiescent = o->heap.n == 0;
   out->error = o->err;
   return BCSIM_OK;
+}
+
+/* test hook: the client port of every edge's socket after a run (0 = never sent), CSR order */
+uint64_t oracle_fq_ports(const bcsim_oracle* o, uint32_t* out, uint64_t cap) {
+  if (!o || !o->fqport) return 0;
+  uint64_t E = o->row[o->N];
+  for (uint64_t e = 0; e < E && e < cap; ++e) out[e] = o->fqport[e];
+  return E;
 }
 
 int bcsim_oracle_destroy(bcsim_oracle* o) {

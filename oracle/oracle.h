@@ -47,6 +47,9 @@ void    oracle_msg_tx(uint32_t payload, uint32_t mtu, uint64_t rate_bps,
 uint32_t oracle_murmur3_32(const uint8_t* data, uint32_t len, uint32_t seed);
 uint32_t oracle_fq_flow(uint32_t src, uint32_t dst, uint32_t sport, uint32_t dport,
                         uint32_t perturbation, uint32_t flows);
+/* the client port each edge's socket bound at its first send (0: never sent), CSR order;
+ * returns the edge count */
+uint64_t oracle_fq_ports(const bcsim_oracle* o, uint32_t* out, uint64_t cap);
 uint32_t oracle_ctr_rand(uint64_t seed, uint32_t replica, uint32_t node,
                          uint64_t k);
 

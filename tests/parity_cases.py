@@ -136,6 +136,14 @@ def fq_cases():
                           queue_dev_pkts=10),
         "paxos32_fq_jitter": _cfg(X, 32, delay_mode=J, rng_mode=K, seed=3, paxos_decrees=3, queue_model=Q,
                                   queue_dev_pkts=2),
+        # few flows: which classes of a link collide depends on the client ports, bound in
+        # first-send order (random delays, Raft's reply-first followers, Paxos's *end() socket)
+        "pbft12_fq_jitter_flows3": _cfg(P, 12, delay_mode=J, rng_mode=K, seed=11, pbft_rounds=30, queue_model=Q,
+                                        fq_flows=3, queue_dev_pkts=20),
+        "raft16_fq_flows2": _cfg(R, 16, delay_mode=F, app_delay_ns=1_000_000, t_end_ns=4_000_000_000,
+                                 queue_model=Q, queue_dev_pkts=10, fq_flows=2),
+        "paxos32_fq_jitter_flows3": _cfg(X, 32, delay_mode=J, rng_mode=K, seed=5, paxos_decrees=3, queue_model=Q,
+                                         queue_dev_pkts=2, fq_flows=3),
     }
 
 

@@ -103,3 +103,39 @@ def test_fqcodel_partitioned_p2_matches_oracle(engine_lib):
         assert err is None, f"{name}: {err}"
         d = compare(oracle.run(FQ[name], topology=topology(name)), merged)
         assert d is None, f"{name} P=2: {d}"
+
+
+def _ports(name):
+    lib = oracle.lib()
+    lib.oracle_fq_ports.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.c_uint64]
+    lib.oracle_fq_ports.restype = C.c_uint64
+    cfg, topo = FQ[name], topology(name)
+    with oracle.OracleSim(cfg) as o:
+        if topo is not None:
+            o.set_topology(*topo)
+        o.run(_abi.INT64_MAX)
+        n = cfg.n_nodes
+        buf = (C.c_uint32 * (n * n))()
+        E = lib.oracle_fq_ports(o.h, buf, n * n)
+    return [list(buf[i * (n - 1):(i + 1) * (n - 1)]) for i in range(n)], E
+
+
+def test_client_ports_bind_at_first_send():
+    """ns-3's UdpSocketImpl::Connect only records the peer; the socket takes the node's next
+    ephemeral port (49153, 49154, ...) at its first Send.  PBFT with fixed delays
+    sends in peer order (the leader's block broadcast, then every node's PREPARE broadcast), so
+    ports follow the peer order; a Raft follower's first send is its vote reply to the
+    candidate (raft-node.cc:166), whose socket therefore holds 49153."""
+    rows, E = _ports("pbft8_fq_40")
+    assert E == 8 * 7
+    for i, r in enumerate(rows):
+        assert r == [49153 + k for k in range(7)], (i, r)
+    rows, _ = _ports("raft16_fq")
+    first = {i: r.index(49153) for i, r in enumerate(rows) if 49153 in r}
+    peers = {i: (k if k < i else k + 1) for i, k in first.items()}
+    cand = {p for p in peers.values()}
+    assert len(cand) <= 2, peers          # one candidate (its own first send goes elsewhere)
+    assert any(r != sorted(r) for r in rows if any(r)), "Raft ports should not follow peer order"
+    for r in rows:                        # bound ports are dense from 49153
+        b = sorted(x for x in r if x)
+        assert b == [49153 + k for k in range(len(b))]
