@@ -50,7 +50,7 @@ def make_topology(n_nodes, workload):
     return bcsim.random_regular(n_nodes, 8, 1)
 
 
-PMC_ROUND = "r03"
+PMC_ROUND = "r04"
 
 
 def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):
@@ -213,6 +213,9 @@ def main():
                          "pbft-node.cc:66-69) with the counter RNG, instead of the fixed 3 ms")
     ap.add_argument("--mode", choices=("pdes", "replicas"), default="pdes",
                     help="multi-GPU mode (N>1): node-partitioned PDES or independent replicas")
+    ap.add_argument("--queue", choices=("infinite", "droptail", "fqcodel"), default="infinite",
+                    help="link queue model: the reference's unbounded FIFO reading (default), or the "
+                         "device queue + pfifo_fast / FqCoDel root queue disc (DESIGN.md §2.2, §2.2b)")
     ap.add_argument("--pdes1", action="store_true",
                     help="one GPU with the partition machinery on (a world-1 RCCL group, the per-window "
                          "control exchange): its cost against the plain single-GPU run")
@@ -251,6 +254,8 @@ def main():
         cfg.delay_mode = bcsim.DELAY_RANDOM
         cfg.rng_mode = bcsim.RNG_COUNTER
         cfg.app_delay_ns = 0
+    cfg.queue_model = {"infinite": bcsim.QUEUE_INFINITE, "droptail": bcsim.QUEUE_DROPTAIL,
+                       "fqcodel": bcsim.QUEUE_FQCODEL}[args.queue]
     topo = make_topology(args.nodes, args.workload)
 
     def new_sim():
@@ -326,12 +331,15 @@ def main():
         # emitted by the timed k_link launches, over their HIP-event time on the engine stream
         ach = (lk["bytes"] / 1e9) / (lk["us"] / 1e6) if lk["us"] > 0 else 0.0
         # PMC traffic of this workload's committed profile (none for the jittered variant)
-        traffic = None if args.jitter else pmc_traffic(args.nodes, workload=args.workload)
+        traffic = None if (args.jitter or args.queue != "infinite") else pmc_traffic(args.nodes, workload=args.workload)
         all_us = sum(v["us"] for v in ks_all.values())
         if args.workload == "pbft":
             data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, %s)" % (
                 args.nodes, "app delay U{3,4,5} ms per send, counter RNG" if args.jitter else "fixed 3 ms app delay")
             wl = f"PBFT n={args.nodes} full O(n^2) prepare/commit (BASELINE configs[3])"
+            if args.queue != "infinite":
+                data = data[:-1] + f", {args.queue} link queues)"
+                wl += f", {args.queue} link queues"
         elif args.workload == "paxos":
             data = ("synthetic (Paxos n=%d full mesh, 3Mbps/3ms links, app delay U{0..49} ms, counter RNG, "
                     "%d replicas, %d decrees, seeds by replica, sparse layout)" % (args.nodes, args.replicas, args.decrees))
@@ -393,6 +401,7 @@ def main():
             try:
                 def tweak(c):
                     c.delay_mode, c.rng_mode, c.app_delay_ns = cfg.delay_mode, cfg.rng_mode, cfg.app_delay_ns
+                    c.queue_model = cfg.queue_model
                     if args.workload == "paxos":
                         c.paxos_decrees = args.decrees
                 out["cpu_baseline"] = cpu_baseline(args.nodes, args.cpu_budget, args.workload, tweak)

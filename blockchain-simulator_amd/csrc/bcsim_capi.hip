@@ -770,9 +770,19 @@ static int setup_device(Sim& s) {
     p.cap_fqm = c.cap_queue_msgs ? std::min<uint32_t>(c.cap_queue_msgs, kFqMaxMsgs) : kFqMaxMsgs;
     p.cap_fqm = (p.cap_fqm + 31) / 32 * 32;
     p.cap_fqp = static_cast<uint32_t>(std::min<uint64_t>(p.fq_limit + 1ull, 4096));
-    if (fq && static_cast<double>(ne) * (3.0 * p.cap_fqp + p.cap_fqm) * 16 > 64e9) {
-      g_detail = "FQCODEL link state exceeds 64 GB";
-      return BCSIM_E_UNSUPPORTED;
+    // per-flow packet rings: MaxSize + 1 packets (at most 4096) when that fits a 150 GB budget
+    // for the whole link state, else the largest ring that does (>= 64; CoDel keeps a flow's
+    // standing queue near rate x target, so a saturated 3 Mb/s link holds tens of packets).  A
+    // flow that outgrows its ring fails the run (BCSIM_E_OVERFLOW), never drops silently.
+    const double fixed_b = kFqH * 4.0 + p.fq_devcap * 8.0 + p.cap_fqm * 16.0 + 16.0 + 8.0;
+    const double budget = 150e9;
+    if (fq && static_cast<double>(ne) * (fixed_b + 48.0 * p.cap_fqp) > budget) {
+      const double fit = (budget / static_cast<double>(ne) - fixed_b) / 48.0;
+      p.cap_fqp = fit >= 64.0 ? static_cast<uint32_t>(std::min<double>(fit, p.cap_fqp)) : 0u;
+      if (p.cap_fqp < 64) {
+        g_detail = "FQCODEL link state exceeds 150 GB even with 64-packet flow rings";
+        return BCSIM_E_UNSUPPORTED;
+      }
     }
     uint32_t* fqlnk = nullptr;
     const size_t nt = fq ? s.NT : 1;
@@ -785,20 +795,14 @@ static int setup_device(Sim& s) {
     p.fq_flows = c.fq_flows ? c.fq_flows : 1024;
     p.fq_pert = c.fq_perturbation;
     if (fq) {
-      std::vector<uint32_t> h0(kFqH, 0);
-      for (uint32_t f = 0; f < 3; ++f) {
-        h0[f * kFqF + FQ_REC] = 0xFFFFu;  // rec_inv_sqrt = ~0U >> REC_INV_SQRT_SHIFT
-        h0[f * kFqF + FQ_CR] = kInvalid;  // queue-disc class not created yet
-      }
-      std::vector<uint32_t> hall(ne * kFqH);
-      for (size_t k = 0; k < ne; ++k) std::copy(h0.begin(), h0.end(), hall.begin() + k * kFqH);
-      HIPCHK(hipMemcpy(p.fqh, hall.data(), hall.size() * 4, hipMemcpyHostToDevice));
+      hipLaunchKernelGGL(k_fq_init, dim3(4096), dim3(256), 0, s.stream, p.fqh, p.fqkey, static_cast<uint64_t>(ne));
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(s.stream));
       const std::vector<uint32_t> lnk = fq_link_numbers(s.N, s.row, s.col, s.rev);
       HIPCHK(hipMemcpy(fqlnk, lnk.data(), s.E * 4, hipMemcpyHostToDevice));
       // sockets unbound (port 0), no first-send keys pending (all ones)
       HIPCHK(hipMemset(p.fqport, 0, ne * 4));
       HIPCHK(hipMemset(p.fqpeer, 0, ne * 4));
-      HIPCHK(hipMemset(p.fqkey, 0xFF, ne * 16));
       HIPCHK(hipMemset(p.fqnport, 0, nt * 4));
       HIPCHK(hipMemset(p.fqphant, 0, nt * 4));
     }

@@ -290,11 +290,17 @@ constexpr uint32_t kEDesc = 2;        // pending echo descriptors per node (LDS:
 // sflag bits of a reply descriptor of the arrival cell (bits 0..3: reply slots due in cell + k)
 constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in this cell / the next
 // tiled mesh link stage: due broadcasts per job, senders x receivers per tile, 64-slot chunks
+// k_mesh_tile build switches (A/B: tools/build_variant.sh): senders per tile; link words through
+// LDS, written after the walk (1) or in the walk (0: 9 % faster, PBFT n=4096); workgroup order
+// receiver-tile-major (1: the slow receiver tile 0 -- the leader's -- goes first) or sender-major
 #ifndef BCSIM_TILE_TS
-#define BCSIM_TILE_TS 16
+#define BCSIM_TILE_TS 32
 #endif
 #ifndef BCSIM_TILE_DEFER
-#define BCSIM_TILE_DEFER 1  // link words through LDS, written after the walk (0: in the walk)
+#define BCSIM_TILE_DEFER 0
+#endif
+#ifndef BCSIM_TILE_RTMAJOR
+#define BCSIM_TILE_RTMAJOR 0
 #endif
 constexpr uint32_t kMeshBc = 2, kTS = BCSIM_TILE_TS, kTR = 64;
 constexpr uint32_t kTileThreads = kTS * 16;  // four senders per wave
@@ -1541,7 +1547,6 @@ constexpr uint32_t kTypeMask = 0xFFu << kTypeShift;
 constexpr uint32_t kIdxMask = (1u << kTypeShift) - 1u;
 __device__ inline uint32_t cls_type(uint32_t w) { return (w & kTypeMask) >> kTypeShift; }
 
-constexpr uint32_t kSortKeys = 32;  // sort_window's counting sort: distinct keys
 struct ScanShared {
   uint32_t wcnt[kMaxWaves];
   uint4 wsum[kMaxWaves];
@@ -1562,10 +1567,6 @@ struct ScanShared {
   uint32_t ocnt[kOpRing];  // reply-slot ops written, by due cell - cell
   uint32_t tr_n, tr_pos;   // gossip: first receipts of the window, next reserved trace position
   unsigned long long ph[8];  // BCSIM_WGT phase clock (debug)
-  // sort_window's counting sort: the distinct keys (ascending once sorted), per-key bases
-  unsigned long long sk[kSortKeys];
-  uint32_t skb[kSortKeys];
-  uint32_t snk, sbad;
 };
 #define SPH(k)                                                         \
   do {                                                                 \
@@ -1720,126 +1721,8 @@ __device__ inline bool sec_less(uint64_t ka, uint32_t sa, uint64_t kb, uint32_t 
   return ka < kb || (ka == kb && sa < sb);
 }
 
-// Counting sort of the staged main-row arrivals [0, n) by key when they carry at most kSortKeys
-// distinct keys (the heavy waves: a few broadcast instants), stable in staging order, which is
-// the slot order (asec ascending) -- the order sec_less gives equal keys.  Positions: the key's
-// base + the same-key arrivals of earlier 64-arrival segments (a per-(segment, key) count table
-// in `tab`, prefix-summed by one wave per key) + the rank inside the segment (a ballot).  Three
-// barriers and O(n) work instead of the bitonic network's O(n log^2 n) with ~90 barriers (the
-// PBFT leader's 8K-arrival windows: ~100 us in one workgroup).  false: not applicable, nothing
-// written.
-__device__ bool sort_window_count(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec, uint32_t* tab,
-                                  uint32_t cap) {
-  const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
-  const uint32_t iters = (n + blockDim.x - 1) / blockDim.x;
-  if (iters * nwv * kSortKeys > cap) return false;
-  if (tid < kSortKeys) S.sk[tid] = ~0ull;
-  if (tid == 0) S.sbad = 0;
-  __syncthreads();
-  for (uint32_t r = tid; r < n; r += blockDim.x) {  // the distinct keys (CAS insert, read first)
-    const unsigned long long k = akey[r];
-    bool done = false;
-    for (uint32_t q = 0; q < kSortKeys && !done; ++q) {
-      const unsigned long long t = __hip_atomic_load(&S.sk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (t == k) done = true;
-      else if (t == ~0ull) done = atomicCAS(&S.sk[q], ~0ull, k) == ~0ull || S.sk[q] == k;
-    }
-    if (!done) S.sbad = 1;
-  }
-  __syncthreads();
-  if (S.sbad) return false;  // (uniform)
-  if (tid == 0) {  // sort the few keys
-    uint32_t nk = 0;
-    while (nk < kSortKeys && S.sk[nk] != ~0ull) ++nk;
-    for (uint32_t a = 1; a < nk; ++a) {
-      const unsigned long long x = S.sk[a];
-      uint32_t b = a;
-      while (b > 0 && S.sk[b - 1] > x) {
-        S.sk[b] = S.sk[b - 1];
-        --b;
-      }
-      S.sk[b] = x;
-    }
-    S.snk = nk;
-  }
-  __syncthreads();
-  const uint32_t nk = S.snk;
-  const uint32_t nseg = iters * nwv;  // segment s = it * nwv + wv: 64 consecutive arrivals
-  const uint64_t lt = (1ull << lane) - 1ull;
-  // each arrival: its key index and rank in the segment (into its own akey word: the key itself
-  // is S.sk[index]); per (segment, key) counts into tab
-  for (uint32_t it = 0; it < iters; ++it) {
-    const uint32_t r = it * blockDim.x + tid;
-    const bool v = r < n;
-    uint32_t d = 0;
-    if (v) {
-      const unsigned long long k = akey[r];
-      for (uint32_t q = 0; q < nk; ++q)
-        if (S.sk[q] == k) d = q;
-    }
-    uint32_t rk = 0, cl = 0;
-    for (uint32_t q = 0; q < nk; ++q) {
-      const uint64_t m = __ballot(v && d == q);
-      if (v && d == q) rk = static_cast<uint32_t>(__popcll(m & lt));
-      if (lane == q) cl = static_cast<uint32_t>(__popcll(m));
-    }
-    if (lane < nk) tab[(it * nwv + wv) * kSortKeys + lane] = cl;
-    if (v) akey[r] = d | (rk << 8);
-  }
-  __syncthreads();
-  // per key: exclusive prefix over the segments (one wave per key, 64 segments per step)
-  for (uint32_t q = wv; q < nk; q += nwv) {
-    uint32_t run = 0;
-    for (uint32_t s0 = 0; s0 < nseg; s0 += 64) {
-      const uint32_t sg = s0 + lane;
-      const uint32_t c = sg < nseg ? tab[sg * kSortKeys + q] : 0u;
-      uint32_t inc = c;
-      for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += y;
-      }
-      if (sg < nseg) tab[sg * kSortKeys + q] = run + inc - c;
-      run += static_cast<uint32_t>(__shfl(inc, 63, 64));
-    }
-    if (lane == 0) S.skb[q] = run;  // (the key's total for now)
-  }
-  __syncthreads();
-  if (tid == 0) {  // key bases in key order
-    uint32_t b = 0;
-    for (uint32_t q = 0; q < nk; ++q) {
-      const uint32_t c = S.skb[q];
-      S.skb[q] = b;
-      b += c;
-    }
-  }
-  __syncthreads();
-  // final position | sec << 32 into the arrival's own akey word, then the scatter of the secs,
-  // then the keys by runs
-  for (uint32_t it = 0; it < iters; ++it) {
-    const uint32_t r = it * blockDim.x + tid;
-    if (r >= n) continue;
-    const uint32_t dr = static_cast<uint32_t>(akey[r]), d = dr & 0xFFu;
-    const uint32_t pos = S.skb[d] + tab[(it * nwv + wv) * kSortKeys + d] + (dr >> 8);
-    akey[r] = pos | (static_cast<uint64_t>(asec[r]) << 32);
-  }
-  __syncthreads();
-  for (uint32_t r = tid; r < n; r += blockDim.x) {
-    const uint64_t w = akey[r];
-    asec[static_cast<uint32_t>(w)] = static_cast<uint32_t>(w >> 32);
-  }
-  __syncthreads();
-  for (uint32_t r = tid; r < n; r += blockDim.x) {
-    uint32_t d = 0;
-    for (uint32_t q = 1; q < nk; ++q)
-      if (S.skb[q] <= r) d = q;
-    akey[r] = S.sk[d];
-  }
-  __syncthreads();
-  return true;
-}
-
-// Sort (akey, asec) pairs of [0, n) unless already ordered (tab: cap words of scratch).
-__device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec, uint32_t* tab, uint32_t cap) {
+// Sort (akey, asec) pairs of [0, n) unless already ordered.
+__device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec) {
   const uint32_t tid = tidx();
   if (tid == 0) S.unsorted = 0;
   __syncthreads();
@@ -1849,7 +1732,6 @@ __device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t*
   if (__ballot(bad) && (tid & 63) == 0) S.unsorted = 1;
   __syncthreads();
   if (!S.unsorted) return;
-  if (n == S.n_main && sort_window_count(S, n, akey, asec, tab, cap)) return;
   uint32_t P2 = 2;
   while (P2 < n) P2 <<= 1;
   for (uint32_t k = n + tid; k < P2; k += blockDim.x) {
@@ -2437,7 +2319,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
     }
     const uint32_t n_main = S.n_main;
     SPH(1);
-    sort_window(S, n, akey, asec, acls, cap);
+    sort_window(S, n, akey, asec);
     SPH(2);
 
     const RecSrc rsrc{slots, xs};
@@ -5907,7 +5789,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
   __shared__ TileShared T;
   const uint32_t nrt = p.n_tiles, nst = p.n_stiles;
   const uint32_t rep = blockIdx.x / (nst * nrt), rem = blockIdx.x % (nst * nrt);
-  const uint32_t st = rem / nrt, rt = rem % nrt;
+  const uint32_t st = BCSIM_TILE_RTMAJOR ? rem % nst : rem / nrt, rt = BCSIM_TILE_RTMAJOR ? rem / nst : rem % nrt;
   if (gbl(p.mtile)[static_cast<size_t>(rep) * nst + st] != epoch) return;  // no job among these senders
   const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
   G<unsigned long long>* tph = p.wgtt ? gbl(p.wgtt) + 8ull * blockIdx.x : nullptr;  // (debug phase clocks)
@@ -7342,6 +7224,21 @@ __device__ inline void import_one(const KP& p, long long g_cur, XRec x, uint32_t
 // ring -> overflow); a range record (xr_ship) is expanded here into its per-edge records
 // (receiver s, its in-slot and sub + k follow from the sender and the first receiver).
 // g_cur = the cell just processed.
+// k_fq_init: every edge's FQCODEL header -- flows empty, rec_inv_sqrt = ~0U >> REC_INV_SQRT_SHIFT,
+// queue-disc classes not created yet -- and no first-send keys pending
+__global__ __launch_bounds__(256) void k_fq_init(uint32_t* __restrict__ h, uint4* __restrict__ key, uint64_t ne) {
+  const uint64_t nw = ne * kFqH;
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + tidx(); k < nw;
+       k += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t w = static_cast<uint32_t>(k % kFqH);
+    uint32_t v = 0;
+    if (w < 3 * kFqF && w % kFqF == FQ_REC) v = 0xFFFFu;
+    if (w < 3 * kFqF && w % kFqF == FQ_CR) v = kInvalid;
+    h[k] = v;
+    if (w == 0) key[k / kFqH] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  }
+}
+
 // k_l2_take (list-2 overlap of a few-node scan window, PBFT full mesh): the window's scan list
 // (the leader's cells: a handful of nodes) becomes list 2 -- scanned and linked on the second
 // stream -- and its nodes are stamped so that the other nodes' link stage skips them

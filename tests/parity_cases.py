@@ -157,7 +157,13 @@ def fullsize_cases():
     c4.stop_ns = -1
     c5 = bcsim.preset("c5_gossip65536")  # bench.py --workload gossip (echo on)
     c5.pbft_rounds = 3
-    return {"c4_bench_r4": c4, "c5_gossip_r3": c5}
+    # the same PBFT configuration under the FQCODEL queue disc (6 rounds: the leader's 35-fragment
+    # blocks overflow the 100-packet device queue into the disc after three)
+    c4f = bcsim.preset("c4_pbft4096")
+    c4f.pbft_rounds = 6
+    c4f.stop_ns = -1
+    c4f.queue_model = _abi.QUEUE_FQCODEL
+    return {"c4_bench_r4": c4, "c5_gossip_r3": c5, "c4_fq_r6": c4f}
 
 
 def any_case(name):

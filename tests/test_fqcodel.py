@@ -139,3 +139,20 @@ def test_client_ports_bind_at_first_send():
     for r in rows:                        # bound ports are dense from 49153
         b = sorted(x for x in r if x)
         assert b == [49153 + k for k in range(len(b))]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_fqcodel_c4_fullsize_conservation(engine_lib):
+    """The bench configuration (PBFT n=4096 full mesh, 50 KB blocks every 50 ms on 3 Mb/s links)
+    under FQCODEL: the leader's saturated links drop (CoDel / overlimit), every application
+    send is delivered, lost or still in flight, and each lost message dropped a fragment."""
+    import bcsim
+    from parity_cases import fullsize_cases
+    c = fullsize_cases()["c4_fq_r6"]
+    tr, cnt, st = bcsim.run(c)[:3]
+    assert st["error"] == 0
+    assert cnt["frames_dropped"] > 0
+    assert cnt["delivered_total"] + cnt["msgs_lost"] + cnt["dropped"] <= cnt["sends"]
+    assert 0 < cnt["msgs_lost"] <= cnt["frames_dropped"]
+    assert cnt["delivered"][2] > 0  # PREPAREs got through

@@ -139,7 +139,7 @@ def test_partitioned_n512_matches_oracle(engine_lib):
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("name,world", [("c4_bench_r4", 2), ("c5_gossip_r3", 2), ("c4_bench_r4", 4), ("c4_bench_r4", 8),
-                                        ("c5_gossip_r3", 4)])
+                                        ("c5_gossip_r3", 4), ("c4_fq_r6", 2)])
 def test_partitioned_fullsize_equals_single(name, world, engine_lib):
     """SURVEY.md §4 item 4 at BASELINE size: the bench configurations themselves --
     C4 PBFT n=4096 (50 KB blocks, glibc lottery on, 4 rounds; blockchain-simulator.cc:34-51
@@ -158,7 +158,7 @@ def test_partitioned_fullsize_equals_single(name, world, engine_lib):
     assert err is None, err
     d = compare(single, merged)
     assert d is None, f"{name} world={world}: {d}"
-    if name.startswith("c4") and world == 2:
+    if name == "c4_bench_r4" and world == 2:
         # broadcast de-dup (k_link_mesh xr_ship -> k_import): about half the 16.8 M records of
         # a heavy cell cross ranks, shipped as range records of up to 64 edges, so the volume
         # is far below one 32-byte record per cross-rank delivery
