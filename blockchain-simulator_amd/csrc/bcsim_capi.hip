@@ -90,6 +90,7 @@ struct Sim {
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   KP* kp_dev2 = nullptr;
+  bool gossip_frontier = true;  // dense gossip: k_gossip_cell over the window's frontier (BCSIM_GOSSIP_FRONTIER=0: all)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -471,6 +472,7 @@ static int setup_device(Sim& s) {
   };
   s.bs_scan = bs_cap("BCSIM_BS_SCAN", s.bs_scan);
   s.bs_link = bs_cap("BCSIM_BS_LINK", s.bs_link);
+  if (p.qmodel == 2) s.bs_link = std::min<uint32_t>(s.bs_link, 256);  // (k_link<2>'s launch bound)
   {  // k_link dynamic LDS: as many workgroups per CU as 1024 lanes make (1024 / bs_link)
     const size_t target = std::max<size_t>(16 * 1024, kLinkLdsTarget * s.bs_link / 512 - (s.bs_link < 512 ? 4096 : 0));
     const size_t room = target / 4 > s.deg_max + 1 + 1024 ? target / 4 - (s.deg_max + 1) : 1024;
@@ -707,6 +709,7 @@ static int setup_device(Sim& s) {
       // testing aid: BCSIM_FEW_SCAN=0 sends small launches (every launch of a small parity case)
       // through k_scan_pbft too
       if (const char* fs = std::getenv("BCSIM_FEW_SCAN"); fs && *fs) s.few_scan = static_cast<uint32_t>(std::atoi(fs));
+      if (const char* gf = std::getenv("BCSIM_GOSSIP_FRONTIER"); gf && *gf == '0') s.gossip_frontier = false;
       if (const char* pf = std::getenv("BCSIM_MESH_PF"); pf && *pf == '0') s.mesh_pf = false;
       if (static_cast<size_t>(s.deg_max) * 8 > 64 * 1024) s.mesh_pf = false;  // (dynamic LDS without an opt-in)
     }
@@ -958,6 +961,10 @@ static int setup_device(Sim& s) {
   }
   p.dbg_tmax = LLONG_MIN;
   if (const char* xv = std::getenv("BCSIM_EXP"); xv && *xv) p.exp = static_cast<uint32_t>(std::strtol(xv, nullptr, 0));
+  {
+    const char* pf = std::getenv("BCSIM_PX_FAST");
+    p.paxos_fast_win = (pf && *pf == '0') ? 0u : 1u;
+  }
   if (const char* fv = std::getenv("BCSIM_DBG_FAIL_CELL"); fv && *fv) s.dbg_fail_cell = std::atoll(fv);
   if (const char* fv = std::getenv("BCSIM_DBG_FAIL_IMPORT"); fv && *fv) s.dbg_fail_import = std::atoll(fv);
   if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
@@ -1122,7 +1129,11 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     // k_link class (it moves every record: the 16 B read, the link word, the 16 B write)
     const bool timed = (kstat_mask() >> KS_LINK) & 1u;
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
-    if ((rc = launch(s, -1, k_gossip_cell, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g, loop, fw)) ||
+    // the frontier list unless START / STOP makes every node active
+    const int fl = s.gossip_frontier && !(lo <= 0 && 0 < hi) && !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi);
+    const uint32_t na = static_cast<uint32_t>(static_cast<uint64_t>(s.R) * s.nloc);
+    if ((fl && (rc = launch(s, -1, k_gossip_active, dim3((na + 255) / 256), dim3(256), 0, s.kp_dev, cell, hi))) ||
+        (rc = launch(s, -1, k_gossip_cell, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g, loop, fw, fl)) ||
         (loop &&
          (rc = launch(s, -1, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), block, lds, s.kp_dev, cell, lo, hi,
                       cs, fw, xa))) ||

@@ -62,6 +62,7 @@ struct KP {
   int64_t pbft_period, raft_hb, raft_prop_delay, stop_ns;
   uint32_t pbft_rounds, pbft_seq_cap, pbft_view_change, raft_blocks;
   uint32_t raft_prop_rounds, paxos_proposers;
+  uint32_t paxos_fast_win;  // Paxos proposer windows data-parallel (paxos_window_fast; BCSIM_PX_FAST=0: off)
   uint64_t seed;
   GP(int64_t) pbft_delay;
   GP(int64_t) raft_delay;
@@ -1566,6 +1567,12 @@ struct ScanShared {
   long long tmax;
   uint32_t ocnt[kOpRing];  // reply-slot ops written, by due cell - cell
   uint32_t tr_n, tr_pos;   // gossip: first receipts of the window, next reserved trace position
+  // Paxos proposer window (paxos_window_fast): decree and vote count on entry, verdict, the
+  // quorum-crossing arrival and its prefix counts, explicit echoes, per-type deliveries
+  int32_t px_dec, px_c0;
+  uint32_t px_bad, px_r, px_cb, px_sb, px_eb, px_ncross, px_nops0;
+  uint32_t px_deliv[3];
+  long long px_tmax;
   unsigned long long ph[8];  // BCSIM_WGT phase clock (debug)
 };
 #define SPH(k)                                                         \
@@ -2196,6 +2203,129 @@ __device__ void gossip_first_flags(const KP& p, ScanShared& S, uint32_t g, uint3
          static_cast<uint64_t>(p.NT) * p.pbft_seq_cap) = 1;
 }
 
+// A Paxos proposer's window of responses, data-parallel (paxos-node.cc:248-353, the serial form
+// is paxos_recv): every arrival is a RESPONSE_TICKET / _PROPOSE / _COMMIT, no timer, START or
+// STOP is due and at most one quorum decision falls in the window, on the arrival whose running
+// count (vote_success + vote_failed, carried in) reaches N - 2 -- and no counted response
+// follows it.  Then the counts are prefix sums over the key-ordered arrivals (block scans), the
+// one decision runs on lane 0 with the counters as of that arrival (its broadcast follows the
+// echoes of the arrivals before it), and the echo ops are written in parallel at their serial
+// positions.  Anything else returns false with nothing changed: the lane-0 event loop takes the
+// window.  All lanes call it; c / s are lane 0's.
+__device__ bool paxos_window_fast(const KP& p, ScanShared& S, Ctx& c, PaxosState& s, uint32_t g, uint32_t n,
+                                  const uint32_t* asec, const RecSrc& rsrc, uint32_t e0, long long cs, long long t_lo,
+                                  long long wb, const TimerEnt* tm, bool start_pending, bool stop_pending) {
+  const uint32_t tid = tidx();
+  Op* ops = p.ops + op_base(p, g);
+  const uint32_t ocap = op_cap(p, g);
+  if (n == 0 || p.dbg_tmax > LLONG_MIN || start_pending || stop_pending) return false;
+  const int32_t N2 = static_cast<int32_t>(p.N) - 2;
+  if (tid == 0) {
+    S.px_dec = s.decree;
+    S.px_c0 = s.vs + s.vf;
+    S.px_bad = 0;
+    S.px_r = kInvalid;
+    S.px_nops0 = c.nops;
+    S.px_tmax = LLONG_MIN;
+    S.px_deliv[0] = S.px_deliv[1] = S.px_deliv[2] = 0;
+    for (uint32_t k = 0; k < c.cap_t; ++k)
+      if (tm[k].alive && !tm[k].pending_draw && tm[k].t < wb && tm[k].t >= t_lo) S.px_bad = 1;
+  }
+  __syncthreads();
+  if (S.px_bad) return false;
+  const int32_t dec = S.px_dec, c0 = S.px_c0;
+  // pass 1: types, counted / successful responses, explicit echoes; the crossing arrival
+  uint4 run = make_uint4(0, 0, 0, 0);
+  long long tmax = LLONG_MIN;
+  for (uint32_t base = 0; base < n; base += blockDim.x) {
+    const uint32_t r = base + tid;
+    uint32_t cnt = 0, suc = 0, ech = 0;
+    if (r < n) {
+      const uint32_t sec = asec[r];
+      const Rec rec = rec_of(rsrc, sec);
+      const int32_t ty = rec.type;
+      if (ty != PX_RES_TICKET && ty != PX_RES_PROPOSE && ty != PX_RES_COMMIT) S.px_bad = 1;
+      else atomicAdd(&S.px_deliv[ty - PX_RES_TICKET], 1u);
+      cnt = rec.f2 == dec ? 1u : 0u;
+      suc = cnt && rec.f0 == '0' ? 1u : 0u;
+      ech = p.echo && !(p.impl && is_main(sec)) ? 1u : 0u;
+      tmax = max(tmax, cs + static_cast<long long>(rec.t_off));
+    }
+    uint4 tot;
+    const uint4 ex = block_scan4(make_uint4(cnt, suc, ech, 0), S.wsum, tot);
+    if (cnt && c0 + static_cast<int32_t>(run.x + ex.x) + 1 == N2) {
+      S.px_r = r;
+      S.px_cb = run.x + ex.x;
+      S.px_sb = run.y + ex.y;
+      S.px_eb = run.z + ex.z + ech;  // explicit echoes up to and including the crossing arrival
+    }
+    run.x += tot.x;
+    run.y += tot.y;
+    run.z += tot.z;
+  }
+  for (int d = 32; d > 0; d >>= 1) tmax = max(tmax, static_cast<long long>(__shfl_xor(tmax, d, 64)));
+  if ((tid & 63u) == 0 && tmax > LLONG_MIN) atomicMax(&S.px_tmax, tmax);
+  __syncthreads();
+  // a second decision in the window, or a counted response after the one: the serial loop
+  const bool cross = S.px_r != kInvalid;
+  if (S.px_bad || c0 + static_cast<int32_t>(run.x) > N2 || (cross && c0 + static_cast<int32_t>(run.x) != N2) ||
+      S.px_nops0 + run.z + (cross ? 1u : 0u) > ocap)
+    return false;
+  // the decision (lane 0): the event of the crossing arrival, its counters as of that arrival
+  if (tid == 0) {
+    for (int k = 0; k < 3; ++k) c.deliv[PX_RES_TICKET + k] += S.px_deliv[k];
+    if (p.echo) c.echoes += n;
+    c.events += n;
+    if (S.px_tmax > S.tmax) S.tmax = S.px_tmax;
+    if (cross) {
+      const uint32_t r = S.px_r, sec = asec[r];
+      const Rec rec = rec_of(rsrc, sec);
+      const uint32_t q = e0 + (sec >> kSlotShift);
+      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
+      c.cur.t = cs + rec.t_off;
+      c.cur.ts = c.cur.t - dt;
+      c.cur.origin = AT(p.col, q, p.E);
+      c.cur.sub = rec.sub;
+      s.vs += static_cast<int32_t>(S.px_sb);
+      s.vf += static_cast<int32_t>(S.px_cb - S.px_sb);
+      c.nops = S.px_nops0 + S.px_eb;
+      paxos_recv(c, s, rec_msg(rec), q);
+      S.px_ncross = c.nops - (S.px_nops0 + S.px_eb);
+      c.nops = S.px_nops0 + run.z + S.px_ncross;
+    } else {
+      s.vs += static_cast<int32_t>(run.y);
+      s.vf += static_cast<int32_t>(run.x - run.y);
+      S.px_ncross = 0;
+      c.nops = S.px_nops0 + run.z;
+    }
+  }
+  __syncthreads();
+  // pass 2: the echo ops at their serial positions
+  const uint32_t rx = S.px_r, ncr = S.px_ncross, nops0 = S.px_nops0;
+  uint32_t eb = 0;
+  for (uint32_t base = 0; base < n; base += blockDim.x) {
+    const uint32_t r = base + tid;
+    uint32_t ech = 0;
+    uint32_t sec = 0;
+    if (r < n) {
+      sec = asec[r];
+      ech = p.echo && !(p.impl && is_main(sec)) ? 1u : 0u;
+    }
+    uint4 tot;
+    const uint4 ex = block_scan4(make_uint4(ech, 0, 0, 0), S.wsum, tot);
+    if (ech) {
+      const Rec rec = rec_of(rsrc, sec);
+      const uint32_t q = e0 + (sec >> kSlotShift);
+      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
+      const long long t = cs + rec.t_off;
+      const uint32_t pos = nops0 + eb + ex.x + (rx != kInvalid && r > rx ? ncr : 0u);
+      st_op(&AT(ops, pos, ocap), mk_op(p, t, dt, AT(p.col, q, p.E), rec.sub, q, rec_msg(rec), OP_ECHO, 0));
+    }
+    eb += tot.x;
+  }
+  return true;
+}
+
 template <int PROTO, bool SP>
 __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, uint32_t g, long long cell, long long t_lo, long long t_hi,
                           long long cs, int final_win, int x_active) {
@@ -2327,10 +2457,22 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
     if (PROTO == BCSIM_PBFT) {
       pbft_window(p, S, g, rep, i, e0, deg, n, n_main, cell, cs, t_lo, akey, asec, rsrc, acls);
       events += (tid == 0) ? n : 0;
-    } else if (tid == 0) {
+    } else {
+    if (tid == 0) {
       c.sub = S.sub;
       c.draws = S.draws;
       c.nops = S.nops;
+    }
+    // (Paxos proposers: the window's responses data-parallel when it qualifies)
+    const bool px_fast = PROTO == BCSIM_PAXOS && p.paxos_fast_win &&
+                         paxos_window_fast(p, S, c, xs_, g, n, asec, rsrc, e0, cs, t_lo, wb, tm, start_pending, stop_pending);
+    if (px_fast) {
+      if (tid == 0) {
+        S.sub = c.sub;
+        S.draws = c.draws;
+        S.nops = c.nops;
+      }
+    } else if (tid == 0) {
       uint32_t ai = 0;
       for (;;) {
         int which = -1;  // 0 arrival, 1 timer, 2 start, 3 stop
@@ -2466,6 +2608,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
       S.sub = c.sub;
       S.draws = c.draws;
       S.nops = c.nops;
+    }
     }
     __syncthreads();
     // consumed slots are free again
@@ -3255,9 +3398,14 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
 // (k_active's rule) that is not simple is appended to list 2 for k_scan<.., LOOP>.
 // The dense-gossip scan of one workgroup's node groups; returns true for a lane whose node the
 // generic k_scan must take (appended to list 2).
+// node k of the dense-gossip walk: the k-th gnode of this rank, or (fl) the k-th entry of the
+// window's frontier list (list 0, built by k_gossip_active)
+__device__ inline uint32_t gossip_gnode(const KP& p, uint32_t k, bool fl) {
+  return fl ? AT(p.act, k, 4ull * p.NT) : (k / p.nloc) * p.N + p.nlo + k % p.nloc;
+}
 __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP* __restrict__ pk, long long cell,
                                                                        long long t_lo, long long t_hi, long long cs,
-                                                                       int x_active, uint32_t G, int loop) {
+                                                                       int x_active, uint32_t G, int loop, bool fl) {
   const KP& p = *pk;
   __shared__ uint32_t s_deliv[BCSIM_MSG_TYPES];
   __shared__ uint32_t s_ev, s_wr, s_nf, s_trbase;
@@ -3270,11 +3418,11 @@ __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP*
     s_tmax = LLONG_MIN;
   }
   __syncthreads();
-  const uint32_t na = p.R * p.nloc;
+  const uint32_t na = fl ? p.act_n[0] : p.R * p.nloc;
   const uint32_t kl = blockIdx.x * per_wg + tid / G;
   const uint32_t k0 = blockIdx.x * per_wg;
-  const uint32_t g0 = (k0 / p.nloc) * p.N + p.nlo + k0 % p.nloc;
-  const uint32_t g = kl < na ? (kl / p.nloc) * p.N + p.nlo + kl % p.nloc : 0u;
+  const uint32_t g0 = k0 < na ? gossip_gnode(p, k0, fl) : 0u;
+  const uint32_t g = kl < na ? gossip_gnode(p, kl, fl) : 0u;
   const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t rep0 = g0 / p.N;  // counters of this replica go through LDS
   const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
@@ -3423,7 +3571,7 @@ __global__ __launch_bounds__(256) void k_gossip_scan(const KP* __restrict__ pk, 
                                                      int loop) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  (void)gossip_scan_body(pk, cell, t_lo, t_hi, cs, x_active, G, loop);
+  (void)gossip_scan_body(pk, cell, t_lo, t_hi, cs, x_active, G, loop, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -4867,8 +5015,10 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
 
 // LOOP: a small grid walks list 3 (the nodes k_gossip_link left over)
 __device__ void node_desc_flush(const KP& p, uint32_t g, long long cell, long long t_lo);
+// (FQCODEL: at most 256 lanes, so that the per-edge queue-disc walk gets the registers it needs
+// instead of spilling them -- 168 B/lane of scratch under the 1024-lane bound)
 template <int QM, bool XR, bool LOOP = false>
-__global__ __launch_bounds__(1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+__global__ __launch_bounds__(QM == 2 ? 256 : 1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                               long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
@@ -6310,7 +6460,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
 // for the generic k_link after it (list 3).
 __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP* __restrict__ pk, long long cell,
                                                                        long long t_lo, long long t_hi, int final_win,
-                                                                       uint32_t G, bool scan_left) {
+                                                                       uint32_t G, bool scan_left, bool fl) {
   const KP& p = *pk;
   __shared__ RawOp sop[256];  // due broadcasts of each group in key order (group base + rank)
   __shared__ uint32_t s_c[6];  // sends, records, due ops, edges, echoes, kept
@@ -6326,10 +6476,10 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
     s_bmin[k] = LLONG_MAX;
   }
   __syncthreads();
-  const uint32_t na = p.R * p.nloc;
+  const uint32_t na = fl ? p.act_n[0] : p.R * p.nloc;
   const uint32_t k0 = blockIdx.x * per_wg, kl = k0 + tid / G;
-  const uint32_t g0 = (k0 / p.nloc) * p.N + p.nlo + k0 % p.nloc;
-  const uint32_t g = kl < na ? (kl / p.nloc) * p.N + p.nlo + kl % p.nloc : 0u;
+  const uint32_t g0 = k0 < na ? gossip_gnode(p, k0, fl) : 0u;
+  const uint32_t g = kl < na ? gossip_gnode(p, kl, fl) : 0u;
   const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t rep0 = g0 / p.N;
   const uint32_t ib = static_cast<uint32_t>(cell % B);
@@ -6532,7 +6682,7 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
                                                      long long t_hi, int final_win, uint32_t G) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  gossip_link_body(pk, cell, t_lo, t_hi, final_win, G, false);
+  gossip_link_body(pk, cell, t_lo, t_hi, final_win, G, false, false);
 }
 
 // Dense gossip, one kernel per window: each workgroup scans its node groups and then runs their
@@ -6541,14 +6691,42 @@ __global__ __launch_bounds__(256) void k_gossip_link(const KP* __restrict__ pk, 
 // inbox row (implicit echoes) -- and writes only records of later cells and its own out-edges,
 // so no other node's scan in this window can affect it.  One launch per window instead of two,
 // and the row is read while still in this CU's cache.
+// fl: the grid walks the window's frontier list (k_gossip_active) instead of every gnode; the
+// workgroups past its end leave at once.
 __global__ __launch_bounds__(256) void k_gossip_cell(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                      long long t_hi, long long cs, int x_active, uint32_t G, int loop,
-                                                     int final_win) {
+                                                     int final_win, int fl) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  const bool left = gossip_scan_body(pk, cell, t_lo, t_hi, cs, x_active, G, loop);
+  if (fl && blockIdx.x * (blockDim.x / G) >= p.act_n[0]) return;
+  const bool left = gossip_scan_body(pk, cell, t_lo, t_hi, cs, x_active, G, loop, fl != 0);
   __syncthreads();  // (the node's new ops, n_ops and node_onext: written by one lane of its group)
-  gossip_link_body(pk, cell, t_lo, t_hi, final_win, G, left);
+  gossip_link_body(pk, cell, t_lo, t_hi, final_win, G, left, fl != 0);
+}
+
+// k_gossip_active: the window's frontier -- the gnodes k_gossip_cell has anything to do for
+// (arrivals in the cell's bucket, a timer or a pending op due before t_hi) -- into list 0,
+// wave-aggregated (any order: each node's work is its own)
+__global__ __launch_bounds__(256) void k_gossip_active(const KP* __restrict__ pk, long long cell, long long t_hi) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  const uint32_t na = p.R * p.nloc, lane = tidx() & 63u;
+  const uint32_t k = blockIdx.x * blockDim.x + tidx();
+  bool a = false;
+  uint32_t g = 0;
+  if (k < na) {
+    g = gossip_gnode(p, k, false);
+    const uint32_t rep = g / p.N, i = g % p.N, b = static_cast<uint32_t>(cell % p.n_buckets);
+    a = node_flagged_w(p, b, g, rep, i, t_hi) || AT(p.node_tnext, g, p.NT) < t_hi ||
+        (AT(p.n_ops, g, p.NT) != 0 && AT(p.node_onext, g, p.NT) < t_hi);
+  }
+  const unsigned long long m = __ballot(a);
+  if (!m) return;
+  const int ld = __ffsll(static_cast<long long>(m)) - 1;
+  uint32_t base = 0;
+  if (lane == static_cast<uint32_t>(ld)) base = gadd_r(&p.act_n[0], static_cast<uint32_t>(__popcll(m)));
+  base = __shfl(base, ld, 64);
+  if (a) AT(p.act, base + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull))), 4ull * p.NT) = g;
 }
 
 // ---------------------------------------------------------------------------
