@@ -56,34 +56,72 @@ def test_c3_paxos4096_multidecree_dense_equals_sparse(engine_lib):
     assert max(commits.values(), default=1) == 1
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(300)
 def test_c3_paxos4096_10k_replicas_fit(engine_lib):
     """The configs[2] batch size itself: 10,000 replicas of Paxos n=4096 (41M nodes, two
-    decrees per proposer) in one sparse engine on one GPU, run to quiescence, with the
-    per-replica equalities of the reference's message flow at the end (the oracle's n=64 run
-    holds them too): every request delivered was answered (paxos-node.cc:177-247), every
-    broadcast reached its N-2 peers plus the one dropped *end() send (:481-496), and every
-    proposer of every replica committed each of its K decrees exactly once."""
+    decrees per proposer) in one sparse engine on one GPU over the first 300 ms, with the
+    per-replica invariants of the reference's message flow that hold at every prefix.  (The
+    batch does not quiesce in a test's time: three dueling proposers per replica exchange
+    tickets for 10-20 s simulated -- the oracle's single n=4096 replica quiesces at 16 s; the
+    quiescence equalities are checked at n=4096 on fewer replicas below.)"""
     import bcsim
     from collections import Counter, defaultdict
-    n, reps, K = 4096, 10_000, 2
+    n, reps = 4096, 10_000
+    c = bcsim.preset("c3_paxos")
+    c.n_replicas = reps
+    c.paxos_decrees = 2
+    c.t_end_ns = 300_000_000
+    with bcsim.Simulator(c) as s:
+        s.run()
+        cnt, st, tr = s.counters(), s.status(), s.trace()
+    assert st["error"] == 0
+    d = cnt["delivered"]
+    assert d[0] > reps * 3 * 4000
+    # a response only for a delivered request (paxos-node.cc:177-247)
+    assert d[3] <= d[0] and d[4] <= d[1] and d[5] <= d[2]
+    # the three proposers of every replica request their first ticket at t = 0
+    # (paxos-node.cc:136-138, :510-522), and every ticket broadcast is logged once (:518)
+    t0 = defaultdict(set)
+    tickets = 0
+    for r in tr:
+        if r[6] == _abi.TR["PAXOS_TICKET"]:
+            tickets += 1
+            if r[1] == 0:
+                t0[r[0]].add(r[5])
+    assert len(t0) == reps and all(v == {0, 1, 2} for v in t0.values())
+    # a broadcast reaches N-2 peers plus one dropped *end() send (:481-496)
+    assert d[0] <= (n - 2) * tickets
+    assert d[0] + d[1] + d[2] <= (n - 2) * cnt["dropped"]
+    # a proposer commits each of its decrees at most once
+    commits = Counter((r[0], r[5], r[8]) for r in tr if r[6] == _abi.TR["PAXOS_COMMIT"])
+    assert max(commits.values(), default=1) == 1
+
+
+@pytest.mark.timeout(600)
+def test_c3_paxos4096_to_quiescence(engine_lib):
+    """configs[2] at full n (Paxos n=4096, three proposers, two decrees each, jittered links)
+    on 64 replicas, run to quiescence, with the equalities of the reference's message flow at
+    the end: every request delivered was answered (paxos-node.cc:177-247), every broadcast
+    reached its N-2 peers plus the one dropped *end() send (:481-496), and every proposer of
+    every replica committed each of its decrees exactly once (:322-339)."""
+    import bcsim
+    from collections import Counter
+    n, reps, K = 4096, 64, 2
     c = bcsim.preset("c3_paxos")
     c.n_replicas = reps
     c.paxos_decrees = K
     c.t_end_ns = 0
     with bcsim.Simulator(c) as s:
-        s.run()
+        t = 0
+        while True:  # (in 5 s steps: a bound on a livelocked run)
+            t += 5_000_000_000
+            s.run(t)
+            if s.status()["quiescent"] or t >= 120_000_000_000:
+                break
         cnt, st, tr = s.counters(), s.status(), s.trace()
     assert st["error"] == 0 and st["quiescent"]
     d = cnt["delivered"]
     assert d[3] == d[0] and d[4] == d[1] and d[5] == d[2]
     assert d[0] + d[1] + d[2] == (n - 2) * cnt["dropped"]
-    # the three proposers of every replica request their first ticket at t = 0 (:136-138, :510-522)
-    t0 = defaultdict(set)
-    for r in tr:
-        if r[6] == _abi.TR["PAXOS_TICKET"] and r[1] == 0:
-            t0[r[0]].add(r[5])
-    assert len(t0) == reps and all(v == {0, 1, 2} for v in t0.values())
-    # every (replica, proposer, decree) commits exactly once
     commits = Counter((r[0], r[5], r[8]) for r in tr if r[6] == _abi.TR["PAXOS_COMMIT"])
     assert len(commits) == reps * 3 * K and set(commits.values()) == {1}
