@@ -65,6 +65,8 @@ struct Sim {
   uint32_t* bcnt_h = nullptr;
   uint32_t* xcnt_h = nullptr;
   void* ctl_d = nullptr;
+  void* ctl_m = nullptr;  // host-mapped mirror of the control block (k_next writes it)
+  uint32_t* act_m = nullptr;  // host-mapped mirror of the active-list lengths (k_active writes it)
   std::vector<uint32_t> bcnt;  // bucket counts (host view)
   std::vector<uint32_t> xcnt;  // extras counts (host view)
   int x_active = 0;            // extras of the grouped cell are in xgrp
@@ -863,6 +865,25 @@ static int setup_device(Sim& s) {
   p.x_cnt = p.bucket_cnt + s.B;
   p.send_cnt = p.x_cnt + s.B;
   HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_h), ctl_bytes));
+#ifndef BCSIM_CHECKED
+  {  // the control block's host-mapped mirror (k_next publishes it; BCSIM_CTL_MIRROR=0: off)
+    const char* cm = std::getenv("BCSIM_CTL_MIRROR");
+    if (!(cm && *cm == '0')) {
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_m), ctl_bytes, hipHostMallocMapped | hipHostMallocCoherent));
+      void* dm = nullptr;
+      HIPCHK(hipHostGetDevicePointer(&dm, s.ctl_m, 0));
+      p.ctl_mirror = reinterpret_cast<uint32_t*>(dm);
+      p.ctl_words = static_cast<uint32_t>(ctl_bytes / 4);
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.act_m), 16, hipHostMallocMapped | hipHostMallocCoherent));
+      HIPCHK(hipHostGetDevicePointer(&dm, s.act_m, 0));
+      p.act_mirror = reinterpret_cast<uint32_t*>(dm);
+      uint32_t* ad = nullptr;
+      if ((rc = dalloc(s, &ad, 1))) return rc;
+      HIPCHK(hipMemset(ad, 0, 4));
+      p.act_done = (decltype(p.act_done))(ad);
+    }
+  }
+#endif
   HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.act_h), 32));  // (+ a pinned LLONG_MAX word at [4])
   *reinterpret_cast<long long*>(s.act_h + 4) = LLONG_MAX;
   s.bcnt_h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.ctl_h) + sizeof(Ctl));
@@ -1166,8 +1187,14 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
       // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
       // per CU: 4096 of them took ~24 us, the read-back takes ~10.
-      HIPCHK(hipMemcpyAsync(s.act_h, s.kp.act_n, 16, hipMemcpyDeviceToHost, s.stream));
-      HIPCHK(hipStreamSynchronize(s.stream));
+      if (s.act_m) {  // (k_active's last workgroup published them)
+        HIPCHK(hipStreamSynchronize(s.stream));
+        s.act_h[0] = s.act_m[0];
+        s.act_h[1] = s.act_m[1];
+      } else {
+        HIPCHK(hipMemcpyAsync(s.act_h, s.kp.act_n, 16, hipMemcpyDeviceToHost, s.stream));
+        HIPCHK(hipStreamSynchronize(s.stream));
+      }
       grid = dim3((s.act_h[0] + 7) / 8 * 8);
       n_link = s.act_h[1];
     } else if (!s.sparse) {
@@ -1475,10 +1502,17 @@ static int group_cell(Sim& s, long long cell) {
   return BCSIM_OK;
 }
 
-static int readback(Sim& s) {
-  HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks, hipMemcpyDeviceToHost,
-                        s.stream));
-  HIPCHK(hipStreamSynchronize(s.stream));
+// after_next: right after k_next, which published the control block to the host-mapped
+// mirror -- the read-back is the stream sync alone
+static int readback(Sim& s, bool after_next = false) {
+  const size_t nb = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
+  if (after_next && s.ctl_m) {
+    HIPCHK(hipStreamSynchronize(s.stream));
+    std::memcpy(s.ctl_h, s.ctl_m, nb);
+  } else {
+    HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, nb, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+  }
   int rc = ev_collect(s);
   if (rc) return rc;
   for (uint32_t k = 0; k < s.B; ++k) {
@@ -1839,7 +1873,7 @@ static int run(Sim& s, int64_t t_until) {
     // (a finished cell's bucket is free again: k_next clears its counts and tile flags)
     const uint32_t clr_b = hi == ce ? static_cast<uint32_t>(c % s.B) : 0xFFFFFFFFu;
     if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b);
-    if (!lrc) lrc = readback(s);
+    if (!lrc) lrc = readback(s, true);
     if (!lrc && s.dbg_fail_cell >= 0 && static_cast<long long>(s.cells) >= s.dbg_fail_cell) {
       g_detail = "injected failure (BCSIM_DBG_FAIL_CELL)";  // test hook: one rank fails alone
       lrc = BCSIM_E_OVERFLOW;
@@ -1984,6 +2018,8 @@ static void destroy(Sim* s) {
     (void)hipEventDestroy(e.second);
   }
   if (s->ctl_h) (void)hipHostFree(s->ctl_h);
+  if (s->ctl_m) (void)hipHostFree(s->ctl_m);
+  if (s->act_m) (void)hipHostFree(s->act_m);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   if (s->stream2) (void)hipStreamDestroy(s->stream2);
   if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);

@@ -212,6 +212,12 @@ struct KP {
   GP(long long) bmin;       // [B] lower bound of the arrival times of the bucket's records (LLONG_MAX: none):
                          // a window that ends before it skips the flagged rows (node_flagged_w)
   GP(uint32_t) bucket_cnt;  // [B] nonzero = the bucket holds records (slots + extras); see mark_busy
+  // host-mapped mirror of the control block (ctl_words words from p.err on): k_next publishes
+  // it at the end of a window, so the host's end-of-window read-back is a sync, no copy
+  GP(uint32_t) ctl_mirror;
+  uint32_t ctl_words;
+  GP(uint32_t) act_mirror;  // host-mapped: k_active's list lengths [0..1] (its last workgroup)
+  GP(uint32_t) act_done;    // k_active workgroups finished (reset by the last)
   GP(uint32_t) x_cnt;       // [B] extras in the bucket
   uint32_t n_buckets;
   GP(XRec) xbuf;            // [B][cap_x]
@@ -6717,8 +6723,11 @@ __global__ __launch_bounds__(256) void k_gossip_active(const KP* __restrict__ pk
   if (k < na) {
     g = gossip_gnode(p, k, false);
     const uint32_t rep = g / p.N, i = g % p.N, b = static_cast<uint32_t>(cell % p.n_buckets);
-    a = node_flagged_w(p, b, g, rep, i, t_hi) || AT(p.node_tnext, g, p.NT) < t_hi ||
-        (AT(p.n_ops, g, p.NT) != 0 && AT(p.node_onext, g, p.NT) < t_hi);
+    // every load issued at once (no short-circuit chain of round trips)
+    const bool f = node_flagged_w(p, b, g, rep, i, t_hi);
+    const long long tn = AT(p.node_tnext, g, p.NT), on = AT(p.node_onext, g, p.NT);
+    const uint32_t no = AT(p.n_ops, g, p.NT);
+    a = f | (tn < t_hi) | ((no != 0) & (on < t_hi));
   }
   const unsigned long long m = __ballot(a);
   if (!m) return;
@@ -7321,7 +7330,23 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
   const uint32_t tid = tidx();
   const uint64_t n_loc = static_cast<uint64_t>(p.R) * p.nloc;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * chunk;
-  if (c0 >= n_loc) return;  // uniform
+  // the last workgroup to take its list positions publishes the lengths to the host-mapped
+  // mirror (the host's read-back is then a sync, no copy)
+  auto publish = [&]() {
+    if (!p.act_mirror) return;
+    __threadfence();
+    if (gadd_r(p.act_done, 1u) == gridDim.x - 1) {
+      __threadfence();
+      p.act_mirror[0] = __hip_atomic_load(&p.act_n[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      p.act_mirror[1] = __hip_atomic_load(&p.act_n[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.act_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+    }
+  };
+  if (c0 >= n_loc) {  // uniform
+    if (tidx() == 0) publish();
+    return;
+  }
   const uint32_t cn = static_cast<uint32_t>(min(static_cast<uint64_t>(chunk), n_loc - c0));
   if (tid < 2) s_n[tid] = 0;
   __syncthreads();
@@ -7348,6 +7373,7 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
   if (tid == 0) {
     s_base[0] = s_n[0] ? gadd_r(&p.act_n[0], s_n[0]) : 0u;
     s_base[1] = s_n[1] ? gadd_r(&p.act_n[1], s_n[1]) : 0u;
+    publish();
   }
   __syncthreads();
   uint32_t ps = s_base[0], pl = s_base[1];
@@ -7738,6 +7764,21 @@ __global__ __launch_bounds__(256) void k_zero16(uint4* __restrict__ dst, uint64_
 // finish (threadfence reduction) combines the partial minima
 // k_next also ends the cell: the next window's active lists start empty, and a finished
 // cell's bucket (clr_b < n_buckets) is free again (its counts and receiver-tile flags).
+// one wave: the control words to the host-mapped mirror, with the window's next event times
+// (scal[0] = words 6-7, scal[3] = words 12-13 of the control block)
+__device__ inline void ctl_publish(const KP& p, long long s0, long long s3) {
+  if (!p.ctl_mirror) return;
+  const uint32_t lane = tidx() & 63u;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(p.err);
+  for (uint32_t k = lane; k < p.ctl_words; k += 64) {
+    uint32_t v = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == 6 || k == 7) v = static_cast<uint32_t>(static_cast<uint64_t>(s0) >> (32 * (k - 6)));
+    if (k == 12 || k == 13) v = static_cast<uint32_t>(static_cast<uint64_t>(s3) >> (32 * (k - 12)));
+    p.ctl_mirror[k] = v;
+  }
+  __threadfence_system();
+}
+
 __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b) {
   const KP& p = *pk;
   BAIL_IF_ERR();
@@ -7786,6 +7827,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
       p.scal[0] = m;
       p.scal[3] = mt;
     }
+    ctl_publish(p, m, mt);
     return;
   }
   bool last = false;
@@ -7806,10 +7848,12 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     mm = min(mm, static_cast<long long>(__shfl_xor(mm, d, 64)));
     mmt = min(mmt, static_cast<long long>(__shfl_xor(mmt, d, 64)));
   }
-  if (lane != 0) return;
-  p.scal[0] = mm;
-  p.scal[3] = mmt;
-  __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    p.scal[0] = mm;
+    p.scal[3] = mmt;
+    __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ctl_publish(p, mm, mmt);
 }
 
 }  // namespace bcsim
