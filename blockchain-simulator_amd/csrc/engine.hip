@@ -1188,7 +1188,6 @@ struct Ctx {
   uint32_t nops, cap_ops;
   TimerEnt* tm;  // LDS copy of the node's timers
   uint32_t cap_t;
-  unsigned long long deliv[BCSIM_MSG_TYPES];
   unsigned long long echoes, wrong, events;
 };
 
@@ -2279,7 +2278,7 @@ __device__ bool paxos_window_fast(const KP& p, ScanShared& S, Ctx& c, PaxosState
     return false;
   // the decision (lane 0): the event of the crossing arrival, its counters as of that arrival
   if (tid == 0) {
-    for (int k = 0; k < 3; ++k) c.deliv[PX_RES_TICKET + k] += S.px_deliv[k];
+    for (int k = 0; k < 3; ++k) S.deliv[PX_RES_TICKET + k] += S.px_deliv[k];
     if (p.echo) c.echoes += n;
     c.events += n;
     if (S.px_tmax > S.tmax) S.tmax = S.px_tmax;
@@ -2403,7 +2402,6 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
     c.cap_ops = op_cap(p, g);
     c.tm = tm;
     c.cap_t = p.cap_timers;
-    for (int k = 0; k < BCSIM_MSG_TYPES; ++k) c.deliv[k] = 0;
     c.echoes = c.wrong = c.events = 0;
     if (PROTO == BCSIM_RAFT) {
       rs.is_leader = AT(p.is_leader, g, p.NT);
@@ -2528,14 +2526,10 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
         if (which == 0) {
           ++ai;
           const Msg msg = rec_msg(rec);
-          // gossip keeps the per-type counts in LDS so that Ctx has no dynamically indexed
-          // member and stays in registers (Raft/Paxos: see DESIGN.md §8 on the miscompile)
-          if (rec.type < BCSIM_MSG_TYPES) {
-            if (PROTO == BCSIM_GOSSIP)
-              ++S.deliv[rec.type];
-            else
-              ++c.deliv[rec.type];
-          }
+          // the per-type counts live in LDS, so that Ctx has no dynamically indexed member and
+          // stays in registers (this once exposed the struct-select miscompile
+          // that key_sel now avoids)
+          if (rec.type < BCSIM_MSG_TYPES) ++S.deliv[rec.type];
           if (p.echo) {  // socket->SendTo(packet, 0, from): reverse-link occupancy
             const Op eo = mk_op(p, best.t, static_cast<uint32_t>(best.t - best.ts), best.origin, rec.sub, q, msg,
                                 OP_ECHO, 0);
@@ -2695,8 +2689,8 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
       AT(p.vote_f, g, p.NT) = xs_.vf;
     }
     for (int k = 0; k < BCSIM_MSG_TYPES; ++k)
-      if (PROTO == BCSIM_GOSSIP ? S.deliv[k] : c.deliv[k]) {
-        const unsigned long long dk = PROTO == BCSIM_GOSSIP ? S.deliv[k] : c.deliv[k];
+      if (S.deliv[k]) {
+        const unsigned long long dk = S.deliv[k];
         atomicAdd(&cnt[CNT_DELIV + k], dk);
         tot += dk;
       }
@@ -2713,8 +2707,10 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
 
 // a fixed grid over the window's active list (k_active); SP: sparse layout (no inbox slots)
 // LOOP: a small grid walks list 2, the nodes k_gossip_scan / k_paxos_scan left over
+// (Raft / Paxos / gossip: at most 256 lanes, so that lane 0's protocol state machine -- Ctx and
+// the node state, live across the event loop -- has the registers it needs instead of scratch)
 template <int PROTO, bool SP, bool LOOP = false>
-__global__ __launch_bounds__(1024) void k_scan(const KP* pk, long long cell, long long t_lo,
+__global__ __launch_bounds__(PROTO == BCSIM_PBFT ? 1024 : 256) void k_scan(const KP* pk, long long cell, long long t_lo,
                                                long long t_hi, long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   BAIL_IF_ERR();
