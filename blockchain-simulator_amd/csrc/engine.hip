@@ -2748,6 +2748,9 @@ __global__ __launch_bounds__(PROTO == BCSIM_PBFT ? 1024 : 256) void k_scan(const
 // another message type, arrivals at different instants, more than kFastKeys (phase, sequence)
 // groups or kFastPP PRE_PREPAREs, a bad index, START / STOP, a due timer) is appended to
 // list 2, untouched, for k_scan<PBFT, false, LOOP>.
+#ifndef BCSIM_SCANPBFT_WPE
+#define BCSIM_SCANPBFT_WPE 4  // k_scan_pbft occupancy target (waves per SIMD; 6 = three 512-lane workgroups per CU)
+#endif
 constexpr uint32_t kFastLanes = 512, kFastRPL = 8, kFastWaves = kFastLanes / 64, kFastKeys = 8, kFastPP = 16;
 constexpr uint32_t kFastSeg = kFastRPL * kFastWaves;  // (chunk, wave) segments in arrival order
 struct FastShared {
@@ -2813,7 +2816,7 @@ __device__ inline uint32_t fast_key_find(const FastShared& F, uint32_t key) {
   do {                                                                                      \
     if (p.wgs && tid == 0) p.wgs[8ull * g + (k)] = __builtin_amdgcn_s_memrealtime();       \
   } while (0)
-__global__ __launch_bounds__(512) void k_scan_pbft(const KP* __restrict__ pk, long long cell, long long t_lo,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANPBFT_WPE, 8))) void k_scan_pbft(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                    long long t_hi, long long cs, int x_active, uint32_t wep) {
   const KP& p = *pk;
   BAIL_IF_ERR();

@@ -12,11 +12,12 @@ launches (roofline.first_timed_launch, roofline.launches); every k_link instanti
 dispatches in that window get a "timed_window" entry: the rocprofv3 average duration (to
 compare with the bench's HIP-event avg_launch_us) and the HBM bytes per launch.
 
-A timed "launch" of the k_link class can be two dispatches: a fast-path kernel
-(k_link_mesh, k_gossip_link, k_paxos_link) followed by the looped generic kernel over the
-nodes it handed on (k_link<.., true> / k_link_sparse).  The "link_class" entry groups the
-dispatches that way and reports the timed window over the groups (bytes and durations summed
-over a group's dispatches): that is the figure bench.py compares with its HIP-event time.
+A timed "launch" of the k_link class is every link-stage dispatch of one window (fast-path
+kernels -- k_link_mesh or k_mesh_prep + k_mesh_tile, k_gossip_cell, k_paxos_link -- and the
+looped generic kernels over the nodes they hand on, both streams).  The "link_class" entry
+groups them by window (k_next delimits windows) and reports the timed window over the groups
+(bytes and durations summed over a group's dispatches): the figure bench.py compares with its
+HIP-event time (which, with the second stream, is the span of the two streams, not the sum).
 """
 import csv
 import json
@@ -53,30 +54,29 @@ def kernel_durations(path, prefix):
     return [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
 
 
-LINK_PRIMARY = ("bcsim::k_link_mesh", "bcsim::k_gossip_link", "bcsim::k_paxos_link")
-
-
-def is_primary(n):
-    """A fast-path link kernel (templated names included: k_link_mesh<false, 2, true>)."""
-    return n is not None and any(n == x or n.startswith(x + "<") for x in LINK_PRIMARY)
+# the kernels of the k_link class as bench.py times it: the fast-path link kernels (full-mesh
+# k_link_mesh, or the tiled k_mesh_prep + k_mesh_tile; dense gossip's fused kernel and its
+# frontier pass; sparse Paxos) and the looped generic k_link / k_link_sparse over the nodes they
+# hand on -- including the second stream's list-2 link stage
+LINK_CLASS = {"bcsim::k_link", "bcsim::k_link_mesh", "bcsim::k_link_sparse", "bcsim::k_mesh_prep",
+              "bcsim::k_mesh_tile", "bcsim::k_gossip_link", "bcsim::k_gossip_cell", "bcsim::k_gossip_active",
+              "bcsim::k_paxos_link"}
 
 
 def link_groups(names):
-    """Dispatch ids of the k_link class grouped into bench launches (see the module doc)."""
-    groups, prev = [], None
+    """Dispatch ids of the k_link class grouped into bench launches: one launch per window,
+    windows delimited by their k_next dispatch (see the module doc)."""
+    groups, cur = [], []
     for d in sorted(names):
-        n = names[d]
-        if not (n.startswith("bcsim::k_link") or is_primary(n)):
-            continue
-        follower = (groups and is_primary(prev) and
-                    ((n.startswith("bcsim::k_link<") and n.endswith("true>")) or
-                     (n == "bcsim::k_link_sparse" and prev == "bcsim::k_paxos_link")))
-        if follower:
-            groups[-1].append(d)
-            prev = None
-        else:
-            groups.append([d])
-            prev = n
+        n = names[d].split("<")[0]
+        if n == "bcsim::k_next":
+            if cur:
+                groups.append(cur)
+            cur = []
+        elif n in LINK_CLASS:
+            cur.append(d)
+    if cur:
+        groups.append(cur)
     return groups
 
 
