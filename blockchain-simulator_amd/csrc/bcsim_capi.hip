@@ -776,13 +776,13 @@ static int setup_device(Sim& s) {
     p.cap_fqm = c.cap_queue_msgs ? std::min<uint32_t>(c.cap_queue_msgs, kFqMaxMsgs) : kFqMaxMsgs;
     p.cap_fqm = (p.cap_fqm + 31) / 32 * 32;
     p.cap_fqp = static_cast<uint32_t>(std::min<uint64_t>(p.fq_limit + 1ull, 4096));
-    // per-flow packet rings: MaxSize + 1 packets (at most 4096) when that fits a 120 GB budget
-    // for the whole link state (per GPU: 120 / P GB per rank -- the ranks of a partition may
+    // per-flow packet rings: MaxSize + 1 packets (at most 4096) when that fits a 150 GB budget
+    // for the whole link state (per GPU: 150 / P GB per rank -- the ranks of a partition may
     // share one GPU), else the largest ring that does (>= 64; CoDel keeps a flow's
     // standing queue near rate x target, so a saturated 3 Mb/s link holds tens of packets).  A
     // flow that outgrows its ring fails the run (BCSIM_E_OVERFLOW), never drops silently.
     const double fixed_b = kFqH * 4.0 + p.fq_devcap * 8.0 + p.cap_fqm * 16.0 + 16.0 + 8.0;
-    const double budget = 120e9 / s.P;
+    const double budget = 150e9 / s.P;
     if (fq && static_cast<double>(ne) * (fixed_b + 48.0 * p.cap_fqp) > budget) {
       const double fit = (budget / static_cast<double>(ne) - fixed_b) / 48.0;
       p.cap_fqp = fit >= 64.0 ? static_cast<uint32_t>(std::min<double>(fit, p.cap_fqp)) : 0u;
