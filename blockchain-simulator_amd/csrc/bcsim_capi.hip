@@ -775,26 +775,50 @@ static int setup_device(Sim& s) {
     const size_t ne = fq ? static_cast<size_t>(s.R) * p.E_loc : 1;
     p.cap_fqm = c.cap_queue_msgs ? std::min<uint32_t>(c.cap_queue_msgs, kFqMaxMsgs) : kFqMaxMsgs;
     p.cap_fqm = (p.cap_fqm + 31) / 32 * 32;
-    p.cap_fqp = static_cast<uint32_t>(std::min<uint64_t>(p.fq_limit + 1ull, 4096));
-    // per-flow packet rings: MaxSize + 1 packets (at most 4096) when that fits a 150 GB budget
+    // per-flow packet rings.  A saturated link's disc holds up to MaxSize packets (the PBFT
+    // leader's block links and the echo links back to it run at 2.7x capacity), so the edges
+    // of the hub nodes -- PBFT / gossip node 0, the Paxos proposers -- get MaxSize + 1 packets
+    // per flow; every other edge gets MaxSize + 1 (at most 4096) when that fits a 150 GB budget
     // for the whole link state (per GPU: 150 / P GB per rank -- the ranks of a partition may
-    // share one GPU), else the largest ring that does (>= 64; CoDel keeps a flow's
-    // standing queue near rate x target, so a saturated 3 Mb/s link holds tens of packets).  A
-    // flow that outgrows its ring fails the run (BCSIM_E_OVERFLOW), never drops silently.
-    const double fixed_b = kFqH * 4.0 + p.fq_devcap * 8.0 + p.cap_fqm * 16.0 + 16.0 + 8.0;
-    const double budget = 150e9 / s.P;
-    if (fq && static_cast<double>(ne) * (fixed_b + 48.0 * p.cap_fqp) > budget) {
-      const double fit = (budget / static_cast<double>(ne) - fixed_b) / 48.0;
-      p.cap_fqp = fit >= 64.0 ? static_cast<uint32_t>(std::min<double>(fit, p.cap_fqp)) : 0u;
-      if (p.cap_fqp < 64) {
+    // share one GPU), else the largest ring that does (>= 64).  A flow that outgrows its ring
+    // fails the run (BCSIM_E_OVERFLOW), never drops silently.
+    const uint32_t cap_hi = static_cast<uint32_t>(std::min<uint64_t>(p.fq_limit + 1ull, 65535));
+    uint32_t cap_lo = static_cast<uint32_t>(std::min<uint64_t>(p.fq_limit + 1ull, 4096));
+    auto hub = [&](uint32_t i) {
+      return c.protocol == BCSIM_PAXOS ? i < p.paxos_proposers : (c.protocol == BCSIM_RAFT ? false : i == 0);
+    };
+    std::vector<uint64_t> poff(fq ? ne : 0);
+    size_t n_hub = 0;
+    if (fq)
+      for (uint32_t i = p.nlo; i < p.nlo + s.nloc; ++i)
+        for (uint32_t e = s.row[i]; e < s.row[i + 1]; ++e)
+          if (hub(i) || hub(s.col[e])) ++n_hub;
+    n_hub *= s.R;
+    const double fixed_b = kFqH * 4.0 + p.fq_devcap * 8.0 + p.cap_fqm * 16.0 + 16.0 + 8.0 + 8.0;
+    const double budget = 150e9 / s.P - static_cast<double>(n_hub) * 48.0 * cap_hi;
+    if (fq && static_cast<double>(ne) * fixed_b + static_cast<double>(ne - n_hub) * 48.0 * cap_lo > budget) {
+      const double fit = ((budget - static_cast<double>(ne) * fixed_b) / std::max<double>(1.0, static_cast<double>(ne - n_hub))) / 48.0;
+      cap_lo = fit >= 64.0 ? static_cast<uint32_t>(std::min<double>(fit, cap_lo)) : 0u;
+      if (cap_lo < 64) {
         g_detail = "FQCODEL link state exceeds its memory budget even with 64-packet flow rings";
         return BCSIM_E_UNSUPPORTED;
       }
     }
+    size_t npk = 0;
+    if (fq)
+      for (uint32_t rep = 0; rep < s.R; ++rep)
+        for (uint32_t i = p.nlo; i < p.nlo + s.nloc; ++i)
+          for (uint32_t e = s.row[i]; e < s.row[i + 1]; ++e) {
+            const uint32_t cap = (hub(i) || hub(s.col[e])) ? cap_hi : cap_lo;
+            poff[static_cast<size_t>(rep) * p.E_loc + (e - p.e_lo)] = npk | (static_cast<uint64_t>(cap) << 48);
+            npk += 3ull * cap;
+          }
+    p.cap_fqp = cap_lo;
     uint32_t* fqlnk = nullptr;
     const size_t nt = fq ? s.NT : 1;
     if ((rc = dalloc(s, &p.fqh, ne * kFqH)) || (rc = dalloc(s, &p.fqdev, fq ? ne * p.fq_devcap : 1)) ||
-        (rc = dalloc(s, &p.fqpk, fq ? ne * 3 * p.cap_fqp : 1)) || (rc = dalloc(s, &p.fqmsg, fq ? ne * p.cap_fqm : 1)) ||
+        (rc = dalloc(s, &p.fqpk, fq ? npk : 1)) || (rc = dalloc(s, &p.fqpoff, ne)) ||
+        (rc = dalloc(s, &p.fqmsg, fq ? ne * p.cap_fqm : 1)) ||
         (rc = dalloc(s, &fqlnk, fq ? s.E : 1)) || (rc = dalloc(s, &p.fqport, ne)) || (rc = dalloc(s, &p.fqpeer, ne)) ||
         (rc = dalloc(s, &p.fqkey, ne)) || (rc = dalloc(s, &p.fqnport, nt)) || (rc = dalloc(s, &p.fqphant, nt)))
       return rc;
@@ -807,6 +831,7 @@ static int setup_device(Sim& s) {
       HIPCHK(hipStreamSynchronize(s.stream));
       const std::vector<uint32_t> lnk = fq_link_numbers(s.N, s.row, s.col, s.rev);
       HIPCHK(hipMemcpy(fqlnk, lnk.data(), s.E * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(const_cast<uint64_t*>(p.fqpoff), poff.data(), ne * 8, hipMemcpyHostToDevice));
       // sockets unbound (port 0), no first-send keys pending (all ones)
       HIPCHK(hipMemset(p.fqport, 0, ne * 4));
       HIPCHK(hipMemset(p.fqpeer, 0, ne * 4));
@@ -1356,8 +1381,9 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       HIPCHK(hipEventRecord(s.ev_join, s.stream2));
     }
     if (s.P > 1) {
-      if ((rc = s.mesh_pf ? launch(s, -1, k_link_mesh<true, 2, true>, grid, dim3(256), mlds, s.kp_dev, cell, lo, hi, fw, z, z)
-                          : launch(s, -1, k_link_mesh<true, 2, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, z, z)) ||
+      // (node-partitioned: one out-edge per lane per step, no parked link words -- 119 VGPRs and
+      // no scratch, where the two-edge / prefetching variants spill at 4 waves per SIMD)
+      if ((rc = launch(s, -1, k_link_mesh<true, 1, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, z, z)) ||
           (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
     } else if (s.mesh_tile && n_link >= s.tile_min) {

@@ -194,6 +194,7 @@ struct KP {
   GP(uint32_t) fqnport;
   GP(uint32_t) fqphant;
   GP(uint4) fqkey;
+  GP(const uint64_t) fqpoff;  // per edge: its packet rings' offset in fqpk | per-flow capacity << 48
   uint32_t fq_flows, fq_pert;
   uint32_t fq_devcap, cap_fqp, cap_fqm, fq_limit, fq_quantum, fq_batch, fq_min_bytes, fq_target_c, fq_interval_c;
   uint32_t ip_full[2], ip_last[2];
@@ -3666,6 +3667,7 @@ struct FqLink {
   uint4* msg;
   uint32_t e, src;  // (src: the op source of the current send, debug log only)
   uint32_t ia, ib;  // the link's sender / receiver IPv4 addresses
+  uint32_t cap;     // packets per flow ring
   uint32_t pa, pe;  // client port of this edge's socket / of the reverse edge's (0: not bound)
 };
 // kinds: 1 enqueue, 2 into the device queue (x = frame start), 3 drop, 4 wake
@@ -3697,7 +3699,9 @@ __device__ inline FqLink fq_link(const KP& p, size_t le, uint32_t e, uint32_t i,
   FqLink L;
   L.h = p.fqh + le * kFqH;
   L.dev = p.fqdev + le * p.fq_devcap;
-  L.pk = p.fqpk + le * 3 * p.cap_fqp;
+  const uint64_t po = p.fqpoff[le];
+  L.pk = p.fqpk + (po & ((1ull << 48) - 1));
+  L.cap = static_cast<uint32_t>(po >> 48);
   L.msg = p.fqmsg + le * p.cap_fqm;
   L.e = e;
   L.src = 0;
@@ -3764,8 +3768,8 @@ __device__ inline bool fq_pop(const KP& p, FqLink& L, uint32_t f, uint4& out) {
   const uint32_t n = F[FQ_N];
   if (n == 0) return false;
   const uint32_t hd = F[FQ_HEAD];
-  out = L.pk[f * p.cap_fqp + hd];
-  F[FQ_HEAD] = hd + 1 == p.cap_fqp ? 0u : hd + 1;
+  out = L.pk[f * L.cap + hd];
+  F[FQ_HEAD] = hd + 1 == L.cap ? 0u : hd + 1;
   F[FQ_N] = n - 1;
   F[FQ_BYTES] -= out.w;
   L.h[FQ_QP] -= 1;
@@ -4027,15 +4031,15 @@ __device__ inline void fq_send(const KP& p, FqLink& L, int64_t now, uint32_t sub
       fq_list_push(L.h, FQ_NNEW, FQ_NEWL, f);
     }
     const uint32_t n = Fh[FQ_N];
-    if (n == p.cap_fqp) {
-      set_err(p, BCSIM_E_OVERFLOW);  // more packets in one flow than cap_fqp
+    if (n == L.cap) {
+      set_err(p, BCSIM_E_OVERFLOW);  // more packets in one flow than its ring holds
       return;
     }
     uint32_t at = Fh[FQ_HEAD] + n;
-    if (at >= p.cap_fqp) at -= p.cap_fqp;
+    if (at >= L.cap) at -= L.cap;
     const uint32_t size = j + 1 == F ? p.ip_last[big] : p.ip_full[big];
-    L.pk[f * p.cap_fqp + at] = make_uint4(now_lo, now_hi, m | (j << 16), size);
-    fq_log(p, L, now, 1, L.pk[f * p.cap_fqp + at], f | (L.src << 8));
+    L.pk[f * L.cap + at] = make_uint4(now_lo, now_hi, m | (j << 16), size);
+    fq_log(p, L, now, 1, L.pk[f * L.cap + at], f | (L.src << 8));
     Fh[FQ_N] = n + 1;
     Fh[FQ_BYTES] += size;
     const uint32_t qp = L.h[FQ_QP] + 1;

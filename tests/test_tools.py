@@ -64,17 +64,20 @@ def test_cpu_baselines_small():
 
 
 def test_pmc_summary_link_class_groups(tmp_path):
-    """A timed k_link-class launch = fast-path dispatch + looped generic dispatch: the
-    link_class entry sums both over the bench's timed window."""
+    """A timed k_link-class launch = the link-stage dispatches of one window (fast path +
+    looped generic kernel; windows end at their k_next): the link_class entry sums them over
+    the bench's timed window."""
     import pmc_summary
     src = tmp_path / "prof"
     mesh = "bcsim::k_link_mesh(bcsim::KP const*, long long, long long, long long, int)"
     loop = "void bcsim::k_link<false, false, true>(bcsim::KP const*, long long, long long, long long, int)"
     scan = "void bcsim::k_scan<0, false, false>(bcsim::KP const*)"
+    nxt = "bcsim::k_next(bcsim::KP const*, unsigned int)"
     rows_f, rows_w, trace = [], [], []
     t, d = 0, 0
     for k in range(5):
-        for name, fv, wv, us in ((scan, 1.0, 1.0, 1), (mesh, float(k), 10.0, 10 * (k + 1)), (loop, 1.0, 2.0, 2)):
+        for name, fv, wv, us in ((scan, 1.0, 1.0, 1), (mesh, float(k), 10.0, 10 * (k + 1)), (loop, 1.0, 2.0, 2),
+                                 (nxt, 0.5, 0.5, 1)):
             rows_f.append((d, name, [fv]))
             rows_w.append((d, name, [wv, 0, 0]))
             trace.append((d, name, t, t + 1000 * us))

@@ -180,6 +180,7 @@ inline bool __hip_atomic_compare_exchange_strong(T* p, T* expected, U desired, i
 }
 #define __HIP_MEMORY_SCOPE_WORKGROUP 2
 inline void __threadfence() { std::atomic_thread_fence(std::memory_order_seq_cst); }
+inline void __threadfence_system() { std::atomic_thread_fence(std::memory_order_seq_cst); }
 
 // ---- runtime API subset ----
 typedef int hipError_t;
