@@ -184,7 +184,7 @@ inline void __threadfence_system() { std::atomic_thread_fence(std::memory_order_
 
 // ---- runtime API subset ----
 typedef int hipError_t;
-enum { hipSuccess = 0, hipErrorUnknown = 999 };
+enum { hipSuccess = 0, hipErrorNotReady = 600, hipErrorUnknown = 999 };
 typedef struct hipemu_stream* hipStream_t;
 typedef struct hipemu_event* hipEvent_t;
 enum hipMemcpyKind { hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice, hipMemcpyDefault };
@@ -196,6 +196,7 @@ hipError_t hipSetDevice(int);
 hipError_t hipStreamCreateWithFlags(hipStream_t*, unsigned);
 hipError_t hipStreamDestroy(hipStream_t);
 hipError_t hipStreamSynchronize(hipStream_t);
+hipError_t hipStreamQuery(hipStream_t);
 hipError_t hipDeviceSynchronize();
 hipError_t hipMalloc(void**, size_t);
 hipError_t hipFree(void*);
