@@ -67,6 +67,7 @@ struct Sim {
   void* ctl_d = nullptr;
   void* ctl_m = nullptr;  // host-mapped mirror of the control block (k_next writes it)
   uint32_t* act_m = nullptr;  // host-mapped mirror of the active-list lengths (k_active writes it)
+  uint32_t mseq = 0;          // sequence number of the last k_active / k_next launch (mirror words)
   std::vector<uint32_t> bcnt;  // bucket counts (host view)
   std::vector<uint32_t> xcnt;  // extras counts (host view)
   int x_active = 0;            // extras of the grouped cell are in xgrp
@@ -186,7 +187,11 @@ static int ev_end(Sim& s) {
   ++s.ev_used;
   return BCSIM_OK;
 }
+// (called with the stream drained -- or it drains it: the end-of-window read-back spins on the
+// control mirror, which k_next writes before the stream's completion is signalled)
+constexpr size_t kEvBatch = 256;  // timing events read back per batch
 static int ev_collect(Sim& s) {
+  if (s.ev_used) HIPCHK(hipStreamSynchronize(s.stream));
   for (size_t k = 0; k < s.ev_used; ++k) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, s.ev_pool[k].first, s.ev_pool[k].second));
@@ -195,6 +200,8 @@ static int ev_collect(Sim& s) {
   s.ev_used = 0;
   return BCSIM_OK;
 }
+
+static int mirror_wait(Sim& s, const uint32_t* w);  // (below, with readback)
 
 static int validate(const bcsim_config& c) {
   if (c.abi_version != BCSIM_ABI_VERSION) return BCSIM_E_INVAL;
@@ -723,8 +730,9 @@ static int setup_device(Sim& s) {
     if (!on) p.eslot = nullptr;
     // k_scan_pbft -> k_link_mesh reply / echo descriptors (BCSIM_NO_DESC=1: off)
     const char* nd = std::getenv("BCSIM_NO_DESC");
-    // (k_link_mesh applies pending echoes to its LDS-parked link words: the PF variant)
-    p.desc = (s.scan_fast && s.mesh_link && s.mesh_pf && s.deg_max <= 32 * kDescWords && !(nd && *nd == '1')) ? 1u : 0u;
+    // (k_link_mesh applies pending echoes to its LDS-parked link words: the PF variant, which
+    // the node-partitioned engine does not launch)
+    p.desc = (s.scan_fast && s.mesh_link && s.mesh_pf && s.P == 1 && s.deg_max <= 32 * kDescWords && !(nd && *nd == '1')) ? 1u : 0u;
     p.dwords = p.desc ? static_cast<uint32_t>((s.deg_max + 31) / 32) : 1u;
     const size_t nrb = p.desc ? static_cast<size_t>(kOpRing) * NT * p.dwords : 1;
     const size_t neb = p.desc ? static_cast<size_t>(NT) * kEDesc * p.dwords : 1;
@@ -895,12 +903,14 @@ static int setup_device(Sim& s) {
   {  // the control block's host-mapped mirror (k_next publishes it; BCSIM_CTL_MIRROR=0: off)
     const char* cm = std::getenv("BCSIM_CTL_MIRROR");
     if (!(cm && *cm == '0')) {
-      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_m), ctl_bytes, hipHostMallocMapped | hipHostMallocCoherent));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctl_m), ctl_bytes + 4, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(s.ctl_m, 0, ctl_bytes + 4);
       void* dm = nullptr;
       HIPCHK(hipHostGetDevicePointer(&dm, s.ctl_m, 0));
       p.ctl_mirror = reinterpret_cast<uint32_t*>(dm);
       p.ctl_words = static_cast<uint32_t>(ctl_bytes / 4);
       HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.act_m), 16, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(s.act_m, 0, 16);
       HIPCHK(hipHostGetDevicePointer(&dm, s.act_m, 0));
       p.act_mirror = reinterpret_cast<uint32_t*>(dm);
       uint32_t* ad = nullptr;
@@ -1180,7 +1190,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     // the frontier list unless START / STOP makes every node active
     const int fl = s.gossip_frontier && !(lo <= 0 && 0 < hi) && !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi);
     const uint32_t na = static_cast<uint32_t>(static_cast<uint64_t>(s.R) * s.nloc);
-    if ((fl && (rc = launch(s, -1, k_gossip_active, dim3((na + 255) / 256), dim3(256), 0, s.kp_dev, cell, hi))) ||
+    if ((fl && (rc = launch(s, -1, k_gossip_active, dim3((na + 1023) / 1024), dim3(1024), 0, s.kp_dev, cell, hi))) ||
         (rc = launch(s, -1, k_gossip_cell, gg, dim3(256), 0, s.kp_dev, cell, lo, hi, cs, xa, s.gossip_g, loop, fw, fl)) ||
         (loop &&
          (rc = launch(s, -1, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), block, lds, s.kp_dev, cell, lo, hi,
@@ -1202,7 +1212,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     const uint64_t nb = std::max<uint64_t>((nl + kActChunk - 1) / kActChunk, std::min<uint64_t>(1024, (nl + 255) / 256));
     const uint32_t chunk = static_cast<uint32_t>(((nl + nb - 1) / nb + 255) / 256 * 256);
     rc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, lo, hi,
-                static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk);
+                static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk, ++s.mseq);
     if (rc) return rc;
     static const bool no_sync = [] {
       const char* e = std::getenv("BCSIM_NO_ACTSYNC");
@@ -1213,8 +1223,9 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
       // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
       // per CU: 4096 of them took ~24 us, the read-back takes ~10.
-      if (s.act_m) {  // (k_active's last workgroup published them)
-        HIPCHK(hipStreamSynchronize(s.stream));
+      const int w = s.act_m ? mirror_wait(s, s.act_m + 2) : 1;
+      if (w < 0) return w;
+      if (w == 0) {  // (k_active's last workgroup published them)
         s.act_h[0] = s.act_m[0];
         s.act_h[1] = s.act_m[1];
       } else {
@@ -1382,7 +1393,8 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     }
     if (s.P > 1) {
       // (node-partitioned: one out-edge per lane per step, no parked link words -- 119 VGPRs and
-      // no scratch, where the two-edge / prefetching variants spill at 4 waves per SIMD)
+      // no scratch, where the two-edge / prefetching variants spill at 4 waves per SIMD; the reply
+      // descriptors, which need the parked words, are off at P > 1)
       if ((rc = launch(s, -1, k_link_mesh<true, 1, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, z, z)) ||
           (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
@@ -1529,18 +1541,46 @@ static int group_cell(Sim& s, long long cell) {
   return BCSIM_OK;
 }
 
+// Wait for the kernel just launched to publish sequence number s.mseq to the host-mapped
+// word w: 0 = published (the mirror holds its data), 1 = the stream drained without it (the
+// kernel bailed on an error flag: read the device copy), < 0 = a HIP error.  The spin sees the
+// kernel's last store ~1 us after it lands; a stream sync adds the completion signal's
+// wake-up and the end-of-kernel cache release (~10-20 us per read-back).  With
+// BCSIM_SPIN=0, a plain stream sync.
+static int mirror_wait(Sim& s, const uint32_t* w) {
+  static const bool spin = [] {
+    const char* e = std::getenv("BCSIM_SPIN");
+    return !(e && *e == '0');
+  }();
+  const uint32_t seq = s.mseq;
+  if (!spin) {
+    HIPCHK(hipStreamSynchronize(s.stream));
+    return __atomic_load_n(w, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
+  }
+  for (uint32_t it = 1;; ++it) {
+    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return 0;
+    if ((it & 255u) == 0) {
+      const hipError_t q = hipStreamQuery(s.stream);
+      if (q == hipSuccess) return __atomic_load_n(w, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
+      if (q != hipErrorNotReady) HIPCHK(q);
+    }
+  }
+}
+
 // after_next: right after k_next, which published the control block to the host-mapped
 // mirror -- the read-back is the stream sync alone
 static int readback(Sim& s, bool after_next = false) {
   const size_t nb = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
-  if (after_next && s.ctl_m) {
-    HIPCHK(hipStreamSynchronize(s.stream));
+  int w = 1;
+  if (after_next && s.ctl_m && (w = mirror_wait(s, reinterpret_cast<uint32_t*>(s.ctl_m) + nb / 4)) < 0) return w;
+  if (w == 0) {
     std::memcpy(s.ctl_h, s.ctl_m, nb);
   } else {
     HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, nb, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipStreamSynchronize(s.stream));
   }
-  int rc = ev_collect(s);
+  // per-launch timing events: read in batches (reading them needs their completion signals)
+  int rc = s.ev_used >= kEvBatch ? ev_collect(s) : 0;
   if (rc) return rc;
   for (uint32_t k = 0; k < s.B; ++k) {
     s.bcnt[k] = s.bcnt_h[k];
@@ -1899,7 +1939,7 @@ static int run(Sim& s, int64_t t_until) {
     const uint32_t nbn = static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
     // (a finished cell's bucket is free again: k_next clears its counts and tile flags)
     const uint32_t clr_b = hi == ce ? static_cast<uint32_t>(c % s.B) : 0xFFFFFFFFu;
-    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b);
+    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b, ++s.mseq);
     if (!lrc) lrc = readback(s, true);
     if (!lrc && s.dbg_fail_cell >= 0 && static_cast<long long>(s.cells) >= s.dbg_fail_cell) {
       g_detail = "injected failure (BCSIM_DBG_FAIL_CELL)";  // test hook: one rank fails alone
@@ -2243,6 +2283,7 @@ int bcsim_read_kernel_stats(bcsim_sim* h, double* us_out4, double* bytes_out4, u
   if (!h) return BCSIM_E_INVAL;
   Sim& s = *h->s;
   unsigned long long ks[8] = {0};
+  if (bcsim::ev_collect(s)) return BCSIM_E_HIP;
   if (s.started) {
     unsigned long long kss[8 * bcsim::kKstStripes];
     hipError_t e = hipMemcpy(kss, s.kp.kstat, sizeof kss, hipMemcpyDeviceToHost);
@@ -2351,6 +2392,7 @@ int bcsim_set_partition_rccl(bcsim_sim* h, uint32_t rank, uint32_t nranks, const
 int bcsim_reset_kernel_stats(bcsim_sim* h) {
   if (!h) return BCSIM_E_INVAL;
   Sim& s = *h->s;
+  s.ev_used = 0;  // (timings not read yet belong to the old period)
   for (int k = 0; k < 4; ++k) {
     s.us[k] = 0;
     s.launches[k] = 0;

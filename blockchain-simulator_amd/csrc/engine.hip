@@ -214,10 +214,11 @@ struct KP {
                          // a window that ends before it skips the flagged rows (node_flagged_w)
   GP(uint32_t) bucket_cnt;  // [B] nonzero = the bucket holds records (slots + extras); see mark_busy
   // host-mapped mirror of the control block (ctl_words words from p.err on): k_next publishes
-  // it at the end of a window, so the host's end-of-window read-back is a sync, no copy
+  // it at the end of a window, then the window's sequence number at word ctl_words, so the
+  // host's end-of-window read-back is a spin on that word, no copy and no stream sync
   GP(uint32_t) ctl_mirror;
   uint32_t ctl_words;
-  GP(uint32_t) act_mirror;  // host-mapped: k_active's list lengths [0..1] (its last workgroup)
+  GP(uint32_t) act_mirror;  // host-mapped: k_active's list lengths [0..1] (its last workgroup), [2] sequence
   GP(uint32_t) act_done;    // k_active workgroups finished (reset by the last)
   GP(uint32_t) x_cnt;       // [B] extras in the bucket
   uint32_t n_buckets;
@@ -2830,6 +2831,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
   const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t e0 = p.mesh ? i * (p.N - 1) : AT(p.row, i, p.N + 1);
   const uint32_t deg = p.mesh ? p.N - 1 : AT(p.row, i + 1, p.N + 1) - e0;
+  // the row's loads go out first: the node's checks below are dependent global reads (its
+  // bucket flag, timer, extras) that would otherwise serialise in front of them.  A node that
+  // does not qualify leaves them unused (the heavy waves' nodes all qualify).
+#ifndef BCSIM_SCANPBFT_SPEC
+#define BCSIM_SCANPBFT_SPEC 1  // (0: the row loads after the checks, for an A/B)
+#endif
+  const bool spec = deg <= kFastLanes * kFastRPL && blockDim.x == kFastLanes;
+  uint4 rv[kFastRPL];
+  const Rec* slots = p.inbox + inbox_idx(p, b, rep, e0);
+  auto row_loads = [&]() {
+#pragma unroll
+    for (uint32_t j = 0; j < kFastRPL; ++j) {  // the whole row in flight at once
+      const uint32_t k = j * kFastLanes + tid;
+      rv[j] = spec && k < deg ? gld4(slots + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (BCSIM_SCANPBFT_SPEC) row_loads();
   const bool flag = node_flagged_w(p, b, g, rep, i, t_hi);
   const bool has_ss = (t_lo <= 0 && 0 < t_hi) || (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
   const bool timer = AT(p.node_tnext, g, p.NT) < t_hi;
@@ -2864,14 +2882,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
       !(AT(p.sflag, static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) &
         (2u | kSfD1));
   const bool echo_dir = echo_here && !p.desc;
-  const Rec* slots = p.inbox + inbox_idx(p, b, rep, e0);
-  uint4 rv[kFastRPL];
-#pragma unroll
-  for (uint32_t j = 0; j < kFastRPL; ++j) {  // the whole row in flight at once
-    const uint32_t k = j * kFastLanes + tid;
-    rv[j] = k < deg ? gld4(slots + k) : make_uint4(0, 0, 0, 0);
-  }
-  // ... and the link words of its out-edges with it (LDS; used by the echo pass at the end)
+  if (!BCSIM_SCANPBFT_SPEC) row_loads();
+  // the link words of its out-edges (LDS; used by the echo pass at the end)
   if (echo_dir) {
     const uint64_t* lrow = p.link + edge_loc(p, rep, e0);
     uint64_t lv[kFastRPL];
@@ -6715,11 +6727,13 @@ __global__ __launch_bounds__(256) void k_gossip_cell(const KP* __restrict__ pk, 
 
 // k_gossip_active: the window's frontier -- the gnodes k_gossip_cell has anything to do for
 // (arrivals in the cell's bucket, a timer or a pending op due before t_hi) -- into list 0,
-// wave-aggregated (any order: each node's work is its own)
-__global__ __launch_bounds__(256) void k_gossip_active(const KP* __restrict__ pk, long long cell, long long t_hi) {
+// workgroup-aggregated: ONE list atomic per 1024 gnodes (a per-wave atomic on the one counter
+// serialised in L2: 14 us per launch at 65536 gnodes); any order, each node's work is its own
+__global__ __launch_bounds__(1024) void k_gossip_active(const KP* __restrict__ pk, long long cell, long long t_hi) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  const uint32_t na = p.R * p.nloc, lane = tidx() & 63u;
+  __shared__ uint32_t wcnt[kMaxWaves], s_base;
+  const uint32_t na = p.R * p.nloc, lane = tidx() & 63u, wv = tidx() >> 6;
   const uint32_t k = blockIdx.x * blockDim.x + tidx();
   bool a = false;
   uint32_t g = 0;
@@ -6733,12 +6747,19 @@ __global__ __launch_bounds__(256) void k_gossip_active(const KP* __restrict__ pk
     a = f | (tn < t_hi) | ((no != 0) & (on < t_hi));
   }
   const unsigned long long m = __ballot(a);
-  if (!m) return;
-  const int ld = __ffsll(static_cast<long long>(m)) - 1;
-  uint32_t base = 0;
-  if (lane == static_cast<uint32_t>(ld)) base = gadd_r(&p.act_n[0], static_cast<uint32_t>(__popcll(m)));
-  base = __shfl(base, ld, 64);
-  if (a) AT(p.act, base + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull))), 4ull * p.NT) = g;
+  if (lane == 0) wcnt[wv] = static_cast<uint32_t>(__popcll(m));
+  __syncthreads();
+  if (tidx() == 0) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
+      const uint32_t c = wcnt[w];
+      wcnt[w] = t;
+      t += c;
+    }
+    s_base = t ? gadd_r(&p.act_n[0], t) : 0u;
+  }
+  __syncthreads();
+  if (a) AT(p.act, s_base + wcnt[wv] + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull))), 4ull * p.NT) = g;
 }
 
 // ---------------------------------------------------------------------------
@@ -7320,7 +7341,7 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
 // loop bound is wave-uniform, so every ballot runs with the whole wave active)
 constexpr uint32_t kActChunk = 16384;  // k_active: gnodes per workgroup at most (LDS flags)
 __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long long t_lo, long long t_hi, uint32_t b,
-                                                uint32_t obp, uint32_t chunk) {
+                                                uint32_t obp, uint32_t chunk, uint32_t seq) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   // each workgroup compacts a contiguous chunk of gnodes: flags to LDS and counts, ONE global
@@ -7344,6 +7365,7 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
       p.act_mirror[1] = __hip_atomic_load(&p.act_n[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(p.act_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence_system();
+      __hip_atomic_store(p.act_mirror + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // (host spins on it)
     }
   };
   if (c0 >= n_loc) {  // uniform
@@ -7769,7 +7791,8 @@ __global__ __launch_bounds__(256) void k_zero16(uint4* __restrict__ dst, uint64_
 // cell's bucket (clr_b < n_buckets) is free again (its counts and receiver-tile flags).
 // one wave: the control words to the host-mapped mirror, with the window's next event times
 // (scal[0] = words 6-7, scal[3] = words 12-13 of the control block)
-__device__ inline void ctl_publish(const KP& p, long long s0, long long s3) {
+// then the window's sequence number in the word after them, which the host spins on
+__device__ inline void ctl_publish(const KP& p, long long s0, long long s3, uint32_t seq) {
   if (!p.ctl_mirror) return;
   const uint32_t lane = tidx() & 63u;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(p.err);
@@ -7779,10 +7802,11 @@ __device__ inline void ctl_publish(const KP& p, long long s0, long long s3) {
     if (k == 12 || k == 13) v = static_cast<uint32_t>(static_cast<uint64_t>(s3) >> (32 * (k - 12)));
     p.ctl_mirror[k] = v;
   }
-  __threadfence_system();
+  __threadfence_system();  // (the wave's stores done before the sequence word)
+  if (lane == 0) __hip_atomic_store(p.ctl_mirror + p.ctl_words, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b) {
+__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b, uint32_t seq) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (blockIdx.x == 0) {
@@ -7830,7 +7854,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
       p.scal[0] = m;
       p.scal[3] = mt;
     }
-    ctl_publish(p, m, mt);
+    ctl_publish(p, m, mt, seq);
     return;
   }
   bool last = false;
@@ -7856,7 +7880,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     p.scal[3] = mmt;
     __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  ctl_publish(p, mm, mmt);
+  ctl_publish(p, mm, mmt, seq);
 }
 
 }  // namespace bcsim

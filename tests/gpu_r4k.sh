@@ -9,3 +9,6 @@ for v in "" "BCSIM_SPIN=0"; do
   env $v timeout -k 10 240 python bench.py --workload gossip --steps 20 --warmup 5 --no-cpu-baseline > $out/gossip.log 2>&1 || exit 1
   echo "gossip [$v] $(tail -1 $out/gossip.log | cut -c1-200)"
 done
+bash tests/gpu_ab.sh ab22 - "BCSIM_LIB=ab_lib/nospec.so" "" "BCSIM_LIB=ab_lib/nospec.so" "" || exit 1
+BCSIM_WGT=1 timeout -k 10 240 python bench.py --steps 3 --warmup 3 --no-cpu-baseline > $out/wgt.log 2>&1 || exit 1
+grep -c wgs $out/wgt.log
