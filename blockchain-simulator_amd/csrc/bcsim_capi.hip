@@ -290,6 +290,12 @@ static int setup_device(Sim& s) {
   p.encoding = c.encoding;
   p.echo = c.echo;
   p.deg_max = s.deg_max;
+  {  // a regular topology with row[i] = i * degree: the dense-gossip kernels skip the row loads
+    bool reg = s.deg_max > 0 && s.row.size() == static_cast<size_t>(s.N) + 1;
+    for (uint32_t i = 0; reg && i <= s.N; ++i) reg = s.row[i] == static_cast<uint64_t>(i) * s.deg_max;
+    p.deg_reg = reg ? s.deg_max : 0u;
+    if (const char* e = std::getenv("BCSIM_NO_DEGREG"); e && *e == '1') p.deg_reg = 0;
+  }
   p.app_delay = c.app_delay_ns;
   // message sizes
   uint32_t small = 3, big = 3;

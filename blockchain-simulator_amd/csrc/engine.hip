@@ -55,6 +55,7 @@ struct KP {
   uint32_t N, R, NT, E;
   uint32_t protocol, delay_mode, rng_mode, encoding, echo;
   uint32_t deg_max;
+  uint32_t deg_reg;  // every node's degree when all are equal and row[i] = i * deg_reg, else 0
   int64_t L;
   uint64_t L_magic;  // ceil(2^64 / L): x / L for x < 2^32 is the high half of x * L_magic
   int64_t app_delay;
@@ -3446,13 +3447,30 @@ __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP*
   const uint32_t b = static_cast<uint32_t>(cell % p.n_buckets);
   const bool has_start = (t_lo <= 0 && 0 < t_hi);
   const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
-  const bool flagged = kl < na && node_flagged_w(p, b, g, rep, i, t_hi);
-  const bool tdue = kl < na && AT(p.node_tnext, g, p.NT) < t_hi;
-  const bool have = kl < na && (has_start || has_stop || flagged || tdue);  // k_active's k_scan rule
-  const uint32_t e0 = have ? AT(p.row, i, p.N + 1) : 0u;
-  const uint32_t deg = have ? AT(p.row, i + 1, p.N + 1) - e0 : 0u;
+  // every load that depends on g alone goes out before any of them is used (one round trip,
+  // not a chain of short-circuit branches each waiting for its load): unconditional, at valid
+  // addresses (g = 0 past the list's end), used only under the conditions below.  On a regular
+  // graph the row offsets are arithmetic and this lane's in-slot record is among them.
+  const bool kin = kl < na;
+  const uint32_t e0r = p.deg_reg ? i * p.deg_reg : 0u;
+  uint4 rsv = make_uint4(0, 0, 0, 0);  // (raw words: unpacking a Rec here would wait for the load)
+  if (p.deg_reg) rsv = gld4(p.inbox + inbox_idx(p, b, rep, e0r + min(j, p.deg_reg - 1u)));
+  const uint8_t f8 = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
+  const uint8_t t8 = p.mesh ? AT(p.rtile, (static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6),
+                                 static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles)
+                            : static_cast<uint8_t>(0);
+  const long long tn = AT(p.node_tnext, g, p.NT);
+  const uint32_t sub0p = AT(p.sub, g, p.NT), nops0p = AT(p.n_ops, g, p.NT);
+  const uint64_t draws0p = p.delay_mode != BCSIM_DELAY_FIXED ? AT(p.draws, g, p.NT) : 0ull;
+  const uint32_t rw0 = p.deg_reg ? 0u : AT(p.row, i, p.N + 1), rw1 = p.deg_reg ? 0u : AT(p.row, i + 1, p.N + 1);
+  const uint32_t so0 = x_active ? AT(p.seg_off, g, p.NT + 1) : 0u, so1 = x_active ? AT(p.seg_off, g + 1, p.NT + 1) : 0u;
+  const bool flagged = kin && (f8 | t8) != 0 && p.bmin[b] < t_hi;  // (node_flagged_w)
+  const bool tdue = kin && tn < t_hi;
+  const bool have = kin && (has_start || has_stop || flagged || tdue);  // k_active's k_scan rule
+  const uint32_t e0 = !have ? 0u : p.deg_reg ? e0r : rw0;
+  const uint32_t deg = !have ? 0u : p.deg_reg ? p.deg_reg : rw1 - rw0;
   bool fast = have && deg <= G && !has_start && !has_stop && !tdue;
-  if (fast && x_active) fast = AT(p.seg_off, g + 1, p.NT + 1) == AT(p.seg_off, g, p.NT + 1);
+  if (fast && x_active) fast = so1 == so0;
   if (have && !fast && j == 0) {
     // (loop == 0: the host skips k_scan<.., LOOP> -- no timer, START, STOP or extras can be
     // due in the window -- so no node may be left over)
@@ -3467,7 +3485,10 @@ __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP*
   long long t = 0;
   uint32_t dt = 0;
   if (fast && j < deg && flagged) {
-    r = ld_rec(p.inbox + inbox_idx(p, b, rep, e0 + j));
+    if (p.deg_reg)
+      __builtin_memcpy(&r, &rsv, sizeof r);
+    else
+      r = ld_rec(p.inbox + inbox_idx(p, b, rep, e0 + j));
     t = cs + r.t_off;
     v = slot_live(r.flags, cell_tag(p, cell)) && t >= t_lo && t < t_hi;
     dt = static_cast<uint32_t>(prop_of_slot(p, e0 + j) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
@@ -3526,13 +3547,8 @@ __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP*
   if (first) li = atomicAdd(&s_nf, 1u);
   // node state: sub (+deg per broadcast), draws (jitter), pending ops -- read by every lane
   // of the group before the barrier, written by lane 0 after it
-  uint32_t sub0 = 0, nops0 = 0;
-  uint64_t draws0 = 0;
-  if (nf) {
-    sub0 = AT(p.sub, g, p.NT);
-    nops0 = AT(p.n_ops, g, p.NT);
-    draws0 = AT(p.draws, g, p.NT);
-  }
+  const uint32_t sub0 = sub0p, nops0 = nops0p;
+  const uint64_t draws0 = draws0p;
   __syncthreads();
   if (tid == 0) s_trbase = s_nf ? gadd_r(p.trace_cnt, s_nf) : 0u;
   __syncthreads();
@@ -6504,20 +6520,46 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
   const uint32_t rep = g / p.N, i = g % p.N;
   const uint32_t rep0 = g0 / p.N;
   const uint32_t ib = static_cast<uint32_t>(cell % B);
-  const bool rx = kl < na && p.impl && node_flagged_w(p, ib, g, rep, i, t_hi);
-  const uint32_t n0 = kl < na ? AT(p.n_ops, g, p.NT) : 0u;
+  // (as in the scan: the loads that depend on g alone at once -- on a regular graph also this
+  // lane's edge words and in-slot record, and its op slot, before it is known they are needed)
+  // (all of them unconditional, at valid addresses -- g = 0 past the list's end, in-slot and op
+  // indices clamped -- and used only under the conditions below)
+  const bool kin = kl < na;
+  const uint32_t e0r = p.deg_reg ? i * p.deg_reg : 0u;
+  const bool pre = p.deg_reg != 0u;
+  uint32_t sp_p = 0, slot_p = 0;
+  uint64_t lw_p = 0;
+  uint4 r0v = make_uint4(0, 0, 0, 0);  // (raw words, as in the scan)
+  if (pre) {
+    const uint32_t jc = min(j, p.deg_reg - 1u), e = e0r + jc;
+    sp_p = AT(p.col, e, p.E);
+    slot_p = AT(p.rev, e, p.E);
+    lw_p = p.link[link_index(p, rep, i, e0r, jc)];
+    if (p.impl) r0v = gld4(p.inbox + inbox_idx(p, ib, rep, e));
+  }
+  Op* const ops_p = p.ops + op_base(p, g);
+  const RawOp o_p = ld_raw(ops_p + min(j, op_cap(p, g) - 1u));
+  const uint8_t f8 = AT(p.iflag, static_cast<size_t>(ib) * p.NT + g, static_cast<uint64_t>(B) * p.NT);
+  const uint8_t t8 = p.mesh ? AT(p.rtile, (static_cast<size_t>(ib) * p.R + rep) * p.n_tiles + (i >> 6),
+                                 static_cast<uint64_t>(B) * p.R * p.n_tiles)
+                            : static_cast<uint8_t>(0);
+  const uint32_t n0l = AT(p.n_ops, g, p.NT);
+  const long long onl = AT(p.node_onext, g, p.NT);
+  const uint32_t rw0 = pre ? 0u : AT(p.row, i, p.N + 1), rw1 = pre ? 0u : AT(p.row, i + 1, p.N + 1);
+  const bool rx = kin && p.impl && (f8 | t8) != 0 && p.bmin[ib] < t_hi;  // (node_flagged_w)
+  const uint32_t n0 = kin ? n0l : 0u;
   // nodes link_node would change: an echo to send, or an op due (k_active's rule minus the
   // nodes for which link_node only recomputes an unchanged node_onext)
-  const bool have = rx || (n0 && AT(p.node_onext, g, p.NT) < t_hi) || scan_left;
+  const bool have = rx || (n0 && onl < t_hi) || scan_left;
   const uint32_t n = have ? n0 : 0u;
-  const uint32_t e0 = have ? AT(p.row, i, p.N + 1) : 0u;
-  const uint32_t deg = have ? AT(p.row, i + 1, p.N + 1) - e0 : 0u;
-  Op* ops = p.ops + (have ? op_base(p, g) : 0);
+  const uint32_t e0 = !have ? 0u : pre ? e0r : rw0;
+  const uint32_t deg = !have ? 0u : pre ? p.deg_reg : rw1 - rw0;
+  Op* ops = have ? ops_p : p.ops;
   // this lane's pending op
   RawOp o = raw_zero();
   bool due = false, bc = false, keep = false;
   if (have && n <= G && j < n) {
-    o = ld_raw(ops + j);
+    o = o_p;
     const uint32_t kind = raw_kind(o);
     due = kind != OP_BCAST_J && raw_t(o) < t_hi;
     bc = due && kind == OP_BCAST;
@@ -6550,14 +6592,17 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
   uint32_t c_rec = 0, c_edges = 0, c_echo = 0;
   if (fast && j < deg && (nb || rx)) {
     const uint32_t e = e0 + j;
-    const uint32_t sp = AT(p.col, e, p.E);
+    const uint32_t sp = pre ? sp_p : AT(p.col, e, p.E);
     uint64_t* lwp = p.link + link_index(p, rep, i, e0, j);
-    uint64_t lw = *lwp;
+    uint64_t lw = pre ? lw_p : *lwp;
     bool he = false;
     RawOp eo = raw_zero();
     if (rx) {
-      Rec* ir = p.inbox + inbox_idx(p, ib, rep, e);
-      const Rec r0 = ld_rec(ir);
+      Rec r0;
+      if (pre)
+        __builtin_memcpy(&r0, &r0v, sizeof r0);
+      else
+        r0 = ld_rec(p.inbox + inbox_idx(p, ib, rep, e));
       const long long ta0 = cell * p.L + r0.t_off;
       if (slot_live(r0.flags, cell_tag(p, cell)) && ta0 >= t_lo && ta0 < t_hi) {
         if (p.echo) {
@@ -6575,7 +6620,7 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
       int64_t bu = static_cast<int64_t>(lw >> 16);
       uint32_t lc = static_cast<uint32_t>(lw & 0xFFFFu);
       const int64_t pr = p.prop_const >= 0 ? p.prop_const : AT(p.prop, e, p.E);
-      const uint32_t slot = AT(p.rev, e, p.E);
+      const uint32_t slot = pre ? slot_p : AT(p.rev, e, p.E);
       const uint32_t dg = rep * p.N + sp;
       uint32_t q = 0;
       for (;;) {
