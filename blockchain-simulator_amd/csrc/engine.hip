@@ -2838,24 +2838,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
 #ifndef BCSIM_SCANPBFT_SPEC
 #define BCSIM_SCANPBFT_SPEC 1  // (0: the row loads after the checks, for an A/B)
 #endif
-  const bool spec = deg <= kFastLanes * kFastRPL && blockDim.x == kFastLanes;
+  const bool spec = deg <= kFastLanes * kFastRPL && blockDim.x == kFastLanes && deg > 0;
   uint4 rv[kFastRPL];
   const Rec* slots = p.inbox + inbox_idx(p, b, rep, e0);
+  // (unconditional loads at clamped slots, used only for k < deg: a per-load `k < deg` branch
+  // made the compiler wait for each load before the next -- eight serial round trips)
+  // (no branch at all: a zeroing else-path made the join wait for every load)
   auto row_loads = [&]() {
+    const uint4* rb = reinterpret_cast<const uint4*>(deg ? slots : p.inbox);
+    const uint32_t dm = deg ? deg - 1u : 0u;
 #pragma unroll
-    for (uint32_t j = 0; j < kFastRPL; ++j) {  // the whole row in flight at once
-      const uint32_t k = j * kFastLanes + tid;
-      rv[j] = spec && k < deg ? gld4(slots + k) : make_uint4(0, 0, 0, 0);
-    }
+    for (uint32_t j = 0; j < kFastRPL; ++j) rv[j] = gld4(rb + min(j * kFastLanes + tid, dm));
   };
   if (BCSIM_SCANPBFT_SPEC) row_loads();
+  // the node's earliest pending op and its two slot-flag bytes (the echo rule below) with them,
+  // unconditionally (a null flag array reads a dummy word)
+  uint8_t* const sfa = p.sflag ? p.sflag : reinterpret_cast<uint8_t*>(p.act_n);
+  const uint8_t sfv0 = gbl(sfa)[p.sflag ? static_cast<size_t>(cell % kOpRing) * p.NT + g : 0u];
+  const uint8_t sfv1 = gbl(sfa)[p.sflag ? static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g : 0u];
+  const long long onext0 = AT(p.node_onext, g, p.NT);  // earliest pending op (LLONG_MIN: unknown)
   const bool flag = node_flagged_w(p, b, g, rep, i, t_hi);
   const bool has_ss = (t_lo <= 0 && 0 < t_hi) || (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
   const bool timer = AT(p.node_tnext, g, p.NT) < t_hi;
   uint32_t xn = 0;
   if (x_active) xn = AT(p.seg_off, g + 1, p.NT + 1) - AT(p.seg_off, g, p.NT + 1);
   if (!flag && !has_ss && !timer) return;  // nothing in the window (scan_node returns too)
-  if (!flag || has_ss || timer || xn || deg > kFastLanes * kFastRPL || deg > p.cap_arr || blockDim.x != kFastLanes ||
+  if (!flag || has_ss || timer || xn || !spec || deg > p.cap_arr ||
       !p.impl || !p.eslot || p.delay_mode != BCSIM_DELAY_FIXED) {
     if (tid == 0) {
       AT(p.act, 2ull * p.NT + gadd_r(&p.act_n[2], 1u), 4ull * p.NT) = g;
@@ -2876,12 +2884,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
   // stage that walks its edges applies before anything else (k_link_mesh: it loads and stores
   // those link words anyway) -- unless kEDesc descriptors are pending: then the link stage
   // does the echoes of this window from the row (no eapp stamp), after the pending ones.
-  const long long onext0 = AT(p.node_onext, g, p.NT);  // earliest pending op (LLONG_MIN: unknown)
-  const bool echo_here =
-      p.echo && p.qmodel == 0 && onext0 >= t_hi &&
-      !(AT(p.sflag, static_cast<size_t>(cell % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & (1u | kSfD0)) &&
-      !(AT(p.sflag, static_cast<size_t>((cell + kOpRing - 1) % kOpRing) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) &
-        (2u | kSfD1));
+  const bool echo_here = p.echo && p.qmodel == 0 && onext0 >= t_hi && !(sfv0 & (1u | kSfD0)) && !(sfv1 & (2u | kSfD1));
   const bool echo_dir = echo_here && !p.desc;
   if (!BCSIM_SCANPBFT_SPEC) row_loads();
   // the link words of its out-edges (LDS; used by the echo pass at the end)
@@ -2889,10 +2892,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
     const uint64_t* lrow = p.link + edge_loc(p, rep, e0);
     uint64_t lv[kFastRPL];
 #pragma unroll
-    for (uint32_t j = 0; j < kFastRPL; ++j) {
-      const uint32_t k = j * kFastLanes + tid;
-      lv[j] = k < deg ? gbl(lrow)[k] : 0ull;
-    }
+    for (uint32_t j = 0; j < kFastRPL; ++j) lv[j] = gbl(lrow)[min(j * kFastLanes + tid, deg - 1u)];  // (as the row)
 #pragma unroll
     for (uint32_t j = 0; j < kFastRPL; ++j) F.lw[j * kFastLanes + tid] = lv[j];
   }
@@ -2914,8 +2914,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
   __syncthreads();
   const uint32_t tag = cell_tag(p, cell);
   const uint64_t lt = (1ull << lane) - 1ull;
+  // (the frame times in scalar registers: indexed by a lane's flag they were a vector load per
+  // record, each waited for before the next)
+  const int64_t txl0 = p.tx_last[0], txl1 = p.tx_last[1], txt0 = p.tx_tot[0], txt1 = p.tx_tot[1];
   auto key_of = [&](const uint4& r, uint32_t k) -> unsigned long long {
-    const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, e0 + k) + p.tx_last[((r.w >> 24) & RF_BIG) ? 1 : 0]);
+    const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, e0 + k) + (((r.w >> 24) & RF_BIG) ? txl1 : txl0));
     return (static_cast<unsigned long long>(r.x) << 32) | static_cast<uint32_t>(~dt);
   };
   // ---- pass 1: window membership, message types and indices, quorum group counts, key range ----
@@ -3131,7 +3134,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
     const uint32_t sp = sub0 + np + nd * deg_u, op = nops0 + nd;
     const uint32_t k = j * kFastLanes + tid;
     const uint32_t q = e0 + k;  // in-slot = the reverse (reply) edge
-    const uint32_t dt = ~static_cast<uint32_t>(key_of(r, k));
+    const uint32_t dt = ~static_cast<uint32_t>(F.kmax);  // (every arrival has the one key)
     const int64_t t = cs + static_cast<int64_t>(r.x);
     const uint32_t origin = p.mesh ? (k < i ? k : k + 1) : AT(p.col, q, p.E);
     const Key key{t, t - static_cast<int64_t>(dt), origin, r.y};
@@ -3184,7 +3187,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
       const uint64_t lw = F.lw[j * kFastLanes + tid];
       const int64_t t = cs + static_cast<int64_t>(r.x);
       const int64_t bu0 = static_cast<int64_t>(lw >> 16);
-      const int64_t bu = (bu0 > t ? bu0 : t) + p.tx_tot[((r.w >> 24) & RF_BIG) ? 1 : 0];
+      const int64_t bu = (bu0 > t ? bu0 : t) + (((r.w >> 24) & RF_BIG) ? txt1 : txt0);
       if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
       gbl(lrow)[j * kFastLanes + tid] = (static_cast<uint64_t>(bu) << 16) | (lw & 0xFFFFull);
     }
@@ -5999,6 +6002,8 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
     const bool v = il < kTS && i < N && s < N && s != i;
     lv[k] = v ? gbl(p.link)[edge_loc(p, rep, i * N1 + (s < i ? s : s - 1))] : 0ull;
   }
+  // the buckets' arrival-time bounds with them (a second round trip for wave 0 otherwise)
+  const long long bm_v = tid < B ? *reinterpret_cast<volatile G<long long>*>(&gbl(p.bmin)[tid]) : LLONG_MAX;
   // jobs, broadcasts and descriptor tile masks of the 32 senders, all loads at once (a stale job
   // is told by its epoch; the other words are used only under its flags)
   if (tid < kTS * 4) {
@@ -6025,7 +6030,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
     T.lmin[k] = ~0u;
   }
   for (uint32_t k = tid; k <= B; k += blockDim.x) T.lst[k] = 0;
-  for (uint32_t k = tid; k < B; k += blockDim.x) T.bmin[k] = *reinterpret_cast<volatile G<long long>*>(&gbl(p.bmin)[k]);
+  if (tid < B) T.bmin[tid] = bm_v;  // (B <= kMaxBuckets <= blockDim.x)
   if (tid < 8) T.csum[tid] = 0;
   if (tid == 0) {
     T.bkm = 0ull;
@@ -6055,7 +6060,8 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
   const uint32_t w3r = static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0))) | (kPbPrepareRes << 16);
   const unsigned long long lbit = 1ull << lane, lbelow = lbit - 1ull;
   // (the fast path's parameters, read once)
-  const int64_t tx0 = p.tx_tot[0], tx1 = p.tx_tot[1], prc = p.prop_const;
+  // (scalar registers: indexed by a lane's flag, a KP array is a vector load per use)
+  const int64_t tx0 = p.tx_tot[0], tx1 = p.tx_tot[1], txl0 = p.tx_last[0], txl1 = p.tx_last[1], prc = p.prop_const;
   const uint64_t Lmag = p.L_magic;
   uint32_t n_rec = 0, st_edges = 0, st_echo = 0, st_ops = 0, sends = 0;
   unsigned long long bkm = 0ull;
@@ -6117,7 +6123,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
         const uint4 q3 = T.job[il][3];
         const int64_t et = static_cast<int64_t>(d ? ((static_cast<uint64_t>(q3.w) << 32) | q3.z)
                                                   : ((static_cast<uint64_t>(q3.y) << 32) | q3.x));
-        const int64_t eb = (bu > et ? bu : et) + p.tx_tot[(fl & (d ? kJBig1 : kJBig0)) ? 1 : 0];
+        const int64_t eb = (bu > et ? bu : et) + ((fl & (d ? kJBig1 : kJBig0)) ? tx1 : tx0);
         const bool hit = v && (m & lbit);
         bu = hit ? eb : bu;
         pe = pe || hit;
@@ -6196,7 +6202,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
         const uint4 q3 = T.job[il][3];
         const int64_t et = static_cast<int64_t>(d ? ((static_cast<uint64_t>(q3.w) << 32) | q3.z)
                                                   : ((static_cast<uint64_t>(q3.y) << 32) | q3.x));
-        bu = (bu > et ? bu : et) + p.tx_tot[(fl & (d ? kJBig1 : kJBig0)) ? 1 : 0];
+        bu = (bu > et ? bu : et) + ((fl & (d ? kJBig1 : kJBig0)) ? tx1 : tx0);
         pe = true;
       }
     }
@@ -6212,7 +6218,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
         ebig = (rfl & RF_BIG) ? 1 : 0;
         const int64_t pin = p.prop_const >= 0 ? p.prop_const : gbl(p.prop_in)[e];
         et = ta0;
-        edt = static_cast<uint32_t>(pin + p.tx_last[ebig]);
+        edt = static_cast<uint32_t>(pin + (ebig ? txl1 : txl0));
         esub = r0.y;
         he = true;
         ++st_echo;
@@ -6233,7 +6239,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
     // extras or overflow)
     auto emit = [&](int64_t ot, uint32_t osub, uint32_t ow2, uint32_t ow3, int big) {
       const int64_t start = bu > ot ? bu : ot;
-      const int64_t end = start + p.tx_tot[big];
+      const int64_t end = start + (big ? tx1 : tx0);
       bu = end;
       const int64_t ta = end + pr;
       long long ca;
@@ -6317,7 +6323,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
         const uint4 w = hr ? w0 : w1;
         emit(hr ? rt1 : rt2, w.z, w.w, w3r, 0);
       } else {  // the echo only occupies the link
-        bu = (bu > et ? bu : et) + p.tx_tot[ebig];
+        bu = (bu > et ? bu : et) + (ebig ? tx1 : tx0);
       }
     } else {
       uint32_t bi = 0;
@@ -6373,7 +6379,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
         else
           he = false;
         if (src == 3) {  // the echo only occupies the link
-          bu = (bu > ot ? bu : ot) + p.tx_tot[big];
+          bu = (bu > ot ? bu : ot) + (big ? tx1 : tx0);
           continue;
         }
         if (src == 2 || src == 4) ++sends;
