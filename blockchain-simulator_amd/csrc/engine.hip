@@ -430,6 +430,14 @@ __device__ inline G<T>& at_(const KP& p, T* base, uint64_t idx, uint64_t cap, in
 #endif
   return gbl(base)[idx];
 }
+// element 0 / 1 of a two-entry KP array (frame times by size class): two scalar loads and a
+// select -- indexed by a lane's flag, the array read is a vector load per use, waited for
+// before the next
+template <typename T>
+__device__ __forceinline__ T sel2(const T* a, bool one) {
+  const T x = a[0], y = a[1];
+  return one ? y : x;
+}
 #ifdef BCSIM_CHECKED
 #define BAIL_IF_ERR() \
   do {                \
@@ -1592,7 +1600,7 @@ __device__ inline int64_t prop_of_slot(const KP& p, uint32_t q) {
   return p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, q, p.E);
 }
 __device__ inline uint64_t arr_key(const KP& p, const Rec& r, uint32_t q) {
-  const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
+  const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + sel2(p.tx_last, (r.flags & RF_BIG) ? 1 : 0));
   return (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~dt);
 }
 
@@ -2289,7 +2297,7 @@ __device__ bool paxos_window_fast(const KP& p, ScanShared& S, Ctx& c, PaxosState
       const uint32_t r = S.px_r, sec = asec[r];
       const Rec rec = rec_of(rsrc, sec);
       const uint32_t q = e0 + (sec >> kSlotShift);
-      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
+      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + sel2(p.tx_last, (rec.flags & RF_BIG) ? 1 : 0));
       c.cur.t = cs + rec.t_off;
       c.cur.ts = c.cur.t - dt;
       c.cur.origin = AT(p.col, q, p.E);
@@ -2324,7 +2332,7 @@ __device__ bool paxos_window_fast(const KP& p, ScanShared& S, Ctx& c, PaxosState
     if (ech) {
       const Rec rec = rec_of(rsrc, sec);
       const uint32_t q = e0 + (sec >> kSlotShift);
-      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
+      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + sel2(p.tx_last, (rec.flags & RF_BIG) ? 1 : 0));
       const long long t = cs + rec.t_off;
       const uint32_t pos = nops0 + eb + ex.x + (rx != kInvalid && r > rx ? ncr : 0u);
       st_op(&AT(ops, pos, ocap), mk_op(p, t, dt, AT(p.col, q, p.E), rec.sub, q, rec_msg(rec), OP_ECHO, 0));
@@ -2491,7 +2499,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
           const uint32_t sec = asec[ai];
           rec = rec_of(rsrc, sec);
           q = e0 + (sec >> kSlotShift);
-          const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[(rec.flags & RF_BIG) ? 1 : 0]);
+          const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + sel2(p.tx_last, (rec.flags & RF_BIG) ? 1 : 0));
           best.t = cs + rec.t_off;
           best.ts = best.t - dt;
           best.origin = AT(p.col, q, p.E);
@@ -3321,7 +3329,7 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
         fast = false;
         break;
       }
-      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, x.slot) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
+      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, x.slot) + sel2(p.tx_last, (r.flags & RF_BIG) ? 1 : 0));
       skey[cnt][tid] = (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~dt);
       sref[cnt][tid] = ((x.slot - e0) << 16) | j;
       ++cnt;
@@ -3361,7 +3369,7 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
       const Rec r = x.r;
       const Msg m = rec_msg(r);
       const int64_t t = cs + r.t_off;
-      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + p.tx_last[m.big]);
+      const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + sel2(p.tx_last, m.big));
       const uint32_t origin = AT(p.col, q, p.E);
       if (t > tmax) tmax = t;
       atomicAdd(&cs_[CNT_DELIV + r.type], 1ull);
@@ -3494,7 +3502,7 @@ __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP*
       r = ld_rec(p.inbox + inbox_idx(p, b, rep, e0 + j));
     t = cs + r.t_off;
     v = slot_live(r.flags, cell_tag(p, cell)) && t >= t_lo && t < t_hi;
-    dt = static_cast<uint32_t>(prop_of_slot(p, e0 + j) + p.tx_last[(r.flags & RF_BIG) ? 1 : 0]);
+    dt = static_cast<uint32_t>(prop_of_slot(p, e0 + j) + sel2(p.tx_last, (r.flags & RF_BIG) ? 1 : 0));
     k64 = (static_cast<uint64_t>(r.t_off) << 32) | static_cast<uint32_t>(~dt);
   }
   // key-order rank within the node's group (ties of (t, dt) by in-slot = origin order)
@@ -3637,8 +3645,8 @@ __device__ inline uint32_t q_started(const KP& p, uint64_t ent, int64_t t) {
   const int64_t s = static_cast<int64_t>(ent >> 17);
   const uint32_t big = static_cast<uint32_t>(ent >> 16) & 1u, k = static_cast<uint32_t>(ent & 0xFFFFu);
   if (t < s) return 0;
-  if (p.nfr[big] == 1) return k;
-  const int64_t j = (t - s) / p.tx_full[big] + 1;
+  if (sel2(p.nfr, big) == 1) return k;
+  const int64_t j = (t - s) / sel2(p.tx_full, big) + 1;
   return j < static_cast<int64_t>(k) ? static_cast<uint32_t>(j) : k;
 }
 // admit a message of class `big` enqueued at t that would start at `start`: pops the
@@ -3656,7 +3664,7 @@ __device__ inline uint32_t q_admit(const KP& p, uint64_t* ring, uint64_t& meta, 
     --n;
   }
   const uint32_t waiting = n ? frames - q_started(p, ring[head], t) : 0u;
-  const uint32_t F = p.nfr[big];
+  const uint32_t F = sel2(p.nfr, big);
   const uint32_t room = waiting >= p.qcap_frames ? 0u : p.qcap_frames - waiting;
   const uint32_t k = room < F ? room : F;
   if (k) {
@@ -3969,7 +3977,7 @@ __device__ inline void fq_dev_push(const KP& p, FqLink& L, const uint4& pk, int6
   const uint32_t m = pk.z & 0xFFFFu, frame = pk.z >> 16;
   const uint4 me = L.msg[m];
   const int big = (me.z >> 24) & 1;
-  const int64_t tx = frame + 1 == p.nfr[big] ? p.tx_last[big] : p.tx_full[big];
+  const int64_t tx = frame + 1 == sel2(p.nfr, big) ? sel2(p.tx_last, big) : sel2(p.tx_full, big);
   const int64_t dend = fq_ld64(L.h + FQ_DEND);
   const int64_t start = dend > now ? dend : now;
   const int64_t end = start + tx;
@@ -4048,7 +4056,7 @@ __device__ inline void fq_send(const KP& p, FqLink& L, int64_t now, uint32_t sub
     return;
   }
   L.h[FQ_MBM + (m >> 5)] |= 1u << (m & 31u);
-  const uint32_t F = p.nfr[big];
+  const uint32_t F = sel2(p.nfr, big);
   L.msg[m] = make_uint4(sub, bz, bw24 | (static_cast<uint32_t>(big) << 24) | (echo ? kFqEcho : 0u), F);
   const uint32_t now_lo = static_cast<uint32_t>(now), now_hi = static_cast<uint32_t>(static_cast<uint64_t>(now) >> 32);
   for (uint32_t j = 0; j < F; ++j) {
@@ -4598,7 +4606,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
         if (slot_live(r0.flags, cell_tag(p, cell)) && ta0 >= t_lo && ta0 < t_hi && p.echo) {
           const int bg = (r0.flags & RF_BIG) ? 1 : 0;
           const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
-          eo = raw_make(ta0, static_cast<uint32_t>(pin + p.tx_last[bg]), s, r0.sub,
+          eo = raw_make(ta0, static_cast<uint32_t>(pin + sel2(p.tx_last, bg)), s, r0.sub,
                         static_cast<uint8_t>(OP_ECHO | (bg ? (OPF_BIG << 2) : 0)));
           he = true;
           ++st_echo;
@@ -4821,7 +4829,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
         if (p.echo) {
           const int bg = (r0.flags & RF_BIG) ? 1 : 0;
           const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
-          eo = raw_make(ta0, static_cast<uint32_t>(pin + p.tx_last[bg]), s, r0.sub,
+          eo = raw_make(ta0, static_cast<uint32_t>(pin + sel2(p.tx_last, bg)), s, r0.sub,
                         static_cast<uint8_t>(OP_ECHO | (bg ? (OPF_BIG << 2) : 0)));
           he = true;
           ++st_echo;
@@ -4928,16 +4936,16 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       const int64_t ot = raw_t(o);
       const int64_t start = bu > ot ? bu : ot;
       if (QM) {  // DROPTAIL: a refused fragment loses the message (its accepted prefix still occupies the link)
-        const uint32_t F = p.nfr[big];
+        const uint32_t F = sel2(p.nfr, big);
         const uint32_t k = q_admit(p, qr, qm, ot, big, start);
         if (k < F) {
           fdrop += F - k;
-          if (k) bu = start + static_cast<int64_t>(k) * p.tx_full[big];
+          if (k) bu = start + static_cast<int64_t>(k) * sel2(p.tx_full, big);
           if (!is_echo) ++lost;
           continue;
         }
       }
-      const int64_t end = start + p.tx_tot[big];
+      const int64_t end = start + sel2(p.tx_tot, big);
       bu = end;
       if (is_echo) continue;
       const int64_t ta = end + pr;
@@ -5223,7 +5231,7 @@ __device__ inline void mesh_desc_flush(const KP& p, MeshDesc& D, uint32_t g, uin
       bool any = false;
       for (uint32_t d = 0; d < ne; ++d)
         if (desc_bit(D.eb[d], le)) {
-          bu = (bu > D.et[d] ? bu : D.et[d]) + p.tx_tot[D.ebig[d] ? 1 : 0];
+          bu = (bu > D.et[d] ? bu : D.et[d]) + sel2(p.tx_tot, D.ebig[d] != 0);
           any = true;
         }
       if (any) {
@@ -5443,7 +5451,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
               bu = static_cast<int64_t>(lw >> 16);
               any = true;
             }
-            bu = (bu > D.et[d] ? bu : D.et[d]) + p.tx_tot[D.ebig[d] ? 1 : 0];
+            bu = (bu > D.et[d] ? bu : D.et[d]) + sel2(p.tx_tot, D.ebig[d] != 0);
           }
         if (any) {
           if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
@@ -5511,7 +5519,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
             ebig = (fl & RF_BIG) ? 1 : 0;
             const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
             et = ta0;
-            edt = static_cast<uint32_t>(pin + p.tx_last[ebig]);
+            edt = static_cast<uint32_t>(pin + sel2(p.tx_last, ebig));
             esub = r0[u].y;
             he = true;
             ++st_echo;
@@ -5590,7 +5598,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
           he = false;
         if (src == 2 || src == 4) ++sends;
         const int64_t start = bu > ot ? bu : ot;
-        const int64_t end = start + p.tx_tot[big];
+        const int64_t end = start + sel2(p.tx_tot, big);
         bu = end;
         if (src == 3) continue;  // the echo only occupies the link
         const int64_t ta = end + pr;
@@ -6614,7 +6622,7 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
         if (p.echo) {
           const int bg = (r0.flags & RF_BIG) ? 1 : 0;
           const int64_t pin = p.prop_const >= 0 ? p.prop_const : AT(p.prop_in, e, p.E);
-          eo = raw_make(ta0, static_cast<uint32_t>(pin + p.tx_last[bg]), sp, r0.sub,
+          eo = raw_make(ta0, static_cast<uint32_t>(pin + sel2(p.tx_last, bg)), sp, r0.sub,
                         static_cast<uint8_t>(OP_ECHO | (bg ? (OPF_BIG << 2) : 0)));
           he = true;
           ++c_echo;
@@ -6651,7 +6659,7 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
         const int big = (raw_flags(x) & OPF_BIG) ? 1 : 0;
         const int64_t ot = raw_t(x);
         const int64_t start = bu > ot ? bu : ot;
-        bu = start + p.tx_tot[big];
+        bu = start + sel2(p.tx_tot, big);
         if (src == 3) continue;  // echo: link occupancy only
         const int64_t ta = bu + pr;
         const long long ca = ta / p.L;
@@ -7029,16 +7037,16 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
         const int64_t ot = raw_t(o);
         const int64_t start = bu > ot ? bu : ot;
         if (p.qmodel) {
-          const uint32_t F = p.nfr[big];
+          const uint32_t F = sel2(p.nfr, big);
           const uint32_t k = q_admit(p, qr, qm, ot, big, start);
           if (k < F) {
             fdrop += F - k;
-            if (k) bu = start + static_cast<int64_t>(k) * p.tx_full[big];
+            if (k) bu = start + static_cast<int64_t>(k) * sel2(p.tx_full, big);
             if (!is_echo) ++lost;
             continue;
           }
         }
-        const int64_t end = start + p.tx_tot[big];
+        const int64_t end = start + sel2(p.tx_tot, big);
         bu = end;
         if (is_echo) {
           ++st_echo;
@@ -7282,7 +7290,7 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
         const int big = (raw_flags(o) & OPF_BIG) ? 1 : 0;
         const int64_t ot = raw_t(o);
         const int64_t start = bu > ot ? bu : ot;
-        bu = start + p.tx_tot[big];
+        bu = start + sel2(p.tx_tot, big);
         if (kind == OP_ECHO) {
           ++c_echo;
           continue;

@@ -13,5 +13,5 @@ step bench_gossip 240 python bench.py --workload gossip
 step bench_gossip_pdes1 240 python bench.py --workload gossip --pdes1 --no-cpu-baseline
 step bench_paxos 400 python bench.py --workload paxos
 step bench_pbft_jitter 300 python bench.py --jitter
-step bench_pbft_fq 600 python bench.py --queue fqcodel --cpu-budget 10
+step bench_pbft_fq 600 python bench.py --queue fqcodel --steps 3 --warmup 4 --cpu-budget 10
 bash tests/gpu_prof.sh r04bench/prof --steps 20 --warmup 5 --no-cpu-baseline > $out/prof.log 2>&1; rc=$?; tail -3 $out/prof.log; exit $rc
