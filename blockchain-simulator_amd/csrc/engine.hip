@@ -7435,14 +7435,23 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
   if (tid < 2) s_n[tid] = 0;
   __syncthreads();
   uint32_t ns = 0, nl = 0;
+  const long long bm = p.bmin[b];
+  uint8_t* const sfa = p.eslot ? p.sflag : reinterpret_cast<uint8_t*>(p.act_n);  // (a dummy word without slots)
   for (uint32_t j = tid; j < cn; j += blockDim.x) {
-    const uint64_t k = c0 + j;
-    const uint32_t g = static_cast<uint32_t>((k / p.nloc) * p.N + p.nlo + k % p.nloc);
+    // (gnode numbers are < 2^32: 32-bit index arithmetic; the node's words all loaded before any
+    // is used -- a short-circuit chain of them was one round trip each)
+    const uint32_t k = static_cast<uint32_t>(c0 + j);
+    const uint32_t g = (k / p.nloc) * p.N + p.nlo + k % p.nloc;
     const uint32_t rep = g / p.N, i = g % p.N;
-    const bool sc = has_start || has_stop || node_flagged_w(p, b, g, rep, i, t_hi) || AT(p.node_tnext, g, p.NT) < t_hi;
+    const uint8_t f8 = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
+    const uint8_t t8 = p.mesh ? AT(p.rtile, (static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6),
+                                   static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles)
+                              : static_cast<uint8_t>(0);
+    const long long tn = AT(p.node_tnext, g, p.NT), on = AT(p.node_onext, g, p.NT);
+    const uint8_t sfb = gbl(sfa)[p.eslot ? static_cast<size_t>(obp) * p.NT + g : 0u];
+    const bool sc = has_start || has_stop || ((f8 | t8) != 0 && bm < t_hi) || tn < t_hi;  // (node_flagged_w)
     // k_link also runs nodes with reply-slot ops of the previous arrival cell due
-    const bool lk = sc || AT(p.node_onext, g, p.NT) < t_hi ||
-                    (p.eslot && (AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, static_cast<uint64_t>(kOpRing) * p.NT) & (2u | kSfD1)));
+    const bool lk = sc || on < t_hi || (p.eslot && (sfb & (2u | kSfD1)));
     fl[j] = static_cast<uint8_t>((sc ? 1u : 0u) | (lk ? 2u : 0u));
     ns += sc ? 1u : 0u;
     nl += lk ? 1u : 0u;
@@ -7464,8 +7473,8 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
   for (uint32_t j0 = 0; j0 < cn; j0 += blockDim.x) {  // uniform
     const uint32_t j = j0 + tid;
     const uint32_t f = j < cn ? fl[j] : 0u;
-    const uint64_t k = c0 + j;
-    const uint32_t g = j < cn ? static_cast<uint32_t>((k / p.nloc) * p.N + p.nlo + k % p.nloc) : 0u;
+    const uint32_t k = static_cast<uint32_t>(c0 + j);
+    const uint32_t g = j < cn ? (k / p.nloc) * p.N + p.nlo + k % p.nloc : 0u;
     uint32_t ts, tl;
     const uint32_t rs = block_rank((f & 1u) != 0, wcnt, ts);
     if (f & 1u) p.act[ps + rs] = g;
