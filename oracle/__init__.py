@@ -29,7 +29,9 @@ def build(force=False):
 def lib():
     global _LIB
     if _LIB is None:
-        _LIB = C.CDLL(build())
+        # BCSIM_ORACLE_LIB: another build of the same source (the ASan/UBSan one of `make asan`,
+        # loaded by tests/test_oracle_asan.py in a child process with the sanitizer runtime)
+        _LIB = C.CDLL(os.environ.get("BCSIM_ORACLE_LIB") or build())
         _abi.declare(_LIB, "bcsim_oracle_")
         _LIB.oracle_glibc_rand_seq.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_int32)]
         _LIB.oracle_glibc_rand_seq.restype = None

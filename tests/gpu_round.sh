@@ -14,12 +14,15 @@ step() {
   echo "== $name rc=$rc"; tail -2 $out/$name.log | cut -c1-300
   [ $rc -eq 0 ] || exit 1
 }
-step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+(while sleep 50; do date +%s >> $out/heartbeat; done) & hb=$!
+trap "kill $hb 2>/dev/null" EXIT
+step pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread
 step bench_pbft 240 python bench.py --steps 20 --warmup 5
 step bench_gossip 240 python bench.py --workload gossip
 step bench_gossip_pdes1 240 python bench.py --workload gossip --pdes1 --no-cpu-baseline
 step bench_paxos 300 python bench.py --workload paxos
 step bench_pbft_jitter 240 python bench.py --jitter
+step bench_pbft_fq 600 python bench.py --queue fqcodel --steps 3 --warmup 4 --cpu-budget 10
 [ "$2" = "noprof" ] && exit 0
-bash tests/gpu_prof.sh $tag/prof > $out/prof.log 2>&1 || { tail -5 $out/prof.log; exit 1; }
+bash tests/gpu_prof.sh $tag/prof --steps 20 --warmup 5 --no-cpu-baseline > $out/prof.log 2>&1 || { tail -5 $out/prof.log; exit 1; }
 tail -3 $out/prof.log
