@@ -1942,7 +1942,9 @@ static int run(Sim& s, int64_t t_until) {
     }
     if (!lrc && s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC)
       lrc = launch(s, KS_AUX, k_draws, dim3(1), dim3(64), 0, s.kp_dev, 0u);
-    const uint32_t nbn = static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
+    // (one workgroup up to 4096 gnodes -- no cross-workgroup combine; above, 2048 per workgroup:
+    // for gossip n=65536 the wider grid measured faster than four gnodes per lane)
+    const uint32_t nbn = s.NT <= 4096u ? 1u : static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
     // (a finished cell's bucket is free again: k_next clears its counts and tile flags)
     const uint32_t clr_b = hi == ce ? static_cast<uint32_t>(c % s.B) : 0xFFFFFFFFu;
     if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b, ++s.mseq);

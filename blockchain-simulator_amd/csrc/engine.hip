@@ -7894,8 +7894,24 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
   // wave minima by shuffles, one LDS slot per wave, one barrier
   __shared__ long long red[kMaxWaves], redt[kMaxWaves];
   long long m = LLONG_MAX, mt = LLONG_MAX;
-  const uint32_t nb = gridDim.x;
-  for (uint32_t k = blockIdx.x * blockDim.x + tidx(); k < p.NT; k += nb * blockDim.x) {
+  const uint32_t nb = gridDim.x, stride = nb * blockDim.x;
+  uint32_t k = blockIdx.x * blockDim.x + tidx();
+  // four gnodes per lane per step, their eight loads issued before any is used (PBFT n=4096:
+  // one workgroup, no cross-workgroup combine)
+  for (; k + 3u * stride < p.NT; k += 4u * stride) {
+    long long a[4], bb[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      a[u] = AT(p.node_tnext, k + u * stride, p.NT);
+      bb[u] = AT(p.node_onext, k + u * stride, p.NT);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      m = min(m, min(a[u], bb[u]));
+      mt = min(mt, a[u]);
+    }
+  }
+  for (; k < p.NT; k += stride) {
     const long long a = AT(p.node_tnext, k, p.NT), b = AT(p.node_onext, k, p.NT);
     m = min(m, min(a, b));
     mt = min(mt, a);
