@@ -7662,12 +7662,26 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
     n_ticked = 0;
   }
   __syncthreads();
-  for (uint32_t i = tid; i < N; i += blockDim.x) {
-    const uint32_t g = rep * N + i;
-    if (p.nranks > 1)
-      lead[i] = p.lead_all[g];
-    else
-      lead[i] = (AT(p.tick_alive, g, p.NT) && AT(p.leader, g, p.NT) == static_cast<int32_t>(i)) ? 1 : 0;
+  if (p.nranks > 1) {
+    for (uint32_t i = tid; i < N; i += blockDim.x) lead[i] = p.lead_all[rep * N + i];
+  } else {
+    // four nodes per lane, both words of each loaded before any is used (a short-circuit
+    // `alive && leader == i` was two round trips per node)
+    for (uint32_t i0 = 0; i0 < N; i0 += 4u * blockDim.x) {
+      uint8_t ta[4];
+      int32_t ld[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t g = rep * N + min(i0 + u * blockDim.x + tid, N - 1u);
+        ta[u] = AT(p.tick_alive, g, p.NT);
+        ld[u] = AT(p.leader, g, p.NT);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t i = i0 + u * blockDim.x + tid;
+        if (i < N) lead[i] = (ta[u] && ld[u] == static_cast<int32_t>(i)) ? 1 : 0;
+      }
+    }
   }
   __syncthreads();
   // leaders, serially in node order (rare: normally exactly one); a wave
