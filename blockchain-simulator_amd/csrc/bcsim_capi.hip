@@ -95,6 +95,8 @@ struct Sim {
   KP* kp_dev2 = nullptr;
   bool gossip_frontier = true;  // dense gossip: k_gossip_cell over the window's frontier (BCSIM_GOSSIP_FRONTIER=0: all)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
+  bool sum = false;        // heavy-wave record summaries (BCSIM_SUM=0: off)
+  uint32_t rt_min = 0;     // summary mode: k_scan_rt takes windows of at least this many scanned nodes (BCSIM_RT_MIN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
   uint32_t* seg_part = nullptr;  // multi-block segment scan partials
@@ -769,6 +771,19 @@ static int setup_device(Sim& s) {
     }
     if ((rc = dalloc(s, &p.l2mark, s.l2_overlap ? NT : 1))) return rc;
     HIPCHK(hipMemset(p.l2mark, 0, (s.l2_overlap ? NT : 1) * 4));
+    // heavy-wave record summaries: the tiled link stage writes them, k_scan_rt
+    // reads them (BCSIM_SUM=0: off); 33 B per (bucket, receiver tile, sender) within 8 GB
+    {
+      const char* sm = std::getenv("BCSIM_SUM");
+      const size_t nsum = static_cast<size_t>(s.B) * s.R * p.n_tiles * s.N;
+      s.sum = s.mesh_tile && s.scan_fast && p.desc && s.P == 1 && c.protocol == BCSIM_PBFT && p.prop_const >= 0 &&
+              nsum * 33 <= (8ull << 30) && !(sm && *sm == '0');
+      p.sum = s.sum ? 1u : 0u;
+      if ((rc = dalloc(s, &p.msum, s.sum ? nsum * 2 : 1)) || (rc = dalloc(s, &p.xsum, s.sum ? nsum : 1))) return rc;
+      HIPCHK(hipMemset(p.msum, 0, (s.sum ? nsum * 2 : 1) * 16));
+      HIPCHK(hipMemset(p.xsum, 0, s.sum ? nsum : 1));
+      if (const char* rm = std::getenv("BCSIM_RT_MIN"); rm && *rm) s.rt_min = static_cast<uint32_t>(std::atoi(rm));
+    }
     p.loop_list = 3;
   }
   const size_t n_link = p.hubs ? static_cast<size_t>(s.R) * (static_cast<size_t>(p.hubs) * (s.N - 1) +
@@ -1250,8 +1265,36 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
 #define BCSIM_SCAN(P)                                                                                   \
   (s.sparse ? launch(s, KS_SCAN, k_scan<P, true>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa) \
             : launch(s, KS_SCAN, k_scan<P, false>, grid, block, lds, s.kp_dev, cell, lo, hi, cs, fw, xa))
+  // summary mode: the scan reads the summaries itself (k_scan_rt), or the rows
+  // of the window's nodes are materialised for the kernels that read slots only
+  const dim3 grid_rt(s.R * s.kp.n_tiles);
+  const bool ss_win = (lo <= 0 && 0 < hi) || (s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi);
+  const bool use_rt = s.sum && grid.x && s.scan_fast && !ss_win && !(s.kp_dev_big && grid.x <= s.few_scan) &&
+                      grid.x >= s.rt_min;
+  if (s.sum && grid.x && !use_rt &&
+      (rc = launch(s, KS_SCAN, k_scan_rt, grid_rt, dim3(1024), 0, s.kp_dev, cell, lo, hi, cs, xa, 0u, 1)))
+    return rc;
   if (grid.x == 0)
     rc = BCSIM_OK;  // no node has work in the window
+  else if (use_rt) {
+    // the scan of every receiver tile; the nodes it leaves (list 2, materialised) to the generic
+    // kernel as after k_scan_pbft
+    const uint32_t wep = s.l2_overlap ? (++s.win_epoch == 0 ? ++s.win_epoch : s.win_epoch) : 0u;
+    rc = launch(s, KS_SCAN, k_scan_rt, grid_rt, dim3(1024), 0, s.kp_dev, cell, lo, hi, cs, xa, wep, 0);
+    if (!rc && wep) {
+      HIPCHK(hipEventRecord(s.ev_fork, s.stream));
+      HIPCHK(hipStreamWaitEvent(s.stream2, s.ev_fork, 0));
+      std::swap(s.stream, s.stream2);
+      s.l2_pending = wep;
+    }
+    if (!rc)
+      rc = s.kp_dev_big
+               ? launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false, true>), dim3(std::min<uint32_t>(grid.x, kLoopGrid)), dim3(1024),
+                        s.lds_big, s.kp_dev_big, cell, lo, hi, cs, fw, xa)
+               : launch(s, KS_SCAN, (k_scan<BCSIM_PBFT, false, true>), dim3(std::min<uint32_t>(grid.x, 512)), block, lds,
+                        s.kp_dev, cell, lo, hi, cs, fw, xa);
+    if (wep) std::swap(s.stream, s.stream2);
+  }
   else if (s.kp_dev_big && !s.sparse && s.P == 1 && grid.x <= s.few_scan) {
     // a few nodes (the leader's cells): the doubled staging window, a 1024-lane workgroup each.
     // With the list-2 overlap they are scanned and linked on the second stream, beside the
@@ -1785,6 +1828,14 @@ static int zero_tag_buckets(Sim& s, long long a, long long b) {
         int rc = launch(s, KS_AUX, k_zero16, dim3(nb), dim3(256), 0, reinterpret_cast<uint4*>(s.kp.inbox + static_cast<size_t>(k) * per),
                         n16);
         if (rc) return rc;
+      }
+      if (s.sum) {  // the bucket's summary entries and explicit-slot bytes carry the same tags
+        const size_t ns = static_cast<size_t>(s.R) * s.kp.n_tiles * s.N;
+        const uint32_t nb = static_cast<uint32_t>(std::min<uint64_t>(8192, (ns * 2 + 255) / 256));
+        int rc = launch(s, KS_AUX, k_zero16, dim3(nb), dim3(256), 0, s.kp.msum + static_cast<size_t>(k) * ns * 2,
+                        static_cast<uint64_t>(ns * 2));
+        if (rc) return rc;
+        HIPCHK(hipMemsetAsync(s.kp.xsum + static_cast<size_t>(k) * ns, 0, ns, s.stream));
       }
       ++s.tag_zeroes;
       // the latest turn of bucket k in [a, b]

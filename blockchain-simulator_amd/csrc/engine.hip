@@ -157,6 +157,17 @@ struct KP {
   GP(uint2) mte;             // [NT][n_tiles][kEDesc] pending echo bitmaps per receiver tile
   GP(uint32_t) mtile;        // [R][n_stiles]
   uint32_t n_stiles;
+  // heavy-wave record summaries (one rank, full mesh, PBFT fast paths): the
+  // slot records ONE sender writes to a 64-receiver tile in one bucket that differ only in the
+  // schedule counter (sub = base + the sender's out-edge index, pbft-node.cc:360-367 fan-out)
+  // are written by k_mesh_tile as one entry {mask lo, mask hi, t_off, base}{f0 | f1 << 16,
+  // f2 | type << 16 | flags << 24, 0, 0} (live: the flags' ring-turn tag, a nonzero mask) instead
+  // of up to 64 16-byte records; k_scan_rt reads a receiver tile's entries of all senders, and a
+  // row leaving the fast kernels is materialised first.  Every other slot record is physical,
+  // and the byte xsum = 0x80 | its tag tells the readers to load the (tile, sender)'s slots.
+  uint32_t sum;
+  GP(uint4) msum;            // [B][R][n_tiles][N][2]
+  GP(uint8_t) xsum;          // [B][R][n_tiles][N]
   // list-2 overlap: k_scan_pbft stamps the nodes it leaves to the generic kernels
   // with the window's epoch; their scan and link stage run on a second stream beside the other
   // nodes' link stage, which skips them.  loop_list: the list k_link<.., LOOP> walks (3; 2 in
@@ -753,6 +764,15 @@ __device__ inline uint32_t cell_tag(const KP& p, long long cell) {
 __device__ inline bool slot_live(uint32_t flags, uint32_t tag) {
   return (flags & RF_VALID) && ((flags >> 3) & 31u) == tag;
 }
+// summary entry / explicit-slot byte of (bucket b, replica rep, receiver tile rt, sender s):
+// receiver-tile-major, so that a receiver tile's entries of consecutive senders are contiguous
+__device__ inline size_t sum_idx(const KP& p, uint32_t b, uint32_t rep, uint32_t rt, uint32_t s) {
+  return ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + rt) * p.N + s;
+}
+// a physical slot record of edge s -> d (record word w3: its ring-turn tag) in bucket b
+__device__ inline void xs_mark(const KP& p, uint32_t b, uint32_t rep, uint32_t s, uint32_t d, uint32_t w3) {
+  if (p.sum) gbl(p.xsum)[sum_idx(p, b, rep, d >> 6, s)] = static_cast<uint8_t>(0x80u | (w3 >> 27));
+}
 // the tag of a record emitted in cell `cell` for cell + rel (1 <= rel < B), without a division:
 // cq = cell / B, cr = cell % B
 __device__ inline uint32_t emit_tag(long long cq, uint32_t cr, long long rel, uint32_t B) {
@@ -1145,6 +1165,10 @@ __device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long lon
     x.r.flags = static_cast<uint8_t>((x.r.flags & (RF_VALID | RF_BIG)) | (cell_tag(p, o.cell) << 3));
     if (owner) {
       st_rec(&AT(p.inbox, inbox_idx(p, b, rep, x.slot), p.cap_inbox), x.r);
+      if (p.sum) {  // (summaries: full mesh, in-slot k of receiver d holds sender k < d ? k : k + 1)
+        const uint32_t d = x.g % p.N, k = x.slot - d * (p.N - 1);
+        xs_mark(p, b, rep, k < d ? k : k + 1, d, static_cast<uint32_t>(x.r.flags) << 24);
+      }
     } else {
       const uint32_t pos = list_append(&p.x_cnt[b]);
       if (pos >= p.cap_x) {
@@ -3286,6 +3310,432 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(BCSIM_SCANP
 }
 
 // ---------------------------------------------------------------------------
+// k_scan_rt (summary mode): the PBFT scan of a window, one workgroup per
+// 64-receiver tile (lane = receiver d), its 16 waves over the senders in chunks of 64.  A chunk
+// is two coalesced loads of the tile's summary entries (lane = sender) and the explicit-slot
+// bytes; a 64 x 64 bit transpose turns the senders' receiver masks into each receiver's
+// arrival bits, and the senders whose slots are explicit are loaded per receiver.  A receiver
+// whose window holds arrivals of ONE message (type, payload) at ONE instant -- the heavy waves:
+// PRE_PREPARE, the PREPAREs, the PREPARE_RES replies of one sequence, the COMMITs of one
+// sequence -- is handled here with the same state changes and outputs as k_scan_pbft
+// (pbft-node.cc:193-265): its quorum crossings are the ranks where the stored vote count plus
+// the rank reaches a multiple of the threshold, so only a COMMIT crossing needs its sender
+// (commit trace key).  Any other receiver with work is materialised (its summary records
+// written as slot records, their mask bits cleared) and goes to list 2 for the generic kernel,
+// as do receivers whose echoes the link stage must do from the row.  mode 1: materialise
+// every receiver with work, nothing else (before a generic scan of list 0).
+constexpr uint32_t kRtWaves = 16, kRtWords = 8;  // N <= 4096: four 64-sender chunks per wave
+struct RtShared {
+  uint32_t bits[kRtWaves][kRtWords][64];  // per wave: the receiver's arrival bits of its senders
+  uint32_t cnt[kRtWaves][64];
+  uint32_t ftof[kRtWaves][64], fw2[kRtWaves][64], fw3[kRtWaves][64];  // the first arrival's words
+  uint32_t fl[kRtWaves][64];  // bit 0: has arrivals, bit 1: not one message / instant
+  uint32_t st[64];            // receiver status (below)
+  uint32_t ne[64];            // pending echo descriptors (the ebits row it writes)
+  unsigned long long any, mat;
+  uint32_t tcount[4];  // deliveries: PRE_PREPARE, PREPARE, COMMIT, PREPARE_RES
+  uint32_t echo, l2;
+  long long tlast;
+};
+enum : uint32_t { kRtWork = 1u, kRtFast = 2u, kRtEchoHere = 4u, kRtEchoDesc = 8u, kRtMat = 16u, kRtGen = 32u,
+                  kRtRbits = 64u, kRtEbits = 128u };
+
+// lane k holds row k (bit j: column j) of a 64 x 64 bit matrix; returns column `lane` (bit k: row k's bit lane)
+__device__ inline unsigned long long transpose64(unsigned long long x, uint32_t lane) {
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const uint32_t sh = 32u >> st;
+    const unsigned long long m = st == 0 ? 0x00000000FFFFFFFFull
+                                 : st == 1 ? 0x0000FFFF0000FFFFull
+                                 : st == 2 ? 0x00FF00FF00FF00FFull
+                                 : st == 3 ? 0x0F0F0F0F0F0F0F0Full
+                                 : st == 4 ? 0x3333333333333333ull
+                                           : 0x5555555555555555ull;
+    const unsigned long long o = static_cast<unsigned long long>(__shfl_xor(x, static_cast<int>(sh), 64));
+    x = (lane & sh) ? ((x & ~m) | ((o & ~m) >> sh)) : ((x & m) | ((o & m) << sh));
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_rt(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
+                                                  long long cs, int x_active, uint32_t wep, int mode) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ RtShared S;
+  const uint32_t N = p.N, nrt = p.n_tiles;
+  const uint32_t rep = blockIdx.x / nrt, rt = blockIdx.x % nrt;
+  const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6;
+  const uint32_t d = rt * 64u + lane;
+  const bool dv = d < N;
+  const uint32_t g = rep * N + (dv ? d : 0u);
+  const uint32_t B = p.n_buckets, b = static_cast<uint32_t>(cell % B), tag = cell_tag(p, cell);
+  const uint32_t ob = static_cast<uint32_t>(cell % kOpRing), obp = static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing);
+  const size_t R4 = static_cast<uint64_t>(kOpRing) * p.NT;
+  // ---- wave 0: the receivers' k_scan_pbft checks ----
+  if (wv == 0) {
+    uint32_t st = 0;
+    if (dv) {
+      const bool flag = node_flagged_w(p, b, g, rep, d, t_hi);
+      const bool has_ss = (t_lo <= 0 && 0 < t_hi) || (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
+      const bool timer = AT(p.node_tnext, g, p.NT) < t_hi;
+      const uint32_t xn = x_active ? AT(p.seg_off, g + 1, p.NT + 1) - AT(p.seg_off, g, p.NT + 1) : 0u;
+      const long long onext0 = AT(p.node_onext, g, p.NT);
+      const uint8_t sfv0 = AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4);
+      const uint8_t sfv1 = AT(p.sflag, static_cast<size_t>(obp) * p.NT + g, R4);
+      const uint32_t ne0 = AT(p.en, g, p.NT);
+      if (flag || has_ss || timer) {
+        st = kRtWork;
+        if (mode || !flag || has_ss || timer || xn || N - 1 > p.cap_arr) {
+          st |= kRtGen | kRtMat;
+        } else {
+          st |= kRtFast;
+          // the echo rule of k_scan_pbft: no op of the node due in the window but the ones this
+          // scan creates (those follow the echoes in key order)
+          if (p.echo && p.qmodel == 0 && onext0 >= t_hi && !(sfv0 & (1u | kSfD0)) && !(sfv1 & (2u | kSfD1)))
+            st |= kRtEchoHere | (ne0 < kEDesc ? kRtEchoDesc : 0u);
+        }
+      }
+      S.ne[lane] = ne0;
+    }
+    S.st[lane] = st;
+    const unsigned long long any = __ballot(st != 0);
+    if (lane == 0) {
+      S.any = any;
+      S.mat = 0ull;
+      S.echo = 0u;
+      S.l2 = 0u;
+      S.tlast = LLONG_MIN;
+    }
+    if (lane < 4) S.tcount[lane] = 0u;
+  }
+  __syncthreads();
+  if (!S.any) return;  // (uniform) no receiver of the tile has work
+  const uint32_t nch = (N + 63u) / 64u, cpw = (nch + kRtWaves - 1u) / kRtWaves;
+  // ---- all waves: each receiver's arrival bits and message words over this wave's senders ----
+  if (!mode) {
+    uint32_t cnt = 0, r_tof = 0, r_w2 = 0, r_w3 = 0;
+    bool have = false, bad = false;
+    auto take = [&](uint32_t tof, uint32_t w2, uint32_t w3) {
+      if (!have) {
+        have = true;
+        r_tof = tof;
+        r_w2 = w2;
+        r_w3 = w3;
+      } else if (tof != r_tof || w2 != r_w2 || w3 != r_w3) {
+        bad = true;
+      }
+    };
+    for (uint32_t c = 0; c < cpw; ++c) {
+      const uint32_t ch = wv * cpw + c;
+      unsigned long long col = 0ull;
+      if (ch < nch) {  // (uniform)
+        const uint32_t sb = ch * 64u + lane;  // this lane loads sender sb's entry
+        const bool sv = sb < N;
+        const size_t si = sum_idx(p, b, rep, rt, sv ? sb : 0u);
+        const uint4 ea = sv ? gld4(p.msum + si * 2) : make_uint4(0, 0, 0, 0);
+        const uint4 eb = sv ? gld4(p.msum + si * 2 + 1) : make_uint4(0, 0, 0, 0);
+        const uint32_t xf = sv ? gbl(p.xsum)[si] : 0u;
+        const long long ts = cs + static_cast<long long>(ea.z);
+        const bool vs = (ea.x | ea.y) != 0u && slot_live(eb.y >> 24, tag) && ts >= t_lo && ts < t_hi;
+        const unsigned long long vm = __ballot(vs);
+        if (vm) {
+          // one message over the chunk's entries of the window, or its receivers take the generic path
+          const int rl = __ffsll(static_cast<long long>(vm)) - 1;
+          const uint32_t c_tof = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ea.z), rl));
+          const uint32_t c_w2 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(eb.x), rl));
+          const uint32_t c_w3 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(eb.y), rl));
+          const bool mixed = __ballot(vs && (ea.z != c_tof || eb.x != c_w2 || eb.y != c_w3)) != 0ull;
+          col = transpose64(vs ? ((static_cast<unsigned long long>(ea.y) << 32) | ea.x) : 0ull, lane);
+          if (col) {
+            if (mixed) bad = true;
+            take(c_tof, c_w2, c_w3);
+          }
+        }
+        // the senders with explicit slot records for this tile: this receiver's slot of each
+        unsigned long long xm = __ballot(sv && xf == (0x80u | tag));
+        while (xm) {  // (uniform) four loads at a time
+          int kx[4];
+          uint4 rx[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            kx[u] = xm ? __ffsll(static_cast<long long>(xm)) - 1 : -1;
+            if (xm) xm &= xm - 1ull;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t s = ch * 64u + static_cast<uint32_t>(kx[u] < 0 ? 0 : kx[u]);
+            const bool ld = kx[u] >= 0 && dv && s != d;
+            rx[u] = ld ? gld4(p.inbox + inbox_idx(p, b, rep, d * (N - 1) + (s < d ? s : s - 1))) : make_uint4(0, 0, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (kx[u] < 0) continue;
+            const uint4 r = rx[u];
+            const long long ta = cs + static_cast<long long>(r.x);
+            if (slot_live(r.w >> 24, tag) && ta >= t_lo && ta < t_hi) {
+              const unsigned long long bit = 1ull << kx[u];
+              if (col & bit) bad = true;  // (a summary record and a slot record of one edge: cannot happen)
+              col |= bit;
+              take(r.x, r.z, r.w);
+            }
+          }
+        }
+      }
+      S.bits[wv][2 * c][lane] = static_cast<uint32_t>(col);
+      S.bits[wv][2 * c + 1][lane] = static_cast<uint32_t>(col >> 32);
+      cnt += static_cast<uint32_t>(__popcll(col));
+    }
+    for (uint32_t j = 2 * cpw; j < kRtWords; ++j) S.bits[wv][j][lane] = 0u;
+    S.cnt[wv][lane] = cnt;
+    S.ftof[wv][lane] = r_tof;
+    S.fw2[wv][lane] = r_w2;
+    S.fw3[wv][lane] = r_w3;
+    S.fl[wv][lane] = (have ? 1u : 0u) | (bad ? 2u : 0u);
+  }
+  __syncthreads();
+  // ---- wave 0: per receiver, one message at one instant -> k_scan_pbft's outputs ----
+  if (wv == 0) {
+    uint32_t st = S.st[lane];
+    uint32_t n = 0, tof = 0, w2 = 0, w3 = 0;
+    bool have = false, bad = false;
+    if (!mode && (st & kRtFast)) {
+      for (uint32_t w = 0; w < kRtWaves; ++w) {
+        const uint32_t f = S.fl[w][lane];
+        n += S.cnt[w][lane];
+        bad = bad || (f & 2u);
+        if (f & 1u) {
+          const uint32_t a = S.ftof[w][lane], bw = S.fw2[w][lane], cw = S.fw3[w][lane];
+          if (!have) {
+            have = true;
+            tof = a;
+            w2 = bw;
+            w3 = cw;
+          } else if (a != tof || bw != w2 || cw != w3) {
+            bad = true;
+          }
+        }
+      }
+    }
+    const uint4 r = make_uint4(tof, 0u, w2, w3);  // (the message's record words)
+    const uint32_t type = fr_type(r);
+    const int32_t idx = c2i(fr_m2(r));
+    const bool inr = idx >= 0 && static_cast<uint32_t>(idx) < p.pbft_seq_cap;
+    const size_t base = static_cast<size_t>(g) * p.pbft_seq_cap;
+    if ((st & kRtFast) && n) {
+      bool ok = !bad && inr;
+      if (type == PB_PRE_PREPARE)
+        ok = ok && n == 1;
+      else if (type == PB_PREPARE_RES)
+        ok = ok && c2i(fr_m3(r)) == 0;
+      else if (type != PB_PREPARE && type != PB_COMMIT)
+        ok = false;  // VIEW_CHANGE / "Wrong msg": the generic path
+      if (ok && type == PB_PREPARE) {  // the replies as one descriptor: the arrival cell's must be free
+        ok = !(AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) & kSfD);
+        if (!ok) {
+          const uint4 od = gld4(p.rdesc + static_cast<size_t>(ob) * p.NT + g);
+          ok = static_cast<long long>((static_cast<uint64_t>(od.y) << 32) | od.x) < t_lo;
+        }
+      }
+      if (!ok) st = (st & ~kRtFast) | kRtGen | kRtMat;
+    }
+    if ((st & kRtFast) && n) {
+      const int64_t t = cs + static_cast<int64_t>(tof);
+      const int big = ((w3 >> 24) & RF_BIG) ? 1 : 0;
+      const uint32_t dt = static_cast<uint32_t>(p.prop_const + (big ? p.tx_last[1] : p.tx_last[0]));
+      const int64_t tk0 = ((t_lo + p.pbft_period - 1) / p.pbft_period) * p.pbft_period;
+      if (t >= tk0 && (t == tk0 || (t - tk0) % p.pbft_period == 0) && t - static_cast<int64_t>(dt) <= t - p.pbft_period)
+        set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
+      const uint32_t deg = N - 1;
+      const int32_t NN = static_cast<int32_t>(N);
+      const uint32_t T1 = static_cast<uint32_t>(NN / 2), T2 = T1 + 1;
+      const uint32_t sub0 = AT(p.sub, g, p.NT), nops0 = AT(p.n_ops, g, p.NT);
+      const int32_t bn0 = AT(p.block_num, g, p.NT);
+      const int64_t app = p.app_delay;
+      const int32_t m1 = fr_f0(r), m2 = fr_m2(r);
+      Op* ops = p.ops + op_base(p, g);
+      uint32_t nd = 0, np = 0, nc = 0;  // broadcasts (PRE_PREPARE, crossing PREPARE_RES), PREPAREs, commits
+      if (type == PB_PRE_PREPARE) {  // :193-211
+        nd = 1;
+      } else if (type == PB_PREPARE) {  // :212-222
+        np = n;
+      } else if (type == PB_PREPARE_RES) {  // :223-240
+        const uint32_t c0 = static_cast<uint32_t>(AT(p.tx_pv, base + idx, p.cap_txn));
+        nd = (c0 + n) / T1;
+        AT(p.tx_pv, base + idx, p.cap_txn) = static_cast<int32_t>((c0 + n) % T1);
+      } else {  // PB_COMMIT :241-265
+        const uint32_t c0 = static_cast<uint32_t>(AT(p.tx_cv, base + idx, p.cap_txn));
+        nc = (c0 + n) / T2;
+        AT(p.tx_cv, base + idx, p.cap_txn) = static_cast<int32_t>((c0 + n) % T2);
+        if (nc) {
+          const int32_t val = AT(p.tx_val, base + idx, p.cap_txn);
+          for (uint32_t j = 0; j < nc; ++j) {
+            // the crossing arrival: rank (j + 1) T2 - c0 - 1 among the window's, in sender order
+            uint32_t rk = (j + 1) * T2 - c0 - 1, w = 0;
+            for (; w < kRtWaves - 1 && rk >= S.cnt[w][lane]; ++w) rk -= S.cnt[w][lane];
+            uint32_t jw = 0, word = 0;
+            for (; jw < kRtWords; ++jw) {
+              word = S.bits[w][jw][lane];
+              const uint32_t pc = static_cast<uint32_t>(__popc(word));
+              if (rk < pc) break;
+              rk -= pc;
+            }
+            for (uint32_t u = 0; u < rk; ++u) word &= word - 1u;
+            const uint32_t s = (w * cpw * 2u + jw) * 32u + static_cast<uint32_t>(__ffs(word) - 1);
+            // its sub: the summary entry's base + d's out-edge index in s's row, or the slot record
+            const size_t si = sum_idx(p, b, rep, rt, s);
+            const uint4 ea = gld4(p.msum + si * 2), eb = gld4(p.msum + si * 2 + 1);
+            const unsigned long long em = (static_cast<unsigned long long>(ea.y) << 32) | ea.x;
+            uint32_t sub_s;
+            if (slot_live(eb.y >> 24, tag) && ((em >> lane) & 1ull))
+              sub_s = ea.w + (d < s ? d : d - 1u);
+            else
+              sub_s = gld4(p.inbox + inbox_idx(p, b, rep, d * (N - 1) + (s < d ? s : s - 1u))).y;
+            const Key key{t, t - static_cast<int64_t>(dt), s, sub_s};
+            emit_trace(p, key, rep, d, BCSIM_TR_PBFT_COMMIT, INT32_MIN, bn0 + static_cast<int32_t>(j), val);
+          }
+        }
+      }
+      if (nops0 + nd > op_cap(p, g)) {
+        set_err(p, BCSIM_E_OVERFLOW);
+        nd = 0;
+      }
+      for (uint32_t j = 0; j < nd; ++j) {
+        const Msg m = type == PB_PRE_PREPARE ? mkmsg(PB_PREPARE, m1, m2, fr_m3(r), 0) : mkmsg(PB_COMMIT, m1, m2, 0, 0);
+        st_op(&ops[nops0 + j], mk_op(p, t + app, static_cast<uint32_t>(app), d, sub0 + j * deg, 0, m, OP_BCAST, 0));
+      }
+      if (type == PB_PRE_PREPARE) AT(p.tx_val, base + idx, p.cap_txn) = c2i(fr_m3(r));
+      if (np) {  // the replies: one descriptor {due, first sub, payload} + the bitmap (all waves, below)
+        const int64_t due = t + app;
+        const uint64_t ud = static_cast<uint64_t>(due);
+        const uint32_t f01 = static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m1))) |
+                             (static_cast<uint32_t>(static_cast<uint16_t>(to16(p, m2))) << 16);
+        gst4(p.rdesc + static_cast<size_t>(ob) * p.NT + g, make_uint4(static_cast<uint32_t>(ud), static_cast<uint32_t>(ud >> 32), sub0, f01));
+        const uint32_t sm = due < cs + p.L ? 1u : 2u;  // due in the arrival cell or the next
+        uint8_t& f = AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4);
+        f = static_cast<uint8_t>((f & ~kSfD) | (sm << 4));
+        mark_busy(&p.bucket_cnt[(cell + (sm == 1u ? 0 : 1)) % B]);
+        st |= kRtRbits;
+      }
+      AT(p.sub, g, p.NT) = sub0 + np + nd * deg;
+      AT(p.n_ops, g, p.NT) = nops0 + nd;
+      if (nd) {
+        const long long on = AT(p.node_onext, g, p.NT);
+        AT(p.node_onext, g, p.NT) = on == LLONG_MIN ? LLONG_MIN : min(on, static_cast<long long>(t + app));
+      }
+      if (nc) AT(p.block_num, g, p.NT) = bn0 + static_cast<int32_t>(nc);
+      if (st & kRtEchoDesc) {  // the echoes as one pending descriptor {t, big} + the bitmap (below)
+        const uint32_t ne0 = S.ne[lane];
+        const uint64_t ut = static_cast<uint64_t>(t);
+        gst4(p.edesc + static_cast<size_t>(g) * kEDesc + ne0,
+             make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), big ? 1u : 0u, 0u));
+        AT(p.en, g, p.NT) = static_cast<uint8_t>(ne0 + 1);
+        AT(p.eapp, g, p.NT) = t_lo;
+        st |= kRtEbits;
+        atomicAdd(&S.echo, n);
+      } else {
+        st |= kRtMat;  // the link stage does the echoes from the row
+      }
+      const uint32_t t4 = type == PB_PRE_PREPARE ? 0u : type == PB_PREPARE ? 1u : type == PB_COMMIT ? 2u : 3u;
+      atomicAdd(&S.tcount[t4], n);
+      atomicMax(&S.tlast, static_cast<long long>(t));
+    } else if ((st & kRtFast) && (st & kRtEchoHere)) {
+      AT(p.eapp, g, p.NT) = t_lo;  // no arrival in the window: no echo to leave to the link stage
+    }
+    S.st[lane] = st;
+    const unsigned long long mat = __ballot((st & kRtMat) != 0u);
+    // the receivers that leave for the generic kernel: list 2 (one atomic per workgroup)
+    const unsigned long long gm = __ballot(!mode && (st & kRtGen));
+    if (lane == 0) S.mat = mat;
+    if (gm) {
+      uint32_t pos0 = 0;
+      if (lane == 0) pos0 = gadd_r(&p.act_n[2], static_cast<uint32_t>(__popcll(gm)));
+      pos0 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(pos0)));
+      if (st & kRtGen) {
+        AT(p.act, 2ull * p.NT + pos0 + static_cast<uint32_t>(__popcll(gm & ((1ull << lane) - 1ull))), 4ull * p.NT) = g;
+        if (wep) AT(p.l2mark, g, p.NT) = wep;
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t st = S.st[lane];
+  // ---- all waves: the descriptor bitmaps in in-slot order (in-slot k of d = sender k < d ? k : k + 1) ----
+  if (st & (kRtRbits | kRtEbits)) {
+    const uint32_t dw = p.dwords;
+    uint32_t* rb = p.rbits + (static_cast<size_t>(ob) * p.NT + g) * dw;
+    uint32_t* eb = p.ebits + (static_cast<size_t>(g) * kEDesc + S.ne[lane]) * dw;
+    const uint32_t nw = 2u * cpw;  // (this wave's sender words: in-slot words wv * nw .. + nw)
+    for (uint32_t j = 0; j < nw; ++j) {
+      const uint32_t m = wv * nw + j;
+      if (m >= dw) break;
+      const uint32_t sw = S.bits[wv][j][lane];
+      const uint32_t nx = j + 1 < nw ? S.bits[wv][j + 1][lane] : (wv + 1 < kRtWaves ? S.bits[wv + 1][0][lane] : 0u);
+      const uint32_t lo = 32u * m;
+      const uint32_t keep = d <= lo ? 0u : (d >= lo + 32u ? ~0u : (1u << (d - lo)) - 1u);
+      const uint32_t word = (sw & keep) | (((sw >> 1) | (nx << 31)) & ~keep);
+      if (st & kRtRbits) gbl(rb)[m] = word;
+      if (st & kRtEbits) gbl(eb)[m] = word;
+    }
+  }
+  // ---- all waves: materialise the summary records of the receivers that need their rows ----
+  const unsigned long long mat = S.mat;
+  if (mat) {
+    for (uint32_t c = 0; c < cpw; ++c) {
+      const uint32_t ch = wv * cpw + c;
+      if (ch >= nch) break;
+      const uint32_t sb = ch * 64u + lane;
+      const bool sv = sb < N;
+      const size_t si = sum_idx(p, b, rep, rt, sv ? sb : 0u);
+      const uint4 ea = sv ? gld4(p.msum + si * 2) : make_uint4(0, 0, 0, 0);
+      const uint4 eb = sv ? gld4(p.msum + si * 2 + 1) : make_uint4(0, 0, 0, 0);
+      const unsigned long long em = (static_cast<unsigned long long>(ea.y) << 32) | ea.x;
+      const unsigned long long mm = (sv && slot_live(eb.y >> 24, tag)) ? (em & mat) : 0ull;
+      if (mm) {  // the entry keeps the other receivers; the slots are explicit from now on
+        if (static_cast<uint32_t>(mm)) atomicAnd(reinterpret_cast<uint32_t*>(p.msum + si * 2), ~static_cast<uint32_t>(mm));
+        if (static_cast<uint32_t>(mm >> 32))
+          atomicAnd(reinterpret_cast<uint32_t*>(p.msum + si * 2) + 1, ~static_cast<uint32_t>(mm >> 32));
+        gbl(p.xsum)[si] = static_cast<uint8_t>(0x80u | tag);
+      }
+      unsigned long long sm = __ballot(mm != 0ull);
+      while (sm) {  // (uniform) per sender with records to write: its receivers' slots
+        const int k = __ffsll(static_cast<long long>(sm)) - 1;
+        sm &= sm - 1ull;
+        const uint32_t lo32 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(mm)), k));
+        const uint32_t hi32 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(mm >> 32)), k));
+        const unsigned long long mk = (static_cast<unsigned long long>(hi32) << 32) | lo32;
+        if (!((mk >> lane) & 1ull)) continue;
+        const uint32_t s = ch * 64u + static_cast<uint32_t>(k);
+        const uint32_t tofk = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ea.z), k));
+        const uint32_t basek = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ea.w), k));
+        const uint32_t w2k = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(eb.x), k));
+        const uint32_t w3k = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(eb.y), k));
+        gst4(p.inbox + inbox_idx(p, b, rep, d * (N - 1) + (s < d ? s : s - 1u)),
+             make_uint4(tofk, basek + (d < s ? d : d - 1u), w2k, w3k));
+      }
+    }
+  }
+  // ---- counters: one add per workgroup ----
+  __syncthreads();
+  if (tid == 0 && !mode) {
+    unsigned long long* cnt = cnt_stripe(p, rep);
+    const uint32_t type_of[4] = {PB_PRE_PREPARE, PB_PREPARE, PB_COMMIT, PB_PREPARE_RES};
+    unsigned long long tot = 0;
+    for (int t4 = 0; t4 < 4; ++t4)
+      if (S.tcount[t4]) {
+        gadd(&cnt[CNT_DELIV + type_of[t4]], static_cast<unsigned long long>(S.tcount[t4]));
+        tot += S.tcount[t4];
+      }
+    if (tot) {
+      gadd(&cnt[CNT_DELIV_TOTAL], tot);
+      if (p.echo) gadd(&cnt[CNT_ECHOES], tot);
+      gadd(&kst_stripe(p)[KST_DELIV], tot);
+      gadd(&cnt[CNT_EVENTS], tot);
+      __hip_atomic_fetch_max(gbl(reinterpret_cast<long long*>(&cnt[CNT_TLAST])), S.tlast, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (S.echo) gadd(&kst_stripe(p)[KST_ECHO], static_cast<unsigned long long>(S.echo));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_paxos_scan (sparse layout, BCSIM_PAXOS): one LANE per active node.  A node whose window
 // holds only acceptor requests (REQ_TICKET / REQ_PROPOSE / REQ_COMMIT, at most kPxCap, no
 // timer, START or STOP due) is handled here in canonical key order exactly as the lane-0
@@ -4989,6 +5439,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
           // scatter from XCD-contiguous senders merges in L2 and costs ~2x a coalesced row
           // write, a third of staging sender-major and transposing (tools/microbench/scatter.hip)
           st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), r);
+          xs_mark(p, bk, rep, i, s, w3);
           if (p.mesh) {
             // receiver-tile flag: one LDS byte per 64-node tile, flushed once per workgroup
             uint32_t tb = kInvalid;
@@ -5659,6 +6110,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
           if (bk >= B) bk -= B;
           if (owner) {
             st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), r);
+            xs_mark(p, bk, rep, i, s, w3);
             uint32_t tb = kInvalid;
             if (tmap) {  // the first bucket seen owns the LDS tile map; others flag directly
               tb = L.tbk;
@@ -5952,6 +6404,8 @@ struct TileShared {
   long long ovmin;
   long long bmin[kMaxBuckets];  // the buckets' arrival-time bounds as of the start (read early)
   uint64_t lwo[BCSIM_TILE_DEFER ? kTS : 1][kTR];  // updated link words (0: unchanged), written out after the walk
+  uint4 sold[kTS][2][2];    // (summaries) the senders' entries of the buckets sbk[0 / 1] as of the start
+  uint32_t sbk[2];
 };
 // (receiver, sender) -> LDS index: the sender index XOR the receiver's low bits, so that a wave
 // writing one sender's 64 receivers and a wave reading two receivers' 32 senders both spread
@@ -6029,6 +6483,15 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
       const uint64_t m = gbl(reinterpret_cast<uint64_t*>(p.mte))[((gb + il) * nrt + rt) * kEDesc + k % kEDesc];
       T.mte[il][k % kEDesc] = make_uint2(static_cast<uint32_t>(m), static_cast<uint32_t>(m >> 32));
     }
+  } else if (p.sum && tid < kTS * 4 + kTS * kMeshBc * 2 + kTS * 2 + kTS * kEDesc + kTS * 4) {
+    // (summaries) the senders' entries of the (at most two) buckets a small message sent in this
+    // window lands in on an idle link -- the heavy waves' jobs -- for the walk's merge check
+    const uint32_t k = tid - (kTS * 4 + kTS * kMeshBc * 2 + kTS * 2 + kTS * kEDesc), il = k >> 2, h = (k >> 1) & 1u;
+    const long long ca = ((h ? t_hi - 1 : t_lo) + p.tx_tot[0] + p.prop_const) / p.L;
+    const bool in = p.prop_const >= 0 && ca - cell >= 1 && ca - cell < static_cast<long long>(B);
+    const uint32_t bk = static_cast<uint32_t>(ca % B);
+    T.sold[il][h][k & 1u] = in && i0 + il < N ? gld4(p.msum + sum_idx(p, bk, rep, rt, i0 + il) * 2 + (k & 1u)) : make_uint4(0, 0, 0, 0);
+    if (il == 0 && (k & 1u) == 0) T.sbk[h] = in && (h == 0 || ca != ((t_lo + p.tx_tot[0] + p.prop_const) / p.L)) ? bk : kInvalid;
   }
   for (uint32_t k = tid; k < kTR * kTS / 4; k += blockDim.x) reinterpret_cast<uint32_t*>(T.rbk)[k] = 0xFFFFFFFFu;
   if (BCSIM_TILE_DEFER)
@@ -6075,6 +6538,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
   unsigned long long bkm = 0ull;
   long long ovmin = LLONG_MAX;
   uint32_t cb = kInvalid, cbn = 0, cmn = ~0u;
+  const bool sum_on = p.sum != 0;
 #pragma unroll 1
   for (uint32_t il = wv; il < kTS; il += nwv) {
     // the sender's job words are uniform: scalar registers, scalar branches
@@ -6147,11 +6611,52 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
       const bool wrap = bq >= B;
       const bool ok = has && (static_cast<uint64_t>(dtf) >> 32) == 0 && qq - 1u < B - 1u && lc0 != ca16;
       const uint32_t lc = ok ? ca16 : lc0;
+      const uint32_t bk = wrap ? bq - B : bq;
+      const uint32_t tof = x - qq * L32;
+      const uint32_t w3f = w3u | (static_cast<uint32_t>((cq_b + (wrap ? 1 : 0)) & 31) << 27);
+      // (summaries) the lanes whose record has the first such lane's bucket, offset
+      // and base (sub - out-edge index) become ONE entry of (bucket, receiver tile, this sender),
+      // merged with the entry an earlier launch left for the same turn when its words are the
+      // same (else they go out as records, below)
+      bool uni = false;
+      if (sum_on) {
+        const unsigned long long okm = __ballot(ok);
+        if (okm) {
+          const int rl = __ffsll(static_cast<long long>(okm)) - 1;
+          const uint32_t r_tof = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(tof), rl));
+          const uint32_t r_base = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(u_sub), rl));
+          const uint32_t r_bk = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bk), rl));
+          const uint32_t r_w2 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(u_w2), rl));
+          const uint32_t r_w3 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w3f), rl));
+          uni = ok && tof == r_tof && u_sub == r_base && bk == r_bk;
+          unsigned long long um = __ballot(uni);
+          uint4 oa, ob;
+          uint4* const se = p.msum + sum_idx(p, r_bk, rep, rt, i) * 2;
+          if (r_bk == T.sbk[0] || r_bk == T.sbk[1]) {  // (prefetched in the prologue)
+            const uint32_t h = r_bk == T.sbk[0] ? 0u : 1u;
+            oa = T.sold[il][h][0];
+            ob = T.sold[il][h][1];
+          } else {
+            oa = gld4(se);
+            ob = gld4(se + 1);
+          }
+          const bool olive = (oa.x | oa.y) != 0u && slot_live(ob.y >> 24, r_w3 >> 27);
+          if (olive && (oa.z != r_tof || oa.w != r_base || ob.x != r_w2 || ob.y != r_w3)) um = 0ull;
+          if (um) {
+            const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oa.y) << 32) | oa.x) : 0ull);
+            if (lane < 2u)
+              gst4(se + lane,
+                   lane ? make_uint4(r_w2, r_w3, 0u, 0u)
+                        : make_uint4(static_cast<uint32_t>(mm), static_cast<uint32_t>(mm >> 32), r_tof, r_base));
+          }
+          uni = (um >> lane) & 1ull;
+        }
+      }
       if (ok) {
-        const uint32_t bk = wrap ? bq - B : bq;
-        const uint32_t tof = x - qq * L32;
-        T.rec[q] = make_uint4(tof, u_sub + le, u_w2, w3u | (static_cast<uint32_t>((cq_b + (wrap ? 1 : 0)) & 31) << 27));
-        T.rbk[q] = static_cast<uint8_t>(bk);
+        if (!uni) {
+          T.rec[q] = make_uint4(tof, u_sub + le, u_w2, w3f);
+          T.rbk[q] = static_cast<uint8_t>(bk);
+        }
         bkm |= 1ull << bk;
         ++n_rec;
         if (!n_bc) {
@@ -6286,6 +6791,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
             in_lds = true;
           } else {
             gst4(p.inbox + inbox_idx(p, bk, rep, slot), rv);
+            xs_mark(p, bk, rep, i, s, w3);
             set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
                               static_cast<uint64_t>(B) * p.R * p.n_tiles));
           }
@@ -6439,7 +6945,9 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
     if (bk == 0xFFu || (p.exp & 4u)) continue;
     const uint32_t sr = s0 + sl, i = i0 + il;
     const uint32_t slot = sr * N1 + (i < sr ? i : i - 1);
-    gst4(p.inbox + inbox_idx(p, bk, rep, slot), T.rec[q]);
+    const uint4 rq = T.rec[q];
+    gst4(p.inbox + inbox_idx(p, bk, rep, slot), rq);
+    xs_mark(p, bk, rep, i, sr, rq.w);
   }
   // staged extras / overflow records: one atomic per list
   if (T.xn) {
