@@ -2,6 +2,7 @@
 // declared in include/bcsim.h.  One translation unit with the kernels.
 #include "engine.hip"
 
+#include <chrono>
 #include <cstdlib>
 
 namespace bcsim {
@@ -807,9 +808,8 @@ static int setup_device(Sim& s) {
     // per-flow packet rings.  A saturated link's disc holds up to MaxSize packets (the PBFT
     // leader's block links and the echo links back to it run at 2.7x capacity), so the edges
     // of the hub nodes -- PBFT / gossip node 0, the Paxos proposers -- get MaxSize + 1 packets
-    // per flow; every other edge gets MaxSize + 1 (at most 4096) when that fits a 150 GB budget
-    // for the whole link state (per GPU: 150 / P GB per rank -- the ranks of a partition may
-    // share one GPU), else the largest ring that does (>= 64).  A flow that outgrows its ring
+    // per flow; every other edge gets MaxSize + 1 (at most 4096) when that fits the link-state
+    // budget (below), else the largest ring that does (>= 64).  A flow that outgrows its ring
     // fails the run (BCSIM_E_OVERFLOW), never drops silently.
     const uint32_t cap_hi = static_cast<uint32_t>(std::min<uint64_t>(p.fq_limit + 1ull, 65535));
     uint32_t cap_lo = static_cast<uint32_t>(std::min<uint64_t>(p.fq_limit + 1ull, 4096));
@@ -824,7 +824,15 @@ static int setup_device(Sim& s) {
           if (hub(i) || hub(s.col[e])) ++n_hub;
     n_hub *= s.R;
     const double fixed_b = kFqH * 4.0 + p.fq_devcap * 8.0 + p.cap_fqm * 16.0 + 16.0 + 8.0 + 8.0;
-    const double budget = 150e9 / s.P - static_cast<double>(n_hub) * 48.0 * cap_hi;
+    // (per rank: 150 GB or 60 % of the free device memory, divided among the ranks only when
+    // they may share the GPU -- the host-callback transport; RCCL runs one rank per device)
+    double dev_b = 150e9;
+    if (fq) {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) == hipSuccess) dev_b = std::min(dev_b, 0.6 * static_cast<double>(fr));
+    }
+    const uint32_t share = (s.P > 1 && s.xp && s.xp->shares_device()) ? s.P : 1u;
+    const double budget = dev_b / share - static_cast<double>(n_hub) * 48.0 * cap_hi;
     if (fq && static_cast<double>(ne) * fixed_b + static_cast<double>(ne - n_hub) * 48.0 * cap_lo > budget) {
       const double fit = ((budget - static_cast<double>(ne) * fixed_b) / std::max<double>(1.0, static_cast<double>(ne - n_hub))) / 48.0;
       cap_lo = fit >= 64.0 ? static_cast<uint32_t>(std::min<double>(fit, cap_lo)) : 0u;
@@ -875,7 +883,7 @@ static int setup_device(Sim& s) {
     const uint64_t nl = (static_cast<uint64_t>(s.R) * s.nloc + 7) / 8 * 8;
     s.grid_scan = s.grid_link = static_cast<uint32_t>(s.sparse ? std::min<uint64_t>(nl, 4096) : nl);
   }
-  const size_t n_rtile = p.mesh ? static_cast<size_t>(s.B) * s.R * p.n_tiles : 1;
+  const size_t n_rtile = p.mesh ? static_cast<size_t>(s.B) * s.R * p.n_tiles * kRtPad : 1;  // (one flag per 128-byte line)
   if ((rc = dalloc(s, &p.rtile, n_rtile))) return rc;
   if ((rc = dalloc(s, &p.bmin, s.B))) return rc;
   if ((rc = dalloc(s, &p.inbox, p.cap_inbox)) || (rc = dalloc(s, &p.iflag, static_cast<size_t>(s.B) * NT)) ||
@@ -1192,6 +1200,19 @@ static int tile_phase_report(Sim& s, long long cell, uint32_t nt) {
   return BCSIM_OK;
 }
 
+// k_mesh_row's cell arithmetic (no 64-bit divisions per workgroup): {cell % B, (cell / B) % 32,
+// the idle-link arrival buckets of a small message sent at lo / hi - 1 (0xFFFF: outside the
+// ring) as lo | hi << 16, 0}
+static uint4 row_hq(const Sim& s, long long cell, long long lo, long long hi) {
+  const long long B = s.B;
+  uint32_t cb[2];
+  for (int h = 0; h < 2; ++h) {
+    const long long ca = ((h ? hi - 1 : lo) + s.kp.tx_tot[0] + s.kp.prop_const) / s.L;
+    cb[h] = s.kp.prop_const >= 0 && ca - cell >= 1 && ca - cell < B ? static_cast<uint32_t>(ca % B) : 0xFFFFu;
+  }
+  return make_uint4(static_cast<uint32_t>(cell % B), static_cast<uint32_t>((cell / B) & 31), cb[0] | (cb[1] << 16), 0u);
+}
+
 static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long cs, bool final_win) {
   const size_t lds = scan_lds_bytes(s.kp);
   dim3 grid(s.grid_scan), block(s.bs_scan);
@@ -1255,6 +1276,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       }
       grid = dim3((s.act_h[0] + 7) / 8 * 8);
       n_link = s.act_h[1];
+      static const bool winlog = std::getenv("BCSIM_WINLOG") != nullptr;  // (debug: one line per window)
+      if (winlog)
+        std::fprintf(stderr, "[win] cell %lld [%lld, %lld) +%lld us scan %u link %u xa %d\n", cell, lo, hi, (lo - cell * s.L) / 1000,
+                     s.act_h[0], s.act_h[1], xa);
     } else if (!s.sparse) {
       // node-partitioned: a rank holds 1/P of the nodes, so a workgroup per local node costs
       // less than the round trip (the cell already has several collectives)
@@ -1453,8 +1478,11 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       const uint32_t ep = ++s.mesh_epoch == 0 ? ++s.mesh_epoch : s.mesh_epoch;
       const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
       if ((rc = launch(s, -1, k_mesh_prep, grid, dim3(64), 0, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
-          (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(kTileThreads), 0, s.kp_dev, cell, lo, hi, ep)) ||
-          (s.kp.wgtt && (rc = tile_phase_report(s, cell, nt))) ||
+          // (summary mode: the uniform jobs' rows; the tiles take the rest)
+          (s.sum && (rc = launch(s, -1, k_mesh_row, grid, dim3(kRowThreads), 0, s.kp_dev, cell, lo, hi, ep, row_hq(s, cell, lo, hi)))) ||
+          (s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, grid.x))) ||
+          (!s.sum && (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(kTileThreads), 0, s.kp_dev, cell, lo, hi, ep))) ||
+          (!s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, nt))) ||
           (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
     } else {
@@ -1493,9 +1521,9 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     HIPCHK(hipStreamSynchronize(s.stream));
     HIPCHK(hipMemcpy(fc, s.kp.fdbg, sizeof fc, hipMemcpyDeviceToHost));
     HIPCHK(hipMemset(s.kp.fdbg, 0, sizeof fc));
-    if (fc[8] | fc[9])
-      std::fprintf(stderr, "[fdbg] cell %lld [%lld,%lld) link grid %u: listed %llu bcasts %llu\n", cell, lo, hi, grid.x,
-                   fc[8], fc[9]);
+    if (fc[8] | fc[9] | fc[10] | fc[11] | fc[12] | fc[13] | fc[14] | fc[15])
+      std::fprintf(stderr, "[fdbg] cell %lld [%lld,%lld) link grid %u: listed %llu bcasts %llu | generic: listed %llu bcasts %llu rxe %llu slots %llu 2desc %llu other %llu\n",
+                   cell, lo, hi, grid.x, fc[8], fc[9], fc[10], fc[11], fc[12], fc[13], fc[14], fc[15]);
   }
   if (rc || !s.kp.wgt) return rc;
   // debug (BCSIM_WGT=1): report the slowest k_link workgroups of this launch
@@ -1596,6 +1624,7 @@ static int group_cell(Sim& s, long long cell) {
 // kernel's last store ~1 us after it lands; a stream sync adds the completion signal's
 // wake-up and the end-of-kernel cache release (~10-20 us per read-back).  With
 // BCSIM_SPIN=0, a plain stream sync.
+constexpr int kSpinUs = 500;  // mirror_wait: spin at most this long, then a stream sync
 static int mirror_wait(Sim& s, const uint32_t* w) {
   static const bool spin = [] {
     const char* e = std::getenv("BCSIM_SPIN");
@@ -1606,12 +1635,20 @@ static int mirror_wait(Sim& s, const uint32_t* w) {
     HIPCHK(hipStreamSynchronize(s.stream));
     return __atomic_load_n(w, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
   }
+  // (a pause per spin, and a stream sync once the wait is long -- a window with heavy kernels --
+  // so that ranks sharing the host's cores do not lose them to spinning peers)
+  const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 1;; ++it) {
     if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return 0;
+    __builtin_ia32_pause();
     if ((it & 255u) == 0) {
       const hipError_t q = hipStreamQuery(s.stream);
       if (q == hipSuccess) return __atomic_load_n(w, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
       if (q != hipErrorNotReady) HIPCHK(q);
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) {
+        HIPCHK(hipStreamSynchronize(s.stream));
+        return __atomic_load_n(w, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
+      }
     }
   }
 }
@@ -1978,7 +2015,12 @@ static int run(Sim& s, int64_t t_until) {
     const bool tick = s.cfg.protocol == BCSIM_PBFT && s.n_alive > 0 && s.next_tick >= lo && s.next_tick < hi;
     if (tick) {
       const long long tk = s.next_tick;
-      if (!lrc && tk > lo) lrc = do_scan(s, c, lo, tk, cs, false);
+      // the part of the cell before the tick, unless nothing can happen in it: no record in the
+      // cell's bucket (slots, extras, rebinned overflow, reply slots due), no timer or pending op
+      // before the tick (the end-of-window read-back), no START / STOP
+      const bool idle = !s.xp && s.bcnt[c % s.B] == 0 && s.next_local >= tk && s.next_timer >= tk &&
+                        !(lo <= 0 && 0 < tk) && !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < tk);
+      if (!lrc && tk > lo && !idle) lrc = do_scan(s, c, lo, tk, cs, false);
       if (s.xp) {
         if ((rc = sync_vlog(s, lrc)) || (rc = sync_leaders(s))) return rc;
       } else if (lrc) {
@@ -2041,6 +2083,9 @@ static int run(Sim& s, int64_t t_until) {
   }
 #undef LOCAL
   if (s.xp && s.cfg.protocol == BCSIM_PBFT && (rc = sync_vlog(s))) return rc;
+  // the end-of-window read-back spins on k_next's mirror word, not on the stream: the kernels
+  // queued after it (the tag zeroing) must be done before the readers' null-stream copies
+  HIPCHK(hipStreamSynchronize(s.stream));
   return BCSIM_OK;
 }
 

@@ -306,6 +306,10 @@ struct KP {
 };
 
 constexpr int kMaxRanks = 16;
+// receiver-tile flags (rtile) one per 128-byte line: every sender of a heavy wave sets its
+// receiver tiles' flags, and same-line stores from thousands of workgroups serialise in an L2
+// channel (k_mesh_row: ~100 us per launch with the 64 flags of a bucket in one line)
+constexpr uint32_t kRtPad = 128;
 constexpr uint32_t kDescWords = 128;  // descriptor bitmaps: in-slots of degree <= 4096
 constexpr uint32_t kEDesc = 2;        // pending echo descriptors per node (LDS: k_link_mesh keeps 4 WGs/CU)
 // sflag bits of a reply descriptor of the arrival cell (bits 0..3: reply slots due in cell + k)
@@ -485,8 +489,7 @@ __device__ inline uint32_t xcd_map(uint32_t b, uint32_t n) {
 __device__ inline bool node_flagged(const KP& p, uint32_t b, uint32_t g, uint32_t rep, uint32_t i) {
   // both bytes are loaded together (no dependent second round trip)
   const uint8_t f = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
-  const uint8_t t = p.mesh ? AT(p.rtile, (static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6),
-                                static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles)
+  const uint8_t t = p.mesh ? AT(p.rtile, kRtPad * ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6)), kRtPad * (static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles))
                            : 0;
   return (f | t) != 0;
 }
@@ -3917,8 +3920,7 @@ __device__ __attribute__((always_inline)) inline bool gossip_scan_body(const KP*
   uint4 rsv = make_uint4(0, 0, 0, 0);  // (raw words: unpacking a Rec here would wait for the load)
   if (p.deg_reg) rsv = gld4(p.inbox + inbox_idx(p, b, rep, e0r + min(j, p.deg_reg - 1u)));
   const uint8_t f8 = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
-  const uint8_t t8 = p.mesh ? AT(p.rtile, (static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6),
-                                 static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles)
+  const uint8_t t8 = p.mesh ? AT(p.rtile, kRtPad * ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6)), kRtPad * (static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles))
                             : static_cast<uint8_t>(0);
   const long long tn = AT(p.node_tnext, g, p.NT);
   const uint32_t sub0p = AT(p.sub, g, p.NT), nops0p = AT(p.n_ops, g, p.NT);
@@ -5131,8 +5133,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
           if (owner) {
             st_rec(&AT(p.inbox, inbox_idx(p, bk, rep, slot), p.cap_inbox), r);
             if (p.mesh)
-              set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
-                                static_cast<uint64_t>(B) * p.R * p.n_tiles));
+              set_flag_once(&AT(p.rtile, kRtPad * ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6)), kRtPad * (static_cast<uint64_t>(B) * p.R * p.n_tiles)));
           } else {
             XRec x;
             x.r = r;
@@ -5453,8 +5454,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
             if (tb == bk)
               L.tflag[s >> 6] = 1;
             else
-              set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
-                                static_cast<uint64_t>(B) * p.R * p.n_tiles));
+              set_flag_once(&AT(p.rtile, kRtPad * ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6)), kRtPad * (static_cast<uint64_t>(B) * p.R * p.n_tiles)));
             flag_rx = false;
           }
         } else {
@@ -5501,7 +5501,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
   if (tmap && L.tbk != kInvalid) {
     const size_t tb = (static_cast<size_t>(L.tbk) * p.R + rep) * p.n_tiles;
     for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x)
-      if (L.tflag[k]) set_flag_once(&AT(p.rtile, tb + k, static_cast<uint64_t>(B) * p.R * p.n_tiles));
+      if (L.tflag[k]) set_flag_once(&AT(p.rtile, kRtPad * (tb + k), kRtPad * (static_cast<uint64_t>(B) * p.R * p.n_tiles)));
   }
 
   if (p.wgt && tid == 0) ph[2] = __builtin_amdgcn_s_memrealtime();
@@ -6122,8 +6122,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
             if (tb == bk)
               L.tflag[s >> 6] = 1;
             else
-              set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
-                                static_cast<uint64_t>(B) * p.R * p.n_tiles));
+              set_flag_once(&AT(p.rtile, kRtPad * ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6)), kRtPad * (static_cast<uint64_t>(B) * p.R * p.n_tiles)));
           } else {
             XRec x;
             x.r = r;
@@ -6172,7 +6171,7 @@ __global__ __launch_bounds__(XR ? 256 : 1024) void k_link_mesh(const KP* __restr
   if (tmap && L.tbk != kInvalid) {  // flush the receiver-tile flags of this sender's records
     const size_t tb = (static_cast<size_t>(L.tbk) * p.R + rep) * p.n_tiles;
     for (uint32_t k = tid; k < p.n_tiles; k += blockDim.x)
-      if (L.tflag[k]) set_flag_once(&AT(p.rtile, tb + k, static_cast<uint64_t>(B) * p.R * p.n_tiles));
+      if (L.tflag[k]) set_flag_once(&AT(p.rtile, kRtPad * (tb + k), kRtPad * (static_cast<uint64_t>(B) * p.R * p.n_tiles)));
   }
   if (tid == 0) {
     if (ne_w) AT(p.en, g, p.NT) = 0;  // every edge walked: the echo descriptors are applied
@@ -6224,6 +6223,15 @@ __device__ inline uint64_t tile_mask(const uint32_t* w, uint32_t dw, uint32_t i,
   }
   const uint32_t nv = N - s0;  // receivers of the tile that exist
   return nv >= 64 ? m : (m & ((1ull << nv) - 1ull));
+}
+
+// the heavy waves' job shape (uniform over the sender's edges): one kind of source per edge -- the
+// one due broadcast, or the one due reply descriptor -- no echo from the row, no reply slot, and a
+// constant propagation delay (k_mesh_tile's fast lanes; in summary mode k_mesh_row takes them)
+__device__ inline bool job_uniform(uint32_t fl, uint32_t jz, int64_t prc) {
+  const uint32_t n_bc = (jz >> 8) & 0xFFu;
+  const bool sd0 = fl & kJSd0, sd1 = fl & kJSd1;
+  return !(fl & (kJRxe | kJSl0 | kJSl1)) && prc >= 0 && ((n_bc == 1 && !sd0 && !sd1) || (n_bc == 0 && sd0 != sd1));
 }
 
 __global__ __launch_bounds__(64) void k_mesh_prep(const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi,
@@ -6302,7 +6310,13 @@ __global__ __launch_bounds__(64) void k_mesh_prep(const KP* __restrict__ pk, lon
   }
   __syncthreads();
   const uint32_t n_bc = L.n_bc;
-  if (L.n_list || n_bc > kMeshBc) {  // the generic kernel takes the node (node_desc_flush first)
+  // (summary mode: k_mesh_row takes the uniform jobs and the generic kernel every other -- no
+  // tile launch)
+  const uint32_t flu = (sl0 ? kJSl0 : 0u) | (sl1 ? kJSl1 : 0u) | (sd0 ? kJSd0 : 0u) | (sd1 ? kJSd1 : 0u) | (rxe ? kJRxe : 0u);
+  if (L.n_list || n_bc > kMeshBc || (p.sum && !job_uniform(flu, n_bc << 8, p.prop_const))) {
+    // the generic kernel takes the node (node_desc_flush first)
+    if (tid == 0 && p.fdbg)
+      FDBG(L.n_list ? 10 : n_bc > kMeshBc ? 11 : rxe ? 12 : (sl0 || sl1) ? 13 : (sd0 && sd1) ? 14 : 15);
     if (tid == 0) {
       const uint32_t pos = gadd_r(&p.act_n[3], 1u);
       AT(p.act, 3ull * p.NT + pos, 4ull * p.NT) = g;
@@ -6362,7 +6376,8 @@ __global__ __launch_bounds__(64) void k_mesh_prep(const KP* __restrict__ pk, lon
     J[2] = rd1;
     J[3] = q3;
     J[0] = make_uint4(epoch, fl, ne_j | (n_bc << 8), 0u);
-    p.mtile[static_cast<size_t>(rep) * p.n_stiles + i / kTS] = epoch;
+    if (!(p.sum && job_uniform(fl, ne_j | (n_bc << 8), p.prop_const)))  // (summary mode: k_mesh_row's)
+      p.mtile[static_cast<size_t>(rep) * p.n_stiles + i / kTS] = epoch;
     if (ne_j) AT(p.en, g, p.NT) = 0;
     // a due reply descriptor is sent whole: its flag goes (as in k_link_mesh)
     if (sd0) AT(p.sflag, static_cast<size_t>(ob) * p.NT + g, R4) = static_cast<uint8_t>(sf0 & ~kSfD0);
@@ -6545,6 +6560,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
     if (static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(T.job[il][0].x))) != epoch) continue;
     const uint32_t fl = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(T.job[il][0].y)));
     const uint32_t jz = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(T.job[il][0].z)));
+    if (sum_on && job_uniform(fl, jz, prc)) continue;  // (summary mode: k_mesh_row's)
     const uint32_t i = i0 + il;
     const uint32_t ne = jz & 0xFFu, n_bc = (jz >> 8) & 0xFFu;
     const bool sl0 = fl & kJSl0, sl1 = fl & kJSl1, sd0 = fl & kJSd0, sd1 = fl & kJSd1, rxe = fl & kJRxe;
@@ -6792,8 +6808,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
           } else {
             gst4(p.inbox + inbox_idx(p, bk, rep, slot), rv);
             xs_mark(p, bk, rep, i, s, w3);
-            set_flag_once(&AT(p.rtile, (static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6),
-                              static_cast<uint64_t>(B) * p.R * p.n_tiles));
+            set_flag_once(&AT(p.rtile, kRtPad * ((static_cast<size_t>(bk) * p.R + rep) * p.n_tiles + (s >> 6)), kRtPad * (static_cast<uint64_t>(B) * p.R * p.n_tiles)));
           }
         } else {
           XRec x;
@@ -6983,7 +6998,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
   // atomics that return nothing (no round trip at the end of the workgroup); the bound is
   // lowered only below the value read at the start
   if (tid < B && ((T.bkm >> tid) & 1ull))
-    gbl(p.rtile)[(static_cast<size_t>(tid) * p.R + rep) * p.n_tiles + rt] = 1;
+    gbl(p.rtile)[kRtPad * ((static_cast<size_t>(tid) * p.R + rep) * p.n_tiles + rt)] = 1;
   for (uint32_t k = tid; k < B; k += blockDim.x)
     if (T.lcnt[k]) {
       gbl(p.bucket_cnt)[k] = 1u;
@@ -7002,6 +7017,432 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
   }
   TPH(5);
 #undef TPH
+}
+
+// ---------------------------------------------------------------------------
+// k_mesh_row (summary mode): the edges of a sender whose job has the heavy
+// waves' uniform shape (job_uniform: the one due broadcast, pbft-node.cc:349-368, or the one
+// due reply descriptor, :212-222), one 256-lane workgroup per sender walking its row one
+// receiver tile (64 out-edges) per wave-iteration.  With summaries no record needs the tile
+// kernel's transpose: the link words are read and written coalesced (a sender's row is
+// contiguous), the tile's records that differ only in sub are ONE summary entry (merged as in
+// k_mesh_tile), any other slot record is stored directly, and second records of an edge
+// (extras) and records beyond the ring (overflow) are staged in LDS and appended with one
+// atomic per list.  The per-edge work and its results are k_mesh_tile's.
+constexpr uint32_t kRowThreads = 512, kRowIt = 8;  // (<= 64 receiver tiles over eight waves)
+struct RowShared {
+  XRec xs[kTX];
+  uint32_t xm[kTX];  // list << 24 | rank
+  uint32_t xn;
+  uint32_t lst[kMaxBuckets + 1];
+  uint32_t lcnt[kMaxBuckets];
+  uint32_t lmin[kMaxBuckets];
+  uint32_t csum[8];
+  long long ovmin;
+  long long bmin[kMaxBuckets];  // the buckets' arrival-time bounds as of the start (read early)
+};
+__device__ inline void row_append(const KP& p, RowShared& T, uint32_t list, const XRec& x) {
+  const uint32_t pos = atomicAdd(&T.xn, 1u);
+  if (pos < kTX) {
+    const uint32_t rank = atomicAdd(&T.lst[list], 1u);
+    T.xs[pos] = x;
+    T.xm[pos] = (list << 24) | rank;
+    return;
+  }
+  uint32_t* ctr = list == p.n_buckets ? p.ov_cnt : &p.x_cnt[list];  // (staging full: a direct append)
+  const uint32_t cap = list == p.n_buckets ? p.cap_ov : p.cap_x;
+  const uint32_t at = gadd_r(ctr, 1u);
+  if (at >= cap) {
+    set_err(p, BCSIM_E_OVERFLOW);
+    return;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(list == p.n_buckets ? p.ov + at : p.xbuf + static_cast<size_t>(list) * p.cap_x + at);
+  const uint4* src = reinterpret_cast<const uint4*>(&x);
+  gst4(dst, src[0]);
+  gst4(dst + 1, src[1]);
+}
+__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_mesh_row(
+    const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi, uint32_t epoch, uint4 hq) {
+  // hq (host arithmetic, no 64-bit divisions per workgroup): {cell % B, (cell / B) % 32, the
+  // buckets a small message sent in [t_lo, t_hi) lands in on an idle link (0xFFFF: outside the
+  // ring) as lo | hi << 16, 0}
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ RowShared T;
+  __shared__ uint4 sj[6];                       // job words, the broadcast's RawOp words
+  __shared__ uint4 pf[kRowThreads / 64][kRowIt][4][2];  // per wave and tile: reply bitmaps (h = 0, 1), echo bitmaps, entries
+  __shared__ uint64_t lwl[kRowThreads / 64][kRowIt][64];  // per wave and tile: the link words (parked: no registers across the walk)
+  const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
+  G<unsigned long long>* tph = p.wgtt ? gbl(p.wgtt) + 8ull * blockIdx.x : nullptr;  // (debug phase clocks)
+#define RPH(k)                                                       \
+  do {                                                               \
+    if (tph && tid == 0) tph[(k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  RPH(0);
+  uint32_t kk;
+  if (!list_one(p.act_n[1], kk)) return;
+  const uint32_t g = p.act[p.NT + kk];
+  RPH(1);
+  const uint32_t N = p.N, N1 = N - 1, B = p.n_buckets, nrt = p.n_tiles;
+  const uint32_t rep = g / N, i = g % N;
+  const int64_t prc = p.prop_const;
+  const long long cs = cell * p.L;
+  const uint32_t cr_b = hq.x;
+  // the job first (a node without a uniform job leaves before loading its row), then ONE round
+  // of loads: the link words of every wave's tiles, and per tile the bitmaps and the summary
+  // entries of the (at most two) buckets a small message sent in this window lands in on an idle
+  // link.  No load after these: a load in the walk (or a register move of a pending load's
+  // destination) made the compiler wait for every outstanding memory operation, the stores
+  // included, once per tile
+  if (tid < 4) sj[tid] = gld4(p.mjob + static_cast<size_t>(g) * 4 + tid);
+  else if (tid < 6) sj[tid] = gld4(p.mbc + static_cast<size_t>(g) * kMeshBc * 2 + (tid - 4));
+  for (uint32_t k = tid; k < B; k += blockDim.x) {
+    T.lcnt[k] = 0;
+    T.lmin[k] = ~0u;
+  }
+  for (uint32_t k = tid; k <= B; k += blockDim.x) T.lst[k] = 0;
+  if (tid < 8) T.csum[tid] = 0;
+  if (tid == 0) {
+    T.ovmin = LLONG_MAX;
+    T.xn = 0;
+  }
+  __syncthreads();
+  // (the job words are uniform: scalar registers)
+  auto u = [](uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x))); };
+  auto u4 = [&](const uint4& x) { return make_uint4(u(x.x), u(x.y), u(x.z), u(x.w)); };
+  const uint32_t fl = u(sj[0].y), jz = u(sj[0].z);
+  if (u(sj[0].x) != epoch || !job_uniform(fl, jz, prc)) {  // (uniform)
+    if (tph && tid == 0) tph[0] = 0;
+    return;
+  }
+  {
+    uint64_t lw[kRowIt];
+#pragma unroll
+    for (uint32_t it = 0; it < kRowIt; ++it) {
+      const uint32_t s = (wv + it * nwv) * 64u + lane;
+      const uint32_t sc = s < N ? s : N - 1u;  // (clamped, unconditional: see k_scan_pbft's row loads)
+      lw[it] = gbl(p.link)[edge_loc(p, rep, i * N1 + (sc < i ? sc : (sc == i ? 0u : sc - 1)))];
+    }
+#pragma unroll
+    for (uint32_t it = 0; it < kRowIt; ++it) lwl[wv][it][lane] = lw[it];
+  }
+  uint32_t cbk[2] = {hq.z & 0xFFFFu, hq.z >> 16};
+  cbk[0] = cbk[0] == 0xFFFFu ? kInvalid : cbk[0];
+  cbk[1] = (cbk[1] == 0xFFFFu || cbk[1] == cbk[0]) ? kInvalid : cbk[1];
+  {
+    const uint32_t it = lane & (kRowIt - 1u), q = lane / kRowIt, rt = wv + it * nwv;
+    uint4 x0 = make_uint4(0, 0, 0, 0), x1 = make_uint4(0, 0, 0, 0);
+    if (rt < nrt && q < 4) {
+      if (q == 0) {
+        x0 = gld4(p.mtb + (static_cast<size_t>(g) * nrt + rt) * 2);
+        x1 = gld4(p.mtb + (static_cast<size_t>(g) * nrt + rt) * 2 + 1);
+      } else if (q == 1) {
+        x0 = gld4(reinterpret_cast<const uint4*>(p.mte + (static_cast<size_t>(g) * nrt + rt) * kEDesc));
+      } else if (cbk[q - 2] != kInvalid) {
+        const uint4* se = p.msum + sum_idx(p, cbk[q - 2], rep, rt, i) * 2;
+        x0 = gld4(se);
+        x1 = gld4(se + 1);
+      }
+    }
+    if (tid >= 64 && tid < 64 + B) T.bmin[tid - 64] = *reinterpret_cast<volatile G<long long>*>(&gbl(p.bmin)[tid - 64]);
+    if (q < 4) {  // (read by this wave only)
+      pf[wv][it][q][0] = x0;
+      pf[wv][it][q][1] = x1;
+    }
+  }
+  RPH(2);
+  const uint32_t L32 = static_cast<uint32_t>(p.L);
+  const uint32_t cq_b = hq.y;
+  const int64_t tx0 = p.tx_tot[0], tx1 = p.tx_tot[1];
+  const uint64_t Lmag = p.L_magic;
+  const unsigned long long lbit = 1ull << lane, lbelow = lbit - 1ull;
+  const uint32_t ne = jz & 0xFFu, n_bc = (jz >> 8) & 0xFFu;
+  const uint32_t h = (fl & kJSd0) ? 0u : 1u;
+  // the source's uniform words: due time, the first edge's sub, payload, frame size
+  const uint4 sa = u4(n_bc ? sj[4] : sj[1 + h]);
+  const uint4 sb5 = u4(sj[5]);
+  const uint32_t u_s0 = n_bc ? sb5.x : sa.z;
+  const uint32_t u_w2 = n_bc ? sb5.z : sa.w;
+  const uint32_t u_w3 = n_bc ? sb5.w : static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0))) | (kPbPrepareRes << 16);
+  const int big = (n_bc && ((u_w3 >> 26) & OPF_BIG)) ? 1 : 0;
+  const int64_t ot = static_cast<int64_t>((static_cast<uint64_t>(sa.y) << 32) | sa.x);
+  const int64_t txu = big ? tx1 : tx0;
+  const uint32_t w3u = (u_w3 & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+  const uint4 q3 = u4(sj[3]);
+  const int64_t et0 = static_cast<int64_t>((static_cast<uint64_t>(q3.y) << 32) | q3.x);
+  const int64_t et1 = static_cast<int64_t>((static_cast<uint64_t>(q3.w) << 32) | q3.z);
+  const int64_t etx0 = (fl & kJBig0) ? tx1 : tx0, etx1 = (fl & kJBig1) ? tx1 : tx0;
+  uint32_t n_rec = 0, st_edges = 0, st_ops = 0;
+  long long ovmin = LLONG_MAX;
+  uint32_t cb = kInvalid, cbn = 0, cmn = ~0u;
+  uint64_t* const lrow = p.link + edge_loc(p, rep, i * N1);
+  auto sidx = [&](uint32_t bk_, uint32_t rt_) { return sum_idx(p, bk_, rep, rt_, i); };
+  // the heavy waves' case, computed once: the link is free by the due time, so every message
+  // starts at it and arrives at one instant in one cell (uniform over the row)
+  const int64_t end_u = ot + txu;
+  uint32_t ca16_u = 0, tof_u = 0, bk_u = 0, w3f_u = 0, hq_u = 0;
+  bool ring_u = false, pfd_u = false;
+  {
+    const int64_t dtf = end_u + prc - cs;
+    if (dtf >= 0 && dtf < (1ll << 32) && end_u < (1ll << 47)) {
+      const uint32_t x = static_cast<uint32_t>(dtf);
+      const uint32_t qq = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), Lmag));
+      ring_u = qq >= 1u && qq < B;
+      ca16_u = static_cast<uint32_t>(cell + qq) & 0xFFFFu;
+      tof_u = x - qq * L32;
+      const uint32_t bq = cr_b + qq;
+      bk_u = bq >= B ? bq - B : bq;
+      w3f_u = w3u | (static_cast<uint32_t>((cq_b + (bq >= B ? 1 : 0)) & 31) << 27);
+      pfd_u = bk_u == cbk[0] || bk_u == cbk[1];
+      hq_u = bk_u == cbk[0] ? 2u : 3u;
+    }
+  }
+  const uint64_t nw_u = (static_cast<uint64_t>(end_u) << 16) | ca16_u;
+  uint32_t nu = 0;  // (this wave's records of the uniform case, all in bucket bk_u)
+#pragma unroll 1
+  for (uint32_t it = 0; it < kRowIt; ++it) {
+    const uint32_t rt = wv + it * nwv;
+    if (rt >= nrt) continue;  // (uniform)
+    const uint32_t s = rt * 64u + lane;
+    const bool v = s < N && s != i;
+    const uint32_t le = s < i ? s : s - 1;
+    const uint64_t lw0 = lwl[wv][it][lane];
+    const uint32_t lc0 = static_cast<uint32_t>(lw0 & 0xFFFFu);
+    bool has = v;
+    uint32_t u_sub = u_s0;
+    if (!n_bc) {  // the reply descriptor's bitmap of this tile: sub = first sub + rank
+      const uint4 mb = pf[wv][it][0][h];
+      const unsigned long long m = (static_cast<unsigned long long>(mb.y) << 32) | mb.x;
+      has = v && (m & lbit);
+      u_sub = u_s0 + mb.z + static_cast<uint32_t>(__popcll(m & lbelow)) - le;
+    }
+    int64_t bu = static_cast<int64_t>(lw0 >> 16);
+    bool pe = false;
+    if (ne) {  // pending echo descriptors, oldest first
+      const uint4 em = pf[wv][it][1][0];
+      const unsigned long long m0 = (static_cast<unsigned long long>(em.y) << 32) | em.x;
+      const bool h0 = v && (m0 & lbit);
+      bu = h0 ? (bu > et0 ? bu : et0) + etx0 : bu;
+      pe = h0;
+      if (ne > 1) {
+        const unsigned long long m1 = (static_cast<unsigned long long>(em.w) << 32) | em.z;
+        const bool h1 = v && (m1 & lbit);
+        bu = h1 ? (bu > et1 ? bu : et1) + etx1 : bu;
+        pe = pe || h1;
+      }
+    }
+    // the uniform case: every edge with a message finds its link free by the due time (after its
+    // pending echoes) and owns the arrival cell -- the tile's records are one summary entry (the
+    // lanes with the first one's base), the link words one value
+    if (ring_u && __ballot(has && !(bu <= ot && lc0 != ca16_u)) == 0ull) {
+      const unsigned long long hm = __ballot(has);
+      if (hm) {
+        const uint32_t r_base = n_bc ? u_s0 : static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(u_sub), __ffsll(static_cast<long long>(hm)) - 1));
+        bool uni = has && u_sub == r_base;
+        unsigned long long um = __ballot(uni);
+        uint4* const se = p.msum + sidx(bk_u, rt) * 2;
+        const uint4 oa = pf[wv][it][hq_u][0], ob = pf[wv][it][hq_u][1];
+        const bool olive = (oa.x | oa.y) != 0u && slot_live(ob.y >> 24, w3f_u >> 27);
+        if (!pfd_u || (olive && (oa.z != tof_u || oa.w != r_base || ob.x != u_w2 || ob.y != w3f_u))) um = 0ull;
+        if (um) {
+          const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oa.y) << 32) | oa.x) : 0ull);
+          if (lane < 2u)
+            gst4(se + lane, lane ? make_uint4(u_w2, w3f_u, 0u, 0u)
+                                 : make_uint4(static_cast<uint32_t>(mm), static_cast<uint32_t>(mm >> 32), tof_u, r_base));
+        }
+        uni = (um >> lane) & 1ull;
+        if (has && !uni) {  // (another base: a slot record)
+          gst4(p.inbox + inbox_idx(p, bk_u, rep, s * N1 + (i < s ? i : i - 1)), make_uint4(tof_u, u_sub + le, u_w2, w3f_u));
+          gbl(p.xsum)[sidx(bk_u, rt)] = static_cast<uint8_t>(0x80u | (w3f_u >> 27));
+        }
+        if (lane == 0) gbl(p.rtile)[kRtPad * ((static_cast<size_t>(bk_u) * p.R + rep) * nrt + rt)] = 1;
+        nu += static_cast<uint32_t>(__popcll(hm));
+      }
+      if (has) {
+        ++n_rec;
+        if (!n_bc) ++st_ops;
+      }
+      if (has || pe) {
+        ++st_edges;
+        gbl(lrow)[le] = has ? nw_u : ((static_cast<uint64_t>(bu) << 16) | lc0);
+      }
+      continue;
+    }
+    // the message through the FIFO (k_mesh_tile's emit)
+    const int64_t start = bu > ot ? bu : ot;
+    const int64_t end = start + txu;
+    const int64_t ta = end + prc;
+    long long ca;
+    uint32_t tof;
+    {
+      const int64_t dtf = ta - cs;
+      if (dtf >= 0 && dtf < (1ll << 32)) {
+        const uint32_t x = static_cast<uint32_t>(dtf);
+        const uint32_t qq = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), Lmag));
+        ca = cell + qq;
+        tof = x - qq * L32;
+      } else {
+        ca = ta / p.L;
+        tof = static_cast<uint32_t>(ta - ca * p.L);
+      }
+    }
+    const long long rel = ca - cell;
+    if (has && rel < 1) set_err(p, BCSIM_E_TIE);  // lookahead violated
+    const bool emit = has && rel >= 1;
+    const bool owner = lc0 != (static_cast<uint32_t>(ca) & 0xFFFFu);
+    const bool inring = rel < static_cast<long long>(B);
+    const uint32_t bq = cr_b + static_cast<uint32_t>(inring ? rel : 0);
+    const bool wrap = bq >= B;
+    const uint32_t bk = wrap ? bq - B : bq;
+    const uint32_t w3f = w3u | (static_cast<uint32_t>((cq_b + (wrap ? 1 : 0)) & 31) << 27);
+    const bool ok = emit && inring && owner;  // the edge's slot record of its arrival cell
+    // (summaries) as k_mesh_tile: the ok lanes with the first one's bucket, offset and base
+    const unsigned long long okm = __ballot(ok);
+    bool uni = false;
+    if (okm) {
+      const int q = __ffsll(static_cast<long long>(okm)) - 1;
+      auto rl = [](uint32_t x, int k) { return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), k)); };
+      const uint32_t r_tof = rl(tof, q), r_base = rl(u_sub, q), r_w3 = rl(w3f, q), r_bk = rl(bk, q);
+      uni = ok && tof == r_tof && u_sub == r_base && bk == r_bk;
+      unsigned long long um = __ballot(uni);
+      uint4* const se = p.msum + sidx(r_bk, rt) * 2;
+      // the entry an earlier launch may have left for this (bucket, tile, sender) turn: prefetched
+      // for the buckets an idle link delivers in; in any other bucket (a busy link) the records
+      // are written as records
+      const bool pfd = r_bk == cbk[0] || r_bk == cbk[1];
+      const uint32_t hq = r_bk == cbk[0] ? 2u : 3u;
+      const uint4 oa = pf[wv][it][hq][0], ob = pf[wv][it][hq][1];
+      const bool olive = (oa.x | oa.y) != 0u && slot_live(ob.y >> 24, r_w3 >> 27);
+      if (!pfd || (olive && (oa.z != r_tof || oa.w != r_base || ob.x != u_w2 || ob.y != r_w3))) um = 0ull;
+      if (um) {
+        const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oa.y) << 32) | oa.x) : 0ull);
+        if (lane < 2u)
+          gst4(se + lane, lane ? make_uint4(u_w2, r_w3, 0u, 0u)
+                               : make_uint4(static_cast<uint32_t>(mm), static_cast<uint32_t>(mm >> 32), r_tof, r_base));
+      }
+      uni = (um >> lane) & 1ull;
+      // the receiver tile's flag of the bucket(s) written (plain stores: a read-first flag here was
+      // a dependent round trip per tile)
+      if (__ballot(ok && bk != r_bk) == 0ull) {
+        if (lane == 0) gbl(p.rtile)[kRtPad * ((static_cast<size_t>(r_bk) * p.R + rep) * nrt + rt)] = 1;
+      } else if (ok) {
+        gbl(p.rtile)[kRtPad * ((static_cast<size_t>(bk) * p.R + rep) * nrt + rt)] = 1;
+      }
+    }
+    if (emit) {
+      ++n_rec;
+      const uint32_t slot = s * N1 + (i < s ? i : i - 1);
+      const uint4 rv = make_uint4(tof, u_sub + le, u_w2, w3f);
+      if (ok) {
+        if (!uni) {
+          gst4(p.inbox + inbox_idx(p, bk, rep, slot), rv);
+          gbl(p.xsum)[sidx(bk, rt)] = static_cast<uint8_t>(0x80u | (w3f >> 27));
+        }
+      } else {
+        XRec x;
+        __builtin_memcpy(&x.r, &rv, sizeof rv);
+        if (!inring && owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+        x.cell = ca;
+        x.slot = slot;
+        x.g = rep * N + s;
+        if (inring) {
+          row_append(p, T, bk, x);  // a second record of the edge in its arrival cell: extras
+          gbl(p.iflag)[static_cast<size_t>(bk) * p.NT + x.g] = 1;
+        } else {
+          row_append(p, T, B, x);  // beyond the ring: overflow
+          if (ca < ovmin) ovmin = ca;
+        }
+      }
+      if (inring) {
+        if (bk != cb) {
+          if (cbn) {
+            atomicAdd(&T.lcnt[cb], cbn);
+            atomicMin(&T.lmin[cb], cmn);
+          }
+          cb = bk;
+          cbn = 0;
+          cmn = ~0u;
+        }
+        ++cbn;
+        if (tof < cmn) cmn = tof;
+      }
+      if (!n_bc) ++st_ops;
+    }
+    const uint64_t nb = static_cast<uint64_t>(emit ? end : bu);
+    if (emit || pe) {
+      ++st_edges;
+      if (nb >= (1ull << 47)) set_err(p, BCSIM_E_OVERFLOW);
+      gbl(lrow)[le] = (nb << 16) | (emit ? (static_cast<uint32_t>(ca) & 0xFFFFu) : lc0);
+    }
+  }
+  RPH(3);
+  if (cbn) {
+    atomicAdd(&T.lcnt[cb], cbn);
+    atomicMin(&T.lmin[cb], cmn);
+  }
+  if (nu && lane == 0) {
+    atomicAdd(&T.lcnt[bk_u], nu);
+    atomicMin(&T.lmin[bk_u], tof_u);
+  }
+  for (int d = 32; d > 0; d >>= 1) ovmin = min(ovmin, static_cast<long long>(__shfl_xor(ovmin, d, 64)));
+  {
+    const uint32_t c4[4] = {n_bc ? 0u : st_ops, n_rec, st_ops, st_edges};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t ws = wave_sum(c4[k]);
+      if (lane == 0 && ws) atomicAdd(&T.csum[k], ws);
+    }
+  }
+  if (lane == 0 && ovmin != LLONG_MAX) atomicMin(&T.ovmin, ovmin);
+  __syncthreads();
+  // staged extras / overflow records: one atomic per list
+  if (T.xn) {
+    for (uint32_t k = tid; k <= B; k += blockDim.x) {
+      const uint32_t c = T.lst[k];
+      if (!c) continue;
+      uint32_t* ctr = k == B ? p.ov_cnt : &p.x_cnt[k];
+      const uint32_t cap = k == B ? p.cap_ov : p.cap_x;
+      const uint32_t base = gadd_r(ctr, c);
+      if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
+      T.lst[k] = base;
+    }
+    __syncthreads();
+    const uint32_t nx = min(T.xn, kTX);
+    for (uint32_t k = tid; k < nx; k += blockDim.x) {
+      const uint32_t list = T.xm[k] >> 24, at = T.lst[list] + (T.xm[k] & 0xFFFFFFu);
+      const uint4* src = reinterpret_cast<const uint4*>(&T.xs[k]);
+      if (list == B) {
+        if (at < p.cap_ov) {
+          uint4* dst = reinterpret_cast<uint4*>(p.ov + at);
+          gst4(dst, src[0]);
+          gst4(dst + 1, src[1]);
+        }
+      } else if (at < p.cap_x) {
+        uint4* dst = reinterpret_cast<uint4*>(p.xbuf + static_cast<size_t>(list) * p.cap_x + at);
+        gst4(dst, src[0]);
+        gst4(dst + 1, src[1]);
+      }
+    }
+  }
+  // busy buckets and their arrival-time bounds, counters
+  for (uint32_t k = tid; k < B; k += blockDim.x)
+    if (T.lcnt[k]) {
+      gbl(p.bucket_cnt)[k] = 1u;
+      const long long t = (cell + static_cast<long long>((k + B - cr_b) % B)) * p.L + T.lmin[k];  // (bucket_t0)
+      if (t < T.bmin[k]) __hip_atomic_fetch_min(gbl(p.bmin) + k, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  if (tid == 0) {
+    unsigned long long* cnt = cnt_stripe(p, rep);
+    unsigned long long* ks = kst_stripe(p);
+    if (T.csum[0]) gadd(&cnt[CNT_SENDS], static_cast<unsigned long long>(T.csum[0]));
+    if (T.csum[1]) gadd(&ks[KST_REC], static_cast<unsigned long long>(T.csum[1]));
+    if (T.csum[2]) gadd(&ks[KST_OPS], static_cast<unsigned long long>(T.csum[2]));
+    if (T.csum[3]) gadd(&ks[KST_EDGES], static_cast<unsigned long long>(T.csum[3]));
+    if (T.ovmin != LLONG_MAX) __hip_atomic_fetch_min(gbl(p.scal) + 1, T.ovmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  RPH(4);
+  RPH(5);
+#undef RPH
 }
 
 // ---------------------------------------------------------------------------
@@ -7062,8 +7503,7 @@ __device__ __attribute__((always_inline)) inline void gossip_link_body(const KP*
   Op* const ops_p = p.ops + op_base(p, g);
   const RawOp o_p = ld_raw(ops_p + min(j, op_cap(p, g) - 1u));
   const uint8_t f8 = AT(p.iflag, static_cast<size_t>(ib) * p.NT + g, static_cast<uint64_t>(B) * p.NT);
-  const uint8_t t8 = p.mesh ? AT(p.rtile, (static_cast<size_t>(ib) * p.R + rep) * p.n_tiles + (i >> 6),
-                                 static_cast<uint64_t>(B) * p.R * p.n_tiles)
+  const uint8_t t8 = p.mesh ? AT(p.rtile, kRtPad * ((static_cast<size_t>(ib) * p.R + rep) * p.n_tiles + (i >> 6)), kRtPad * (static_cast<uint64_t>(B) * p.R * p.n_tiles))
                             : static_cast<uint8_t>(0);
   const uint32_t n0l = AT(p.n_ops, g, p.NT);
   const long long onl = AT(p.node_onext, g, p.NT);
@@ -7952,8 +8392,7 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
     const uint32_t g = (k / p.nloc) * p.N + p.nlo + k % p.nloc;
     const uint32_t rep = g / p.N, i = g % p.N;
     const uint8_t f8 = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
-    const uint8_t t8 = p.mesh ? AT(p.rtile, (static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6),
-                                   static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles)
+    const uint8_t t8 = p.mesh ? AT(p.rtile, kRtPad * ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6)), kRtPad * (static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles))
                               : static_cast<uint8_t>(0);
     const long long tn = AT(p.node_tnext, g, p.NT), on = AT(p.node_onext, g, p.NT);
     const uint8_t sfb = gbl(sfa)[p.eslot ? static_cast<size_t>(obp) * p.NT + g : 0u];
@@ -8218,16 +8657,24 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
             }
             continue;
           }
+          // (every word the leader's tick reads, loaded before its first store: the trace record's
+          // atomic and stores made the compiler issue each later load as its own round trip)
           uint32_t sub = AT(p.sub, g, p.NT);
           const uint32_t deg = AT(p.row, i + 1, p.N + 1) - AT(p.row, i, p.N + 1);
           const int32_t n_seq = AT(p.g_n, rep, p.R);
-          const Key tkey{tk, ts_tick, i, AT(p.tick_sub, g, p.NT)};
+          const uint32_t tsub = AT(p.tick_sub, g, p.NT);
+          uint32_t nops = AT(p.n_ops, g, p.NT);
+          uint64_t draws = AT(p.draws, g, p.NT);
+          const int32_t ldr = AT(p.leader, g, p.NT);
+          const uint32_t gpos = AT(p.glibc_pos, rep, p.R);
+          const int32_t gr = (p.pbft_view_change && p.rng_mode == BCSIM_RNG_GLIBC)
+                                 ? AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + (gpos % p.glibc_len), p.cap_glibc)
+                                 : 0;
+          const Key tkey{tk, ts_tick, i, tsub};
           emit_trace(p, tkey, rep, i, BCSIM_TR_PBFT_BLOCK, n_seq, v_cur, 0);  // :387 leader log
           // block = generateTX header '1', v, n, n (:79-95)
           Msg blk = mkmsg(PB_PRE_PREPARE, enc_raw(p, v_cur), enc_raw(p, n_seq), enc_raw(p, n_seq), 1);
-          uint32_t nops = AT(p.n_ops, g, p.NT);
           Op* ops = p.ops + op_base(p, g);
-          uint64_t draws = AT(p.draws, g, p.NT);
           auto push_bcast = [&](const Msg& m) {
             if (nops >= p.cap_ops) {
               set_err(p, BCSIM_E_OVERFLOW);
@@ -8248,14 +8695,14 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
           if (p.pbft_view_change) {  // rand() % 100 == 5 -> viewChange() :401-403
             int32_t r;
             if (p.rng_mode == BCSIM_RNG_GLIBC) {
-              const uint32_t pos = AT(p.glibc_pos, rep, p.R)++;
-              if (pos >= p.glibc_len) set_err(p, BCSIM_E_OVERFLOW);
-              r = AT(p.glibc, static_cast<size_t>(rep) * p.glibc_len + (pos % p.glibc_len), p.cap_glibc);
+              if (gpos >= p.glibc_len) set_err(p, BCSIM_E_OVERFLOW);
+              AT(p.glibc_pos, rep, p.R) = gpos + 1;
+              r = gr;
             } else {
               r = ctr_rand(p.seed, rep, i, draws++);
             }
             if (r % 100 == 5) {  // viewChange :293-303
-              const int32_t nl = (AT(p.leader, g, p.NT) + 1) % static_cast<int32_t>(N);
+              const int32_t nl = (ldr + 1) % static_cast<int32_t>(N);
               AT(p.leader, g, p.NT) = nl;
               v_cur += 1;
               emit_vlog(p, tkey, rep, i, v_cur);
@@ -8276,9 +8723,56 @@ __global__ __launch_bounds__(1024) void k_pbft_tick(const KP* __restrict__ pk, l
   // (prefix over the leader flags), reschedule, stop check.
   __shared__ int32_t chunk_base;
   __shared__ int32_t sc[1024];
+  if (N <= 4096u) {
+    // (one chunk: the leader bits of lmask, a prefix of their popcounts per word, and each lane's
+    // nodes with all their words loaded at once -- no scan barriers between dependent loads)
+    if (tid < 64) {
+      const int32_t c = __popcll(lmask[tid]);
+      int32_t x = c;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(x, off, 64);
+        if (tid >= static_cast<uint32_t>(off)) x += y;
+      }
+      sc[tid] = x - c;
+    }
+    __syncthreads();
+    uint8_t al[4];
+    uint32_t fs[4], ss[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t g = rep * N + min(u * blockDim.x + tid, N - 1u);
+      al[u] = AT(p.tick_alive, g, p.NT);
+      fs[u] = AT(p.tick_sub, g, p.NT);
+      ss[u] = AT(p.sub, g, p.NT);
+    }
+    int32_t na = 0, nt = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t i = u * blockDim.x + tid;
+      if (i >= N || i < p.nlo || i >= p.nlo + p.nloc || !al[u]) continue;
+      const uint32_t g = rep * N + i;
+      const int32_t nr = nround0 + sc[i >> 6] + __popcll(lmask[i >> 6] & (~0ull >> (63u - (i & 63u))));
+      AT(p.tick_sub, g, p.NT) = ss[u];  // blockEvent = Schedule(Seconds(timeout), SendBlock) :406
+      AT(p.sub, g, p.NT) = ss[u] + 1;
+      ++nt;
+      if (nr == static_cast<int32_t>(p.pbft_rounds)) {  // :407-410
+        emit_trace(p, Key{tk, ts_tick, i, fs[u]}, rep, i, BCSIM_TR_PBFT_STOP, nr, 0, 0);
+        AT(p.tick_alive, g, p.NT) = 0;
+      } else {
+        ++na;
+      }
+    }
+    na = static_cast<int32_t>(wave_sum(static_cast<uint32_t>(na)));
+    nt = static_cast<int32_t>(wave_sum(static_cast<uint32_t>(nt)));
+    if ((tid & 63u) == 0) {
+      if (na) atomicAdd(&n_alive, na);
+      if (nt) atomicAdd(&n_ticked, nt);
+    }
+    __syncthreads();
+  }
   if (tid == 0) chunk_base = 0;
   __syncthreads();
-  for (uint32_t base = 0; base < N; base += blockDim.x) {
+  for (uint32_t base = 0; N > 4096u && base < N; base += blockDim.x) {
     const uint32_t i = base + tid;
     const uint32_t f = (i < N) ? lead[i] : 0u;
     sc[tid] = static_cast<int32_t>(f);
@@ -8409,7 +8903,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
       }
       if (p.mesh)
         for (uint32_t k = tidx(); k < p.R * p.n_tiles; k += blockDim.x)
-          p.rtile[static_cast<size_t>(clr_b) * p.R * p.n_tiles + k] = 0;
+          p.rtile[kRtPad * (static_cast<size_t>(clr_b) * p.R * p.n_tiles + k)] = 0;
     }
   }
   // scal[0] = the next event time (timers and pending ops), scal[3] = the next timer alone;

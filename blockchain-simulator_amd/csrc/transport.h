@@ -22,6 +22,9 @@ constexpr uint64_t kPeerErr = 1ull << 62;
 struct Xport {
   uint32_t rank = 0, nranks = 1;
   virtual ~Xport() = default;
+  // the ranks of the partition may share this rank's GPU (the host-callback transport of the
+  // tests); RCCL runs one rank per device
+  virtual bool shares_device() const { return true; }
   // in-place all-reduce of n int64 host values; op 0 = MIN, 1 = SUM
   virtual int allreduce_i64(hipStream_t st, int64_t* v, uint32_t n, int op) = 0;
   // device segments send_dev + r*stride of send_bytes[r] bytes -> recv_dev,
@@ -59,6 +62,7 @@ struct Xport {
   } while (0)
 
 struct RcclXport : Xport {
+  bool shares_device() const override { return false; }
   ncclComm_t comm = nullptr;
   int64_t* d_red = nullptr;    // all-reduce scratch
   uint64_t* d_cnt = nullptr;   // [2][nranks] byte counts
