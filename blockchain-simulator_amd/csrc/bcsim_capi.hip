@@ -780,7 +780,11 @@ static int setup_device(Sim& s) {
       s.sum = s.mesh_tile && s.scan_fast && p.desc && s.P == 1 && c.protocol == BCSIM_PBFT && p.prop_const >= 0 &&
               nsum * 33 <= (8ull << 30) && !(sm && *sm == '0');
       p.sum = s.sum ? 1u : 0u;
-      if ((rc = dalloc(s, &p.msum, s.sum ? nsum * 2 : 1)) || (rc = dalloc(s, &p.xsum, s.sum ? nsum : 1))) return rc;
+      if ((rc = dalloc(s, &p.msum, s.sum ? nsum * 2 : 1)) || (rc = dalloc(s, &p.xsum, s.sum ? nsum : 1)) ||
+          (rc = dalloc(s, &p.rul, s.sum ? NT : 1)) || (rc = dalloc(s, &p.rex, s.sum ? static_cast<size_t>(NT) * p.n_tiles : 1)))
+        return rc;
+      HIPCHK(hipMemset(p.rul, 0, (s.sum ? NT : 1) * 8));  // (no row-uniform state: every word its own)
+      HIPCHK(hipMemset(p.rex, 0, (s.sum ? static_cast<size_t>(NT) * p.n_tiles : 1) * 8));
       HIPCHK(hipMemset(p.msum, 0, (s.sum ? nsum * 2 : 1) * 16));
       HIPCHK(hipMemset(p.xsum, 0, s.sum ? nsum : 1));
       if (const char* rm = std::getenv("BCSIM_RT_MIN"); rm && *rm) s.rt_min = static_cast<uint32_t>(std::atoi(rm));
@@ -1472,15 +1476,16 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       if ((rc = launch(s, -1, k_link_mesh<true, 1, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, z, z)) ||
           (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
-    } else if (s.mesh_tile && n_link >= s.tile_min) {
+    } else if (s.mesh_tile && (n_link >= s.tile_min || s.sum)) {  // (summary mode: k_mesh_row keeps row-uniform link state)
       // the simple nodes' edges by 32 x 64 (sender x receiver) tiles; a launch
       // epoch tells this launch's jobs from stale ones
       const uint32_t ep = ++s.mesh_epoch == 0 ? ++s.mesh_epoch : s.mesh_epoch;
       const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
       if ((rc = launch(s, -1, k_mesh_prep, grid, dim3(64), 0, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
           // (summary mode: the uniform jobs' rows; the tiles take the rest)
-          (s.sum && (rc = launch(s, -1, k_mesh_row, grid, dim3(kRowThreads), 0, s.kp_dev, cell, lo, hi, ep, row_hq(s, cell, lo, hi)))) ||
-          (s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, grid.x))) ||
+          (s.sum && (rc = launch(s, -1, k_mesh_row, dim3((n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)), dim3(kRowThreads), 0,
+                                 s.kp_dev, cell, lo, hi, ep, row_hq(s, cell, lo, hi)))) ||
+          (s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, (n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)))) ||
           (!s.sum && (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(kTileThreads), 0, s.kp_dev, cell, lo, hi, ep))) ||
           (!s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, nt))) ||
           (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))

@@ -168,6 +168,12 @@ struct KP {
   uint32_t sum;
   GP(uint4) msum;            // [B][R][n_tiles][N][2]
   GP(uint8_t) xsum;          // [B][R][n_tiles][N]
+  // (summary mode) row-uniform link state: rul[g] = 1 << 63 | w means that every out-edge of gnode g
+  // whose receiver's bit in rex[g] is clear has the link word w (k_mesh_row keeps a heavy wave's
+  // rows so: one word per sender instead of 4095); 0 = the physical words hold every edge.  The
+  // generic link stage writes the words out first (rul_flush)
+  GP(uint64_t) rul;          // [NT]
+  GP(uint64_t) rex;          // [NT][n_tiles] bit k: receiver tile * 64 + k's edge has its own word
   // list-2 overlap: k_scan_pbft stamps the nodes it leaves to the generic kernels
   // with the window's epoch; their scan and link stage run on a second stream beside the other
   // nodes' link stage, which skips them.  loop_list: the list k_link<.., LOOP> walks (3; 2 in
@@ -5516,6 +5522,22 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
 __device__ void node_desc_flush(const KP& p, uint32_t g, long long cell, long long t_lo);
 // (FQCODEL: at most 256 lanes, so that the per-edge queue-disc walk gets the registers it needs
 // instead of spilling them -- 168 B/lane of scratch under the 1024-lane bound)
+// (summary mode) gnode g's row-uniform link state written out to its out-edges' words (the
+// generic kernels read and write physical words only); every thread of the workgroup calls it
+__device__ void rul_flush(const KP& p, uint32_t g) {
+  const uint64_t ru = gbl(p.rul)[g];
+  if (!(ru >> 63)) return;  // (uniform)
+  const uint32_t rep = g / p.N, i = g % p.N, N1 = p.N - 1;
+  const uint64_t w = ru & ~(1ull << 63);
+  uint64_t* lrow = p.link + edge_loc(p, rep, i * N1);
+  for (uint32_t le = tidx(); le < N1; le += blockDim.x) {
+    const uint32_t s = le < i ? le : le + 1;
+    if (!((gbl(p.rex)[static_cast<size_t>(g) * p.n_tiles + (s >> 6)] >> (s & 63u)) & 1ull)) gbl(lrow)[le] = w;
+  }
+  __syncthreads();
+  if (tidx() == 0) gbl(p.rul)[g] = 0ull;
+}
+
 template <int QM, bool XR, bool LOOP = false>
 __global__ __launch_bounds__(QM == 2 ? 256 : 1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                               long long t_hi, int final_win) {
@@ -5527,6 +5549,7 @@ __global__ __launch_bounds__(QM == 2 ? 256 : 1024) void k_link(const KP* __restr
       const uint32_t g = p.act[static_cast<size_t>(ll) * p.NT + lr.k];
       // (the nodes the descriptor-aware kernels handed on: their descriptors first, as
       // pending echoes on the link words and reply slots -- this kernel knows no descriptors)
+      if (!QM && !XR && p.sum) rul_flush(p, g);  // (then its descriptors, below)
       if (!QM && !XR && p.desc) {
         node_desc_flush(p, g, cell, t_lo);
         __syncthreads();
@@ -7029,7 +7052,7 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
 // k_mesh_tile), any other slot record is stored directly, and second records of an edge
 // (extras) and records beyond the ring (overflow) are staged in LDS and appended with one
 // atomic per list.  The per-edge work and its results are k_mesh_tile's.
-constexpr uint32_t kRowThreads = 512, kRowIt = 8;  // (<= 64 receiver tiles over eight waves)
+constexpr uint32_t kRowThreads = 256;  // four senders per workgroup, one wave each
 struct RowShared {
   XRec xs[kTX];
   uint32_t xm[kTX];  // list << 24 | rank
@@ -7061,17 +7084,13 @@ __device__ inline void row_append(const KP& p, RowShared& T, uint32_t list, cons
   gst4(dst, src[0]);
   gst4(dst + 1, src[1]);
 }
-__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_mesh_row(
+__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_mesh_row(
     const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi, uint32_t epoch, uint4 hq) {
-  // hq (host arithmetic, no 64-bit divisions per workgroup): {cell % B, (cell / B) % 32, the
-  // buckets a small message sent in [t_lo, t_hi) lands in on an idle link (0xFFFF: outside the
-  // ring) as lo | hi << 16, 0}
+  // hq (host arithmetic, no 64-bit divisions here): {cell % B, (cell / B) % 32, the bucket a small
+  // message sent at t_lo lands in on an idle link (0xFFFF: outside the ring), 0}
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ RowShared T;
-  __shared__ uint4 sj[6];                       // job words, the broadcast's RawOp words
-  __shared__ uint4 pf[kRowThreads / 64][kRowIt][4][2];  // per wave and tile: reply bitmaps (h = 0, 1), echo bitmaps, entries
-  __shared__ uint64_t lwl[kRowThreads / 64][kRowIt][64];  // per wave and tile: the link words (parked: no registers across the walk)
   const uint32_t tid = tidx(), lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
   G<unsigned long long>* tph = p.wgtt ? gbl(p.wgtt) + 8ull * blockIdx.x : nullptr;  // (debug phase clocks)
 #define RPH(k)                                                       \
@@ -7079,23 +7098,26 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(6, 
     if (tph && tid == 0) tph[(k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
   RPH(0);
-  uint32_t kk;
-  if (!list_one(p.act_n[1], kk)) return;
-  const uint32_t g = p.act[p.NT + kk];
-  RPH(1);
   const uint32_t N = p.N, N1 = N - 1, B = p.n_buckets, nrt = p.n_tiles;
-  const uint32_t rep = g / N, i = g % N;
   const int64_t prc = p.prop_const;
   const long long cs = cell * p.L;
-  const uint32_t cr_b = hq.x;
-  // the job first (a node without a uniform job leaves before loading its row), then ONE round
-  // of loads: the link words of every wave's tiles, and per tile the bitmaps and the summary
-  // entries of the (at most two) buckets a small message sent in this window lands in on an idle
-  // link.  No load after these: a load in the walk (or a register move of a pending load's
-  // destination) made the compiler wait for every outstanding memory operation, the stores
-  // included, once per tile
-  if (tid < 4) sj[tid] = gld4(p.mjob + static_cast<size_t>(g) * 4 + tid);
-  else if (tid < 6) sj[tid] = gld4(p.mbc + static_cast<size_t>(g) * kMeshBc * 2 + (tid - 4));
+  const uint32_t cr_b = hq.x, cq_b = hq.y;
+  const uint32_t cbk0 = (hq.z & 0xFFFFu) == 0xFFFFu ? kInvalid : (hq.z & 0xFFFFu);
+  auto rl = [](uint32_t x, uint32_t k) { return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), static_cast<int>(k))); };
+  // this wave's sender (list-1 entry blockIdx * 4 + wave) and, all at once, its job words (lanes
+  // 0-3), its broadcast (4-5) and its row's uniform link word (6)
+  const uint32_t kk = blockIdx.x * nwv + wv;
+  bool act = kk < p.act_n[1];
+  const uint32_t g = act ? rl(p.act[p.NT + kk], 0) : 0u;
+  uint4 jw = make_uint4(0, 0, 0, 0);
+  if (act) {
+    if (lane < 4) jw = gld4(p.mjob + static_cast<size_t>(g) * 4 + lane);
+    else if (lane < 6) jw = gld4(p.mbc + static_cast<size_t>(g) * kMeshBc * 2 + (lane - 4));
+    else if (lane == 6) {
+      const uint64_t r = gbl(p.rul)[g];
+      jw = make_uint4(static_cast<uint32_t>(r), static_cast<uint32_t>(r >> 32), 0u, 0u);
+    }
+  }
   for (uint32_t k = tid; k < B; k += blockDim.x) {
     T.lcnt[k] = 0;
     T.lmin[k] = ~0u;
@@ -7106,276 +7128,263 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(6, 
     T.ovmin = LLONG_MAX;
     T.xn = 0;
   }
-  __syncthreads();
-  // (the job words are uniform: scalar registers)
-  auto u = [](uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x))); };
-  auto u4 = [&](const uint4& x) { return make_uint4(u(x.x), u(x.y), u(x.z), u(x.w)); };
-  const uint32_t fl = u(sj[0].y), jz = u(sj[0].z);
-  if (u(sj[0].x) != epoch || !job_uniform(fl, jz, prc)) {  // (uniform)
-    if (tph && tid == 0) tph[0] = 0;
-    return;
-  }
-  {
-    uint64_t lw[kRowIt];
-#pragma unroll
-    for (uint32_t it = 0; it < kRowIt; ++it) {
-      const uint32_t s = (wv + it * nwv) * 64u + lane;
-      const uint32_t sc = s < N ? s : N - 1u;  // (clamped, unconditional: see k_scan_pbft's row loads)
-      lw[it] = gbl(p.link)[edge_loc(p, rep, i * N1 + (sc < i ? sc : (sc == i ? 0u : sc - 1)))];
-    }
-#pragma unroll
-    for (uint32_t it = 0; it < kRowIt; ++it) lwl[wv][it][lane] = lw[it];
-  }
-  uint32_t cbk[2] = {hq.z & 0xFFFFu, hq.z >> 16};
-  cbk[0] = cbk[0] == 0xFFFFu ? kInvalid : cbk[0];
-  cbk[1] = (cbk[1] == 0xFFFFu || cbk[1] == cbk[0]) ? kInvalid : cbk[1];
-  {
-    const uint32_t it = lane & (kRowIt - 1u), q = lane / kRowIt, rt = wv + it * nwv;
-    uint4 x0 = make_uint4(0, 0, 0, 0), x1 = make_uint4(0, 0, 0, 0);
-    if (rt < nrt && q < 4) {
-      if (q == 0) {
-        x0 = gld4(p.mtb + (static_cast<size_t>(g) * nrt + rt) * 2);
-        x1 = gld4(p.mtb + (static_cast<size_t>(g) * nrt + rt) * 2 + 1);
-      } else if (q == 1) {
-        x0 = gld4(reinterpret_cast<const uint4*>(p.mte + (static_cast<size_t>(g) * nrt + rt) * kEDesc));
-      } else if (cbk[q - 2] != kInvalid) {
-        const uint4* se = p.msum + sum_idx(p, cbk[q - 2], rep, rt, i) * 2;
-        x0 = gld4(se);
-        x1 = gld4(se + 1);
-      }
-    }
-    if (tid >= 64 && tid < 64 + B) T.bmin[tid - 64] = *reinterpret_cast<volatile G<long long>*>(&gbl(p.bmin)[tid - 64]);
-    if (q < 4) {  // (read by this wave only)
-      pf[wv][it][q][0] = x0;
-      pf[wv][it][q][1] = x1;
-    }
-  }
-  RPH(2);
-  const uint32_t L32 = static_cast<uint32_t>(p.L);
-  const uint32_t cq_b = hq.y;
-  const int64_t tx0 = p.tx_tot[0], tx1 = p.tx_tot[1];
-  const uint64_t Lmag = p.L_magic;
-  const unsigned long long lbit = 1ull << lane, lbelow = lbit - 1ull;
+  if (tid >= 64 && tid < 64 + B) T.bmin[tid - 64] = *reinterpret_cast<volatile G<long long>*>(&gbl(p.bmin)[tid - 64]);
+  const uint32_t fl = rl(jw.y, 0), jz = rl(jw.z, 0);
+  act = act && rl(jw.x, 0) == epoch && job_uniform(fl, jz, prc);
   const uint32_t ne = jz & 0xFFu, n_bc = (jz >> 8) & 0xFFu;
   const uint32_t h = (fl & kJSd0) ? 0u : 1u;
-  // the source's uniform words: due time, the first edge's sub, payload, frame size
-  const uint4 sa = u4(n_bc ? sj[4] : sj[1 + h]);
-  const uint4 sb5 = u4(sj[5]);
-  const uint32_t u_s0 = n_bc ? sb5.x : sa.z;
-  const uint32_t u_w2 = n_bc ? sb5.z : sa.w;
-  const uint32_t u_w3 = n_bc ? sb5.w : static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0))) | (kPbPrepareRes << 16);
-  const int big = (n_bc && ((u_w3 >> 26) & OPF_BIG)) ? 1 : 0;
-  const int64_t ot = static_cast<int64_t>((static_cast<uint64_t>(sa.y) << 32) | sa.x);
-  const int64_t txu = big ? tx1 : tx0;
-  const uint32_t w3u = (u_w3 & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
-  const uint4 q3 = u4(sj[3]);
-  const int64_t et0 = static_cast<int64_t>((static_cast<uint64_t>(q3.y) << 32) | q3.x);
-  const int64_t et1 = static_cast<int64_t>((static_cast<uint64_t>(q3.w) << 32) | q3.z);
-  const int64_t etx0 = (fl & kJBig0) ? tx1 : tx0, etx1 = (fl & kJBig1) ? tx1 : tx0;
-  uint32_t n_rec = 0, st_edges = 0, st_ops = 0;
+  const uint32_t rep = g / N, i = g % N;
+  // per receiver tile k (lane k): its exception bits, reply bitmap {lo, hi, rank base}, pending
+  // echo bitmaps, and the summary entry of the bucket an idle link delivers in -- one round
+  uint64_t rexo = 0;
+  uint4 tmb = make_uint4(0, 0, 0, 0), tme = make_uint4(0, 0, 0, 0), soa = make_uint4(0, 0, 0, 0), sob = make_uint4(0, 0, 0, 0);
+  if (act && lane < nrt) {
+    rexo = gbl(p.rex)[static_cast<size_t>(g) * nrt + lane];
+    if (!n_bc) tmb = gld4(p.mtb + (static_cast<size_t>(g) * nrt + lane) * 2 + h);
+    if (ne) tme = gld4(reinterpret_cast<const uint4*>(p.mte + (static_cast<size_t>(g) * nrt + lane) * kEDesc));
+    if (cbk0 != kInvalid) {
+      const uint4* se = p.msum + sum_idx(p, cbk0, rep, lane, i) * 2;
+      soa = gld4(se);
+      sob = gld4(se + 1);
+    }
+  }
+  RPH(1);
+  uint32_t n_rec = 0, st_edges = 0, st_ops = 0, nu = 0;
   long long ovmin = LLONG_MAX;
   uint32_t cb = kInvalid, cbn = 0, cmn = ~0u;
-  uint64_t* const lrow = p.link + edge_loc(p, rep, i * N1);
-  auto sidx = [&](uint32_t bk_, uint32_t rt_) { return sum_idx(p, bk_, rep, rt_, i); };
-  // the heavy waves' case, computed once: the link is free by the due time, so every message
-  // starts at it and arrives at one instant in one cell (uniform over the row)
-  const int64_t end_u = ot + txu;
-  uint32_t ca16_u = 0, tof_u = 0, bk_u = 0, w3f_u = 0, hq_u = 0;
-  bool ring_u = false, pfd_u = false;
-  {
-    const int64_t dtf = end_u + prc - cs;
-    if (dtf >= 0 && dtf < (1ll << 32) && end_u < (1ll << 47)) {
-      const uint32_t x = static_cast<uint32_t>(dtf);
-      const uint32_t qq = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), Lmag));
-      ring_u = qq >= 1u && qq < B;
-      ca16_u = static_cast<uint32_t>(cell + qq) & 0xFFFFu;
-      tof_u = x - qq * L32;
-      const uint32_t bq = cr_b + qq;
-      bk_u = bq >= B ? bq - B : bq;
-      w3f_u = w3u | (static_cast<uint32_t>((cq_b + (bq >= B ? 1 : 0)) & 31) << 27);
-      pfd_u = bk_u == cbk[0] || bk_u == cbk[1];
-      hq_u = bk_u == cbk[0] ? 2u : 3u;
-    }
-  }
-  const uint64_t nw_u = (static_cast<uint64_t>(end_u) << 16) | ca16_u;
-  uint32_t nu = 0;  // (this wave's records of the uniform case, all in bucket bk_u)
-#pragma unroll 1
-  for (uint32_t it = 0; it < kRowIt; ++it) {
-    const uint32_t rt = wv + it * nwv;
-    if (rt >= nrt) continue;  // (uniform)
-    const uint32_t s = rt * 64u + lane;
-    const bool v = s < N && s != i;
-    const uint32_t le = s < i ? s : s - 1;
-    const uint64_t lw0 = lwl[wv][it][lane];
-    const uint32_t lc0 = static_cast<uint32_t>(lw0 & 0xFFFFu);
-    bool has = v;
-    uint32_t u_sub = u_s0;
-    if (!n_bc) {  // the reply descriptor's bitmap of this tile: sub = first sub + rank
-      const uint4 mb = pf[wv][it][0][h];
-      const unsigned long long m = (static_cast<unsigned long long>(mb.y) << 32) | mb.x;
-      has = v && (m & lbit);
-      u_sub = u_s0 + mb.z + static_cast<uint32_t>(__popcll(m & lbelow)) - le;
-    }
-    int64_t bu = static_cast<int64_t>(lw0 >> 16);
-    bool pe = false;
-    if (ne) {  // pending echo descriptors, oldest first
-      const uint4 em = pf[wv][it][1][0];
-      const unsigned long long m0 = (static_cast<unsigned long long>(em.y) << 32) | em.x;
-      const bool h0 = v && (m0 & lbit);
-      bu = h0 ? (bu > et0 ? bu : et0) + etx0 : bu;
-      pe = h0;
-      if (ne > 1) {
-        const unsigned long long m1 = (static_cast<unsigned long long>(em.w) << 32) | em.z;
-        const bool h1 = v && (m1 & lbit);
-        bu = h1 ? (bu > et1 ? bu : et1) + etx1 : bu;
-        pe = pe || h1;
-      }
-    }
-    // the uniform case: every edge with a message finds its link free by the due time (after its
-    // pending echoes) and owns the arrival cell -- the tile's records are one summary entry (the
-    // lanes with the first one's base), the link words one value
-    if (ring_u && __ballot(has && !(bu <= ot && lc0 != ca16_u)) == 0ull) {
-      const unsigned long long hm = __ballot(has);
-      if (hm) {
-        const uint32_t r_base = n_bc ? u_s0 : static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(u_sub), __ffsll(static_cast<long long>(hm)) - 1));
-        bool uni = has && u_sub == r_base;
-        unsigned long long um = __ballot(uni);
-        uint4* const se = p.msum + sidx(bk_u, rt) * 2;
-        const uint4 oa = pf[wv][it][hq_u][0], ob = pf[wv][it][hq_u][1];
-        const bool olive = (oa.x | oa.y) != 0u && slot_live(ob.y >> 24, w3f_u >> 27);
-        if (!pfd_u || (olive && (oa.z != tof_u || oa.w != r_base || ob.x != u_w2 || ob.y != w3f_u))) um = 0ull;
-        if (um) {
-          const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oa.y) << 32) | oa.x) : 0ull);
-          if (lane < 2u)
-            gst4(se + lane, lane ? make_uint4(u_w2, w3f_u, 0u, 0u)
-                                 : make_uint4(static_cast<uint32_t>(mm), static_cast<uint32_t>(mm >> 32), tof_u, r_base));
-        }
-        uni = (um >> lane) & 1ull;
-        if (has && !uni) {  // (another base: a slot record)
-          gst4(p.inbox + inbox_idx(p, bk_u, rep, s * N1 + (i < s ? i : i - 1)), make_uint4(tof_u, u_sub + le, u_w2, w3f_u));
-          gbl(p.xsum)[sidx(bk_u, rt)] = static_cast<uint8_t>(0x80u | (w3f_u >> 27));
-        }
-        if (lane == 0) gbl(p.rtile)[kRtPad * ((static_cast<size_t>(bk_u) * p.R + rep) * nrt + rt)] = 1;
-        nu += static_cast<uint32_t>(__popcll(hm));
-      }
-      if (has) {
-        ++n_rec;
-        if (!n_bc) ++st_ops;
-      }
-      if (has || pe) {
-        ++st_edges;
-        gbl(lrow)[le] = has ? nw_u : ((static_cast<uint64_t>(bu) << 16) | lc0);
-      }
-      continue;
-    }
-    // the message through the FIFO (k_mesh_tile's emit)
-    const int64_t start = bu > ot ? bu : ot;
-    const int64_t end = start + txu;
-    const int64_t ta = end + prc;
-    long long ca;
-    uint32_t tof;
+  uint64_t rexn = 0, rtm = 0;  // (lane k: tile k's new exception bits; bit k: tile k holds records of bucket bk_u)
+  uint32_t tof_u = 0, bk_u = 0;
+  bool ring_u = false;
+  uint64_t nw_u = 0;
+  if (act) {
+    const uint32_t L32 = static_cast<uint32_t>(p.L);
+    const int64_t tx0 = p.tx_tot[0], tx1 = p.tx_tot[1];
+    const uint64_t Lmag = p.L_magic;
+    const unsigned long long lbit = 1ull << lane, lbelow = lbit - 1ull;
+    // the source's uniform words: due time, the first edge's sub, payload, frame size
+    const uint32_t sa_x = rl(n_bc ? jw.x : (h ? jw.x : jw.x), n_bc ? 4 : 1 + h), sa_y = rl(jw.y, n_bc ? 4 : 1 + h);
+    const uint32_t sa_z = rl(jw.z, 1 + h), sa_w = rl(jw.w, 1 + h);
+    const uint32_t u_s0 = n_bc ? rl(jw.x, 5) : sa_z;
+    const uint32_t u_w2 = n_bc ? rl(jw.z, 5) : sa_w;
+    const uint32_t u_w3 = n_bc ? rl(jw.w, 5) : static_cast<uint32_t>(static_cast<uint16_t>(enc_raw(p, 0))) | (kPbPrepareRes << 16);
+    const int big = (n_bc && ((u_w3 >> 26) & OPF_BIG)) ? 1 : 0;
+    const int64_t ot = static_cast<int64_t>((static_cast<uint64_t>(sa_y) << 32) | sa_x);
+    const int64_t txu = big ? tx1 : tx0;
+    const uint32_t w3u = (u_w3 & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+    const int64_t et0 = static_cast<int64_t>((static_cast<uint64_t>(rl(jw.y, 3)) << 32) | rl(jw.x, 3));
+    const int64_t et1 = static_cast<int64_t>((static_cast<uint64_t>(rl(jw.w, 3)) << 32) | rl(jw.z, 3));
+    const int64_t etx0 = (fl & kJBig0) ? tx1 : tx0, etx1 = (fl & kJBig1) ? tx1 : tx0;
+    const uint64_t ru = (static_cast<uint64_t>(rl(jw.y, 6)) << 32) | rl(jw.x, 6);
+    const bool ruv = (ru >> 63) != 0;
+    const uint64_t ruw = ru & ~(1ull << 63);
+    uint64_t* const lrow = p.link + edge_loc(p, rep, i * N1);
+    // the heavy waves' case, computed once: the link is free by the due time, so every message
+    // starts at it and arrives at one instant in one cell (uniform over the row)
+    const int64_t end_u = ot + txu;
+    uint32_t ca16_u = 0, w3f_u = 0;
     {
-      const int64_t dtf = ta - cs;
-      if (dtf >= 0 && dtf < (1ll << 32)) {
+      const int64_t dtf = end_u + prc - cs;
+      if (dtf >= 0 && dtf < (1ll << 32) && end_u < (1ll << 47)) {
         const uint32_t x = static_cast<uint32_t>(dtf);
         const uint32_t qq = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), Lmag));
-        ca = cell + qq;
-        tof = x - qq * L32;
-      } else {
-        ca = ta / p.L;
-        tof = static_cast<uint32_t>(ta - ca * p.L);
+        ring_u = qq >= 1u && qq < B;
+        ca16_u = static_cast<uint32_t>(cell + qq) & 0xFFFFu;
+        tof_u = x - qq * L32;
+        const uint32_t bq = cr_b + qq;
+        bk_u = bq >= B ? bq - B : bq;
+        w3f_u = w3u | (static_cast<uint32_t>((cq_b + (bq >= B ? 1 : 0)) & 31) << 27);
       }
     }
-    const long long rel = ca - cell;
-    if (has && rel < 1) set_err(p, BCSIM_E_TIE);  // lookahead violated
-    const bool emit = has && rel >= 1;
-    const bool owner = lc0 != (static_cast<uint32_t>(ca) & 0xFFFFu);
-    const bool inring = rel < static_cast<long long>(B);
-    const uint32_t bq = cr_b + static_cast<uint32_t>(inring ? rel : 0);
-    const bool wrap = bq >= B;
-    const uint32_t bk = wrap ? bq - B : bq;
-    const uint32_t w3f = w3u | (static_cast<uint32_t>((cq_b + (wrap ? 1 : 0)) & 31) << 27);
-    const bool ok = emit && inring && owner;  // the edge's slot record of its arrival cell
-    // (summaries) as k_mesh_tile: the ok lanes with the first one's bucket, offset and base
-    const unsigned long long okm = __ballot(ok);
-    bool uni = false;
-    if (okm) {
-      const int q = __ffsll(static_cast<long long>(okm)) - 1;
-      auto rl = [](uint32_t x, int k) { return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), k)); };
-      const uint32_t r_tof = rl(tof, q), r_base = rl(u_sub, q), r_w3 = rl(w3f, q), r_bk = rl(bk, q);
-      uni = ok && tof == r_tof && u_sub == r_base && bk == r_bk;
-      unsigned long long um = __ballot(uni);
-      uint4* const se = p.msum + sidx(r_bk, rt) * 2;
-      // the entry an earlier launch may have left for this (bucket, tile, sender) turn: prefetched
-      // for the buckets an idle link delivers in; in any other bucket (a busy link) the records
-      // are written as records
-      const bool pfd = r_bk == cbk[0] || r_bk == cbk[1];
-      const uint32_t hq = r_bk == cbk[0] ? 2u : 3u;
-      const uint4 oa = pf[wv][it][hq][0], ob = pf[wv][it][hq][1];
-      const bool olive = (oa.x | oa.y) != 0u && slot_live(ob.y >> 24, r_w3 >> 27);
-      if (!pfd || (olive && (oa.z != r_tof || oa.w != r_base || ob.x != u_w2 || ob.y != r_w3))) um = 0ull;
-      if (um) {
-        const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oa.y) << 32) | oa.x) : 0ull);
-        if (lane < 2u)
-          gst4(se + lane, lane ? make_uint4(u_w2, r_w3, 0u, 0u)
-                               : make_uint4(static_cast<uint32_t>(mm), static_cast<uint32_t>(mm >> 32), r_tof, r_base));
+    nw_u = (static_cast<uint64_t>(end_u) << 16) | ca16_u;
+    const bool pfd_u = bk_u == cbk0;
+#pragma unroll 1
+    for (uint32_t rt = 0; rt < nrt; ++rt) {
+      const uint32_t s = rt * 64u + lane;
+      const bool v = s < N && s != i;
+      const uint32_t le = s < i ? s : s - 1;
+      const uint64_t xo = (static_cast<uint64_t>(rl(static_cast<uint32_t>(rexo >> 32), rt)) << 32) | rl(static_cast<uint32_t>(rexo), rt);
+      const bool wex = ruv && ((xo >> lane) & 1ull);  // (had its own word under the row's uniform state)
+      // the edge's link word: its own (loaded here: a row's exception edges, or every edge of a
+      // row without a uniform state), else the row's uniform word
+      const bool own = v && (!ruv || wex);
+      uint64_t lw0 = ruw;
+      if (__ballot(own)) {
+        const uint64_t x = own ? gbl(lrow)[le] : 0ull;
+        lw0 = own ? x : ruw;
       }
-      uni = (um >> lane) & 1ull;
-      // the receiver tile's flag of the bucket(s) written (plain stores: a read-first flag here was
-      // a dependent round trip per tile)
-      if (__ballot(ok && bk != r_bk) == 0ull) {
-        if (lane == 0) gbl(p.rtile)[kRtPad * ((static_cast<size_t>(r_bk) * p.R + rep) * nrt + rt)] = 1;
-      } else if (ok) {
-        gbl(p.rtile)[kRtPad * ((static_cast<size_t>(bk) * p.R + rep) * nrt + rt)] = 1;
+      const uint32_t lc0 = static_cast<uint32_t>(lw0 & 0xFFFFu);
+      // its new link word: the row's new uniform word nw_u (no store, exception bit clear), else its
+      // own -- stored when it changed, or when it was the row's old uniform word
+      auto put_lw = [&](uint64_t nv) {
+        const bool un = ring_u && v && nv == nw_u;
+        if (v && !un && (nv != lw0 || (ruv && !wex))) gbl(lrow)[le] = nv;
+        const unsigned long long xm = __ballot(v && !un);
+        rexn = lane == rt ? xm : rexn;
+      };
+      bool has = v;
+      uint32_t u_sub = u_s0;
+      if (!n_bc) {  // the reply descriptor's bitmap of this tile: sub = first sub + rank
+        const unsigned long long m = (static_cast<unsigned long long>(rl(tmb.y, rt)) << 32) | rl(tmb.x, rt);
+        has = v && (m & lbit);
+        u_sub = u_s0 + rl(tmb.z, rt) + static_cast<uint32_t>(__popcll(m & lbelow)) - le;
       }
-    }
-    if (emit) {
-      ++n_rec;
-      const uint32_t slot = s * N1 + (i < s ? i : i - 1);
-      const uint4 rv = make_uint4(tof, u_sub + le, u_w2, w3f);
-      if (ok) {
-        if (!uni) {
-          gst4(p.inbox + inbox_idx(p, bk, rep, slot), rv);
-          gbl(p.xsum)[sidx(bk, rt)] = static_cast<uint8_t>(0x80u | (w3f >> 27));
-        }
-      } else {
-        XRec x;
-        __builtin_memcpy(&x.r, &rv, sizeof rv);
-        if (!inring && owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
-        x.cell = ca;
-        x.slot = slot;
-        x.g = rep * N + s;
-        if (inring) {
-          row_append(p, T, bk, x);  // a second record of the edge in its arrival cell: extras
-          gbl(p.iflag)[static_cast<size_t>(bk) * p.NT + x.g] = 1;
-        } else {
-          row_append(p, T, B, x);  // beyond the ring: overflow
-          if (ca < ovmin) ovmin = ca;
+      int64_t bu = static_cast<int64_t>(lw0 >> 16);
+      bool pe = false;
+      if (ne) {  // pending echo descriptors, oldest first
+        const unsigned long long m0 = (static_cast<unsigned long long>(rl(tme.y, rt)) << 32) | rl(tme.x, rt);
+        const bool h0 = v && (m0 & lbit);
+        bu = h0 ? (bu > et0 ? bu : et0) + etx0 : bu;
+        pe = h0;
+        if (ne > 1) {
+          const unsigned long long m1 = (static_cast<unsigned long long>(rl(tme.w, rt)) << 32) | rl(tme.z, rt);
+          const bool h1 = v && (m1 & lbit);
+          bu = h1 ? (bu > et1 ? bu : et1) + etx1 : bu;
+          pe = pe || h1;
         }
       }
-      if (inring) {
-        if (bk != cb) {
-          if (cbn) {
-            atomicAdd(&T.lcnt[cb], cbn);
-            atomicMin(&T.lmin[cb], cmn);
+      // the uniform case: every edge with a message finds its link free by the due time (after its
+      // pending echoes) and owns the arrival cell -- the tile's records are one summary entry (the
+      // lanes with the first one's base), the link words one value
+      if (ring_u && __ballot(has && !(bu <= ot && lc0 != ca16_u)) == 0ull) {
+        const unsigned long long hm = __ballot(has);
+        if (hm) {
+          const uint32_t r_base = n_bc ? u_s0 : rl(u_sub, static_cast<uint32_t>(__ffsll(static_cast<long long>(hm)) - 1));
+          bool uni = has && u_sub == r_base;
+          unsigned long long um = __ballot(uni);
+          // the entry an earlier launch may have left for this (bucket, tile, sender) turn
+          const uint32_t oax = rl(soa.x, rt), oay = rl(soa.y, rt), oaz = rl(soa.z, rt), oaw = rl(soa.w, rt);
+          const uint32_t obx = rl(sob.x, rt), oby = rl(sob.y, rt);
+          const bool olive = (oax | oay) != 0u && slot_live(oby >> 24, w3f_u >> 27);
+          if (!pfd_u || (olive && (oaz != tof_u || oaw != r_base || obx != u_w2 || oby != w3f_u))) um = 0ull;
+          if (um) {
+            const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oay) << 32) | oax) : 0ull);
+            uint4* const se = p.msum + sum_idx(p, bk_u, rep, rt, i) * 2;
+            if (lane < 2u)
+              gst4(se + lane, lane ? make_uint4(u_w2, w3f_u, 0u, 0u)
+                                   : make_uint4(static_cast<uint32_t>(mm), static_cast<uint32_t>(mm >> 32), tof_u, r_base));
           }
-          cb = bk;
-          cbn = 0;
-          cmn = ~0u;
+          uni = (um >> lane) & 1ull;
+          if (has && !uni) {  // (another base, or an entry of other words: a slot record)
+            gst4(p.inbox + inbox_idx(p, bk_u, rep, s * N1 + (i < s ? i : i - 1)), make_uint4(tof_u, u_sub + le, u_w2, w3f_u));
+            gbl(p.xsum)[sum_idx(p, bk_u, rep, rt, i)] = static_cast<uint8_t>(0x80u | (w3f_u >> 27));
+          }
+          rtm |= 1ull << rt;
+          nu += static_cast<uint32_t>(__popcll(hm));
         }
-        ++cbn;
-        if (tof < cmn) cmn = tof;
+        if (has) {
+          ++n_rec;
+          if (!n_bc) ++st_ops;
+        }
+        if (has || pe) ++st_edges;
+        put_lw(has ? nw_u : pe ? ((static_cast<uint64_t>(bu) << 16) | lc0) : lw0);
+        continue;
       }
-      if (!n_bc) ++st_ops;
+      // the message through the FIFO (k_mesh_tile's emit)
+      const int64_t start = bu > ot ? bu : ot;
+      const int64_t end = start + txu;
+      const int64_t ta = end + prc;
+      long long ca;
+      uint32_t tof;
+      {
+        const int64_t dtf = ta - cs;
+        if (dtf >= 0 && dtf < (1ll << 32)) {
+          const uint32_t x = static_cast<uint32_t>(dtf);
+          const uint32_t qq = static_cast<uint32_t>(__umul64hi(static_cast<uint64_t>(x), Lmag));
+          ca = cell + qq;
+          tof = x - qq * L32;
+        } else {
+          ca = ta / p.L;
+          tof = static_cast<uint32_t>(ta - ca * p.L);
+        }
+      }
+      const long long rel = ca - cell;
+      if (has && rel < 1) set_err(p, BCSIM_E_TIE);  // lookahead violated
+      const bool emit = has && rel >= 1;
+      const bool owner = lc0 != (static_cast<uint32_t>(ca) & 0xFFFFu);
+      const bool inring = rel < static_cast<long long>(B);
+      const uint32_t bq = cr_b + static_cast<uint32_t>(inring ? rel : 0);
+      const bool wrap = bq >= B;
+      const uint32_t bk = wrap ? bq - B : bq;
+      const uint32_t w3f = w3u | (static_cast<uint32_t>((cq_b + (wrap ? 1 : 0)) & 31) << 27);
+      const bool ok = emit && inring && owner;  // the edge's slot record of its arrival cell
+      // (summaries) the ok lanes with the first one's bucket, offset and base -- merged only with a
+      // prefetched entry (the idle-link bucket), else written as records
+      const unsigned long long okm = __ballot(ok);
+      bool uni = false;
+      if (okm) {
+        const uint32_t q = static_cast<uint32_t>(__ffsll(static_cast<long long>(okm)) - 1);
+        const uint32_t r_tof = rl(tof, q), r_base = rl(u_sub, q), r_w3 = rl(w3f, q), r_bk = rl(bk, q);
+        uni = ok && tof == r_tof && u_sub == r_base && bk == r_bk;
+        unsigned long long um = __ballot(uni);
+        const uint32_t oax = rl(soa.x, rt), oay = rl(soa.y, rt), oaz = rl(soa.z, rt), oaw = rl(soa.w, rt);
+        const uint32_t obx = rl(sob.x, rt), oby = rl(sob.y, rt);
+        const bool olive = (oax | oay) != 0u && slot_live(oby >> 24, r_w3 >> 27);
+        if (r_bk != cbk0 || (olive && (oaz != r_tof || oaw != r_base || obx != u_w2 || oby != r_w3))) um = 0ull;
+        if (um) {
+          const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oay) << 32) | oax) : 0ull);
+          uint4* const se = p.msum + sum_idx(p, r_bk, rep, rt, i) * 2;
+          if (lane < 2u)
+            gst4(se + lane, lane ? make_uint4(u_w2, r_w3, 0u, 0u)
+                                 : make_uint4(static_cast<uint32_t>(mm), static_cast<uint32_t>(mm >> 32), r_tof, r_base));
+        }
+        uni = (um >> lane) & 1ull;
+        if (ok) gbl(p.rtile)[kRtPad * ((static_cast<size_t>(bk) * p.R + rep) * nrt + rt)] = 1;
+      }
+      if (emit) {
+        ++n_rec;
+        const uint32_t slot = s * N1 + (i < s ? i : i - 1);
+        const uint4 rv = make_uint4(tof, u_sub + le, u_w2, w3f);
+        if (ok) {
+          if (!uni) {
+            gst4(p.inbox + inbox_idx(p, bk, rep, slot), rv);
+            gbl(p.xsum)[sum_idx(p, bk, rep, rt, i)] = static_cast<uint8_t>(0x80u | (w3f >> 27));
+          }
+        } else {
+          XRec x;
+          __builtin_memcpy(&x.r, &rv, sizeof rv);
+          if (!inring && owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+          x.cell = ca;
+          x.slot = slot;
+          x.g = rep * N + s;
+          if (inring) {
+            row_append(p, T, bk, x);  // a second record of the edge in its arrival cell: extras
+            gbl(p.iflag)[static_cast<size_t>(bk) * p.NT + x.g] = 1;
+          } else {
+            row_append(p, T, B, x);  // beyond the ring: overflow
+            if (ca < ovmin) ovmin = ca;
+          }
+        }
+        if (inring) {
+          if (bk != cb) {
+            if (cbn) {
+              atomicAdd(&T.lcnt[cb], cbn);
+              atomicMin(&T.lmin[cb], cmn);
+            }
+            cb = bk;
+            cbn = 0;
+            cmn = ~0u;
+          }
+          ++cbn;
+          if (tof < cmn) cmn = tof;
+        }
+        if (!n_bc) ++st_ops;
+      }
+      const uint64_t nb = static_cast<uint64_t>(emit ? end : bu);
+      if (emit || pe) {
+        ++st_edges;
+        if (nb >= (1ull << 47)) set_err(p, BCSIM_E_OVERFLOW);
+      }
+      put_lw((emit || pe) ? ((nb << 16) | (emit ? (static_cast<uint32_t>(ca) & 0xFFFFu) : lc0)) : lw0);
     }
-    const uint64_t nb = static_cast<uint64_t>(emit ? end : bu);
-    if (emit || pe) {
-      ++st_edges;
-      if (nb >= (1ull << 47)) set_err(p, BCSIM_E_OVERFLOW);
-      gbl(lrow)[le] = (nb << 16) | (emit ? (static_cast<uint32_t>(ca) & 0xFFFFu) : lc0);
+    // the row's new state: the exception bits per tile (lane k: tile k), the tiles' flags of the
+    // uniform records' bucket, the uniform word (or none: every edge has its own word now)
+    if (lane < nrt) {
+      if (ring_u) gbl(p.rex)[static_cast<size_t>(g) * nrt + lane] = rexn;
+      if ((rtm >> lane) & 1ull) gbl(p.rtile)[kRtPad * ((static_cast<size_t>(bk_u) * p.R + rep) * nrt + lane)] = 1;
     }
+    if (lane == 0) gbl(p.rul)[g] = ring_u ? ((1ull << 63) | nw_u) : 0ull;
   }
-  RPH(3);
+  RPH(2);
   if (cbn) {
     atomicAdd(&T.lcnt[cb], cbn);
     atomicMin(&T.lmin[cb], cmn);
@@ -7395,6 +7404,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(6, 
   }
   if (lane == 0 && ovmin != LLONG_MAX) atomicMin(&T.ovmin, ovmin);
   __syncthreads();
+  RPH(3);
   // staged extras / overflow records: one atomic per list
   if (T.xn) {
     for (uint32_t k = tid; k <= B; k += blockDim.x) {
