@@ -7197,10 +7197,62 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
     }
     nw_u = (static_cast<uint64_t>(end_u) << 16) | ca16_u;
     const bool pfd_u = bk_u == cbk0;
+    // ---- the heavy waves' case over the whole row at once, lane = receiver tile: under a
+    // row-uniform link state every edge without its own word has the row's word; after the pending
+    // echoes (at most four classes of edges) the ones with a message whose link is free by the due
+    // time (and that own the arrival cell) send one uniform record each -- the tile's records are
+    // ONE summary entry (one base when the reply bitmap is contiguous), and their new link word is
+    // the row's new word nw_u, i.e. nothing per edge.  The rest of the tile (its residue) takes the
+    // per-tile walk below.
+    uint64_t fset = 0, res = 0;
+    if (lane < nrt) {
+      const uint32_t s0 = lane * 64u, nvr = min(64u, N - s0);
+      uint64_t vm = nvr >= 64u ? ~0ull : ((1ull << nvr) - 1ull);
+      if (i >= s0 && i < s0 + 64u) vm &= ~(1ull << (i - s0));
+      const uint64_t hm = n_bc ? vm : (((static_cast<uint64_t>(tmb.y) << 32) | tmb.x) & vm);
+      if (ruv && ring_u && pfd_u && hm) {
+        const uint64_t e0m = ne ? (((static_cast<uint64_t>(tme.y) << 32) | tme.x) & vm) : 0ull;
+        const uint64_t e1m = ne > 1 ? (((static_cast<uint64_t>(tme.w) << 32) | tme.z) & vm) : 0ull;
+        const int64_t bA = static_cast<int64_t>(ruw >> 16);
+        const int64_t bB = (bA > et0 ? bA : et0) + etx0, bC = (bA > et1 ? bA : et1) + etx1;
+        const int64_t bD = (bB > et1 ? bB : et1) + etx1;
+        const bool own_c = static_cast<uint32_t>(ruw & 0xFFFFu) != ca16_u;
+        const uint64_t okm = ((bA <= ot) ? (~e0m & ~e1m) : 0ull) | ((bB <= ot) ? (e0m & ~e1m) : 0ull) |
+                             ((bC <= ot) ? (~e0m & e1m) : 0ull) | ((bD <= ot) ? (e0m & e1m) : 0ull);
+        uint64_t fs = own_c ? (hm & ~(rexo & vm) & okm) : 0ull;
+        uint32_t base = u_s0;
+        if (!n_bc && fs) {  // sub = first sub + rank: sub - out-edge index is one value on a contiguous bitmap
+          const uint32_t lo = static_cast<uint32_t>(__builtin_ctzll(hm));
+          const uint32_t slo = s0 + lo;
+          if ((vm & ~hm) >> lo) fs = 0ull;
+          else base = u_s0 + tmb.z - (slo < i ? slo : slo - 1u);
+        }
+        const bool olive = (soa.x | soa.y) != 0u && slot_live(sob.y >> 24, w3f_u >> 27);
+        if (olive && (soa.z != tof_u || soa.w != base || sob.x != u_w2 || sob.y != w3f_u)) fs = 0ull;
+        if (fs) {
+          const uint64_t mm = fs | (olive ? ((static_cast<uint64_t>(soa.y) << 32) | soa.x) : 0ull);
+          uint4* const se = p.msum + sum_idx(p, bk_u, rep, lane, i) * 2;
+          gst4(se, make_uint4(static_cast<uint32_t>(mm), static_cast<uint32_t>(mm >> 32), tof_u, base));
+          gst4(se + 1, make_uint4(u_w2, w3f_u, 0u, 0u));
+          const uint32_t nf = static_cast<uint32_t>(__popcll(fs));
+          n_rec += nf;
+          st_edges += nf;
+          if (!n_bc) st_ops += nf;
+        }
+        fset = fs;
+      }
+      res = vm & ~fset;
+    }
+    rtm = __ballot(fset != 0ull);
+    nu = wave_sum(static_cast<uint32_t>(__popcll(fset)));
 #pragma unroll 1
     for (uint32_t rt = 0; rt < nrt; ++rt) {
+      const uint64_t rmask = (static_cast<uint64_t>(rl(static_cast<uint32_t>(res >> 32), rt)) << 32) | rl(static_cast<uint32_t>(res), rt);
+      if (!rmask) continue;  // (uniform) every edge of the tile done above
+      // (a tile with an entry from above writes its other records as records)
+      const bool fdone = (rl(static_cast<uint32_t>(fset), rt) | rl(static_cast<uint32_t>(fset >> 32), rt)) != 0u;
       const uint32_t s = rt * 64u + lane;
-      const bool v = s < N && s != i;
+      const bool v = (rmask >> lane) & 1ull;
       const uint32_t le = s < i ? s : s - 1;
       const uint64_t xo = (static_cast<uint64_t>(rl(static_cast<uint32_t>(rexo >> 32), rt)) << 32) | rl(static_cast<uint32_t>(rexo), rt);
       const bool wex = ruv && ((xo >> lane) & 1ull);  // (had its own word under the row's uniform state)
@@ -7255,7 +7307,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
           const uint32_t oax = rl(soa.x, rt), oay = rl(soa.y, rt), oaz = rl(soa.z, rt), oaw = rl(soa.w, rt);
           const uint32_t obx = rl(sob.x, rt), oby = rl(sob.y, rt);
           const bool olive = (oax | oay) != 0u && slot_live(oby >> 24, w3f_u >> 27);
-          if (!pfd_u || (olive && (oaz != tof_u || oaw != r_base || obx != u_w2 || oby != w3f_u))) um = 0ull;
+          if (fdone || !pfd_u || (olive && (oaz != tof_u || oaw != r_base || obx != u_w2 || oby != w3f_u))) um = 0ull;
           if (um) {
             const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oay) << 32) | oax) : 0ull);
             uint4* const se = p.msum + sum_idx(p, bk_u, rep, rt, i) * 2;
@@ -7319,7 +7371,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
         const uint32_t oax = rl(soa.x, rt), oay = rl(soa.y, rt), oaz = rl(soa.z, rt), oaw = rl(soa.w, rt);
         const uint32_t obx = rl(sob.x, rt), oby = rl(sob.y, rt);
         const bool olive = (oax | oay) != 0u && slot_live(oby >> 24, r_w3 >> 27);
-        if (r_bk != cbk0 || (olive && (oaz != r_tof || oaw != r_base || obx != u_w2 || oby != r_w3))) um = 0ull;
+        if (fdone || r_bk != cbk0 || (olive && (oaz != r_tof || oaw != r_base || obx != u_w2 || oby != r_w3))) um = 0ull;
         if (um) {
           const unsigned long long mm = um | (olive ? ((static_cast<unsigned long long>(oay) << 32) | oax) : 0ull);
           uint4* const se = p.msum + sum_idx(p, r_bk, rep, rt, i) * 2;
