@@ -43,6 +43,9 @@ struct Sim {
   std::vector<uint32_t> row, col, rev;
   std::vector<int64_t> prop;
   bool started = false;
+  // the node-partitioned kernels (P > 1, or forced at one rank with BCSIM_PDES_KERNELS=1 under a
+  // transport: the partitioned path, k_link_mesh<XR> -> exchange -> k_import, on one GPU)
+  bool pdes = false;
   bool topo_ready = false;  // CSR set by bcsim_set_topology_csr, else the full mesh at first run
   int32_t err = 0;
   int64_t L = 0;
@@ -74,6 +77,7 @@ struct Sim {
   int x_active = 0;            // extras of the grouped cell are in xgrp
   uint32_t bs_scan = 64, bs_link = 64;
   long long dbg_fail_cell = -1;  // test hook (BCSIM_DBG_FAIL_CELL): this rank fails at that cell
+  long long dbg_dev_err = -1;  // test hook (BCSIM_DBG_DEV_ERR): a device error flag raised before that cell's k_next
   long long dbg_fail_import = -1;  // test hook (BCSIM_DBG_FAIL_IMPORT): ... after that cell's exchange
   bool sparse = false;
   uint32_t grid_scan = 0, grid_link = 0;  // k_scan / k_link workgroups (walking the active lists)
@@ -96,7 +100,8 @@ struct Sim {
   KP* kp_dev2 = nullptr;
   bool gossip_frontier = true;  // dense gossip: k_gossip_cell over the window's frontier (BCSIM_GOSSIP_FRONTIER=0: all)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
-  bool sum = false;        // heavy-wave record summaries (BCSIM_SUM=0: off)
+  bool sum = false;
+  uint32_t row_split_max = 64;  // k_mesh_row: launches of at most this many senders split rows (BCSIM_ROW_SPLIT)        // heavy-wave record summaries (BCSIM_SUM=0: off)
   uint32_t rt_min = 0;     // summary mode: k_scan_rt takes windows of at least this many scanned nodes (BCSIM_RT_MIN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -605,6 +610,10 @@ static int setup_device(Sim& s) {
   if (c.protocol == BCSIM_PBFT && s.N > 60 * 1024) return BCSIM_E_UNSUPPORTED;  // k_pbft_tick: one LDS flag per node
 
   // node partition: rank prank owns [nlo, nlo + nloc) of every replica
+  {
+    const char* pk = std::getenv("BCSIM_PDES_KERNELS");
+    s.pdes = s.P > 1 || (s.xp && pk && *pk == '1');
+  }
   if (s.P > 1) {
     if (s.P > static_cast<uint32_t>(kMaxRanks) || s.N < s.P) return BCSIM_E_INVAL;
     if (c.protocol == BCSIM_RAFT && c.rng_mode == BCSIM_RNG_GLIBC) {
@@ -709,7 +718,7 @@ static int setup_device(Sim& s) {
       const char* px = std::getenv("BCSIM_NO_PXFAST");
       s.paxos_fast = s.sparse && c.protocol == BCSIM_PAXOS && !(px && *px == '1');
     }
-    s.gossip_link = s.gossip_g && !p.mesh && s.P == 1 && c.delay_mode == BCSIM_DELAY_FIXED &&
+    s.gossip_link = s.gossip_g && !p.mesh && !s.pdes && c.delay_mode == BCSIM_DELAY_FIXED &&
                     c.queue_model == BCSIM_QUEUE_INFINITE;
     // full mesh, fixed app delay: k_link_mesh takes the nodes whose due ops are all broadcasts
     // (BCSIM_NO_MFAST=1: off)
@@ -741,7 +750,7 @@ static int setup_device(Sim& s) {
     const char* nd = std::getenv("BCSIM_NO_DESC");
     // (k_link_mesh applies pending echoes to its LDS-parked link words: the PF variant, which
     // the node-partitioned engine does not launch)
-    p.desc = (s.scan_fast && s.mesh_link && s.mesh_pf && s.P == 1 && s.deg_max <= 32 * kDescWords && !(nd && *nd == '1')) ? 1u : 0u;
+    p.desc = (s.scan_fast && s.mesh_link && s.mesh_pf && !s.pdes && s.deg_max <= 32 * kDescWords && !(nd && *nd == '1')) ? 1u : 0u;
     p.dwords = p.desc ? static_cast<uint32_t>((s.deg_max + 31) / 32) : 1u;
     const size_t nrb = p.desc ? static_cast<size_t>(kOpRing) * NT * p.dwords : 1;
     const size_t neb = p.desc ? static_cast<size_t>(NT) * kEDesc * p.dwords : 1;
@@ -754,7 +763,7 @@ static int setup_device(Sim& s) {
     // the tiled mesh link stage: one rank, degree <= 4096 (the descriptor bitmaps)
     {
       const char* mt = std::getenv("BCSIM_MESH_TILE");
-      s.mesh_tile = s.mesh_link && s.mesh_pf && s.P == 1 && s.deg_max <= 32 * kDescWords && !(mt && *mt == '0');
+      s.mesh_tile = s.mesh_link && s.mesh_pf && !s.pdes && s.deg_max <= 32 * kDescWords && !(mt && *mt == '0');
       if (const char* tm = std::getenv("BCSIM_TILE_MIN"); tm && *tm) s.tile_min = static_cast<uint32_t>(std::atoi(tm));
     }
     p.n_stiles = (s.N + kTS - 1) / kTS;
@@ -777,7 +786,7 @@ static int setup_device(Sim& s) {
     {
       const char* sm = std::getenv("BCSIM_SUM");
       const size_t nsum = static_cast<size_t>(s.B) * s.R * p.n_tiles * s.N;
-      s.sum = s.mesh_tile && s.scan_fast && p.desc && s.P == 1 && c.protocol == BCSIM_PBFT && p.prop_const >= 0 &&
+      s.sum = s.mesh_tile && s.scan_fast && p.desc && !s.pdes && c.protocol == BCSIM_PBFT && p.prop_const >= 0 &&
               nsum * 33 <= (8ull << 30) && !(sm && *sm == '0');
       p.sum = s.sum ? 1u : 0u;
       if ((rc = dalloc(s, &p.msum, s.sum ? nsum * 2 : 1)) || (rc = dalloc(s, &p.xsum, s.sum ? nsum : 1)) ||
@@ -1058,6 +1067,8 @@ static int setup_device(Sim& s) {
   }
   if (const char* fv = std::getenv("BCSIM_DBG_FAIL_CELL"); fv && *fv) s.dbg_fail_cell = std::atoll(fv);
   if (const char* fv = std::getenv("BCSIM_DBG_FAIL_IMPORT"); fv && *fv) s.dbg_fail_import = std::atoll(fv);
+  if (const char* fv = std::getenv("BCSIM_DBG_DEV_ERR"); fv && *fv) s.dbg_dev_err = std::atoll(fv);
+  if (const char* rs = std::getenv("BCSIM_ROW_SPLIT"); rs && *rs) s.row_split_max = static_cast<uint32_t>(std::atoi(rs));
   if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -1085,7 +1096,7 @@ static int setup_device(Sim& s) {
     HIPCHK(hipEventCreateWithFlags(&s.ev_fork, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming | hipEventDisableSystemFence));
   }
-  if (!s.sparse && s.P == 1 && c.protocol == BCSIM_PBFT) {
+  if (!s.sparse && !s.pdes && c.protocol == BCSIM_PBFT) {
     KP kb = s.kp;
     kb.cap_arr = 2 * s.kp.cap_arr;
     const size_t lb = scan_lds_bytes(kb);
@@ -1264,7 +1275,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       const char* e = std::getenv("BCSIM_NO_ACTSYNC");
       return e && *e == '1';
     }();
-    if (!s.sparse && s.P == 1 && !no_sync) {
+    if (!s.sparse && !s.pdes && !no_sync) {
       // dense layout: read the list lengths back and launch exactly one workgroup per entry
       // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
       // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
@@ -1324,7 +1335,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
                         s.kp_dev, cell, lo, hi, cs, fw, xa);
     if (wep) std::swap(s.stream, s.stream2);
   }
-  else if (s.kp_dev_big && !s.sparse && s.P == 1 && grid.x <= s.few_scan) {
+  else if (s.kp_dev_big && !s.sparse && !s.pdes && grid.x <= s.few_scan) {
     // a few nodes (the leader's cells): the doubled staging window, a 1024-lane workgroup each.
     // With the list-2 overlap they are scanned and linked on the second stream, beside the
     // other nodes' link stage (which skips them)
@@ -1435,11 +1446,11 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   if (grid.x == 0 && s.l2_pending) grid = dim3(8);  // (list 2 is in list 1; the join below must run anyway)
   if (grid.x == 0)
     rc = BCSIM_OK;
-  else if (s.sparse && s.paxos_fast && s.kp.qmodel == 0 && s.P == 1) {
+  else if (s.sparse && s.paxos_fast && s.kp.qmodel == 0 && !s.pdes) {
     // sparse Paxos: one lane per acceptor first, the generic kernel over the rest (list 3)
     const bool timed = (kstat_mask() >> KS_LINK) & 1u;
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
-    if ((rc = launch(s, -1, k_paxos_link, grid, dim3(128), 0, s.kp_dev, cell, lo, hi)) ||
+    if ((rc = launch(s, -1, k_paxos_link, grid, dim3(kPxLinkThreads), 0, s.kp_dev, cell, lo, hi)) ||
         (rc = launch(s, -1, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw, 3)))
       return rc;
     if (timed) {
@@ -1469,7 +1480,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       if (rc) return rc;
       HIPCHK(hipEventRecord(s.ev_join, s.stream2));
     }
-    if (s.P > 1) {
+    if (s.pdes) {
       // (node-partitioned: one out-edge per lane per step, no parked link words -- 119 VGPRs and
       // no scratch, where the two-edge / prefetching variants spill at 4 waves per SIMD; the reply
       // descriptors, which need the parked words, are off at P > 1)
@@ -1481,11 +1492,15 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       // epoch tells this launch's jobs from stale ones
       const uint32_t ep = ++s.mesh_epoch == 0 ? ++s.mesh_epoch : s.mesh_epoch;
       const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
+      // k_mesh_row: a wave per sender, four per workgroup; a launch of few senders (the leader's
+      // block broadcast) gives each sender a 1024-lane workgroup, 16 waves over its tiles
+      const uint32_t rsplit = n_link <= s.row_split_max ? 16u : 1u;
+      const dim3 rgrid(rsplit > 1 ? n_link : (n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)),
+          rblock(rsplit > 1 ? 1024 : kRowThreads);
       if ((rc = launch(s, -1, k_mesh_prep, grid, dim3(64), 0, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
           // (summary mode: the uniform jobs' rows; the tiles take the rest)
-          (s.sum && (rc = launch(s, -1, k_mesh_row, dim3((n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)), dim3(kRowThreads), 0,
-                                 s.kp_dev, cell, lo, hi, ep, row_hq(s, cell, lo, hi)))) ||
-          (s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, (n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)))) ||
+          (s.sum && (rc = launch(s, -1, k_mesh_row, rgrid, rblock, 0, s.kp_dev, cell, lo, hi, ep, row_hq(s, cell, lo, hi), rsplit))) ||
+          (s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, rgrid.x))) ||
           (!s.sum && (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(kTileThreads), 0, s.kp_dev, cell, lo, hi, ep))) ||
           (!s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, nt))) ||
           (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
@@ -2045,6 +2060,8 @@ static int run(Sim& s, int64_t t_until) {
     const uint32_t nbn = s.NT <= 4096u ? 1u : static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
     // (a finished cell's bucket is free again: k_next clears its counts and tile flags)
     const uint32_t clr_b = hi == ce ? static_cast<uint32_t>(c % s.B) : 0xFFFFFFFFu;
+    if (!lrc && s.dbg_dev_err >= 0 && static_cast<long long>(s.cells) >= s.dbg_dev_err)
+      lrc = launch(s, KS_AUX, k_dbg_err, dim3(1), dim3(64), 0, s.kp_dev);
     if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b, ++s.mseq);
     if (!lrc) lrc = readback(s, true);
     if (!lrc && s.dbg_fail_cell >= 0 && static_cast<long long>(s.cells) >= s.dbg_fail_cell) {

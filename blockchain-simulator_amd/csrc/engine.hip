@@ -4570,7 +4570,8 @@ struct LinkShared {
 // Stage one extras / overflow record of k_link (list = bucket, or B for the
 // overflow list): LDS ranks now, one global atomic per list at the flush.
 // A full staging area falls back to a direct (contended) global append.
-__device__ inline void link_stage(const KP& p, LinkShared& L, uint32_t g, uint32_t list, const XRec& x) {
+template <class LS>
+__device__ inline void link_stage(const KP& p, LS& L, uint32_t g, uint32_t list, const XRec& x) {
   const uint32_t spos = atomicAdd(&L.nst, 1u);
   if (spos < p.cap_stage) {
     const uint32_t rank = atomicAdd(&L.lst[list], 1u);
@@ -7050,42 +7051,19 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
 // kernel's transpose: the link words are read and written coalesced (a sender's row is
 // contiguous), the tile's records that differ only in sub are ONE summary entry (merged as in
 // k_mesh_tile), any other slot record is stored directly, and second records of an edge
-// (extras) and records beyond the ring (overflow) are staged in LDS and appended with one
-// atomic per list.  The per-edge work and its results are k_mesh_tile's.
-constexpr uint32_t kRowThreads = 256;  // four senders per workgroup, one wave each
+// (extras) and records beyond the ring (overflow) are appended with one atomic per list and
+// wave.  The first pass takes a row-uniform sender's whole row at once (lane = receiver tile).
+// The per-edge work and its results are k_mesh_tile's.
+constexpr uint32_t kRowThreads = 256;  // four senders per workgroup, one wave each (1024 lanes: split rows)
 struct RowShared {
-  XRec xs[kTX];
-  uint32_t xm[kTX];  // list << 24 | rank
-  uint32_t xn;
-  uint32_t lst[kMaxBuckets + 1];
   uint32_t lcnt[kMaxBuckets];
   uint32_t lmin[kMaxBuckets];
   uint32_t csum[8];
   long long ovmin;
   long long bmin[kMaxBuckets];  // the buckets' arrival-time bounds as of the start (read early)
 };
-__device__ inline void row_append(const KP& p, RowShared& T, uint32_t list, const XRec& x) {
-  const uint32_t pos = atomicAdd(&T.xn, 1u);
-  if (pos < kTX) {
-    const uint32_t rank = atomicAdd(&T.lst[list], 1u);
-    T.xs[pos] = x;
-    T.xm[pos] = (list << 24) | rank;
-    return;
-  }
-  uint32_t* ctr = list == p.n_buckets ? p.ov_cnt : &p.x_cnt[list];  // (staging full: a direct append)
-  const uint32_t cap = list == p.n_buckets ? p.cap_ov : p.cap_x;
-  const uint32_t at = gadd_r(ctr, 1u);
-  if (at >= cap) {
-    set_err(p, BCSIM_E_OVERFLOW);
-    return;
-  }
-  uint4* dst = reinterpret_cast<uint4*>(list == p.n_buckets ? p.ov + at : p.xbuf + static_cast<size_t>(list) * p.cap_x + at);
-  const uint4* src = reinterpret_cast<const uint4*>(&x);
-  gst4(dst, src[0]);
-  gst4(dst + 1, src[1]);
-}
-__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_mesh_row(
-    const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi, uint32_t epoch, uint4 hq) {
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_mesh_row(
+    const KP* __restrict__ pk, long long cell, long long t_lo, long long t_hi, uint32_t epoch, uint4 hq, uint32_t split) {
   // hq (host arithmetic, no 64-bit divisions here): {cell % B, (cell / B) % 32, the bucket a small
   // message sent at t_lo lands in on an idle link (0xFFFF: outside the ring), 0}
   const KP& p = *pk;
@@ -7104,9 +7082,13 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
   const uint32_t cr_b = hq.x, cq_b = hq.y;
   const uint32_t cbk0 = (hq.z & 0xFFFFu) == 0xFFFFu ? kInvalid : (hq.z & 0xFFFFu);
   auto rl = [](uint32_t x, uint32_t k) { return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), static_cast<int>(k))); };
-  // this wave's sender (list-1 entry blockIdx * 4 + wave) and, all at once, its job words (lanes
-  // 0-3), its broadcast (4-5) and its row's uniform link word (6)
-  const uint32_t kk = blockIdx.x * nwv + wv;
+  // this wave's sender (list-1 entry blockIdx * (waves / split) + wave / split; `split` waves share
+  // a sender's row when the launch has few senders -- the leader's block broadcast -- each one a
+  // contiguous range of its receiver tiles) and, all at once, its job words (lanes 0-3), its
+  // broadcast (4-5) and its row's uniform link word (6)
+  const uint32_t part = wv % split, kk = blockIdx.x * (nwv / split) + wv / split;
+  const uint32_t tpp = (p.n_tiles + split - 1) / split, t0 = min(p.n_tiles, part * tpp), t1 = min(p.n_tiles, t0 + tpp);
+  const bool own_t = lane >= t0 && lane < t1;  // (lane k: tile k is this wave's)
   bool act = kk < p.act_n[1];
   const uint32_t g = act ? rl(p.act[p.NT + kk], 0) : 0u;
   uint4 jw = make_uint4(0, 0, 0, 0);
@@ -7122,12 +7104,8 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
     T.lcnt[k] = 0;
     T.lmin[k] = ~0u;
   }
-  for (uint32_t k = tid; k <= B; k += blockDim.x) T.lst[k] = 0;
   if (tid < 8) T.csum[tid] = 0;
-  if (tid == 0) {
-    T.ovmin = LLONG_MAX;
-    T.xn = 0;
-  }
+  if (tid == 0) T.ovmin = LLONG_MAX;
   if (tid >= 64 && tid < 64 + B) T.bmin[tid - 64] = *reinterpret_cast<volatile G<long long>*>(&gbl(p.bmin)[tid - 64]);
   const uint32_t fl = rl(jw.y, 0), jz = rl(jw.z, 0);
   act = act && rl(jw.x, 0) == epoch && job_uniform(fl, jz, prc);
@@ -7138,7 +7116,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
   // echo bitmaps, and the summary entry of the bucket an idle link delivers in -- one round
   uint64_t rexo = 0;
   uint4 tmb = make_uint4(0, 0, 0, 0), tme = make_uint4(0, 0, 0, 0), soa = make_uint4(0, 0, 0, 0), sob = make_uint4(0, 0, 0, 0);
-  if (act && lane < nrt) {
+  if (act && own_t) {
     rexo = gbl(p.rex)[static_cast<size_t>(g) * nrt + lane];
     if (!n_bc) tmb = gld4(p.mtb + (static_cast<size_t>(g) * nrt + lane) * 2 + h);
     if (ne) tme = gld4(reinterpret_cast<const uint4*>(p.mte + (static_cast<size_t>(g) * nrt + lane) * kEDesc));
@@ -7205,7 +7183,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
     // the row's new word nw_u, i.e. nothing per edge.  The rest of the tile (its residue) takes the
     // per-tile walk below.
     uint64_t fset = 0, res = 0;
-    if (lane < nrt) {
+    if (own_t) {
       const uint32_t s0 = lane * 64u, nvr = min(64u, N - s0);
       uint64_t vm = nvr >= 64u ? ~0ull : ((1ull << nvr) - 1ull);
       if (i >= s0 && i < s0 + 64u) vm &= ~(1ull << (i - s0));
@@ -7246,7 +7224,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
     rtm = __ballot(fset != 0ull);
     nu = wave_sum(static_cast<uint32_t>(__popcll(fset)));
 #pragma unroll 1
-    for (uint32_t rt = 0; rt < nrt; ++rt) {
+    for (uint32_t rt = t0; rt < t1; ++rt) {
       const uint64_t rmask = (static_cast<uint64_t>(rl(static_cast<uint32_t>(res >> 32), rt)) << 32) | rl(static_cast<uint32_t>(res), rt);
       if (!rmask) continue;  // (uniform) every edge of the tile done above
       // (a tile with an entry from above writes its other records as records)
@@ -7386,25 +7364,13 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
         ++n_rec;
         const uint32_t slot = s * N1 + (i < s ? i : i - 1);
         const uint4 rv = make_uint4(tof, u_sub + le, u_w2, w3f);
-        if (ok) {
-          if (!uni) {
-            gst4(p.inbox + inbox_idx(p, bk, rep, slot), rv);
-            gbl(p.xsum)[sum_idx(p, bk, rep, rt, i)] = static_cast<uint8_t>(0x80u | (w3f >> 27));
-          }
-        } else {
-          XRec x;
-          __builtin_memcpy(&x.r, &rv, sizeof rv);
-          if (!inring && owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
-          x.cell = ca;
-          x.slot = slot;
-          x.g = rep * N + s;
-          if (inring) {
-            row_append(p, T, bk, x);  // a second record of the edge in its arrival cell: extras
-            gbl(p.iflag)[static_cast<size_t>(bk) * p.NT + x.g] = 1;
-          } else {
-            row_append(p, T, B, x);  // beyond the ring: overflow
-            if (ca < ovmin) ovmin = ca;
-          }
+        if (ok && !uni) {
+          gst4(p.inbox + inbox_idx(p, bk, rep, slot), rv);
+          gbl(p.xsum)[sum_idx(p, bk, rep, rt, i)] = static_cast<uint8_t>(0x80u | (w3f >> 27));
+        }
+        if (!ok) {
+          if (inring) gbl(p.iflag)[static_cast<size_t>(bk) * p.NT + rep * N + s] = 1;  // (extras)
+          else if (ca < ovmin) ovmin = ca;
         }
         if (inring) {
           if (bk != cb) {
@@ -7427,14 +7393,58 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
         if (nb >= (1ull << 47)) set_err(p, BCSIM_E_OVERFLOW);
       }
       put_lw((emit || pe) ? ((nb << 16) | (emit ? (static_cast<uint32_t>(ca) & 0xFFFFu) : lc0)) : lw0);
+      // the records that are not their edge's slot record -- a second record of the edge in its
+      // arrival cell (extras of bucket bk) or one beyond the ring (overflow) -- appended with one
+      // atomic per list and wave (a leader's block broadcast puts its whole row beyond the ring)
+      unsigned long long xmk = __ballot(emit && !ok);
+      if (xmk) {
+        const uint32_t list = inring ? bk : B;
+        XRec x;
+        {
+          const uint4 rv = make_uint4(tof, u_sub + le, u_w2, w3f);
+          __builtin_memcpy(&x.r, &rv, sizeof rv);
+        }
+        if (!inring && owner) x.r.flags = static_cast<uint8_t>(x.r.flags | RF_OWNER);
+        x.cell = ca;
+        x.slot = s * N1 + (i < s ? i : i - 1);
+        x.g = rep * N + s;
+        // the lanes grouped by list: each group's lowest lane reserves the group's span, all
+        // groups in one atomic instruction (one round trip per tile)
+        uint32_t ldr = 0, rk = 0, gc = 0;
+        unsigned long long rem = xmk;
+        while (rem) {
+          const uint32_t q = static_cast<uint32_t>(__ffsll(static_cast<long long>(rem)) - 1);
+          const uint32_t lq = rl(list, q);
+          const unsigned long long mm = __ballot(((rem >> lane) & 1ull) && list == lq);
+          if ((mm >> lane) & 1ull) {
+            ldr = q;
+            rk = static_cast<uint32_t>(__popcll(mm & lbelow));
+          }
+          if (lane == q) gc = static_cast<uint32_t>(__popcll(mm));
+          rem &= ~mm;
+        }
+        uint32_t b0 = 0;
+        if (gc) b0 = gadd_r(list == B ? p.ov_cnt : &p.x_cnt[list], gc);
+        b0 = static_cast<uint32_t>(__shfl(static_cast<int>(b0), static_cast<int>(ldr), 64));
+        if ((xmk >> lane) & 1ull) {
+          const uint32_t at = b0 + rk;
+          if (at >= (list == B ? p.cap_ov : p.cap_x)) {
+            set_err(p, BCSIM_E_OVERFLOW);
+          } else {
+            uint4* dst = reinterpret_cast<uint4*>(list == B ? p.ov + at : p.xbuf + static_cast<size_t>(list) * p.cap_x + at);
+            const uint4* src = reinterpret_cast<const uint4*>(&x);
+            gst4(dst, src[0]);
+            gst4(dst + 1, src[1]);
+          }
+        }
+      }
     }
     // the row's new state: the exception bits per tile (lane k: tile k), the tiles' flags of the
     // uniform records' bucket, the uniform word (or none: every edge has its own word now)
-    if (lane < nrt) {
+    if (own_t) {
       if (ring_u) gbl(p.rex)[static_cast<size_t>(g) * nrt + lane] = rexn;
       if ((rtm >> lane) & 1ull) gbl(p.rtile)[kRtPad * ((static_cast<size_t>(bk_u) * p.R + rep) * nrt + lane)] = 1;
     }
-    if (lane == 0) gbl(p.rul)[g] = ring_u ? ((1ull << 63) | nw_u) : 0ull;
   }
   RPH(2);
   if (cbn) {
@@ -7457,35 +7467,8 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(5, 
   if (lane == 0 && ovmin != LLONG_MAX) atomicMin(&T.ovmin, ovmin);
   __syncthreads();
   RPH(3);
-  // staged extras / overflow records: one atomic per list
-  if (T.xn) {
-    for (uint32_t k = tid; k <= B; k += blockDim.x) {
-      const uint32_t c = T.lst[k];
-      if (!c) continue;
-      uint32_t* ctr = k == B ? p.ov_cnt : &p.x_cnt[k];
-      const uint32_t cap = k == B ? p.cap_ov : p.cap_x;
-      const uint32_t base = gadd_r(ctr, c);
-      if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
-      T.lst[k] = base;
-    }
-    __syncthreads();
-    const uint32_t nx = min(T.xn, kTX);
-    for (uint32_t k = tid; k < nx; k += blockDim.x) {
-      const uint32_t list = T.xm[k] >> 24, at = T.lst[list] + (T.xm[k] & 0xFFFFFFu);
-      const uint4* src = reinterpret_cast<const uint4*>(&T.xs[k]);
-      if (list == B) {
-        if (at < p.cap_ov) {
-          uint4* dst = reinterpret_cast<uint4*>(p.ov + at);
-          gst4(dst, src[0]);
-          gst4(dst + 1, src[1]);
-        }
-      } else if (at < p.cap_x) {
-        uint4* dst = reinterpret_cast<uint4*>(p.xbuf + static_cast<size_t>(list) * p.cap_x + at);
-        gst4(dst, src[0]);
-        gst4(dst + 1, src[1]);
-      }
-    }
-  }
+  // (after the barrier: every wave of the sender has read the old word)
+  if (act && part == 0 && lane == 0) gbl(p.rul)[g] = ring_u ? ((1ull << 63) | nw_u) : 0ull;
   // busy buckets and their arrival-time bounds, counters
   for (uint32_t k = tid; k < B; k += blockDim.x)
     if (T.lcnt[k]) {
@@ -8204,14 +8187,24 @@ __global__ __launch_bounds__(256) void k_link_sparse(const KP* __restrict__ pk, 
 // acceptors.  Same result as link_node_sparse: the due ops in (edge, canonical key) order
 // through each edge's FIFO, one list record per SEND (staged per workgroup, one global
 // atomic per list and batch), the ops not yet due compacted in order.  Other nodes go to
-// list 3 for k_link_sparse.  128 lanes per workgroup, the lane's ops in LDS (32 KB).
-__global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                    long long t_hi) {
+// list 3 for k_link_sparse.  256 lanes per workgroup; the lane's ops live in registers (the
+// selection and compaction loops are unrolled over kPxCap), so the workgroup's LDS is the
+// list staging alone (~0.5 KB) and occupancy is set by VGPRs.
+struct PxLinkShared {
+  uint32_t lcnt[kMaxBuckets];
+  uint32_t lmin[kMaxBuckets];
+  uint32_t nst;
+  uint32_t lst[kMaxBuckets + 1];  // per list (bucket extras..., overflow)
+  uint32_t lbase[kMaxBuckets + 1];
+  long long ovmin;
+  uint32_t c[5];  // records, due ops, edges, echoes, kept
+};
+constexpr uint32_t kPxLinkThreads = 256;
+__global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                               long long t_hi) {
   const KP& p = *pk;
   BAIL_IF_ERR();
-  __shared__ LinkShared L;
-  __shared__ uint4 sa[kPxCap][128], sb[kPxCap][128];
-  __shared__ uint32_t s_c[7];  // records, due ops, edges, echoes, kept, (unused)
+  __shared__ PxLinkShared L;
   const uint32_t tid = tidx(), bs = blockDim.x;
   const uint32_t na = p.act_n[1];
   const uint32_t B = p.n_buckets;
@@ -8222,7 +8215,7 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
       L.lmin[k] = ~0u;
     }
     for (uint32_t k = tid; k < n_lists; k += bs) L.lst[k] = 0;
-    if (tid < 7) s_c[tid] = 0;
+    if (tid < 5) L.c[tid] = 0;
     if (tid == 0) {
       L.nst = 0;
       L.ovmin = LLONG_MAX;
@@ -8233,17 +8226,17 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
     const uint32_t n = kl < na ? AT(p.n_ops, g, p.NT) : 0u;
     bool fast = kl < na && n <= static_cast<uint32_t>(kPxCap);
     Op* ops = p.ops + (kl < na ? op_base(p, g) : 0);
-    uint32_t due = 0;  // bit c: op c is due
-    for (uint32_t c = 0; fast && c < n; ++c) {
-      const RawOp o = ld_raw(ops + c);
-      const uint32_t kind = raw_kind(o);
-      if ((kind != OP_SEND && kind != OP_ECHO) || o.b.y == kInvalid) {
-        fast = false;
-        break;
-      }
-      sa[c][tid] = o.a;
-      sb[c][tid] = o.b;
-      if (raw_t(o) < t_hi) due |= 1u << c;
+    // the ops, all loads in flight at once; bit c of due: op c is due
+    RawOp o[kPxCap];
+#pragma unroll
+    for (int c = 0; c < kPxCap; ++c) o[c] = (fast && static_cast<uint32_t>(c) < n) ? ld_raw(ops + c) : raw_zero();
+    uint32_t due = 0;
+#pragma unroll
+    for (int c = 0; c < kPxCap; ++c) {
+      if (static_cast<uint32_t>(c) >= n) continue;
+      const uint32_t kind = raw_kind(o[c]);
+      if ((kind != OP_SEND && kind != OP_ECHO) || o[c].b.y == kInvalid) fast = false;
+      if (raw_t(o[c]) < t_hi) due |= 1u << c;
     }
     if (kl < na && !fast) {
       const uint32_t pos = gadd_r(&p.act_n[3], 1u);
@@ -8258,25 +8251,22 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
       uint32_t cur_e = kInvalid;
       uint64_t* lwp = nullptr;
       int64_t bu = 0;
-      uint32_t lc = 0, sn = 0, slot = 0, dg = 0;
+      uint32_t lc = 0, slot = 0, dg = 0;
       int64_t pr = 0;
       while (left) {
-        // next due op in (edge, key) order
-        uint32_t best = 0;
-        bool have = false;
-        for (uint32_t c = 0; c < n; ++c) {
-          if (!(left & (1u << c))) continue;
-          if (!have) {
-            best = c;
-            have = true;
-            continue;
-          }
-          const RawOp oc{sa[c][tid], sb[c][tid]}, ob{sa[best][tid], sb[best][tid]};
-          if (oc.b.y < ob.b.y || (oc.b.y == ob.b.y && raw_key_less(oc, raw_sub(oc), ob, raw_sub(ob)))) best = c;
+        // next due op in (edge, key) order: a scan over the register-resident ops
+        RawOp ob = raw_zero();
+        uint32_t best = kInvalid;
+#pragma unroll
+        for (int c = 0; c < kPxCap; ++c) {
+          const bool cand = (left >> c) & 1u;
+          const bool take = cand && (best == kInvalid || o[c].b.y < ob.b.y ||
+                                     (o[c].b.y == ob.b.y && raw_key_less(o[c], raw_sub(o[c]), ob, raw_sub(ob))));
+          raw_sel(ob, o[c], take);
+          best = take ? static_cast<uint32_t>(c) : best;
         }
         left &= ~(1u << best);
-        const RawOp o{sa[best][tid], sb[best][tid]};
-        const uint32_t e = o.b.y;
+        const uint32_t e = ob.b.y;
         if (e != cur_e) {  // a new edge: store the previous one's link word, load this one's
           if (lwp) {
             if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
@@ -8288,17 +8278,17 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
           const uint64_t lw = *lwp;
           bu = static_cast<int64_t>(lw >> 16);
           lc = static_cast<uint32_t>(lw & 0xFFFFu);
-          sn = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e, p.E);
+          const uint32_t sn = p.mesh ? (le < i ? le : le + 1) : AT(p.col, e, p.E);
           slot = p.mesh ? sn * (p.N - 1) + (i < sn ? i : i - 1) : AT(p.rev, e, p.E);
           dg = rep * p.N + sn;
           pr = p.prop_const >= 0 ? p.prop_const : AT(p.prop, e, p.E);
           ++c_edges;
         }
         ++c_ops;
-        const uint32_t kind = raw_kind(o);
+        const uint32_t kind = raw_kind(ob);
         if (kind == OP_SEND) ++c_sends;
-        const int big = (raw_flags(o) & OPF_BIG) ? 1 : 0;
-        const int64_t ot = raw_t(o);
+        const int big = (raw_flags(ob) & OPF_BIG) ? 1 : 0;
+        const int64_t ot = raw_t(ob);
         const int64_t start = bu > ot ? bu : ot;
         bu = start + sel2(p.tx_tot, big);
         if (kind == OP_ECHO) {
@@ -8316,8 +8306,8 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
         lc = static_cast<uint32_t>(ca) & 0xFFFFu;
         XRec x;
         {
-          const uint32_t w3 = (o.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
-          const uint4 rv = make_uint4(static_cast<uint32_t>(ta - ca * p.L), raw_sub(o), o.b.z, w3);
+          const uint32_t w3 = (ob.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
+          const uint4 rv = make_uint4(static_cast<uint32_t>(ta - ca * p.L), raw_sub(ob), ob.b.z, w3);
           __builtin_memcpy(&x.r, &rv, sizeof x.r);
         }
         x.cell = ca;
@@ -8342,24 +8332,24 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
     if (fast && (due || n)) {  // ordered compaction of the ops not yet due
       uint32_t kept = 0;
       long long omin = LLONG_MAX;
-      for (uint32_t c = 0; c < n; ++c) {
-        if (due & (1u << c)) continue;
-        const RawOp o{sa[c][tid], sb[c][tid]};
-        if (raw_t(o) < omin) omin = raw_t(o);
+#pragma unroll
+      for (int c = 0; c < kPxCap; ++c) {
+        if (static_cast<uint32_t>(c) >= n || ((due >> c) & 1u)) continue;
+        if (raw_t(o[c]) < omin) omin = raw_t(o[c]);
         uint4* w = reinterpret_cast<uint4*>(ops + kept);
-        w[0] = o.a;
-        w[1] = o.b;
+        w[0] = o[c].a;
+        w[1] = o[c].b;
         ++kept;
       }
       AT(p.n_ops, g, p.NT) = kept;
       AT(p.node_onext, g, p.NT) = omin;
-      atomicAdd(&s_c[4], kept);
+      atomicAdd(&L.c[4], kept);
       if (c_sends) atomicAdd(&cnt_stripe(p, g / p.N)[CNT_SENDS], static_cast<unsigned long long>(c_sends));
     }
-    if (c_rec) atomicAdd(&s_c[0], c_rec);
-    if (c_ops) atomicAdd(&s_c[1], c_ops);
-    if (c_edges) atomicAdd(&s_c[2], c_edges);
-    if (c_echo) atomicAdd(&s_c[3], c_echo);
+    if (c_rec) atomicAdd(&L.c[0], c_rec);
+    if (c_ops) atomicAdd(&L.c[1], c_ops);
+    if (c_edges) atomicAdd(&L.c[2], c_edges);
+    if (c_echo) atomicAdd(&L.c[3], c_echo);
     if (ovmin != LLONG_MAX) atomicMin(&L.ovmin, ovmin);
     __syncthreads();
     // flush the staged records: one global atomic per list
@@ -8386,22 +8376,21 @@ __global__ __launch_bounds__(128) void k_paxos_link(const KP* __restrict__ pk, l
     }
     for (uint32_t k = tid; k < B; k += bs)
       if (L.lcnt[k]) {
-      mark_busy(&p.bucket_cnt[k]);
-      bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + L.lmin[k]);
-    }
+        mark_busy(&p.bucket_cnt[k]);
+        bmin_lower(p, k, bucket_t0(p, (t_hi - 1) / p.L, k) + L.lmin[k]);
+      }
     if (tid == 0) {
       if (L.ovmin != LLONG_MAX) gmin(&p.scal[1], L.ovmin);
       unsigned long long* ks = kst_stripe(p);
-      if (s_c[0]) atomicAdd(&ks[KST_REC], static_cast<unsigned long long>(s_c[0]));
-      if (s_c[1]) atomicAdd(&ks[KST_OPS], static_cast<unsigned long long>(s_c[1]));
-      if (s_c[2]) atomicAdd(&ks[KST_EDGES], static_cast<unsigned long long>(s_c[2]));
-      if (s_c[3]) atomicAdd(&ks[KST_ECHO], static_cast<unsigned long long>(s_c[3]));
-      if (s_c[4]) atomicAdd(&ks[KST_KEPT], static_cast<unsigned long long>(s_c[4]));
+      if (L.c[0]) atomicAdd(&ks[KST_REC], static_cast<unsigned long long>(L.c[0]));
+      if (L.c[1]) atomicAdd(&ks[KST_OPS], static_cast<unsigned long long>(L.c[1]));
+      if (L.c[2]) atomicAdd(&ks[KST_EDGES], static_cast<unsigned long long>(L.c[2]));
+      if (L.c[3]) atomicAdd(&ks[KST_ECHO], static_cast<unsigned long long>(L.c[3]));
+      if (L.c[4]) atomicAdd(&ks[KST_KEPT], static_cast<unsigned long long>(L.c[4]));
     }
     __syncthreads();
   }
 }
-
 
 // ---------------------------------------------------------------------------
 // k_active (sparse mode): the gnodes of this rank that have work in [t_lo, t_hi) --
@@ -8924,6 +8913,12 @@ __global__ void k_draws(const KP* __restrict__ pk, uint32_t) {
 
 // Zero n16 16-byte words (an inbox bucket for the ring-turn tag invariant): dwordx4 stores,
 // a grid-stride loop over a few thousand workgroups
+// test hook (BCSIM_DBG_DEV_ERR): raise a device error flag, as an overflow found by a kernel
+// would, so that the next kernels bail and the host's read-back takes its fallback path
+__global__ void k_dbg_err(const KP* __restrict__ pk) {
+  if (tidx() == 0) set_err(*pk, BCSIM_E_OVERFLOW);
+}
+
 __global__ __launch_bounds__(256) void k_zero16(uint4* __restrict__ dst, uint64_t n16) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < n16; k += stride)

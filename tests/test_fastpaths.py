@@ -73,6 +73,9 @@ def test_c4_bench_config_fast_scan_equals_generic(engine_lib):
     gen = _run(cfg, None, {"BCSIM_NO_SFAST": "1"})
     assert fast[1]["delivered_total"] == 6 * (3 * 4095 ** 2 + 4095)
     assert compare(gen, fast) is None
+    # k_mesh_row with every row on one wave (no split of the leader's row over 16 waves)
+    whole = _run(cfg, None, {"BCSIM_ROW_SPLIT": "0"})
+    assert compare(whole, fast) is None
 
 
 def _pbft_cases():

@@ -139,7 +139,7 @@ def test_partitioned_n512_matches_oracle(engine_lib):
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("name,world", [("c4_bench_r4", 2), ("c5_gossip_r3", 2), ("c4_bench_r4", 4), ("c4_bench_r4", 8),
-                                        ("c5_gossip_r3", 4), ("c4_fq_r6", 2)])
+                                        ("c5_gossip_r3", 4), ("c5_gossip_r3", 8), ("c4_fq_r6", 2)])
 def test_partitioned_fullsize_equals_single(name, world, engine_lib):
     """SURVEY.md §4 item 4 at BASELINE size: the bench configurations themselves --
     C4 PBFT n=4096 (50 KB blocks, glibc lottery on, 4 rounds; blockchain-simulator.cc:34-51
@@ -169,17 +169,18 @@ def test_partitioned_fullsize_equals_single(name, world, engine_lib):
     assert merged[1]["collectives"] <= 2 * merged[1]["windows"] + 8 * 2 * 8, merged[1]
 
 
-def _rccl1_worker(port, names, q):
+def _rccl1_worker(port, names, q, env=None):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [repo, os.path.join(repo, "tests"), os.path.join(repo, "blockchain-simulator_amd")]
+    os.environ.update(env or {})
     import torch.distributed as dist
     import bcsim
-    from parity_cases import cases, topology
+    from parity_cases import any_case, topology
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=0, world_size=1)
     for name in names:
-        with bcsim.Simulator(cases()[name]) as s:
+        with bcsim.Simulator(any_case(name)) as s:
             topo = topology(name)
             if topo is not None:
                 s.set_topology(*topo)
@@ -206,6 +207,32 @@ def test_rccl_transport_world1(engine_lib):
     for name in names:
         d = compare(oracle.run(allc[name], topology=topology(name)), got[name])
         assert d is None, f"{name}: {d}"
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["c4_bench_r4", "c5_gossip_r3"])
+def test_rccl_world1_fullsize_partitioned_kernels(name, engine_lib):
+    """BASELINE configs[3]/[4] at full size through the RCCL transport with the node-partitioned
+    kernels forced at one rank (BCSIM_PDES_KERNELS=1): k_link_mesh<XR> / the partitioned generic
+    kernels, the per-window RCCL control all-to-all and record sendrecv, k_import, the leader-flag
+    all-reduce -- every device-side step of the P > 1 loop runs at n=4096 / n=65536 on the one GPU
+    of the box (RCCL refuses two ranks on one device, so the cross-rank volume itself is covered by
+    the host-transport P=2/4/8 tests above) and must equal the plain single-GPU run bit for bit."""
+    import bcsim
+    from parity_cases import any_case
+    topo = topology(name)
+    single = bcsim.run(any_case(name), topology=topo)
+    assert single[2]["error"] == 0 and single[2]["quiescent"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl1_worker, args=(_free_port(), [name], q, {"BCSIM_PDES_KERNELS": "1"}))
+    p.start()
+    got_name, tr, cnt = q.get(timeout=540)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and got_name == name
+    d = compare(single, (tr, cnt))
+    assert d is None, f"{name}: {d}"
 
 
 def _fail_worker(rank, world, port, fail_rank, q, fail_cell="3", t_until=None, hook="BCSIM_DBG_FAIL_CELL"):

@@ -56,23 +56,26 @@ def test_c3_paxos4096_multidecree_dense_equals_sparse(engine_lib):
     assert max(commits.values(), default=1) == 1
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(900)
 def test_c3_paxos4096_10k_replicas_fit(engine_lib):
     """The configs[2] batch size itself: 10,000 replicas of Paxos n=4096 (41M nodes, two
-    decrees per proposer) in one sparse engine on one GPU over the first 300 ms, with the
-    per-replica invariants of the reference's message flow that hold at every prefix.  (The
-    batch does not quiesce in a test's time: three dueling proposers per replica exchange
-    tickets for 10-20 s simulated -- the oracle's single n=4096 replica quiesces at 16 s; the
-    quiescence equalities are checked at n=4096 on fewer replicas below.)"""
+    decrees per proposer) in one sparse engine on one GPU over the first 16 s simulated -- the
+    horizon where the dueling proposers start to win (the oracle's single n=4096 replicas commit
+    first at 13-15 s for seeds 1-3) -- with the per-replica invariants of the reference's message
+    flow that hold at every prefix, and commits that happened: at least one, and at most one per
+    (replica, proposer, decree).  (The batch does not quiesce in a test's time; the quiescence
+    equalities are checked at n=4096 on fewer replicas below.)"""
     import bcsim
     from collections import Counter, defaultdict
     n, reps = 4096, 10_000
     c = bcsim.preset("c3_paxos")
     c.n_replicas = reps
     c.paxos_decrees = 2
-    c.t_end_ns = 300_000_000
+    c.t_end_ns = 0
     with bcsim.Simulator(c) as s:
-        s.run()
+        for k in range(1, 9):  # (in 2 s steps, each a bounded run)
+            s.run(2_000_000_000 * k)
+            print(f"[c3 10k] t={2 * k} s", flush=True)
         cnt, st, tr = s.counters(), s.status(), s.trace()
     assert st["error"] == 0
     d = cnt["delivered"]
@@ -94,7 +97,8 @@ def test_c3_paxos4096_10k_replicas_fit(engine_lib):
     assert d[0] + d[1] + d[2] <= (n - 2) * cnt["dropped"]
     # a proposer commits each of its decrees at most once
     commits = Counter((r[0], r[5], r[8]) for r in tr if r[6] == _abi.TR["PAXOS_COMMIT"])
-    assert max(commits.values(), default=1) == 1
+    assert len(commits) > 0, "no replica committed by 16 s"
+    assert max(commits.values()) == 1
 
 
 @pytest.mark.timeout(600)
