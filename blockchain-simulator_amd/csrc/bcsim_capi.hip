@@ -1187,6 +1187,16 @@ static int tile_phase_report(Sim& s, long long cell, uint32_t nt) {
     for (int k = 0; k < 5; ++k) m[k] += static_cast<double>(q[k + 1] - q[k]);
   }
   if (!n || t1 - t0 < 5000) return BCSIM_OK;
+  {  // (k_mesh_row: tiles walked, row classes)
+    unsigned long long a6 = 0, a7 = 0;
+    for (uint32_t b = 0; b < nt; ++b) {
+      a6 += w[8ull * b + 6];
+      a7 += w[8ull * b + 7];
+    }
+    if (a7)
+      std::fprintf(stderr, "[row] cell %lld rows %llu no-uniform %llu beyond-ring %llu off-idle-bucket %llu tiles walked %llu\n", cell,
+                   a7 & 0xFFFF, (a7 >> 16) & 0xFFFF, (a7 >> 32) & 0xFFFF, a7 >> 48, a6);
+  }
   std::fprintf(stderr, "[tile] cell %lld span %.1f us, %u WGs, mean us: prologue %.2f lw %.2f edges %.2f barrier %.2f out %.2f; running per 10 us:",
                cell, (t1 - t0) / 100.0, n, m[0] / n / 100, m[1] / n / 100, m[2] / n / 100, m[3] / n / 100, m[4] / n / 100);
   for (unsigned long long t = t0; t < t1; t += 1000) {
@@ -1492,11 +1502,10 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       // epoch tells this launch's jobs from stale ones
       const uint32_t ep = ++s.mesh_epoch == 0 ? ++s.mesh_epoch : s.mesh_epoch;
       const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
-      // k_mesh_row: a wave per sender, four per workgroup; a launch of few senders (the leader's
-      // block broadcast) gives each sender a 1024-lane workgroup, 16 waves over its tiles
+      // k_mesh_row: a wave per sender, 16 per workgroup; a launch of few senders (the leader's
+      // block broadcast) gives each sender a workgroup, its 16 waves over the sender's tiles
       const uint32_t rsplit = n_link <= s.row_split_max ? 16u : 1u;
-      const dim3 rgrid(rsplit > 1 ? n_link : (n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)),
-          rblock(rsplit > 1 ? 1024 : kRowThreads);
+      const dim3 rgrid(rsplit > 1 ? n_link : (n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)), rblock(kRowThreads);
       if ((rc = launch(s, -1, k_mesh_prep, grid, dim3(64), 0, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
           // (summary mode: the uniform jobs' rows; the tiles take the rest)
           (s.sum && (rc = launch(s, -1, k_mesh_row, rgrid, rblock, 0, s.kp_dev, cell, lo, hi, ep, row_hq(s, cell, lo, hi), rsplit))) ||

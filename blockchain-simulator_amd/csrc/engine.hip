@@ -7054,8 +7054,12 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
 // (extras) and records beyond the ring (overflow) are appended with one atomic per list and
 // wave.  The first pass takes a row-uniform sender's whole row at once (lane = receiver tile).
 // The per-edge work and its results are k_mesh_tile's.
-constexpr uint32_t kRowThreads = 256;  // four senders per workgroup, one wave each (1024 lanes: split rows)
+constexpr uint32_t kRowThreads = 1024;  // 16 senders per workgroup, one wave each (or one sender over 16 waves)
 struct RowShared {
+  XRec xs[kTX];  // staged extras / overflow records: one global atomic per list and workgroup
+  uint32_t xm[kTX];  // list << 24 | rank
+  uint32_t xn;
+  uint32_t lst[kMaxBuckets + 1];
   uint32_t lcnt[kMaxBuckets];
   uint32_t lmin[kMaxBuckets];
   uint32_t csum[8];
@@ -7104,8 +7108,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
     T.lcnt[k] = 0;
     T.lmin[k] = ~0u;
   }
+  for (uint32_t k = tid; k <= B; k += blockDim.x) T.lst[k] = 0;
   if (tid < 8) T.csum[tid] = 0;
-  if (tid == 0) T.ovmin = LLONG_MAX;
+  if (tid == 0) {
+    T.ovmin = LLONG_MAX;
+    T.xn = 0;
+  }
   if (tid >= 64 && tid < 64 + B) T.bmin[tid - 64] = *reinterpret_cast<volatile G<long long>*>(&gbl(p.bmin)[tid - 64]);
   const uint32_t fl = rl(jw.y, 0), jz = rl(jw.z, 0);
   act = act && rl(jw.x, 0) == epoch && job_uniform(fl, jz, prc);
@@ -7223,10 +7231,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
     }
     rtm = __ballot(fset != 0ull);
     nu = wave_sum(static_cast<uint32_t>(__popcll(fset)));
+    unsigned long long* const tdb = tph ? reinterpret_cast<unsigned long long*>(const_cast<unsigned long long*>(
+                                              reinterpret_cast<volatile unsigned long long*>(tph))) : nullptr;
+    if (tdb && lane == 0)  // (debug, BCSIM_WGT: rows / without a uniform state / beyond the ring / off the idle bucket)
+      atomicAdd(tdb + 7, 1ull | ((ruv ? 0ull : 1ull) << 16) | ((ring_u ? 0ull : 1ull) << 32) | ((pfd_u ? 0ull : 1ull) << 48));
 #pragma unroll 1
     for (uint32_t rt = t0; rt < t1; ++rt) {
       const uint64_t rmask = (static_cast<uint64_t>(rl(static_cast<uint32_t>(res >> 32), rt)) << 32) | rl(static_cast<uint32_t>(res), rt);
       if (!rmask) continue;  // (uniform) every edge of the tile done above
+      if (tdb && lane == 0) atomicAdd(tdb + 6, 1ull);  // (debug: tiles walked)
       // (a tile with an entry from above writes its other records as records)
       const bool fdone = (rl(static_cast<uint32_t>(fset), rt) | rl(static_cast<uint32_t>(fset >> 32), rt)) != 0u;
       const uint32_t s = rt * 64u + lane;
@@ -7423,8 +7436,35 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
           if (lane == q) gc = static_cast<uint32_t>(__popcll(mm));
           rem &= ~mm;
         }
+        // staged in LDS while the workgroup's area has room (one global atomic per list at the
+        // end: the heavy waves' extras all go to one list), else reserved in the global lists
+        const uint32_t nxa = static_cast<uint32_t>(__popcll(xmk));
+        uint32_t p0 = kInvalid;
+        if (lane == 0) {
+          uint32_t cur = __hip_atomic_load(&T.xn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          while (cur + nxa <= kTX) {
+            const uint32_t prev = atomicCAS(&T.xn, cur, cur + nxa);
+            if (prev == cur) {
+              p0 = cur;
+              break;
+            }
+            cur = prev;
+          }
+        }
+        p0 = rl(p0, 0);
+        if (p0 != kInvalid) {
+          uint32_t lb = 0;
+          if (gc) lb = atomicAdd(&T.lst[list], gc);
+          lb = static_cast<uint32_t>(__shfl(static_cast<int>(lb), static_cast<int>(ldr), 64));
+          if ((xmk >> lane) & 1ull) {
+            const uint32_t pos = p0 + static_cast<uint32_t>(__popcll(xmk & lbelow));
+            T.xs[pos] = x;
+            T.xm[pos] = (list << 24) | (lb + rk);
+          }
+          xmk = 0;
+        }
         uint32_t b0 = 0;
-        if (gc) b0 = gadd_r(list == B ? p.ov_cnt : &p.x_cnt[list], gc);
+        if (gc && xmk) b0 = gadd_r(list == B ? p.ov_cnt : &p.x_cnt[list], gc);
         b0 = static_cast<uint32_t>(__shfl(static_cast<int>(b0), static_cast<int>(ldr), 64));
         if ((xmk >> lane) & 1ull) {
           const uint32_t at = b0 + rk;
@@ -7469,6 +7509,29 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
   RPH(3);
   // (after the barrier: every wave of the sender has read the old word)
   if (act && part == 0 && lane == 0) gbl(p.rul)[g] = ring_u ? ((1ull << 63) | nw_u) : 0ull;
+  // the staged extras / overflow records: one atomic per list
+  if (T.xn) {
+    for (uint32_t k = tid; k <= B; k += blockDim.x) {
+      const uint32_t c = T.lst[k];
+      if (!c) continue;
+      uint32_t* ctr = k == B ? p.ov_cnt : &p.x_cnt[k];
+      const uint32_t cap = k == B ? p.cap_ov : p.cap_x;
+      const uint32_t base = gadd_r(ctr, c);
+      if (base + c > cap) set_err(p, BCSIM_E_OVERFLOW);
+      T.lst[k] = base;
+    }
+    __syncthreads();
+    const uint32_t nx = min(T.xn, kTX);
+    for (uint32_t k = tid; k < nx; k += blockDim.x) {
+      const uint32_t list = T.xm[k] >> 24, at = T.lst[list] + (T.xm[k] & 0xFFFFFFu);
+      const uint4* src = reinterpret_cast<const uint4*>(&T.xs[k]);
+      if (at < (list == B ? p.cap_ov : p.cap_x)) {
+        uint4* dst = reinterpret_cast<uint4*>(list == B ? p.ov + at : p.xbuf + static_cast<size_t>(list) * p.cap_x + at);
+        gst4(dst, src[0]);
+        gst4(dst + 1, src[1]);
+      }
+    }
+  }
   // busy buckets and their arrival-time bounds, counters
   for (uint32_t k = tid; k < B; k += blockDim.x)
     if (T.lcnt[k]) {
