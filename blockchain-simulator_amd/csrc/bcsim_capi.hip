@@ -1478,7 +1478,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
     // (list 3 holds a few nodes, the leader's cells among them: wide workgroups)
     // (node-partitioned: the kernels that stage records for other ranks)
-    const dim3 gl(std::min<uint32_t>(kLoopGrid, s.grid_link)), bl(std::min<uint32_t>(1024, 4 * s.bs_link));
+    const dim3 gl(std::min<uint32_t>(kLoopGrid, s.grid_link)), bl(std::min<uint32_t>(kLinkLoopThreads, 4 * s.bs_link));
     const size_t mlds = static_cast<size_t>(s.deg_max) * 8;  // (the PF variant's link words)
     const uint32_t z = 0, wep = s.l2_pending;
     if (wep) {  // list 2's link stage on the second stream, after its scan there

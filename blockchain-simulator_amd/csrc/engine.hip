@@ -336,6 +336,7 @@ constexpr uint32_t kSfD0 = 16u, kSfD1 = 32u, kSfD = kSfD0 | kSfD1;  // due in th
 constexpr uint32_t kMeshBc = 2, kTS = BCSIM_TILE_TS, kTR = 64;
 constexpr uint32_t kTileThreads = kTS * 16;  // four senders per wave
 constexpr uint32_t kLoopGrid = 256;  // workgroups of the looped generic grids (lists 2, 3) at most
+constexpr uint32_t kLinkLoopThreads = 512;  // k_link<.., LOOP> lanes per workgroup (its launch bound: no scratch)
 // job flags (mjob[g][0].y)
 constexpr uint32_t kJSl0 = 1u, kJSl1 = 2u, kJSd0 = 4u, kJSd1 = 8u, kJRxe = 16u, kJBig0 = 32u, kJBig1 = 64u;
 
@@ -5540,7 +5541,7 @@ __device__ void rul_flush(const KP& p, uint32_t g) {
 }
 
 template <int QM, bool XR, bool LOOP = false>
-__global__ __launch_bounds__(QM == 2 ? 256 : 1024) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+__global__ __launch_bounds__(QM == 2 ? 256 : (LOOP ? kLinkLoopThreads : 1024)) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                               long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();

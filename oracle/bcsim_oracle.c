@@ -264,8 +264,9 @@ typedef struct {
 typedef struct {
   fqflow f[3];
   int newl[3], oldl[3], n_new, n_old, n_created;
-  int64_t* dev; /* start times of the waiting device frames (ring) */
-  uint32_t dh, dn;
+  int64_t* dev; /* start times of the waiting device frames (ring of dcap <= fq_devcap, grown) */
+  uint32_t dh, dn, dcap;
+  uint32_t edge;
   int64_t dev_end;
   int stopped;
   uint32_t qpkts;
@@ -294,7 +295,9 @@ struct bcsim_oracle {
   uint32_t K;            /* Paxos decrees (>= 1) */
   int64_t* busy;         /* per edge */
   oqueue* q;             /* per edge (DROPTAIL only) */
-  fqlink* fq;            /* per edge (FQCODEL only) */
+  fqlink** fq;           /* per edge (FQCODEL only), created at the edge's first packet: at
+                          * n=4096 the full mesh has 16.8 M links, most of them holding a few
+                          * packets, so every per-link array starts small and grows */
   uint32_t* fqlnk;       /* per edge: its link's number in the mesh loop (the /24 network) */
   uint32_t* fqport;      /* per edge: UDP port of the sender's client socket, 0 = not bound yet */
   uint32_t* fqnport;     /* per node: client sockets bound so far (ephemeral ports 49153, ...) */
@@ -306,6 +309,7 @@ struct bcsim_oracle {
   uint32_t* flog;
   size_t nflog, capflog;
   int64_t flog_t0, flog_t1;
+  int flog_on;
   uint32_t nfr[2];       /* frames per message class (small, big) */
   int64_t tx_full[2];    /* time of a full (non-last) fragment frame */
   oheap heap;
@@ -759,29 +763,37 @@ static uint32_t fq_class_slot(bcsim_oracle* o, uint32_t edge, fqlink* l, int cls
   return slot;
 }
 
-static void fq_reset(bcsim_oracle* o) {
-  for (uint32_t e = 0; e < o->row[o->N]; ++e) {
-    fqlink* l = &o->fq[e];
-    for (int f = 0; f < 3; ++f) {
-      fqflow* F = &l->f[f];
-      F->head = F->n = 0;
-      F->bytes = 0;
-      F->first_above = F->drop_next = F->count = F->last_count = 0;
-      F->rec_inv_sqrt = (uint16_t)(~0u >> 16);
-      F->dropping = 0;
-      F->status = 0;
-      F->deficit = 0;
-      F->created = -1;
-    }
-    l->n_new = l->n_old = l->n_created = 0;
-    l->dh = l->dn = 0;
-    l->dev_end = 0;
-    l->stopped = 0;
-    l->qpkts = 0;
-    for (uint32_t m = 0; m < l->nmsg; ++m) l->msg[m].used = 0;
-    l->nmsg = 0;
-    for (int c = 0; c < 3; ++c) l->cbound[c] = 0;
+static void fq_free_link(fqlink* l) {
+  for (int f = 0; f < 3; ++f) free(l->f[f].a);
+  free(l->dev);
+  free(l->msg);
+  free(l);
+}
+
+/* the edge's link state, created at its first use */
+static fqlink* fq_get(bcsim_oracle* o, uint32_t edge) {
+  fqlink* l = o->fq[edge];
+  if (l) return l;
+  l = (fqlink*)calloc(1, sizeof(fqlink));
+  if (!l) {
+    set_err(o, BCSIM_E_NOMEM);
+    return NULL;
   }
+  for (int f = 0; f < 3; ++f) {
+    l->f[f].rec_inv_sqrt = (uint16_t)(~0u >> 16);
+    l->f[f].created = -1;
+  }
+  l->edge = edge;
+  o->fq[edge] = l;
+  return l;
+}
+
+static void fq_reset(bcsim_oracle* o) {
+  for (uint32_t e = 0; e < o->row[o->N]; ++e)
+    if (o->fq[e]) {
+      fq_free_link(o->fq[e]);
+      o->fq[e] = NULL;
+    }
   memset(o->fqport, 0, (size_t)o->row[o->N] * sizeof(uint32_t));
   memset(o->fqnport, 0, (size_t)o->N * sizeof(uint32_t));
   memset(o->fqphant, 0, o->N);
@@ -789,11 +801,8 @@ static void fq_reset(bcsim_oracle* o) {
 
 static void free_fq(bcsim_oracle* o) {
   if (o->fq && o->row)
-    for (uint32_t e = 0; e < o->row[o->N]; ++e) {
-      for (int f = 0; f < 3; ++f) free(o->fq[e].f[f].a);
-      free(o->fq[e].dev);
-      free(o->fq[e].msg);
-    }
+    for (uint32_t e = 0; e < o->row[o->N]; ++e)
+      if (o->fq[e]) fq_free_link(o->fq[e]);
   free(o->fq);
   free(o->fqlnk);
   free(o->fqport);
@@ -827,7 +836,7 @@ static void fq_free_msg(fqlink* l, uint32_t m) {
 /* kinds: 1 enqueue (x = flow slot), 2 into the device queue (x = frame start), 3 drop, 4 wake
  * (x = packets in the disc) */
 static void fq_log(bcsim_oracle* o, const fqlink* l, uint32_t kind, const fqpkt* pk, int64_t x) {
-  if (!getenv("ORACLE_FQLOG") || o->now < o->flog_t0 || o->now >= o->flog_t1) return;
+  if (!o->flog_on || o->now < o->flog_t0 || o->now >= o->flog_t1) return;
   if (o->nflog == o->capflog) {
     size_t nc = o->capflog ? 2 * o->capflog : 4096;
     uint32_t* na = (uint32_t*)realloc(o->flog, nc * 8 * sizeof(uint32_t));
@@ -836,7 +845,7 @@ static void fq_log(bcsim_oracle* o, const fqlink* l, uint32_t kind, const fqpkt*
     o->capflog = nc;
   }
   uint32_t* r = o->flog + 8 * o->nflog++;
-  uint32_t e = (uint32_t)(l - o->fq);
+  uint32_t e = l->edge;
   r[0] = (uint32_t)o->now;
   r[1] = (uint32_t)((uint64_t)o->now >> 32);
   r[2] = e;
@@ -998,7 +1007,7 @@ static void fq_schedule_wake(bcsim_oracle* o, uint32_t edge, int64_t t) {
 /* frames of the device queue that started transmission by now are no longer waiting */
 static void fq_dev_settle(bcsim_oracle* o, fqlink* l) {
   while (l->dn && l->dev[l->dh] <= o->now) {
-    l->dh = (l->dh + 1) % o->fq_devcap;
+    l->dh = (l->dh + 1) % l->dcap;
     --l->dn;
   }
 }
@@ -1014,7 +1023,21 @@ static void fq_dev_push(bcsim_oracle* o, uint32_t edge, fqlink* l, const fqpkt* 
   l->dev_end = end;
   fq_dev_settle(o, l);
   if (start > o->now) {
-    l->dev[(l->dh + l->dn) % o->fq_devcap] = start;
+    if (l->dn == l->dcap) { /* grow the ring (capacity fq_devcap at most: the queue stops there) */
+      uint32_t nc = l->dcap ? 2 * l->dcap : 4;
+      if (nc > o->fq_devcap) nc = o->fq_devcap;
+      int64_t* na = (int64_t*)malloc(nc * sizeof(int64_t));
+      if (!na) {
+        set_err(o, BCSIM_E_NOMEM);
+        return;
+      }
+      for (uint32_t k = 0; k < l->dn; ++k) na[k] = l->dev[(l->dh + k) % l->dcap];
+      free(l->dev);
+      l->dev = na;
+      l->dh = 0;
+      l->dcap = nc;
+    }
+    l->dev[(l->dh + l->dn) % l->dcap] = start;
     ++l->dn;
     if (l->dn == o->fq_devcap) { /* the queue cannot take another packet: stop the disc */
       l->stopped = 1;
@@ -1047,7 +1070,8 @@ static void fq_run(bcsim_oracle* o, uint32_t edge, fqlink* l) {
 
 /* the device queue wakes the disc (its oldest waiting frame starts now) */
 static void fq_wake(bcsim_oracle* o, uint32_t edge) {
-  fqlink* l = &o->fq[edge];
+  fqlink* l = fq_get(o, edge);
+  if (!l) return;
   fq_log(o, l, 4, NULL, l->qpkts);
   fq_dev_settle(o, l);
   l->stopped = 0;
@@ -1079,7 +1103,7 @@ static void fq_overlimit(bcsim_oracle* o, fqlink* l) {
 
 static int fq_push(bcsim_oracle* o, fqflow* F, const fqpkt* pk) {
   if (F->n == F->cap) {
-    uint32_t nc = F->cap ? 2 * F->cap : 64;
+    uint32_t nc = F->cap ? 2 * F->cap : 4;
     fqpkt* na = (fqpkt*)malloc(nc * sizeof(fqpkt));
     if (!na) return BCSIM_E_NOMEM;
     for (uint32_t i = 0; i < F->n; ++i) na[i] = F->a[(F->head + i) % F->cap];
@@ -1097,11 +1121,12 @@ static int fq_push(bcsim_oracle* o, fqflow* F, const fqpkt* pk) {
 /* a message (application send or echo) handed to the link at o->now: IPv4 fragments
  * it and hands each fragment to the traffic-control layer (enqueue, then Run) */
 static void fq_send(bcsim_oracle* o, uint32_t edge, const omsg* msg, uint32_t sub, int echo) {
-  fqlink* l = &o->fq[edge];
+  fqlink* l = fq_get(o, edge);
+  if (!l) return;
   uint32_t mi = 0;
   while (mi < l->nmsg && l->msg[mi].used) ++mi;
   if (mi == l->capmsg) {
-    uint32_t nc = l->capmsg ? 2 * l->capmsg : 16;
+    uint32_t nc = l->capmsg ? 2 * l->capmsg : 2;
     fqmsg* na = (fqmsg*)realloc(l->msg, nc * sizeof(fqmsg));
     if (!na) {
       set_err(o, BCSIM_E_NOMEM);
@@ -1784,16 +1809,12 @@ int bcsim_oracle_set_topology_csr(bcsim_oracle* o, uint32_t n,
     }
   free(t);
   if (o->cfg.queue_model == BCSIM_QUEUE_FQCODEL) {
-    o->fq = (fqlink*)calloc(E ? E : 1, sizeof(fqlink));
+    o->fq = (fqlink**)calloc(E ? E : 1, sizeof(fqlink*));
     o->fqlnk = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
     o->fqport = (uint32_t*)calloc(E ? E : 1, sizeof(uint32_t));
     o->fqnport = (uint32_t*)calloc(o->N, sizeof(uint32_t));
     o->fqphant = (uint8_t*)calloc(o->N, 1);
     if (!o->fq || !o->fqlnk || !o->fqport || !o->fqnport || !o->fqphant) return BCSIM_E_NOMEM;
-    for (uint32_t e = 0; e < E; ++e) {
-      o->fq[e].dev = (int64_t*)malloc(o->fq_devcap * sizeof(int64_t));
-      if (!o->fq[e].dev) return BCSIM_E_NOMEM;
-    }
     fq_build_links(o);
   }
   o->topo_set = 1;
@@ -1865,6 +1886,7 @@ int bcsim_oracle_create(const bcsim_config* cfg, bcsim_oracle** out) {
     o->fq_devcap = o->cfg.queue_dev_pkts;
     o->flog_t0 = getenv("BCSIM_FQLOG_T0") ? atoll(getenv("BCSIM_FQLOG_T0")) : 0;
     o->flog_t1 = getenv("BCSIM_FQLOG_T1") ? atoll(getenv("BCSIM_FQLOG_T1")) : INT64_MAX;
+    o->flog_on = getenv("ORACLE_FQLOG") != NULL;
     if (o->fq_devcap == 0) {
       bcsim_oracle_destroy(o);
       return BCSIM_E_INVAL;

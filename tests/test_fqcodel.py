@@ -156,3 +156,24 @@ def test_fqcodel_c4_fullsize_conservation(engine_lib):
     assert cnt["delivered_total"] + cnt["msgs_lost"] + cnt["dropped"] <= cnt["sends"]
     assert 0 < cnt["msgs_lost"] <= cnt["frames_dropped"]
     assert cnt["delivered"][2] > 0  # PREPAREs got through
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_fqcodel_c4_n4096_matches_oracle_200ms(engine_lib):
+    """The bench configuration under FQCODEL at BASELINE size (PBFT n=4096 full mesh, 16.8 M
+    links each with its FqCoDel disc and device queue, blockchain-simulator.cc:41-42) against the
+    oracle over the first 200 ms simulated: the leader's 50 KB PRE_PREPARE through 4095 discs
+    (35 fragments each) and the PREPARE wave, 16.8 M deliveries -- traces and counters bit for
+    bit.  (The oracle creates a link's FQ state at its first packet: ~60 s and ~13 GB here.)"""
+    import bcsim
+    c = bcsim.preset("c4_pbft4096")
+    c.stop_ns = -1
+    c.queue_model = _abi.QUEUE_FQCODEL
+    c.t_end_ns = 200_000_000
+    got = bcsim.run(c)
+    assert got[2]["error"] == 0
+    want = oracle.run(c)
+    assert want[1]["delivered_total"] > 16_000_000
+    d = compare(want, got)
+    assert d is None, d
