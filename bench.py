@@ -371,6 +371,9 @@ def main():
             "config": {"workload": wl,
                        "nodes": args.nodes, "step": "one 50 ms block interval",
                        "engine": args.engine,
+                       "link_queue": {"infinite": "unbounded FIFO per link (no queue disc)",
+                                      "droptail": "100-packet device queue + pfifo_fast",
+                                      "fqcodel": "100-packet device queue + FqCoDel"}[args.queue],
                        "parallelism": f"{mode}{world}" if world > 1 or args.pdes1 else "single"},
             "committed_rounds_per_s": rounds / dt,
             "roofline": {"kernel": "k_link (inbox scatter)", "bound": "hbm", "achieved": ach,

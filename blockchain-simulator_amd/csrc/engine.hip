@@ -4145,10 +4145,15 @@ __device__ inline uint32_t q_admit(const KP& p, uint64_t* ring, uint64_t& meta, 
 // One lane owns one directed edge and walks its events in time order (the link's ops in key
 // order, the device-queue wakes in between), so the disc state lives in global memory and is
 // read and written by that lane only.  Words only (no sub-dword struct members: DESIGN §8).
+// While the lane works on the edge its 64-word header (flows, DRR lists, device-queue ring
+// state) is staged in the lane's slot of LDS: every step of the disc is a chain of dependent
+// header accesses (the class's flow, then its ring position, then the DRR lists ...), ~40 per
+// packet, which in global memory were one round trip each.
 constexpr uint32_t kFqH = 64, kFqF = 12;
 enum : uint32_t { FQ_HEAD = 0, FQ_N, FQ_BYTES, FQ_FA, FQ_DNEXT, FQ_CNT, FQ_LCNT, FQ_REC, FQ_DROP, FQ_ST, FQ_DEF, FQ_CR };
 enum : uint32_t { FQ_NNEW = 36, FQ_NEWL = 37, FQ_NOLD = 40, FQ_OLDL = 41, FQ_NCR = 44, FQ_STOP = 45, FQ_DH = 46,
                   FQ_DN = 47, FQ_DEND = 48, FQ_QP = 50, FQ_MBM = 52 };
+constexpr uint32_t kFqLanes = 256;   // k_link<2>'s launch bound: LDS header slots per workgroup
 constexpr uint32_t kFqMaxMsgs = 128;  // message-table bitmap words FQ_MBM..FQ_MBM+3
 constexpr uint32_t kFqEcho = 1u << 25, kFqLost = 1u << 26;
 
@@ -4158,8 +4163,9 @@ constexpr uint32_t FQ_MAP = 56, FQ_HSH = 57;
 // a FQCODEL record shipped to another rank carries its socket's port - 49152 in cell bits 48-61
 constexpr int kXPortShift = 48;
 static_assert(FQ_MBM + kFqMaxMsgs / 32 <= FQ_MAP && FQ_HSH + 3 <= kFqH, "FQCODEL header layout");
+using FqW = __attribute__((address_space(3))) uint32_t;  // (the staged header: LDS)
 struct FqLink {
-  uint32_t* h;
+  FqW* h;
   int64_t* dev;
   uint4* pk;
   uint4* msg;
@@ -4184,18 +4190,31 @@ struct FqCount {
   unsigned long long fdrop, lost;
 };
 
-__device__ inline int64_t fq_ld64(const uint32_t* w) {
+__device__ inline int64_t fq_ld64(const FqW* w) {
   return static_cast<int64_t>((static_cast<uint64_t>(w[1]) << 32) | w[0]);
 }
-__device__ inline void fq_st64(uint32_t* w, int64_t v) {
+__device__ inline void fq_st64(FqW* w, int64_t v) {
   w[0] = static_cast<uint32_t>(v);
   w[1] = static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32);
 }
 // edge e = (i -> j) at rank-local index le.  Addresses: the k-th link of the mesh loop
 // (blockchain-simulator.cc:34-51) is network 1.0.0.0 + k*256, its larger endpoint .1
-__device__ inline FqLink fq_link(const KP& p, size_t le, uint32_t e, uint32_t i, uint32_t j) {
+__device__ inline FqLink fq_link(const KP& p, size_t le, uint32_t e, uint32_t i, uint32_t j, FqW* hl) {
   FqLink L;
-  L.h = p.fqh + le * kFqH;
+  {  // the header into the lane's LDS slot (16 loads in flight)
+    const uint4* src = reinterpret_cast<const uint4*>(p.fqh + le * kFqH);
+    uint4 v[kFqH / 4];
+#pragma unroll
+    for (uint32_t k = 0; k < kFqH / 4; ++k) v[k] = gld4(src + k);
+#pragma unroll
+    for (uint32_t k = 0; k < kFqH / 4; ++k) {
+      hl[4 * k] = v[k].x;
+      hl[4 * k + 1] = v[k].y;
+      hl[4 * k + 2] = v[k].z;
+      hl[4 * k + 3] = v[k].w;
+    }
+  }
+  L.h = hl;
   L.dev = p.fqdev + le * p.fq_devcap;
   const uint64_t po = p.fqpoff[le];
   L.pk = p.fqpk + (po & ((1ull << 48) - 1));
@@ -4212,6 +4231,12 @@ __device__ inline FqLink fq_link(const KP& p, size_t le, uint32_t e, uint32_t i,
 }
 // Ipv4QueueDiscItem::Hash: Murmur3-32 (seed 0x8BADF00D) of src | dst | proto 17 | sport |
 // dport | perturbation, big endian (17 bytes; oracle_fq_flow)
+// the staged header back to global memory (edge done)
+__device__ inline void fq_unlink(const KP& p, const FqLink& L, size_t le) {
+  uint4* dst = reinterpret_cast<uint4*>(p.fqh + le * kFqH);
+#pragma unroll
+  for (uint32_t k = 0; k < kFqH / 4; ++k) gst4(dst + k, make_uint4(L.h[4 * k], L.h[4 * k + 1], L.h[4 * k + 2], L.h[4 * k + 3]));
+}
 __device__ inline uint32_t fq_hash(uint32_t src, uint32_t dst, uint32_t sp, uint32_t dp, uint32_t pert) {
   auto bs = [](uint32_t x) { return __builtin_bswap32(x); };
   auto mix = [](uint32_t h, uint32_t k) {
@@ -4262,7 +4287,7 @@ __device__ inline uint32_t fq_class_slot(const KP& p, FqLink& L, uint32_t cls) {
   return slot;
 }
 __device__ inline bool fq_pop(const KP& p, FqLink& L, uint32_t f, uint4& out) {
-  uint32_t* F = L.h + f * kFqF;
+  FqW* F = L.h + f * kFqF;
   const uint32_t n = F[FQ_N];
   if (n == 0) return false;
   const uint32_t hd = F[FQ_HEAD];
@@ -4289,7 +4314,7 @@ __device__ inline void fq_drop(const KP& p, FqLink& L, const uint4& pk, FqCount&
   if (left == 1) fq_free_msg(L, m);
 }
 // CoDelQueueDisc::OkToDrop (has: a packet was dequeued)
-__device__ inline bool codel_ok(const KP& p, uint32_t* F, bool has, const uint4& pk, int64_t now, uint32_t now_c) {
+__device__ inline bool codel_ok(const KP& p, FqW* F, bool has, const uint4& pk, int64_t now, uint32_t now_c) {
   if (!has) {
     F[FQ_FA] = 0;
     return false;
@@ -4319,7 +4344,7 @@ __device__ inline uint32_t codel_law(uint32_t t, uint32_t interval, uint32_t rec
 }
 // CoDelQueueDisc::DoDequeue of flow f
 __device__ inline bool codel_deq(const KP& p, FqLink& L, uint32_t f, int64_t now, uint4& out, FqCount& c) {
-  uint32_t* F = L.h + f * kFqF;
+  FqW* F = L.h + f * kFqF;
   uint4 pk;
   if (!fq_pop(p, L, f, pk)) {
     F[FQ_DROP] = 0;
@@ -4362,24 +4387,24 @@ __device__ inline bool codel_deq(const KP& p, FqLink& L, uint32_t f, int64_t now
   if (have) out = pk;
   return have;
 }
-__device__ inline void fq_list_pop(uint32_t* h, uint32_t nidx, uint32_t lidx) {
+__device__ inline void fq_list_pop(FqW* h, uint32_t nidx, uint32_t lidx) {
   const uint32_t n = h[nidx];
   for (uint32_t k = 1; k < n; ++k) h[lidx + k - 1] = h[lidx + k];
   h[nidx] = n - 1;
 }
-__device__ inline void fq_list_push(uint32_t* h, uint32_t nidx, uint32_t lidx, uint32_t f) {
+__device__ inline void fq_list_push(FqW* h, uint32_t nidx, uint32_t lidx, uint32_t f) {
   const uint32_t n = h[nidx];
   h[lidx + n] = f;
   h[nidx] = n + 1;
 }
 // FqCoDelQueueDisc::DoDequeue: DRR over the new, then the old flows
 __device__ inline bool fq_deq(const KP& p, FqLink& L, int64_t now, uint4& out, FqCount& c) {
-  uint32_t* h = L.h;
+  FqW* h = L.h;
   for (;;) {
     int f = -1;
     while (f < 0 && h[FQ_NNEW]) {
       const uint32_t q = h[FQ_NEWL];
-      uint32_t* F = h + q * kFqF;
+      FqW* F = h + q * kFqF;
       if (static_cast<int32_t>(F[FQ_DEF]) <= 0) {
         F[FQ_DEF] += p.fq_quantum;
         F[FQ_ST] = 2;
@@ -4391,7 +4416,7 @@ __device__ inline bool fq_deq(const KP& p, FqLink& L, int64_t now, uint4& out, F
     }
     while (f < 0 && h[FQ_NOLD]) {
       const uint32_t q = h[FQ_OLDL];
-      uint32_t* F = h + q * kFqF;
+      FqW* F = h + q * kFqF;
       if (static_cast<int32_t>(F[FQ_DEF]) <= 0) {
         F[FQ_DEF] += p.fq_quantum;
         fq_list_pop(h, FQ_NOLD, FQ_OLDL);
@@ -4401,7 +4426,7 @@ __device__ inline bool fq_deq(const KP& p, FqLink& L, int64_t now, uint4& out, F
       }
     }
     if (f < 0) return false;
-    uint32_t* F = h + f * kFqF;
+    FqW* F = h + f * kFqF;
     if (codel_deq(p, L, static_cast<uint32_t>(f), now, out, c)) {
       F[FQ_DEF] -= out.w;
       return true;
@@ -4505,6 +4530,26 @@ __device__ inline void fq_overlimit(const KP& p, FqLink& L, FqCount& c, int64_t 
 template <typename Emit>
 __device__ inline void fq_send(const KP& p, FqLink& L, int64_t now, uint32_t sub, uint32_t bz, uint32_t bw24, int big,
                                bool echo, Emit& emit, FqCount& c) {
+  const uint32_t F = sel2(p.nfr, big);
+  if (F == 1 && !p.fqlog && p.fq_limit >= 1 && L.h[FQ_QP] == 0 && !L.h[FQ_STOP] && fq_ld64(L.h + FQ_DEND) <= now) {
+    // the heavy waves' case: a one-fragment message on a link whose disc is empty (so both DRR
+    // lists are and every flow is inactive) and whose device is idle.  The slow path below would
+    // enqueue the packet into its (new) flow, dequeue it at once (sojourn 0: CoDel leaves the
+    // drop state), transmit it from now, then empty the lists again; its net effect is this:
+    const uint32_t fs = fq_class_slot(p, L, echo ? 1u : 0u);
+    FqW* Fh = L.h + fs * kFqF;
+    if (Fh[FQ_CR] == kInvalid) Fh[FQ_CR] = L.h[FQ_NCR]++;
+    int32_t d = static_cast<int32_t>(p.fq_quantum) - static_cast<int32_t>(p.ip_last[big]);
+    if (d <= 0) d += static_cast<int32_t>(p.fq_quantum);  // (a second DRR round on the old list)
+    Fh[FQ_DEF] = static_cast<uint32_t>(d);
+    Fh[FQ_FA] = 0;
+    Fh[FQ_DROP] = 0;
+    fq_settle(p, L, now);  // (every waiting frame started by the idle device's end)
+    const int64_t end = now + sel2(p.tx_last, big);
+    fq_st64(L.h + FQ_DEND, end);
+    if (!echo) emit(sub, bz, bw24, big, end);
+    return;
+  }
   uint32_t m = kInvalid;
   for (uint32_t w = 0; w < p.cap_fqm / 32u && m == kInvalid; ++w) {
     const uint32_t free_bits = ~L.h[FQ_MBM + w];
@@ -4515,13 +4560,12 @@ __device__ inline void fq_send(const KP& p, FqLink& L, int64_t now, uint32_t sub
     return;
   }
   L.h[FQ_MBM + (m >> 5)] |= 1u << (m & 31u);
-  const uint32_t F = sel2(p.nfr, big);
   L.msg[m] = make_uint4(sub, bz, bw24 | (static_cast<uint32_t>(big) << 24) | (echo ? kFqEcho : 0u), F);
   const uint32_t now_lo = static_cast<uint32_t>(now), now_hi = static_cast<uint32_t>(static_cast<uint64_t>(now) >> 32);
   for (uint32_t j = 0; j < F; ++j) {
     const uint32_t cls = j ? 2u : echo ? 1u : 0u;
     const uint32_t f = fq_class_slot(p, L, cls);
-    uint32_t* Fh = L.h + f * kFqF;
+    FqW* Fh = L.h + f * kFqF;
     if (Fh[FQ_CR] == kInvalid) Fh[FQ_CR] = L.h[FQ_NCR]++;
     if (Fh[FQ_ST] == 0) {
       Fh[FQ_ST] = 1;
@@ -5047,6 +5091,9 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     // wakes in between and up to the window end; records are emitted when a message's last
     // fragment enters the device queue (oracle fq_*) ----
     long long fq_wmin = LLONG_MAX;
+    __shared__ uint32_t fq_hl_s[kFqLanes * kFqH];  // each lane's staged link header
+    FqW* const fq_hl = (FqW*)(fq_hl_s);
+    if (blockDim.x > kFqLanes) set_err(p, BCSIM_E_STATE);
     for (uint32_t le = tid; le < deg; le += blockDim.x) {
       const uint32_t eb = n_list && le ? ecnt[le - 1] : 0u, ee = n_list ? ecnt[le] : 0u;
       const uint32_t e = e0 + le;
@@ -5101,7 +5148,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       const int64_t pr = p.prop_const >= 0 ? p.prop_const : prop[le];
       const uint32_t slot = p.mesh ? s * (p.N - 1) + (i < s ? i : i - 1) : AT(p.rev, e, p.E);
       const uint32_t dg = rep * p.N + s;
-      FqLink FL = fq_link(p, eb0 + le, e, i, s);
+      FqLink FL = fq_link(p, eb0 + le, e, i, s, fq_hl + tid * kFqH);
       FqCount fc{0, 0};
       // a delivery: the record for the receiver's inbox slot / extras / overflow (as link_node)
       auto emit = [&](uint32_t sub, uint32_t bz, uint32_t bw24, int big, int64_t end) {
@@ -5241,6 +5288,7 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       const int64_t bu = fq_ld64(FL.h + FQ_DEND);
       if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
       *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
+      fq_unlink(p, FL, eb0 + le);
     }
     if (fq_wmin != LLONG_MAX) atomicMin(&L.omin, fq_wmin);
     __syncthreads();
