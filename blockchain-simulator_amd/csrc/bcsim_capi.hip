@@ -100,8 +100,11 @@ struct Sim {
   KP* kp_dev2 = nullptr;
   bool gossip_frontier = true;  // dense gossip: k_gossip_cell over the window's frontier (BCSIM_GOSSIP_FRONTIER=0: all)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
-  bool sum = false;
-  uint32_t row_split_max = 64;  // k_mesh_row: launches of at most this many senders split rows (BCSIM_ROW_SPLIT)        // heavy-wave record summaries (BCSIM_SUM=0: off)
+  bool sum = false;  // heavy-wave record summaries (BCSIM_SUM=0: off)
+  uint32_t row_split_max = 64;  // k_mesh_row: launches of at most this many senders split rows (BCSIM_ROW_SPLIT)
+  // summary mode, opt-in (BCSIM_ACT_RB=0): the window's kernels sized on the device, no read-back
+  // of k_active's list lengths (measured slower: 0.73 vs 0.53 ms per step)
+  bool dev_sized = false;
   uint32_t rt_min = 0;     // summary mode: k_scan_rt takes windows of at least this many scanned nodes (BCSIM_RT_MIN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -1069,6 +1072,7 @@ static int setup_device(Sim& s) {
   if (const char* fv = std::getenv("BCSIM_DBG_FAIL_IMPORT"); fv && *fv) s.dbg_fail_import = std::atoll(fv);
   if (const char* fv = std::getenv("BCSIM_DBG_DEV_ERR"); fv && *fv) s.dbg_dev_err = std::atoll(fv);
   if (const char* rs = std::getenv("BCSIM_ROW_SPLIT"); rs && *rs) s.row_split_max = static_cast<uint32_t>(std::atoi(rs));
+  if (const char* ab = std::getenv("BCSIM_ACT_RB"); ab && *ab == '0') s.dev_sized = true;
   if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -1272,6 +1276,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     return BCSIM_OK;
   }
   uint32_t n_link = 1;
+  bool scan_dsz = false;  // (summary mode: the scan grids are sized on the device)
   {  // compact lists of the window's active gnodes
     // contiguous chunks of >= 256 gnodes (<= kActChunk), at most ~1024 workgroups (N=4096:
     // 16 workgroups of one gnode per lane; 2 of 2048 took 14-22 us of dependent loads per lane)
@@ -1285,7 +1290,19 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       const char* e = std::getenv("BCSIM_NO_ACTSYNC");
       return e && *e == '1';
     }();
-    if (!s.sparse && !s.pdes && !no_sync) {
+    // summary mode (heavy and light PBFT windows alike): k_scan_rt's fixed grid, looped generic
+    // grids and device-sized link kernels -- the window makes no round trip to the host here
+    const bool ss = (lo <= 0 && 0 < hi) || (s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi);
+    static const uint32_t dmask = [] {  // (A/B: bit 0 the scan, bit 1 the link stage device-sized)
+      const char* e = std::getenv("BCSIM_DEVSZ");
+      return e && *e ? static_cast<uint32_t>(std::atoi(e)) : 3u;
+    }();
+    const bool dsz = s.sum && s.dev_sized && s.scan_fast && !ss && s.kp.wgtt == nullptr && !s.kp.wgs;
+    if (dsz && dmask == 3u) {
+      grid = dim3((s.NT + 7) / 8 * 8);  // (list_range: a multiple of 8 workgroups)
+      scan_dsz = true;
+      n_link = kDevSized;
+    } else if (!s.sparse && !s.pdes && !no_sync) {
       // dense layout: read the list lengths back and launch exactly one workgroup per entry
       // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
       // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
@@ -1301,6 +1318,11 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       }
       grid = dim3((s.act_h[0] + 7) / 8 * 8);
       n_link = s.act_h[1];
+      if (dsz && (dmask & 1u)) {
+        grid = dim3((s.NT + 7) / 8 * 8);
+        scan_dsz = true;
+      }
+      if (dsz && (dmask & 2u)) n_link = kDevSized;
       static const bool winlog = std::getenv("BCSIM_WINLOG") != nullptr;  // (debug: one line per window)
       if (winlog)
         std::fprintf(stderr, "[win] cell %lld [%lld, %lld) +%lld us scan %u link %u xa %d\n", cell, lo, hi, (lo - cell * s.L) / 1000,
@@ -1319,8 +1341,8 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   // of the window's nodes are materialised for the kernels that read slots only
   const dim3 grid_rt(s.R * s.kp.n_tiles);
   const bool ss_win = (lo <= 0 && 0 < hi) || (s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi);
-  const bool use_rt = s.sum && grid.x && s.scan_fast && !ss_win && !(s.kp_dev_big && grid.x <= s.few_scan) &&
-                      grid.x >= s.rt_min;
+  const bool use_rt = s.sum && grid.x && s.scan_fast && !ss_win &&
+                      (scan_dsz || (!(s.kp_dev_big && grid.x <= s.few_scan) && grid.x >= s.rt_min));
   if (s.sum && grid.x && !use_rt &&
       (rc = launch(s, KS_SCAN, k_scan_rt, grid_rt, dim3(1024), 0, s.kp_dev, cell, lo, hi, cs, xa, 0u, 1)))
     return rc;
@@ -1452,7 +1474,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       std::fprintf(stderr, "\n");
     }
   }
-  grid = dim3(s.sparse ? s.grid_link : (n_link + 7) / 8 * 8);
+  grid = dim3(s.sparse ? s.grid_link : n_link == kDevSized ? (s.NT + 7) / 8 * 8 : (n_link + 7) / 8 * 8);
   if (grid.x == 0 && s.l2_pending) grid = dim3(8);  // (list 2 is in list 1; the join below must run anyway)
   if (grid.x == 0)
     rc = BCSIM_OK;
@@ -1504,8 +1526,12 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       const uint32_t nt = s.R * s.kp.n_stiles * s.kp.n_tiles;
       // k_mesh_row: a wave per sender, 16 per workgroup; a launch of few senders (the leader's
       // block broadcast) gives each sender a workgroup, its 16 waves over the sender's tiles
-      const uint32_t rsplit = n_link <= s.row_split_max ? 16u : 1u;
-      const dim3 rgrid(rsplit > 1 ? n_link : (n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)), rblock(kRowThreads);
+      // (device-sized: the kernel decides from the list length; its grid covers both shapes)
+      const bool dsz = n_link == kDevSized;
+      const uint32_t rsplit = dsz ? (kRowSplitDev | s.row_split_max) : n_link <= s.row_split_max ? 16u : 1u;
+      const dim3 rgrid(dsz ? std::max<uint32_t>(s.row_split_max, (s.NT + kRowThreads / 64 - 1) / (kRowThreads / 64))
+                           : rsplit > 1 ? n_link : (n_link + kRowThreads / 64 - 1) / (kRowThreads / 64)),
+          rblock(kRowThreads);
       if ((rc = launch(s, -1, k_mesh_prep, grid, dim3(64), 0, s.kp_dev, cell, lo, hi, fw, ep, wep)) ||
           // (summary mode: the uniform jobs' rows; the tiles take the rest)
           (s.sum && (rc = launch(s, -1, k_mesh_row, rgrid, rblock, 0, s.kp_dev, cell, lo, hi, ep, row_hq(s, cell, lo, hi), rsplit))) ||

@@ -7103,6 +7103,8 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(6,
 // (extras) and records beyond the ring (overflow) are appended with one atomic per list and
 // wave.  The first pass takes a row-uniform sender's whole row at once (lane = receiver tile).
 // The per-edge work and its results are k_mesh_tile's.
+constexpr uint32_t kRowSplitDev = 1u << 31;  // k_mesh_row's split argument: decide from the list length
+constexpr uint32_t kDevSized = 0xFFFFFFFFu;    // (host) a window whose kernels are sized on the device
 constexpr uint32_t kRowThreads = 1024;  // 16 senders per workgroup, one wave each (or one sender over 16 waves)
 struct RowShared {
   XRec xs[kTX];  // staged extras / overflow records: one global atomic per list and workgroup
@@ -7139,6 +7141,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
   // a sender's row when the launch has few senders -- the leader's block broadcast -- each one a
   // contiguous range of its receiver tiles) and, all at once, its job words (lanes 0-3), its
   // broadcast (4-5) and its row's uniform link word (6)
+  if (split & kRowSplitDev) split = p.act_n[1] <= (split & 0xFFFFu) ? 16u : 1u;  // (device-sized launch)
   const uint32_t part = wv % split, kk = blockIdx.x * (nwv / split) + wv / split;
   const uint32_t tpp = (p.n_tiles + split - 1) / split, t0 = min(p.n_tiles, part * tpp), t1 = min(p.n_tiles, t0 + tpp);
   const bool own_t = lane >= t0 && lane < t1;  // (lane k: tile k is this wave's)
