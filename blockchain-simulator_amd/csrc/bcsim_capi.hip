@@ -129,6 +129,10 @@ struct Sim {
   uint32_t P = 1, prank = 0, nlo = 0, nloc = 0;
   Xport* xp = nullptr;
   uint32_t* scnt_h = nullptr;  // host view of the per-rank send counts (control block)
+  // node-partitioned over RCCL: the control words of the window's exchange on the device
+  // ([2][P][kCtlWords] int64: this rank's, then the received ones; BCSIM_CTL_DEV=0: off)
+  int64_t* ctlw_d = nullptr;
+  int64_t* ctlw_h = nullptr;  // pinned
   XRec* recvbuf = nullptr;
   uint64_t cap_recv = 0;
   uint32_t vsync = 0;          // v-log entries already exchanged
@@ -213,6 +217,7 @@ static int ev_collect(Sim& s) {
 }
 
 static int mirror_wait(Sim& s, const uint32_t* w);  // (below, with readback)
+static int readback_apply(Sim& s);
 
 static int validate(const bcsim_config& c) {
   if (c.abi_version != BCSIM_ABI_VERSION) return BCSIM_E_INVAL;
@@ -970,6 +975,13 @@ static int setup_device(Sim& s) {
   s.bcnt_h = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s.ctl_h) + sizeof(Ctl));
   s.xcnt_h = s.bcnt_h + s.B;
   s.scnt_h = s.xcnt_h + s.B;
+  if (s.xp && s.xp->device_ctl()) {
+    const char* cd = std::getenv("BCSIM_CTL_DEV");
+    if (!(cd && *cd == '0')) {
+      if ((rc = dalloc(s, &s.ctlw_d, 2ull * s.P * Xport::kCtlWords))) return rc;
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&s.ctlw_h), 2ull * s.P * Xport::kCtlWords * 8));
+    }
+  }
 
   // glibc stream tables
   const bool need_glibc = c.rng_mode == BCSIM_RNG_GLIBC &&
@@ -1105,6 +1117,8 @@ static int setup_device(Sim& s) {
     kb.cap_arr = 2 * s.kp.cap_arr;
     const size_t lb = scan_lds_bytes(kb);
     if (lb + sizeof(ScanShared) <= 160 * 1024) {
+      // (sort_window's merge area: one per workgroup of these launches -- at most kLoopGrid)
+      if ((rc = dalloc(s, &kb.sortbuf, static_cast<size_t>(std::max<uint32_t>(kLoopGrid, s.few_scan)) * kb.cap_arr))) return rc;
       if ((rc = dalloc(s, &s.kp_dev_big, 1))) return rc;
       HIPCHK(hipMemcpy(s.kp_dev_big, &kb, sizeof(KP), hipMemcpyHostToDevice));
       HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan<BCSIM_PBFT, false>),
@@ -1720,6 +1734,11 @@ static int readback(Sim& s, bool after_next = false) {
     HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, nb, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipStreamSynchronize(s.stream));
   }
+  return readback_apply(s);
+}
+
+// the host's copy of the control block (in ctl_h) into its bookkeeping
+static int readback_apply(Sim& s) {
   // per-launch timing events: read in batches (reading them needs their completion signals)
   int rc = s.ev_used >= kEvBatch ? ev_collect(s) : 0;
   if (rc) return rc;
@@ -1753,6 +1772,39 @@ static long long local_next_cell(const Sim& s, bool with_tick);
 // and status; then the records themselves (sizes known on both sides) and k_import.
 static int exchange(Sim& s, long long cell, int lrc, bool tick) {
   const uint32_t P = s.P, W = Xport::kCtlWords;
+  std::vector<int64_t> snd(static_cast<size_t>(P) * W), rcv(static_cast<size_t>(P) * W);
+  std::vector<uint64_t> sb(P), rb(P);
+  int rc;
+  if (s.ctlw_d) {
+    // device control words (RCCL): k_ctl computes this rank's words from the control block on the
+    // device, the all-to-all runs on device buffers, and ONE sync brings back the words received
+    // and the control block -- the end-of-window read-back and the control exchange in one round
+    // trip (the old path: a read-back, then a host -> device -> all-to-all -> host exchange)
+    long long ch = LLONG_MAX;  // the candidate's host-only terms (local_next_cell)
+    if (s.start_pending) ch = 0;
+    if (s.grouped_cell >= 0) ch = std::min(ch, s.grouped_cell);
+    if (s.stop_pending && s.cfg.stop_ns >= 0 && s.cfg.stop_ns >= s.t_done) ch = std::min<long long>(ch, s.cfg.stop_ns / s.L);
+    if ((rc = launch(s, KS_AUX, k_ctl, dim3(1), dim3(64), 0, s.kp_dev, s.ctlw_d, P, ch, static_cast<long long>(s.t_done),
+                     tick ? 1 : 0, lrc)))
+      return rc;
+    rc = s.xp->ctl_exchange_dev(s.stream, s.ctlw_d);
+    ++s.ctl_collectives;
+    if (rc) return rc;
+    const size_t nb = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
+    HIPCHK(hipMemcpyAsync(s.ctlw_h, s.ctlw_d, 2ull * P * W * 8, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, nb, hipMemcpyDeviceToHost, s.stream));
+    HIPCHK(hipStreamSynchronize(s.stream));
+    const int arc = readback_apply(s);
+    if (!lrc) lrc = arc;
+    for (uint32_t r = 0; r < P && !lrc; ++r)
+      if (s.scnt_h[r] > s.kp.cap_send) {
+        g_detail = "multi-GPU send list overflowed";
+        lrc = BCSIM_E_OVERFLOW;
+      }
+    for (uint32_t r = 0; r < P; ++r) sb[r] = static_cast<uint64_t>(s.ctlw_h[r * W]);
+    std::memcpy(rcv.data(), s.ctlw_h + static_cast<size_t>(P) * W, static_cast<size_t>(P) * W * 8);
+    if (lrc) return lrc;
+  } else {
   for (uint32_t r = 0; r < P && !lrc; ++r)
     if (s.scnt_h[r] > s.kp.cap_send) {
       g_detail = "multi-GPU send list overflowed";
@@ -1761,8 +1813,6 @@ static int exchange(Sim& s, long long cell, int lrc, bool tick) {
   const long long cand = lrc ? LLONG_MAX : local_next_cell(s, false);
   const long long xmin = lrc ? LLONG_MAX : s.ctl_h->scal[4];
   const int64_t alive = (tick && !lrc) ? s.ctl_h->scal[2] : 0;
-  std::vector<int64_t> snd(static_cast<size_t>(P) * W), rcv(static_cast<size_t>(P) * W);
-  std::vector<uint64_t> sb(P), rb(P);
   for (uint32_t r = 0; r < P; ++r) {
     sb[r] = lrc ? kPeerErr : static_cast<uint64_t>(s.scnt_h[r]) * sizeof(XRec);
     snd[r * W + 0] = static_cast<int64_t>(sb[r]);
@@ -1770,10 +1820,11 @@ static int exchange(Sim& s, long long cell, int lrc, bool tick) {
     snd[r * W + 2] = xmin;
     snd[r * W + 3] = alive;
   }
-  int rc = s.xp->ctl_exchange(s.stream, snd.data(), rcv.data());
+  rc = s.xp->ctl_exchange(s.stream, snd.data(), rcv.data());
   ++s.ctl_collectives;
   if (rc) return rc;
   if (lrc) return lrc;
+  }
   long long nx = LLONG_MAX;
   int64_t na = 0;
   uint64_t n = 0;
@@ -2098,7 +2149,8 @@ static int run(Sim& s, int64_t t_until) {
     if (!lrc && s.dbg_dev_err >= 0 && static_cast<long long>(s.cells) >= s.dbg_dev_err)
       lrc = launch(s, KS_AUX, k_dbg_err, dim3(1), dim3(64), 0, s.kp_dev);
     if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b, ++s.mseq);
-    if (!lrc) lrc = readback(s, true);
+    // (device control words: the read-back rides the exchange below)
+    if (!lrc && !s.ctlw_d) lrc = readback(s, true);
     if (!lrc && s.dbg_fail_cell >= 0 && static_cast<long long>(s.cells) >= s.dbg_fail_cell) {
       g_detail = "injected failure (BCSIM_DBG_FAIL_CELL)";  // test hook: one rank fails alone
       lrc = BCSIM_E_OVERFLOW;

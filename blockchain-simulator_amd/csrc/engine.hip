@@ -276,6 +276,9 @@ struct KP {
   GP(unsigned long long) wgtt;   // BCSIM_WGT: per-workgroup k_mesh_tile phase clocks [tiles][8] (debug)
   uint32_t exp;               // BCSIM_EXP: performance experiments that break results (debug, never in tests)
   GP(unsigned long long) wgs;    // BCSIM_WGT: per-workgroup k_scan phase timing [NT][8] (debug)
+  // (the doubled-window KP of the few-node launches only) sort_window's merge area, cap_arr
+  // entries per workgroup: the leader's main and extras runs are merged through it
+  GP(uint4) sortbuf;
   GP(unsigned long long) fdbg;   // BCSIM_FDBG: why nodes leave the fast kernels [16] (debug; see FDBG)
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   GP(long long) node_tnext;
@@ -1778,8 +1781,81 @@ __device__ inline bool sec_less(uint64_t ka, uint32_t sa, uint64_t kb, uint32_t 
   return ka < kb || (ka == kb && sa < sb);
 }
 
-// Sort (akey, asec) pairs of [0, n) unless already ordered.
-__device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec) {
+// The leader's window (the few-node launches' doubled staging window): its main-slot run
+// [0, n_main) is in order -- one instant, in-slot order -- and its extras run is one key (the
+// other message of the same edges, so its in-slots are distinct and in-slot order is sec
+// order).  Then the two runs are merged by rank instead of the bitonic network: an extra's rank
+// among the extras is the count of extras' in-slots below its own (a bitmap of in-slots in LDS
+// and prefix counts), a main arrival's rank among the extras is 0, all or that count by key, and
+// the rank in the other run of an extra is a binary search of the main run.  The pairs go out
+// to the workgroup's area of p.sortbuf at their destination and come back in order -- no
+// register staging (k_scan is at its 128-VGPR bound).  false: not this shape, nothing changed.
+__device__ bool merge_runs(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec, G<uint4>* mg) {
+  const uint32_t tid = tidx(), bs = blockDim.x, n_main = S.n_main;
+  if (n_main == 0 || n_main >= n) return false;
+  const uint64_t xk = akey[n_main];
+  bool bad = false;
+  for (uint32_t r = tid; r < n; r += bs) {
+    if (r + 1 < n_main && sec_less(akey[r + 1], asec[r + 1], akey[r], asec[r])) bad = true;
+    if (r > n_main && akey[r] != xk) bad = true;
+    if (r >= n_main && (asec[r] >> kSlotShift) >= 32u * kQuorumTab) bad = true;
+  }
+  uint32_t* bm = S.tkey;
+  for (uint32_t k = tid; k < static_cast<uint32_t>(kQuorumTab); k += bs) bm[k] = 0;
+  if (tid == 0) S.hsel = 0;
+  __syncthreads();
+  if (__ballot(bad) && (tid & 63u) == 0) S.hsel = 1;
+  if (!bad)
+    for (uint32_t r = n_main + tid; r < n; r += bs) {
+      const uint32_t sl = asec[r] >> kSlotShift;
+      atomicOr(&bm[sl >> 5], 1u << (sl & 31u));
+    }
+  __syncthreads();
+  if (S.hsel) return false;
+  for (uint32_t k = tid; k < static_cast<uint32_t>(kQuorumTab); k += bs) S.tcnt[k] = static_cast<uint32_t>(__popc(bm[k]));
+  __syncthreads();
+  if (tid == 0) {  // (prefix over 256 words: one lane)
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < static_cast<uint32_t>(kQuorumTab); ++k) {
+      const uint32_t c = S.tcnt[k];
+      S.tcnt[k] = run;
+      run += c;
+    }
+    S.hsel = run != n - n_main ? 1u : 0u;  // (in-slots not distinct)
+  }
+  __syncthreads();
+  if (S.hsel) return false;
+  const uint32_t nx = n - n_main;
+  for (uint32_t r = tid; r < n; r += bs) {
+    const uint64_t k = akey[r];
+    const uint32_t sc = asec[r], sl = sc >> kSlotShift;
+    const uint32_t xr = S.tcnt[sl >> 5] + static_cast<uint32_t>(__popc(bm[sl >> 5] & ((1u << (sl & 31u)) - 1u)));
+    uint32_t d;
+    if (r < n_main) {
+      d = r + (k < xk ? 0u : k > xk ? nx : xr);
+    } else {
+      uint32_t lo = 0, hi = n_main;  // main arrivals before it
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sec_less(akey[mid], asec[mid], k, sc)) lo = mid + 1;
+        else hi = mid;
+      }
+      d = xr + lo;
+    }
+    mg[d] = make_uint4(static_cast<uint32_t>(k), static_cast<uint32_t>(k >> 32), sc, 0u);
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += bs) {
+    const uint4 v = mg[r];
+    akey[r] = (static_cast<uint64_t>(v.y) << 32) | v.x;
+    asec[r] = v.z;
+  }
+  __syncthreads();
+  return true;
+}
+
+// Sort (akey, asec) pairs of [0, n) unless already ordered (mg: the merge area, or null).
+__device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t* asec, G<uint4>* mg) {
   const uint32_t tid = tidx();
   if (tid == 0) S.unsorted = 0;
   __syncthreads();
@@ -1789,6 +1865,7 @@ __device__ void sort_window(ScanShared& S, uint32_t n, uint64_t* akey, uint32_t*
   if (__ballot(bad) && (tid & 63) == 0) S.unsorted = 1;
   __syncthreads();
   if (!S.unsorted) return;
+  if (mg && merge_runs(S, n, akey, asec, mg)) return;
   uint32_t P2 = 2;
   while (P2 < n) P2 <<= 1;
   for (uint32_t k = n + tid; k < P2; k += blockDim.x) {
@@ -2498,7 +2575,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
     }
     const uint32_t n_main = S.n_main;
     SPH(1);
-    sort_window(S, n, akey, asec);
+    sort_window(S, n, akey, asec, p.sortbuf ? gbl(p.sortbuf) + static_cast<size_t>(blockIdx.x) * p.cap_arr : nullptr);
     SPH(2);
 
     const RecSrc rsrc{slots, xs};
@@ -9028,6 +9105,42 @@ __global__ void k_draws(const KP* __restrict__ pk, uint32_t) {
 
 // Zero n16 16-byte words (an inbox bucket for the ring-turn tag invariant): dwordx4 stores,
 // a grid-stride loop over a few thousand workgroups
+// k_ctl (node-partitioned over RCCL): this rank's control words of the window's
+// exchange, from the control block after k_next -- per peer {segment bytes (1 << 62: this rank
+// failed), next-cell candidate, earliest cell shipped, PBFT nodes alive at a tick} -- the same
+// words the host computes on the other path (bcsim_capi.hip exchange / local_next_cell: ch holds
+// its host-only terms, START / STOP and a partly processed cell)
+__global__ void k_ctl(const KP* __restrict__ pk, int64_t* __restrict__ w, uint32_t P, long long ch, long long t_done,
+                      int tick, int lrc) {
+  const KP& p = *pk;
+  if (tidx() != 0) return;
+  bool fail = lrc != 0 || *reinterpret_cast<volatile G<int32_t>*>(gbl(p.err)) != 0;
+  for (uint32_t r = 0; r < P; ++r)
+    if (p.send_cnt[r] > p.cap_send) fail = true;
+  long long c = ch;
+  const uint32_t B = p.n_buckets;
+  const long long cdone = t_done / p.L;
+  for (uint32_t b = 0; b < B; ++b)
+    if (p.bucket_cnt[b]) {
+      const long long cb = cdone + ((static_cast<long long>(b) - cdone % B) % B + B) % B;
+      c = cb < c ? cb : c;
+    }
+  const long long nl = p.scal[0], ov = p.scal[1];
+  if (nl != LLONG_MAX) {
+    const long long x = (nl > t_done ? nl : t_done) / p.L;
+    c = x < c ? x : c;
+  }
+  if (ov != LLONG_MAX) c = ov < c ? ov : c;
+  const long long xmin = fail ? LLONG_MAX : p.scal[4];
+  const long long alive = (tick && !fail) ? p.scal[2] : 0;
+  for (uint32_t r = 0; r < P; ++r) {
+    w[4 * r] = fail ? static_cast<long long>(1ull << 62) : static_cast<long long>(p.send_cnt[r]) * static_cast<long long>(sizeof(XRec));
+    w[4 * r + 1] = fail ? LLONG_MAX : c;
+    w[4 * r + 2] = xmin;
+    w[4 * r + 3] = alive;
+  }
+}
+
 // test hook (BCSIM_DBG_DEV_ERR): raise a device error flag, as an overflow found by a kernel
 // would, so that the next kernels bail and the host's read-back takes its fallback path
 __global__ void k_dbg_err(const KP* __restrict__ pk) {

@@ -25,6 +25,10 @@ struct Xport {
   // the ranks of the partition may share this rank's GPU (the host-callback transport of the
   // tests); RCCL runs one rank per device
   virtual bool shares_device() const { return true; }
+  // the control exchange can run on device buffers (ctl_exchange_dev, no host sync)
+  virtual bool device_ctl() const { return false; }
+  // device words [0, nranks*kCtlWords) -> [nranks*kCtlWords, 2*nranks*kCtlWords), queued on st
+  virtual int ctl_exchange_dev(hipStream_t, int64_t*) { return BCSIM_E_UNSUPPORTED; }
   // in-place all-reduce of n int64 host values; op 0 = MIN, 1 = SUM
   virtual int allreduce_i64(hipStream_t st, int64_t* v, uint32_t n, int op) = 0;
   // device segments send_dev + r*stride of send_bytes[r] bytes -> recv_dev,
@@ -63,6 +67,11 @@ struct Xport {
 
 struct RcclXport : Xport {
   bool shares_device() const override { return false; }
+  bool device_ctl() const override { return true; }
+  int ctl_exchange_dev(hipStream_t st, int64_t* w) override {
+    NCCLCHK(ncclAllToAll(w, w + nranks * kCtlWords, kCtlWords, ncclInt64, comm, st));
+    return BCSIM_OK;
+  }
   ncclComm_t comm = nullptr;
   int64_t* d_red = nullptr;    // all-reduce scratch
   uint64_t* d_cnt = nullptr;   // [2][nranks] byte counts
