@@ -226,7 +226,9 @@ def test_rccl_world1_fullsize_partitioned_kernels(name, engine_lib):
     assert single[2]["error"] == 0 and single[2]["quiescent"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_rccl1_worker, args=(_free_port(), [name], q, {"BCSIM_PDES_KERNELS": "1"}))
+    # (C5 with the control words computed on the device: k_ctl -> all-to-all on device buffers)
+    env = {"BCSIM_PDES_KERNELS": "1", "BCSIM_CTL_DEV": "1" if name.startswith("c5") else "0"}
+    p = ctx.Process(target=_rccl1_worker, args=(_free_port(), [name], q, env))
     p.start()
     got_name, tr, cnt = q.get(timeout=540)
     p.join(timeout=60)
