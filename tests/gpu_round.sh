@@ -2,6 +2,7 @@
 # Round-end GPU evidence: the GPU test suite, the bench lines of every workload (with the
 # CPU baseline), and the rocprofv3 kernel trace + PMC passes of the headline.
 #   bash tests/gpu_round.sh <tag> [noprof]     (outputs under gpurun_out/<tag>/)
+#   (ONLY_PYTEST=1: the suite alone; SKIP_PYTEST=1: the rest -- two calls within gpurun's limit)
 set -o pipefail
 tag=${1:-round}
 out=gpurun_out/$tag
@@ -16,7 +17,8 @@ step() {
 }
 (while sleep 50; do date +%s >> $out/heartbeat; done) & hb=$!
 trap "kill $hb 2>/dev/null" EXIT
-step pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread
+[ -n "$SKIP_PYTEST" ] || step pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread
+[ -n "$ONLY_PYTEST" ] && exit 0
 step bench_pbft 240 python bench.py --steps 20 --warmup 5
 step bench_gossip 240 python bench.py --workload gossip
 step bench_gossip_pdes1 240 python bench.py --workload gossip --pdes1 --no-cpu-baseline
