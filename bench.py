@@ -50,7 +50,7 @@ def make_topology(n_nodes, workload):
     return bcsim.random_regular(n_nodes, 8, 1)
 
 
-PMC_ROUND = "r04"
+PMC_ROUND = "r05"
 
 
 def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):
@@ -381,6 +381,12 @@ def main():
                          "traffic": traffic, "algorithmic_bytes_per_launch": lk_launch_bytes,
                          "bytes_per_record": 48, "records": lk["bytes"] / 48.0,
                          "implementation_bytes_per_launch": impl_launch_bytes,
+                         # the measured HBM bytes per launch (PMC) over the same time, and their
+                         # ratio to the algorithmic bytes: < 1 where the heavy waves' records travel
+                         # as summaries, > 1 where bytes are re-read
+                         "traffic_GBs": (traffic / 1e9) / (lk["us"] / max(1, lk["launches"]) / 1e6)
+                         if traffic and lk["us"] > 0 else None,
+                         "traffic_over_algorithmic": traffic / lk_launch_bytes if traffic and lk_launch_bytes else None,
                          "avg_launch_us": lk["us"] / max(1, lk["launches"]),
                          "launches": lk["launches"],
                          # the timed launches are k_link dispatches [first, first + launches) of the

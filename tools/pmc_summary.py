@@ -55,10 +55,10 @@ def kernel_durations(path, prefix):
 
 
 # the kernels of the k_link class as bench.py times it: the fast-path link kernels (full-mesh
-# k_link_mesh, or the tiled k_mesh_prep + k_mesh_tile; dense gossip's fused kernel and its
+# k_link_mesh, or the tiled k_mesh_prep + k_mesh_tile (summary mode: + k_mesh_row); dense gossip's fused kernel and its
 # frontier pass; sparse Paxos) and the looped generic k_link / k_link_sparse over the nodes they
 # hand on -- including the second stream's list-2 link stage
-LINK_CLASS = {"bcsim::k_link", "bcsim::k_link_mesh", "bcsim::k_link_sparse", "bcsim::k_mesh_prep",
+LINK_CLASS = {"bcsim::k_link", "bcsim::k_link_mesh", "bcsim::k_link_sparse", "bcsim::k_mesh_prep", "bcsim::k_mesh_row",
               "bcsim::k_mesh_tile", "bcsim::k_gossip_link", "bcsim::k_gossip_cell", "bcsim::k_gossip_active",
               "bcsim::k_paxos_link"}
 
