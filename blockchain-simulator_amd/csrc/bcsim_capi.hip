@@ -105,6 +105,7 @@ struct Sim {
   // summary mode, opt-in (BCSIM_ACT_RB=0): the window's kernels sized on the device, no read-back
   // of k_active's list lengths (measured slower: 0.73 vs 0.53 ms per step)
   bool dev_sized = false;
+  uint64_t idle_parts = 0;  // part cells cut by a run limit skipped as idle
   uint32_t rt_min = 0;     // summary mode: k_scan_rt takes windows of at least this many scanned nodes (BCSIM_RT_MIN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -2092,6 +2093,16 @@ static int run(Sim& s, int64_t t_until) {
       break;
     }
     const long long cs = c * L, ce = cs + L;
+    {
+      static const bool cwlog = std::getenv("BCSIM_WINLOG") != nullptr;  // (debug: why this cell)
+      if (cwlog) {
+        uint32_t nb = 0;
+        for (uint32_t b = 0; b < s.B; ++b) nb += s.bcnt[b] ? 1u : 0u;
+        std::fprintf(stderr, "[cell] %lld t_done %lld next_local %lld next_timer %lld ov_min %lld busy buckets %u (this %u) tick %lld grouped %lld\n",
+                     c, static_cast<long long>(s.t_done), s.next_local, s.next_timer, s.ov_min, nb, s.bcnt[c % s.B],
+                     static_cast<long long>(s.next_tick), s.grouped_cell);
+      }
+    }
     const long long lo = std::max<long long>(cs, s.t_done);
     const long long hi = std::min<long long>(ce, lim);
     if (lo >= hi) {  // nothing left before the limit inside this cell
@@ -2137,6 +2148,18 @@ static int run(Sim& s, int64_t t_until) {
         lrc = launch(s, KS_AUX, k_pbft_tick, dim3(s.R), dim3(1024), static_cast<size_t>(s.N), s.kp_dev, tk);
       if (!lrc) lrc = do_scan(s, c, tk, hi, cs, hi == ce);
     } else if (!lrc) {
+      // a part of a cell cut by the run limit (bcsim_run(t_until): the bench's step ends at the
+      // next tick) in which nothing can happen -- the idle rule above, to the limit -- launches
+      // nothing: it only moves t_done (no bucket is finished, so no clear or tag zeroing is due)
+      const bool idle = s.cfg.protocol == BCSIM_PBFT && !s.xp && hi < ce && s.bcnt[c % s.B] == 0 && s.next_local >= hi &&
+                        s.next_timer >= hi && !(lo <= 0 && 0 < hi) &&
+                        !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi);
+      if (idle) {
+        s.t_done = hi;
+        ++s.cells;
+        ++s.idle_parts;
+        continue;
+      }
       lrc = do_scan(s, c, lo, hi, cs, hi == ce);
     }
     if (!lrc && s.cfg.protocol == BCSIM_RAFT && s.cfg.rng_mode == BCSIM_RNG_GLIBC)
