@@ -34,6 +34,7 @@ struct Ctl {
   uint32_t trace_cnt, vlog_cnt, dreq_cnt, ov_cnt;
   int32_t dbg;
   long long scal[6];  // next_local, ov_min_cell, n_alive_ticks, next timer, min shipped cell, (pad)
+  long long pred[4];  // k_next's prediction of the next window: valid, cell, lo, hi (engine.hip k_next)
   // followed by bucket_cnt[B] and x_cnt[B]
 };
 
@@ -72,6 +73,10 @@ struct Sim {
   void* ctl_m = nullptr;  // host-mapped mirror of the control block (k_next writes it)
   uint32_t* act_m = nullptr;  // host-mapped mirror of the active-list lengths (k_active writes it)
   uint32_t mseq = 0;          // sequence number of the last k_active / k_next launch (mirror words)
+  uint32_t next_seq = 0;      // ... of the last k_next
+  uint32_t spec_seq = 0;      // ... of a speculative k_active not consumed yet (0: none)
+  bool spec_on = false;       // speculative k_active behind k_next (BCSIM_SPEC=0: off)
+  uint64_t spec_hits = 0;
   std::vector<uint32_t> bcnt;  // bucket counts (host view)
   std::vector<uint32_t> xcnt;  // extras counts (host view)
   int x_active = 0;            // extras of the grouped cell are in xgrp
@@ -217,7 +222,7 @@ static int ev_collect(Sim& s) {
   return BCSIM_OK;
 }
 
-static int mirror_wait(Sim& s, const uint32_t* w);  // (below, with readback)
+static int mirror_wait(Sim& s, const uint32_t* w, uint32_t seq);  // (below, with readback)
 static int readback_apply(Sim& s);
 
 static int validate(const bcsim_config& c) {
@@ -944,6 +949,7 @@ static int setup_device(Sim& s) {
   p.dreq_cnt = (decltype(p.dreq_cnt))(&cd->dreq_cnt);
   p.ov_cnt = (decltype(p.ov_cnt))(&cd->ov_cnt);
   p.scal = (decltype(p.scal))(cd->scal);
+  p.pred = (decltype(p.pred))(cd->pred);
   if ((rc = dalloc(s, &p.nxt_part, 2 * kNextBlocks)) || (rc = dalloc(s, &p.nxt_done, 1))) return rc;
   HIPCHK(hipMemset(p.nxt_done, 0, 4));
   p.bucket_cnt = (decltype(p.bucket_cnt))(reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl)));
@@ -1086,6 +1092,11 @@ static int setup_device(Sim& s) {
   if (const char* fv = std::getenv("BCSIM_DBG_DEV_ERR"); fv && *fv) s.dbg_dev_err = std::atoll(fv);
   if (const char* rs = std::getenv("BCSIM_ROW_SPLIT"); rs && *rs) s.row_split_max = static_cast<uint32_t>(std::atoi(rs));
   if (const char* ab = std::getenv("BCSIM_ACT_RB"); ab && *ab == '0') s.dev_sized = true;
+  {
+    const char* sp = std::getenv("BCSIM_SPEC");
+    s.spec_on = !(sp && *sp == '0') && !s.sparse && !s.pdes && !s.xp && s.cfg.protocol == BCSIM_PBFT && s.act_m != nullptr &&
+                s.ctl_m != nullptr;
+  }
   if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -1298,9 +1309,21 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     const uint64_t nl = static_cast<uint64_t>(s.R) * s.nloc;
     const uint64_t nb = std::max<uint64_t>((nl + kActChunk - 1) / kActChunk, std::min<uint64_t>(1024, (nl + 255) / 256));
     const uint32_t chunk = static_cast<uint32_t>(((nl + nb - 1) / nb + 255) / 256 * 256);
-    rc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, lo, hi,
-                static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk, ++s.mseq);
-    if (rc) return rc;
+    // (speculation: k_next predicted this window and k_active already ran for it behind k_next)
+    uint32_t act_seq = 0;
+    const bool spec_hit = s.spec_seq && s.ctl_h->pred[0] && s.ctl_h->pred[1] == cell && s.ctl_h->pred[2] == lo &&
+                          s.ctl_h->pred[3] == hi;
+    if (spec_hit) {
+      act_seq = s.spec_seq;
+      ++s.spec_hits;
+    } else {
+      if (s.spec_seq && s.ctl_h->pred[0]) HIPCHK(hipMemsetAsync(s.kp.act_n, 0, 16, s.stream));  // (its lists)
+      act_seq = ++s.mseq;
+      rc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, lo, hi,
+                  static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk, act_seq, 0);
+      if (rc) return rc;
+    }
+    s.spec_seq = 0;
     static const bool no_sync = [] {
       const char* e = std::getenv("BCSIM_NO_ACTSYNC");
       return e && *e == '1';
@@ -1322,7 +1345,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       // (an idle node costs nothing; an empty list no launch).  A k_scan workgroup holds
       // ~140 KB of LDS, so even workgroups that exit at once go through the CUs one at a time
       // per CU: 4096 of them took ~24 us, the read-back takes ~10.
-      const int w = s.act_m ? mirror_wait(s, s.act_m + 2) : 1;
+      const int w = s.act_m ? mirror_wait(s, s.act_m + 2, act_seq) : 1;
       if (w < 0) return w;
       if (w == 0) {  // (k_active's last workgroup published them)
         s.act_h[0] = s.act_m[0];
@@ -1340,8 +1363,9 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       if (dsz && (dmask & 2u)) n_link = kDevSized;
       static const bool winlog = std::getenv("BCSIM_WINLOG") != nullptr;  // (debug: one line per window)
       if (winlog)
-        std::fprintf(stderr, "[win] cell %lld [%lld, %lld) +%lld us scan %u link %u xa %d\n", cell, lo, hi, (lo - cell * s.L) / 1000,
-                     s.act_h[0], s.act_h[1], xa);
+        std::fprintf(stderr, "[win] cell %lld [%lld, %lld) +%lld us scan %u link %u xa %d spec %d (pred %lld %lld %lld %lld)\n", cell, lo,
+                     hi, (lo - cell * s.L) / 1000, s.act_h[0], s.act_h[1], xa, spec_hit ? 1 : 0, s.ctl_h->pred[0], s.ctl_h->pred[1],
+                     s.ctl_h->pred[2], s.ctl_h->pred[3]);
     } else if (!s.sparse) {
       // node-partitioned: a rank holds 1/P of the nodes, so a workgroup per local node costs
       // less than the round trip (the cell already has several collectives)
@@ -1695,12 +1719,11 @@ static int group_cell(Sim& s, long long cell) {
 // wake-up and the end-of-kernel cache release (~10-20 us per read-back).  With
 // BCSIM_SPIN=0, a plain stream sync.
 constexpr int kSpinUs = 500;  // mirror_wait: spin at most this long, then a stream sync
-static int mirror_wait(Sim& s, const uint32_t* w) {
+static int mirror_wait(Sim& s, const uint32_t* w, uint32_t seq) {
   static const bool spin = [] {
     const char* e = std::getenv("BCSIM_SPIN");
     return !(e && *e == '0');
   }();
-  const uint32_t seq = s.mseq;
   if (!spin) {
     HIPCHK(hipStreamSynchronize(s.stream));
     return __atomic_load_n(w, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
@@ -1728,7 +1751,7 @@ static int mirror_wait(Sim& s, const uint32_t* w) {
 static int readback(Sim& s, bool after_next = false) {
   const size_t nb = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
   int w = 1;
-  if (after_next && s.ctl_m && (w = mirror_wait(s, reinterpret_cast<uint32_t*>(s.ctl_m) + nb / 4)) < 0) return w;
+  if (after_next && s.ctl_m && (w = mirror_wait(s, reinterpret_cast<uint32_t*>(s.ctl_m) + nb / 4, s.next_seq)) < 0) return w;
   if (w == 0) {
     std::memcpy(s.ctl_h, s.ctl_m, nb);
   } else {
@@ -2171,7 +2194,33 @@ static int run(Sim& s, int64_t t_until) {
     const uint32_t clr_b = hi == ce ? static_cast<uint32_t>(c % s.B) : 0xFFFFFFFFu;
     if (!lrc && s.dbg_dev_err >= 0 && static_cast<long long>(s.cells) >= s.dbg_dev_err)
       lrc = launch(s, KS_AUX, k_dbg_err, dim3(1), dim3(64), 0, s.kp_dev);
-    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b, ++s.mseq);
+    // speculation (dense PBFT, one rank, one k_next workgroup): k_next predicts the next window from
+    // the state after this one -- the host's next-cell rule with its host-only terms passed in --
+    // and k_active runs for it at once; the next do_scan uses its lists when the host's window is
+    // the predicted one (else it resets them and runs k_active itself): one round trip less
+    const bool spec = s.spec_on && !lrc && nbn == 1;
+    PredArgs pa{};
+    if (spec) {
+      const long long td = hi;  // (t_done after this window)
+      long long ch = LLONG_MAX;
+      if (hi != ce) ch = c;  // (a part cell: grouped_cell stays)
+      if (s.stop_pending && s.cfg.stop_ns >= 0 && s.cfg.stop_ns >= hi) ch = std::min<long long>(ch, s.cfg.stop_ns / L);
+      int64_t tk = s.next_tick;
+      const bool ticked = s.cfg.protocol == BCSIM_PBFT && s.n_alive > 0 && s.next_tick >= lo && s.next_tick < hi;
+      if (ticked) tk = s.next_tick + s.kp.pbft_period;  // (the tick of this window is done)
+      pa = PredArgs{td, static_cast<long long>(lim), (s.n_alive > 0 || ticked) ? static_cast<long long>(tk) : LLONG_MAX, ch,
+                    s.cfg.stop_ns, 1};
+    }
+    s.next_seq = ++s.mseq;
+    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b, s.next_seq, pa);
+    if (!lrc && spec) {
+      const uint64_t nl = static_cast<uint64_t>(s.R) * s.nloc;
+      const uint64_t nb = std::max<uint64_t>((nl + kActChunk - 1) / kActChunk, std::min<uint64_t>(1024, (nl + 255) / 256));
+      const uint32_t chunk = static_cast<uint32_t>(((nl + nb - 1) / nb + 255) / 256 * 256);
+      s.spec_seq = ++s.mseq;
+      lrc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, 0ll, 0ll,
+                   0u, 0u, chunk, s.spec_seq, 1);
+    }
     // (device control words: the read-back rides the exchange below)
     if (!lrc && !s.ctlw_d) lrc = readback(s, true);
     if (!lrc && s.dbg_fail_cell >= 0 && static_cast<long long>(s.cells) >= s.dbg_fail_cell) {

@@ -283,6 +283,7 @@ struct KP {
   uint64_t cap_E, cap_txn, cap_glibc, cap_inbox, cap_xbuf;
   GP(long long) node_tnext;
   GP(long long) node_onext;
+  GP(long long) pred;  // k_next's prediction of the next window {valid, cell, lo, hi} (control block)
   GP(long long) scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks, [3] next timer,
                     // [4] earliest arrival cell shipped to another rank (node-partitioned)
   GP(long long) nxt_part;  // [kNextBlocks] k_next per-workgroup minima
@@ -8591,9 +8592,17 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
 // loop bound is wave-uniform, so every ballot runs with the whole wave active)
 constexpr uint32_t kActChunk = 16384;  // k_active: gnodes per workgroup at most (LDS flags)
 __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long long t_lo, long long t_hi, uint32_t b,
-                                                uint32_t obp, uint32_t chunk, uint32_t seq) {
+                                                uint32_t obp, uint32_t chunk, uint32_t seq, int spec) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  if (spec) {  // (speculative, behind k_next: the window it predicted, or nothing)
+    if (!p.pred[0]) return;
+    const long long c = p.pred[1];
+    t_lo = p.pred[2];
+    t_hi = p.pred[3];
+    b = static_cast<uint32_t>(c % p.n_buckets);
+    obp = static_cast<uint32_t>((c + kOpRing - 1) % kOpRing);
+  }
   // each workgroup compacts a contiguous chunk of gnodes: flags to LDS and counts, ONE global
   // atomic per list for the chunk (a per-wave atomic on the two list counters serialised:
   // 1.5 ms per launch at 8 M gnodes), then the ordered writes
@@ -9161,7 +9170,8 @@ __global__ __launch_bounds__(256) void k_zero16(uint4* __restrict__ dst, uint64_
 // one wave: the control words to the host-mapped mirror, with the window's next event times
 // (scal[0] = words 6-7, scal[3] = words 12-13 of the control block)
 // then the window's sequence number in the word after them, which the host spins on
-__device__ inline void ctl_publish(const KP& p, long long s0, long long s3, uint32_t seq) {
+// (the prediction's four words follow scal[6]: words 18-25)
+__device__ inline void ctl_publish(const KP& p, long long s0, long long s3, uint32_t seq, const long long* pv = nullptr) {
   if (!p.ctl_mirror) return;
   const uint32_t lane = tidx() & 63u;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(p.err);
@@ -9169,13 +9179,57 @@ __device__ inline void ctl_publish(const KP& p, long long s0, long long s3, uint
     uint32_t v = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (k == 6 || k == 7) v = static_cast<uint32_t>(static_cast<uint64_t>(s0) >> (32 * (k - 6)));
     if (k == 12 || k == 13) v = static_cast<uint32_t>(static_cast<uint64_t>(s3) >> (32 * (k - 12)));
+    if (pv && k >= 18 && k < 26) v = static_cast<uint32_t>(static_cast<uint64_t>(pv[(k - 18) >> 1]) >> (32 * ((k - 18) & 1)));
     p.ctl_mirror[k] = v;
   }
   __threadfence_system();  // (the wave's stores done before the sequence word)
   if (lane == 0) __hip_atomic_store(p.ctl_mirror + p.ctl_words, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b, uint32_t seq) {
+// The host's next-window rule (bcsim_capi.hip run() / local_next_cell / group_cell), restated for
+// k_next's prediction: its host-only terms come in PredArgs (t_done after the window, the run
+// limit, the next PBFT tick, the candidate of a part cell / STOP).  A window is predicted only
+// when the host would run k_active for it with nothing launched in between: no tick inside it,
+// no START / STOP, no extras to group or overflow to rebin for its cell.
+struct PredArgs {
+  long long t_done, lim, tick, ch, stop_ns;
+  int on;
+};
+__device__ inline void predict_window(const KP& p, const PredArgs& a, long long next_local, long long* pv) {
+  pv[0] = 0;
+  pv[1] = pv[2] = pv[3] = 0;
+  if (!a.on) return;
+  const uint32_t B = p.n_buckets;
+  const long long L = p.L, cdone = a.t_done / L;
+  long long c = a.ch;
+  for (uint32_t b = 0; b < B; ++b)
+    if (p.bucket_cnt[b]) {
+      const long long cb = cdone + ((static_cast<long long>(b) - cdone % B) % B + B) % B;
+      c = cb < c ? cb : c;
+    }
+  if (next_local != LLONG_MAX) {
+    const long long x = (next_local > a.t_done ? next_local : a.t_done) / L;
+    c = x < c ? x : c;
+  }
+  const long long ov = p.scal[1];
+  if (ov != LLONG_MAX) c = ov < c ? ov : c;
+  if (a.tick != LLONG_MAX) c = a.tick / L < c ? a.tick / L : c;
+  if (c == LLONG_MAX || c * L >= a.lim) return;
+  const long long cs = c * L, lo = cs > a.t_done ? cs : a.t_done, hi = cs + L < a.lim ? cs + L : a.lim;
+  if (lo >= hi) return;
+  if (a.tick >= lo && a.tick < hi) return;                       // (the tick splits it)
+  if (lo <= 0 && 0 < hi) return;                                 // START
+  if (a.stop_ns >= 0 && lo <= a.stop_ns && a.stop_ns < hi) return;  // STOP
+  if (p.x_cnt[c % B]) return;                                    // extras to group
+  if (ov != LLONG_MAX && ov <= c + static_cast<long long>(B) - 1) return;  // overflow to rebin
+  if (c - cdone >= static_cast<long long>(B)) return;
+  pv[0] = 1;
+  pv[1] = c;
+  pv[2] = lo;
+  pv[3] = hi;
+}
+
+__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b, uint32_t seq, PredArgs pa) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (blockIdx.x == 0) {
@@ -9235,11 +9289,14 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     mt = min(mt, static_cast<long long>(__shfl_xor(mt, d, 64)));
   }
   if (nb == 1) {
+    long long pv[4];
+    predict_window(p, pa, m, pv);
     if (lane == 0) {
       p.scal[0] = m;
       p.scal[3] = mt;
+      for (int k = 0; k < 4; ++k) p.pred[k] = pv[k];
     }
-    ctl_publish(p, m, mt, seq);
+    ctl_publish(p, m, mt, seq, pv);
     return;
   }
   bool last = false;
@@ -9263,6 +9320,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
   if (lane == 0) {
     p.scal[0] = mm;
     p.scal[3] = mmt;
+    p.pred[0] = 0;  // (no prediction with several workgroups)
     __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   ctl_publish(p, mm, mmt, seq);

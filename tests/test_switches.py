@@ -27,6 +27,7 @@ SWITCHES = [
     {"BCSIM_MESH_TILE": "0", "BCSIM_FEW_SCAN": "0"},  # k_link_mesh instead of the tiled mesh
     {"BCSIM_SUM": "0", "BCSIM_FEW_SCAN": "0"},        # no record summaries (k_mesh_tile, k_scan_pbft)
     {"BCSIM_NO_DESC": "1"},         # no reply / echo descriptors
+    {"BCSIM_SPEC": "0"},            # no speculative k_active behind k_next
 ]
 
 
