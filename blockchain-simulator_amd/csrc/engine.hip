@@ -4916,20 +4916,19 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
         return;
       }
       for (uint32_t b2 = 0; b2 < nb; ++b2) {
-        const Op o = ops[L.bc[b2]];
-        const bool paxos = (op_flags(o) & OPF_PAXOS) != 0;
-        const uint64_t dbase = static_cast<uint64_t>(o.edge);
+        // (raw words: an Op copy, sub-dword members and all, went through scratch)
+        const RawOp o = ld_raw(&ops[L.bc[b2]]);
+        const bool paxos = (raw_flags(o) & OPF_PAXOS) != 0;
+        const uint64_t dbase = static_cast<uint64_t>(o.b.y);
         const uint32_t at = n + b2 * deg;
+        const uint32_t w3 = (o.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(OP_SEND | ((raw_flags(o) & OPF_BIG) << 2)) << 24);
         for (uint32_t it = tid; it < deg; it += blockDim.x) {
           const int32_t r = ctr_rand(p.seed, rep, i, dbase + it);
           const int64_t d = delay_from_draw(p, r);
-          Op s = o;
-          s.t = o.t + d;
-          s.dt = static_cast<uint32_t>(d);
-          s.sub = o.sub + it;
-          s.edge = paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it;
-          s.kind_flags = static_cast<uint8_t>(OP_SEND | ((op_flags(o) & OPF_BIG) << 2));
-          AT(ops, at + it, ocap) = s;
+          const uint64_t t = static_cast<uint64_t>(raw_t(o) + d);
+          uint4* w = reinterpret_cast<uint4*>(&AT(ops, at + it, ocap));
+          w[0] = make_uint4(static_cast<uint32_t>(t), static_cast<uint32_t>(t >> 32), static_cast<uint32_t>(d), o.a.w);
+          w[1] = make_uint4(raw_sub(o) + it, paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it, o.b.z, w3);
         }
       }
       __syncthreads();
@@ -5211,11 +5210,11 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
       }
       for (uint32_t a = eb + 1; a < ee; ++a) {  // insertion sort of this edge's ops (few)
         const uint32_t x = eidx[a];
-        const Op ox = ops[x];
+        const RawOp ox = ld_raw(&ops[x]);  // (raw words: an Op copy went through scratch)
         uint32_t b2 = a;
         while (b2 > eb) {
-          const Op& oy = ops[eidx[b2 - 1]];
-          if (!op_key_less(ox, ox.sub, oy, oy.sub)) break;
+          const RawOp oy = ld_raw(&ops[eidx[b2 - 1]]);
+          if (!raw_key_less(ox, raw_sub(ox), oy, raw_sub(oy))) break;
           eidx[b2] = eidx[b2 - 1];
           --b2;
         }
@@ -5437,11 +5436,11 @@ __device__ __attribute__((always_inline)) inline void link_node(const KP* __rest
     if (ee == eb && n_bc == 0 && !he && !hr && !hr2) continue;
     for (uint32_t a = eb + 1; a < ee; ++a) {  // insertion sort of this edge's ops (few)
       const uint32_t x = eidx[a];
-      const Op ox = ops[x];
+      const RawOp ox = ld_raw(&ops[x]);  // (raw words: an Op copy went through scratch)
       uint32_t b2 = a;
       while (b2 > eb) {
-        const Op& oy = ops[eidx[b2 - 1]];
-        if (!op_key_less(ox, ox.sub, oy, oy.sub)) break;
+        const RawOp oy = ld_raw(&ops[eidx[b2 - 1]]);
+        if (!raw_key_less(ox, raw_sub(ox), oy, raw_sub(oy))) break;
         eidx[b2] = eidx[b2 - 1];
         --b2;
       }
