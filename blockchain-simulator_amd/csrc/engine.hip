@@ -8052,20 +8052,20 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
       return;
     }
     for (uint32_t b2 = 0; b2 < nb; ++b2) {
-      const Op o = ops[L.bc[b2]];
-      const bool jit = op_kind(o) == OP_BCAST_J;
-      const bool paxos = (op_flags(o) & OPF_PAXOS) != 0;
+      // (raw words: an Op copy, sub-dword members and all, went through scratch per edge)
+      const RawOp o = ld_raw(&ops[L.bc[b2]]);
+      const bool jit = raw_kind(o) == OP_BCAST_J;
+      const bool paxos = (raw_flags(o) & OPF_PAXOS) != 0;
       const uint32_t at = n + b2 * deg;
+      const uint32_t w3 = (o.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(OP_SEND | ((raw_flags(o) & OPF_BIG) << 2)) << 24);
       for (uint32_t it = tid; it < deg; it += bs) {
         int64_t d = 0;
-        if (jit) d = delay_from_draw(p, ctr_rand(p.seed, rep, i, static_cast<uint64_t>(o.edge) + it));
-        Op sop = o;
-        sop.t = o.t + d;
-        sop.dt = jit ? static_cast<uint32_t>(d) : o.dt;
-        sop.sub = o.sub + it;  // Paxos: edge it + 1 (peers[0] skipped), the last one *end()
-        sop.edge = paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it;
-        sop.kind_flags = static_cast<uint8_t>(OP_SEND | ((op_flags(o) & OPF_BIG) << 2));
-        AT(ops, at + it, ocap) = sop;
+        if (jit) d = delay_from_draw(p, ctr_rand(p.seed, rep, i, static_cast<uint64_t>(o.b.y) + it));
+        const uint64_t t = static_cast<uint64_t>(raw_t(o) + d);
+        uint4* w = reinterpret_cast<uint4*>(&AT(ops, at + it, ocap));
+        w[0] = make_uint4(static_cast<uint32_t>(t), static_cast<uint32_t>(t >> 32), jit ? static_cast<uint32_t>(d) : o.a.z, o.a.w);
+        // (Paxos: edge it + 1 -- peers[0] skipped -- and the last one *end())
+        w[1] = make_uint4(raw_sub(o) + it, paxos ? (it + 1 < deg ? e0 + it + 1 : kInvalid) : e0 + it, o.b.z, w3);
       }
     }
     __syncthreads();
@@ -8282,21 +8282,26 @@ __device__ void link_node_sparse(const KP& p, uint32_t g, long long cell, long l
   uint32_t kept = 0;
   for (uint32_t k0 = 0; k0 < n; k0 += bs) {
     const uint32_t k = k0 + tid;
-    Op o{};
+    RawOp o = raw_zero();  // (raw words: an Op copy went through scratch per op)
     bool keep = false;
     if (k < n) {
-      o = ops[k];
-      const uint8_t kind = op_kind(o);
+      o = ld_raw(&ops[k]);
+      const uint32_t kind = raw_kind(o);
+      const int64_t ot = raw_t(o);
       if (kind == OP_BCAST_J)
-        keep = !(op_flags(o) & OPF_DONE);
-      else if (o.t >= t_hi) {
+        keep = !(raw_flags(o) & OPF_DONE);
+      else if (ot >= t_hi) {
         keep = true;
-        if (o.t < omin) omin = o.t;
+        if (ot < omin) omin = ot;
       }
     }
     uint32_t tot;
     const uint32_t pos = kept + block_rank(keep, L.wcnt, tot);
-    if (keep) ops[pos] = o;
+    if (keep) {
+      uint4* w = reinterpret_cast<uint4*>(&ops[pos]);
+      w[0] = o.a;
+      w[1] = o.b;
+    }
     kept += tot;
   }
   if (tid == 0) L.n_keep = kept;
