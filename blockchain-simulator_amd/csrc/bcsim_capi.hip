@@ -509,7 +509,7 @@ static int setup_device(Sim& s) {
   };
   s.bs_scan = bs_cap("BCSIM_BS_SCAN", s.bs_scan);
   s.bs_link = bs_cap("BCSIM_BS_LINK", s.bs_link);
-  if (p.qmodel == 2) s.bs_link = std::min<uint32_t>(s.bs_link, 256);  // (k_link<2>'s launch bound)
+  if (p.qmodel != 0) s.bs_link = std::min<uint32_t>(s.bs_link, 256);  // (k_link<1|2>'s launch bound)
   if (c.protocol != BCSIM_PBFT) s.bs_scan = std::min<uint32_t>(s.bs_scan, 256);  // (k_scan's launch bound)
   {  // k_link dynamic LDS: as many workgroups per CU as 1024 lanes make (1024 / bs_link)
     const size_t target = std::max<size_t>(16 * 1024, kLinkLdsTarget * s.bs_link / 512 - (s.bs_link < 512 ? 4096 : 0));

@@ -5666,7 +5666,7 @@ __device__ void rul_flush(const KP& p, uint32_t g) {
 }
 
 template <int QM, bool XR, bool LOOP = false>
-__global__ __launch_bounds__(QM == 2 ? 256 : (LOOP ? kLinkLoopThreads : 1024)) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
+__global__ __launch_bounds__(QM != 0 ? 256 : (LOOP ? kLinkLoopThreads : 1024)) void k_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                               long long t_hi, int final_win) {
   const KP& p = *pk;
   BAIL_IF_ERR();
