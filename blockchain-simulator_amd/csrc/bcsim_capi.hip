@@ -111,6 +111,7 @@ struct Sim {
   // of k_active's list lengths (measured slower: 0.73 vs 0.53 ms per step)
   bool dev_sized = false;
   uint64_t idle_parts = 0;  // part cells cut by a run limit skipped as idle
+  uint32_t gossip_l3_grid = 256;  // dense gossip: workgroups of the looped list-3 link grid (BCSIM_GL3; x8)
   uint32_t rt_min = 0;     // summary mode: k_scan_rt takes windows of at least this many scanned nodes (BCSIM_RT_MIN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
   bool paxos_fast = false;  // sparse Paxos: k_paxos_scan first (BCSIM_NO_PXFAST=1: off)  // dense gossip: k_gossip_link first (not the full mesh, fixed delay, infinite queues, 1 rank)
@@ -1092,6 +1093,7 @@ static int setup_device(Sim& s) {
   if (const char* fv = std::getenv("BCSIM_DBG_DEV_ERR"); fv && *fv) s.dbg_dev_err = std::atoll(fv);
   if (const char* rs = std::getenv("BCSIM_ROW_SPLIT"); rs && *rs) s.row_split_max = static_cast<uint32_t>(std::atoi(rs));
   if (const char* ab = std::getenv("BCSIM_ACT_RB"); ab && *ab == '0') s.dev_sized = true;
+  if (const char* g3 = std::getenv("BCSIM_GL3"); g3 && *g3) s.gossip_l3_grid = std::max<uint32_t>(8, static_cast<uint32_t>(std::atoi(g3)) / 8 * 8);
   {
     const char* sp = std::getenv("BCSIM_SPEC");
     s.spec_on = !(sp && *sp == '0') && !s.sparse && !s.pdes && !s.xp && s.cfg.protocol == BCSIM_PBFT && s.act_m != nullptr &&
@@ -1294,7 +1296,8 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
                       cs, fw, xa))) ||
         // (the looped grid may not exceed the workgroups the per-workgroup staging areas
         // were allocated for: xstage / xmeta hold grid_link of them)
-        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(256, s.grid_link)), dim3(s.bs_link),
+        // (list 3 is almost always empty here; BCSIM_GL3: its grid, 8-256 measured alike)
+        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(s.gossip_l3_grid, s.grid_link)), dim3(s.bs_link),
                      link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
       return rc;
     if (timed) return ev_end(s);
