@@ -1497,7 +1497,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       }
       acc[0] += static_cast<double>(q[7] - q[0]);
     }
-    if (nw && tmax - tmin > 10000) {
+    if (nw && tmax - tmin > 5000) {
       std::fprintf(stderr, "[wgs] cell %lld k_scan span %.2f ms, %u WGs, mean us: total %.1f stage %.1f sort %.1f A %.1f B %.1f C %.1f D %.1f E+wb %.1f\n",
                    cell, (tmax - tmin) / 1e5, nw, acc[0] / nw / 100, acc[1] / nw / 100, acc[2] / nw / 100,
                    acc[3] / nw / 100, acc[4] / nw / 100, acc[5] / nw / 100, acc[6] / nw / 100, acc[7] / nw / 100);

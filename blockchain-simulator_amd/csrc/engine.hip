@@ -2120,6 +2120,7 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
   // the first tick time at or after the window start: an arrival at a tick time is checked
   // against it without a 64-bit division per arrival
   const int64_t tk0 = ((t_lo + p.pbft_period - 1) / p.pbft_period) * p.pbft_period;
+  const bool one_tick = p.L < p.pbft_period;  // (windows lie inside one cell)
   // t and dt come from the staged key; the record is read only by arrivals that produce output
   // (the PREPARE_RES / COMMIT waves are almost all non-crossing: nothing to read), one arrival
   // ahead, so its load is in flight while the previous arrival's output is written
@@ -2150,10 +2151,11 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
     const uint32_t le = q - e0;
     const uint32_t origin = p.mesh ? (le < i ? le : le + 1) : AT(p.col, q, p.E);
     const Key key{t, t - static_cast<int64_t>(dt), origin, rec.sub};
-    if (t >= tk0 && (t == tk0 || (t - tk0) % p.pbft_period == 0) && key.ts <= t - p.pbft_period)
+    // (a window is shorter than the period, so tk0 is its only tick time: no 64-bit modulo)
+    if (t >= tk0 && (t == tk0 || (!one_tick && (t - tk0) % p.pbft_period == 0)) && key.ts <= t - p.pbft_period)
       set_err(p, BCSIM_E_TIE);  // arrival ordered before a same-time tick
     // pbft-node.cc:175 echo: implicit for main-slot records (k_link), listed otherwise
-    if (lecho) ops[op++] = mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0);
+    if (lecho) st_op(&ops[op++], mk_op(p, t, dt, origin, rec.sub, q, m, OP_ECHO, 0));  // (two dwordx4 stores)
     switch (type) {
       case PB_PRE_PREPARE: {  // :193-211
         const Msg rr = mkmsg(PB_PREPARE, mch(m, 1), mch(m, 2), mch(m, 3), 0);
@@ -2169,7 +2171,8 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
         if (!fixed) d = delay_from_draw(p, ctr_rand(p.seed, rep, i, dp++));
         const Op ro = mk_op(p, t + d, static_cast<uint32_t>(d), i, sp++, q, rr, OP_SEND, 0);
         if (rslot & (1u << (r - r0))) {
-          const long long dc = ro.t / p.L;
+          // (the reply is due in this cell or the next: app delay < L -- no 64-bit division)
+          const long long dc = ro.t < cs + p.L ? cell : cell + 1;
           const uint64_t ut = static_cast<uint64_t>(ro.t);
           *eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q) =
               make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), ro.sub,
