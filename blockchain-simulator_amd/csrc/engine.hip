@@ -2174,10 +2174,10 @@ __device__ __attribute__((always_inline)) inline void pbft_window(const KP& p, S
           // (the reply is due in this cell or the next: app delay < L -- no 64-bit division)
           const long long dc = ro.t < cs + p.L ? cell : cell + 1;
           const uint64_t ut = static_cast<uint64_t>(ro.t);
-          *eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q) =
-              make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), ro.sub,
-                         (static_cast<uint32_t>(static_cast<uint16_t>(ro.f0))) |
-                             (static_cast<uint32_t>(static_cast<uint16_t>(ro.f1)) << 16));
+          gst4(eslot_at(p, static_cast<uint32_t>(cell % kOpRing), rep, q),
+               make_uint4(static_cast<uint32_t>(ut), static_cast<uint32_t>(ut >> 32), ro.sub,
+                          (static_cast<uint32_t>(static_cast<uint16_t>(ro.f0))) |
+                              (static_cast<uint32_t>(static_cast<uint16_t>(ro.f1)) << 16)));
           if (dc == cell)
             ++n_slot0;
           else
