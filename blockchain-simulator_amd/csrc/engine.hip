@@ -1624,7 +1624,7 @@ struct ScanShared {
   // Paxos proposer window (paxos_window_fast): decree and vote count on entry, verdict, the
   // quorum-crossing arrival and its prefix counts, explicit echoes, per-type deliveries
   int32_t px_dec, px_c0;
-  uint32_t px_bad, px_r, px_cb, px_sb, px_eb, px_ncross, px_nops0;
+  uint32_t px_bad, px_r, px_cb, px_sb, px_eb, px_ncross, px_nops0, px_nx, px_adv, px_sr;
   uint32_t px_deliv[3];
   long long px_tmax;
   unsigned long long ph[8];  // BCSIM_WGT phase clock (debug)
@@ -2359,8 +2359,10 @@ __device__ bool paxos_window_fast(const KP& p, ScanShared& S, Ctx& c, PaxosState
     S.px_nops0 = c.nops;
     S.px_tmax = LLONG_MIN;
     S.px_deliv[0] = S.px_deliv[1] = S.px_deliv[2] = 0;
+    S.px_nx = 0;
     for (uint32_t k = 0; k < c.cap_t; ++k)
       if (tm[k].alive && !tm[k].pending_draw && tm[k].t < wb && tm[k].t >= t_lo) S.px_bad = 1;
+    if (S.px_bad && p.fdbg) gadd_r(&p.fdbg[1], 1ull);
   }
   __syncthreads();
   if (S.px_bad) return false;
@@ -2379,6 +2381,7 @@ __device__ bool paxos_window_fast(const KP& p, ScanShared& S, Ctx& c, PaxosState
       else atomicAdd(&S.px_deliv[ty - PX_RES_TICKET], 1u);
       cnt = rec.f2 == dec ? 1u : 0u;
       suc = cnt && rec.f0 == '0' ? 1u : 0u;
+      if (rec.f2 == dec + 1) atomicMax(&S.px_nx, r + 1);  // a response of the next decree
       ech = p.echo && !(p.impl && is_main(sec)) ? 1u : 0u;
       tmax = max(tmax, cs + static_cast<long long>(rec.t_off));
     }
@@ -2397,11 +2400,30 @@ __device__ bool paxos_window_fast(const KP& p, ScanShared& S, Ctx& c, PaxosState
   for (int d = 32; d > 0; d >>= 1) tmax = max(tmax, static_cast<long long>(__shfl_xor(tmax, d, 64)));
   if ((tid & 63u) == 0 && tmax > LLONG_MIN) atomicMax(&S.px_tmax, tmax);
   __syncthreads();
-  // a second decision in the window, or a counted response after the one: the serial loop
+  // Counting restarts at 0 after the decision (paxos-node.cc:263-353): the counted responses after
+  // it add to the fresh counters when the decree stays, unless they reach a second decision; when
+  // the decision commits and opens the next decree, the rest of the window's responses are of a
+  // finished decree (not counted) unless one is of the new decree.  Those cases, and foreign
+  // types, take the serial loop.
   const bool cross = S.px_r != kInvalid;
-  if (S.px_bad || c0 + static_cast<int32_t>(run.x) > N2 || (cross && c0 + static_cast<int32_t>(run.x) != N2) ||
-      S.px_nops0 + run.z + (cross ? 1u : 0u) > ocap)
-    return false;
+  if (tid == 0 && !S.px_bad) {
+    uint32_t why = 0;
+    if (!cross && c0 + static_cast<int32_t>(run.x) > N2) why = 3;
+    if (cross) {
+      const Rec rx = rec_of(rsrc, asec[S.px_r]);
+      const uint32_t suc_r = rx.f0 == '0' ? 1u : 0u;
+      const bool adv = rx.type == PX_RES_COMMIT && s.vs + static_cast<int32_t>(S.px_sb + suc_r) >= static_cast<int32_t>(p.N) / 2 &&
+                       static_cast<uint32_t>(dec) + 1 < p.K;
+      if (adv ? S.px_nx > S.px_r + 1 : run.x - S.px_cb - 1 >= static_cast<uint32_t>(N2)) why = 3;
+      S.px_adv = adv ? 1u : 0u;
+      S.px_sr = suc_r;
+    }
+    if (!why && S.px_nops0 + run.z + (cross ? 1u : 0u) > ocap) why = 4;
+    if (why) S.px_bad = 1;
+    if (p.fdbg) gadd_r(&p.fdbg[why ? why : S.px_bad ? 2 : 0], 1ull);
+  }
+  __syncthreads();
+  if (S.px_bad) return false;
   // the decision (lane 0): the event of the crossing arrival, its counters as of that arrival
   if (tid == 0) {
     for (int k = 0; k < 3; ++k) S.deliv[PX_RES_TICKET + k] += S.px_deliv[k];
@@ -2421,6 +2443,11 @@ __device__ bool paxos_window_fast(const KP& p, ScanShared& S, Ctx& c, PaxosState
       s.vf += static_cast<int32_t>(S.px_cb - S.px_sb);
       c.nops = S.px_nops0 + S.px_eb;
       paxos_recv(c, s, rec_msg(rec), q);
+      if (!S.px_adv) {  // the counted responses after the decision, on the fresh counters
+        const uint32_t ca = run.x - S.px_cb - 1, sa = run.y - S.px_sb - S.px_sr;
+        s.vs += static_cast<int32_t>(sa);
+        s.vf += static_cast<int32_t>(ca - sa);
+      }
       S.px_ncross = c.nops - (S.px_nops0 + S.px_eb);
       c.nops = S.px_nops0 + run.z + S.px_ncross;
     } else {
