@@ -3864,20 +3864,17 @@ __global__ __launch_bounds__(1024) void k_scan_rt(const KP* __restrict__ pk, lon
 // k_scan<PAXOS, true, LOOP>.  The lane keeps its window's keys in LDS and selects them in
 // order (<= kPxCap^2 LDS reads).
 constexpr int kPxCap = 8;
-__global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
-                                                    long long t_hi, long long cs, int x_active) {
-  const KP& p = *pk;
-  BAIL_IF_ERR();
-  __shared__ uint64_t skey[kPxCap][256];
-  __shared__ uint32_t sref[kPxCap][256];  // slot << 16 | index in the node's list segment
-  const uint32_t tid = tidx();
-  const uint32_t na = p.act_n[0];
-  const bool has_start = (t_lo <= 0 && 0 < t_hi);
-  const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
-  const bool jit = p.delay_mode != BCSIM_DELAY_FIXED;
-  const bool can = !has_start && !has_stop && t_lo >= p.dbg_tmax && (!jit || p.rng_mode == BCSIM_RNG_COUNTER);
-  for (uint32_t k = blockIdx.x * blockDim.x + tid; k < na; k += gridDim.x * blockDim.x) {
-    const uint32_t g = p.act[k];
+// The per-replica counters of one lane's acceptor window (arrivals, REQ_TICKET and REQ_PROPOSE
+// among them, latest arrival): added once per wave when the wave's nodes are of one replica.
+struct PxCnt {
+  uint32_t rep, n, d0, d1;
+  long long tmax;
+};
+__device__ __attribute__((always_inline)) inline void px_accept(const KP& p, uint32_t g, long long t_lo, long long t_hi,
+                                                                long long cs, int x_active, bool can, bool jit,
+                                                                uint64_t (*skey)[256], uint32_t (*sref)[256], uint32_t tid,
+                                                                PxCnt& o) {
+  {
     const uint32_t rep = g / p.N, i = g % p.N;
     bool fast = can && AT(p.node_tnext, g, p.NT) >= t_hi;
     uint32_t xb = 0, xn = 0;
@@ -3911,14 +3908,14 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
     if (!fast) {
       const uint32_t pos = gadd_r(&p.act_n[2], 1u);
       AT(p.act, 2ull * p.NT + pos, 4ull * p.NT) = g;
-      continue;
+      return;
     }
-    if (cnt == 0) continue;  // only arrivals of a later window of this cell
+    if (cnt == 0) return;  // only arrivals of a later window of this cell
     uint32_t sub = AT(p.sub, g, p.NT);
     uint64_t draws = AT(p.draws, g, p.NT);
     Op* ops = p.ops + op_base(p, g);
-    unsigned long long* cs_ = cnt_stripe(p, rep);
     long long tmax = LLONG_MIN;
+    uint32_t d0 = 0, d1 = 0;
     uint32_t done = 0;
     for (uint32_t s2 = 0; s2 < cnt; ++s2) {
       uint32_t best = 0;
@@ -3940,7 +3937,8 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
       const uint32_t dt = static_cast<uint32_t>(prop_of_slot(p, q) + sel2(p.tx_last, m.big));
       const uint32_t origin = AT(p.col, q, p.E);
       if (t > tmax) tmax = t;
-      atomicAdd(&cs_[CNT_DELIV + r.type], 1ull);
+      d0 += r.type == PX_REQ_TICKET ? 1u : 0u;
+      d1 += r.type == PX_REQ_PROPOSE ? 1u : 0u;
       if (p.echo) AT(ops, nops++, ocap) = mk_op(p, t, dt, origin, r.sub, q, m, OP_ECHO, 0);
       int32_t* a = &AT(p.px, (static_cast<size_t>(g) * p.K + static_cast<uint32_t>(r.f2)) * 4,
                        static_cast<uint64_t>(p.NT) * p.K * 4);
@@ -3976,11 +3974,69 @@ __global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, l
     if (jit) AT(p.draws, g, p.NT) = draws;
     AT(p.n_ops, g, p.NT) = nops;
     AT(p.node_onext, g, p.NT) = LLONG_MIN;  // k_link recomputes
-    atomicAdd(&cs_[CNT_DELIV_TOTAL], static_cast<unsigned long long>(cnt));
-    atomicAdd(&kst_stripe(p)[KST_DELIV], static_cast<unsigned long long>(cnt));
-    if (p.echo) atomicAdd(&cs_[CNT_ECHOES], static_cast<unsigned long long>(cnt));
-    atomicAdd(&cs_[CNT_EVENTS], static_cast<unsigned long long>(cnt));
-    atomicMax(reinterpret_cast<long long*>(&cs_[CNT_TLAST]), tmax);
+    o = PxCnt{rep, cnt, d0, d1, tmax};
+  }
+}
+// v added to replica rep's counter idx (all 64 lanes call it): one atomic per wave when the
+// wave's nonzero lanes are of one replica
+__device__ inline void wave_cnt_add(const KP& p, uint32_t rep, uint32_t v, int idx) {
+  const unsigned long long any = __ballot(v != 0);
+  if (!any) return;
+  const int first = __ffsll(static_cast<long long>(any)) - 1;
+  const uint32_t r0 = __shfl(rep, first, 64);
+  if (__ballot(v != 0 && rep != r0) == 0) {
+    uint32_t sum = v;
+    for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    if ((tidx() & 63u) == static_cast<uint32_t>(first)) atomicAdd(&cnt_stripe(p, r0)[idx], static_cast<unsigned long long>(sum));
+  } else if (v) {
+    atomicAdd(&cnt_stripe(p, rep)[idx], static_cast<unsigned long long>(v));
+  }
+}
+__device__ inline void px_count_add(const KP& p, const PxCnt& o) {
+  unsigned long long* cs_ = cnt_stripe(p, o.rep);
+  const unsigned long long n = o.n, d2 = o.n - o.d0 - o.d1;
+  if (o.d0) atomicAdd(&cs_[CNT_DELIV + PX_REQ_TICKET], static_cast<unsigned long long>(o.d0));
+  if (o.d1) atomicAdd(&cs_[CNT_DELIV + PX_REQ_PROPOSE], static_cast<unsigned long long>(o.d1));
+  if (d2) atomicAdd(&cs_[CNT_DELIV + PX_REQ_COMMIT], d2);
+  atomicAdd(&cs_[CNT_DELIV_TOTAL], n);
+  atomicAdd(&kst_stripe(p)[KST_DELIV], n);
+  if (p.echo) atomicAdd(&cs_[CNT_ECHOES], n);
+  atomicAdd(&cs_[CNT_EVENTS], n);
+  atomicMax(reinterpret_cast<long long*>(&cs_[CNT_TLAST]), o.tmax);
+}
+__global__ __launch_bounds__(256) void k_paxos_scan(const KP* __restrict__ pk, long long cell, long long t_lo,
+                                                    long long t_hi, long long cs, int x_active) {
+  const KP& p = *pk;
+  BAIL_IF_ERR();
+  __shared__ uint64_t skey[kPxCap][256];
+  __shared__ uint32_t sref[kPxCap][256];  // slot << 16 | index in the node's list segment
+  const uint32_t tid = tidx();
+  const uint32_t na = p.act_n[0];
+  const bool has_start = (t_lo <= 0 && 0 < t_hi);
+  const bool has_stop = (p.stop_ns >= 0 && t_lo <= p.stop_ns && p.stop_ns < t_hi);
+  const bool jit = p.delay_mode != BCSIM_DELAY_FIXED;
+  const bool can = !has_start && !has_stop && t_lo >= p.dbg_tmax && (!jit || p.rng_mode == BCSIM_RNG_COUNTER);
+  // (the trip count is uniform over the workgroup, so the wave reduction below has every lane)
+  for (uint32_t kb = blockIdx.x * blockDim.x; kb < na; kb += gridDim.x * blockDim.x) {
+    const uint32_t k = kb + tid;
+    PxCnt o{0, 0, 0, 0, LLONG_MIN};
+    if (k < na) px_accept(p, p.act[k], t_lo, t_hi, cs, x_active, can, jit, skey, sref, tid, o);
+    const unsigned long long any = __ballot(o.n != 0);
+    if (!any) continue;
+    const int first = __ffsll(static_cast<long long>(any)) - 1;
+    const uint32_t r0 = __shfl(o.rep, first, 64);
+    if (__ballot(o.n != 0 && o.rep != r0) == 0) {  // one replica: one lane adds the wave's sums
+      uint32_t v = o.n | (o.d0 << 10) | (o.d1 << 20);  // <= 64 * kPxCap per field
+      long long tm = o.tmax;
+      for (int d = 32; d > 0; d >>= 1) {
+        v += __shfl_xor(v, d, 64);
+        tm = max(tm, static_cast<long long>(__shfl_xor(tm, d, 64)));
+      }
+      if ((tid & 63u) == static_cast<uint32_t>(first))
+        px_count_add(p, PxCnt{r0, v & 1023u, (v >> 10) & 1023u, (v >> 20) & 1023u, tm});
+    } else if (o.n) {
+      px_count_add(p, o);
+    }
   }
 }
 
@@ -8571,8 +8627,8 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
       AT(p.n_ops, g, p.NT) = kept;
       AT(p.node_onext, g, p.NT) = omin;
       atomicAdd(&L.c[4], kept);
-      if (c_sends) atomicAdd(&cnt_stripe(p, g / p.N)[CNT_SENDS], static_cast<unsigned long long>(c_sends));
     }
+    wave_cnt_add(p, g / p.N, c_sends, CNT_SENDS);
     if (c_rec) atomicAdd(&L.c[0], c_rec);
     if (c_ops) atomicAdd(&L.c[1], c_ops);
     if (c_edges) atomicAdd(&L.c[2], c_edges);
