@@ -50,7 +50,7 @@ namespace bcsim {
 // instructions instead of flat_* ones.
 #define GP(T) T*
 constexpr uint32_t kKstStripes = 64;
-constexpr uint32_t kNextBlocks = 64;  // k_next workgroups at most  // kstat[kKstStripes][8]: per-workgroup stripes, summed on the host
+constexpr uint32_t kNextBlocks = 512;  // k_next workgroups at most (41 M gnodes: 2 per CU)  // kstat[kKstStripes][8]: per-workgroup stripes, summed on the host
 struct KP {
   uint32_t N, R, NT, E;
   uint32_t protocol, delay_mode, rng_mode, encoding, echo;
