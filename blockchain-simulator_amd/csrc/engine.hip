@@ -1152,20 +1152,26 @@ __global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
   const bool v = k < n;
   XRec x{};
   if (v) x = AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + k, p.cap_xbuf);
-  unsigned long long rem = __ballot(v);
-  uint32_t pos = 0;
+  // the wave's receiver groups first (register work only), then every group's leader takes its
+  // range at once: the atomics' round trips overlap instead of following one another (a
+  // broadcast's records are 64 different receivers per wave)
+  unsigned long long rem = __ballot(v), mine = 0;
+  uint32_t leader = lane;
   while (rem) {
     const int ld = __ffsll(static_cast<long long>(rem)) - 1;
     const uint32_t gl = __shfl(x.g, ld, 64);
     const unsigned long long same = __ballot(v && x.g == gl);
-    uint32_t base = 0;
-    if (lane == static_cast<uint32_t>(ld))
-      base = AT(p.seg_off, gl, p.NT + 1) + __hip_atomic_fetch_add(&AT(p.cursor, gl, p.NT), static_cast<uint32_t>(__popcll(same)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    base = __shfl(base, ld, 64);
-    if (v && x.g == gl) pos = base + static_cast<uint32_t>(__popcll(same & ((1ull << lane) - 1ull)));
+    if (v && x.g == gl) {
+      leader = static_cast<uint32_t>(ld);
+      mine = same;
+    }
     rem &= ~same;
   }
-  if (v) AT(p.xgrp, pos, p.cap_x) = x;
+  uint32_t base = 0;
+  if (v && leader == lane)
+    base = AT(p.seg_off, x.g, p.NT + 1) + __hip_atomic_fetch_add(&AT(p.cursor, x.g, p.NT), static_cast<uint32_t>(__popcll(mine)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  base = __shfl(base, leader, 64);
+  if (v) AT(p.xgrp, base + static_cast<uint32_t>(__popcll(mine & ((1ull << lane) - 1ull))), p.cap_x) = x;
 }
 
 // one overflow record: into its bucket if its cell entered the ring, else `stay` = its cell
