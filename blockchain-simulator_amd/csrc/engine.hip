@@ -8733,23 +8733,36 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
   uint32_t ns = 0, nl = 0;
   const long long bm = p.bmin[b];
   uint8_t* const sfa = p.eslot ? p.sflag : reinterpret_cast<uint8_t*>(p.act_n);  // (a dummy word without slots)
-  for (uint32_t j = tid; j < cn; j += blockDim.x) {
-    // (gnode numbers are < 2^32: 32-bit index arithmetic; the node's words all loaded before any
-    // is used -- a short-circuit chain of them was one round trip each)
-    const uint32_t k = static_cast<uint32_t>(c0 + j);
-    const uint32_t g = (k / p.nloc) * p.N + p.nlo + k % p.nloc;
-    const uint32_t rep = g / p.N, i = g % p.N;
-    const uint8_t f8 = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
-    const uint8_t t8 = p.mesh ? AT(p.rtile, kRtPad * ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6)), kRtPad * (static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles))
-                              : static_cast<uint8_t>(0);
-    const long long tn = AT(p.node_tnext, g, p.NT), on = AT(p.node_onext, g, p.NT);
-    const uint8_t sfb = gbl(sfa)[p.eslot ? static_cast<size_t>(obp) * p.NT + g : 0u];
-    const bool sc = has_start || has_stop || ((f8 | t8) != 0 && bm < t_hi) || tn < t_hi;  // (node_flagged_w)
-    // k_link also runs nodes with reply-slot ops of the previous arrival cell due
-    const bool lk = sc || on < t_hi || (p.eslot && (sfb & (2u | kSfD1)));
-    fl[j] = static_cast<uint8_t>((sc ? 1u : 0u) | (lk ? 2u : 0u));
-    ns += sc ? 1u : 0u;
-    nl += lk ? 1u : 0u;
+  // (gnode numbers are < 2^32: 32-bit index arithmetic; the words of kActU nodes per lane all
+  // loaded before any is used -- one round trip per kActU nodes, not per node)
+  constexpr uint32_t kActU = 4;
+  for (uint32_t j0 = tid; j0 < cn; j0 += kActU * blockDim.x) {
+    uint8_t f8[kActU], t8[kActU], sfb[kActU];
+    long long tn[kActU], on[kActU];
+#pragma unroll
+    for (uint32_t u = 0; u < kActU; ++u) {
+      const uint32_t j = j0 + u * blockDim.x;
+      const uint32_t k = static_cast<uint32_t>(c0 + (j < cn ? j : 0u));
+      const uint32_t g = (k / p.nloc) * p.N + p.nlo + k % p.nloc;
+      const uint32_t rep = g / p.N, i = g % p.N;
+      f8[u] = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
+      t8[u] = p.mesh ? AT(p.rtile, kRtPad * ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6)), kRtPad * (static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles))
+                     : static_cast<uint8_t>(0);
+      tn[u] = AT(p.node_tnext, g, p.NT);
+      on[u] = AT(p.node_onext, g, p.NT);
+      sfb[u] = gbl(sfa)[p.eslot ? static_cast<size_t>(obp) * p.NT + g : 0u];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kActU; ++u) {
+      const uint32_t j = j0 + u * blockDim.x;
+      if (j >= cn) continue;
+      const bool sc = has_start || has_stop || ((f8[u] | t8[u]) != 0 && bm < t_hi) || tn[u] < t_hi;  // (node_flagged_w)
+      // k_link also runs nodes with reply-slot ops of the previous arrival cell due
+      const bool lk = sc || on[u] < t_hi || (p.eslot && (sfb[u] & (2u | kSfD1)));
+      fl[j] = static_cast<uint8_t>((sc ? 1u : 0u) | (lk ? 2u : 0u));
+      ns += sc ? 1u : 0u;
+      nl += lk ? 1u : 0u;
+    }
   }
   ns = wave_sum(ns);
   nl = wave_sum(nl);
