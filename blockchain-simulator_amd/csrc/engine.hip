@@ -9349,11 +9349,13 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
         p.x_cnt[clr_b] = 0;
         p.bmin[clr_b] = LLONG_MAX;
       }
-      if (p.mesh)
-        for (uint32_t k = tidx(); k < p.R * p.n_tiles; k += blockDim.x)
-          p.rtile[kRtPad * (static_cast<size_t>(clr_b) * p.R * p.n_tiles + k)] = 0;
     }
   }
+  // (the finished bucket's receiver-tile flags: one padded line each, cleared by every
+  // workgroup -- 10,000 replicas x 64 tiles was ~0.4 ms for workgroup 0 alone)
+  if (clr_b < p.n_buckets && p.mesh)
+    for (uint32_t k = blockIdx.x * blockDim.x + tidx(); k < p.R * p.n_tiles; k += gridDim.x * blockDim.x)
+      p.rtile[kRtPad * (static_cast<size_t>(clr_b) * p.R * p.n_tiles + k)] = 0;
   // scal[0] = the next event time (timers and pending ops), scal[3] = the next timer alone;
   // wave minima by shuffles, one LDS slot per wave, one barrier
   __shared__ long long red[kMaxWaves], redt[kMaxWaves];
