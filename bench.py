@@ -50,20 +50,42 @@ def make_topology(n_nodes, workload):
     return bcsim.random_regular(n_nodes, 8, 1)
 
 
-PMC_ROUND = "r05"
+PMC_ROUNDS = ("r06", "r05")  # newest first: the committed PMC summaries this line reads
 
 
-def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft"):
-    """HBM bytes per launch of `kernel` from this round's committed rocprofv3 PMC
-    summary (tools/pmc_summary.py over tests/gpu_prof.sh: FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE, separate passes), same workload, over the timed window's
-    dispatches when the summary has them; None if absent."""
-    path = os.path.join(REPO, "profiles", f"{PMC_ROUND}_pmc_{workload}{n_nodes}.json")
-    try:
-        with open(path) as f:
-            ks = json.load(f)["kernels"]
-    except (OSError, KeyError, ValueError):
-        return None
+def pmc_name(n_nodes, workload="pbft", replicas=1, queue="infinite", jitter=False):
+    """profiles/<round>_pmc_<name>.json: the workload's PMC summary (tests/gpu_prof.sh with the
+    same bench arguments, tools/pmc_summary.py)."""
+    name = f"{workload}{n_nodes}"
+    if replicas > 1:
+        name += f"_r{replicas}"
+    if queue != "infinite":
+        name += f"_{queue}"
+    if jitter:
+        name += "_jitter"
+    return name
+
+
+def pmc_traffic(n_nodes, kernel="bcsim::k_link", workload="pbft", replicas=1, queue="infinite", jitter=False):
+    """(HBM bytes per launch of `kernel`, source file) from the newest committed rocprofv3 PMC
+    summary of this workload (tools/pmc_summary.py over tests/gpu_prof.sh: FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE, separate passes), over the bench's own timed window of dispatches
+    when the summary has it; (None, None) if absent."""
+    name = pmc_name(n_nodes, workload, replicas, queue, jitter)
+    for rnd in PMC_ROUNDS:
+        path = os.path.join(REPO, "profiles", f"{rnd}_pmc_{name}.json")
+        try:
+            with open(path) as f:
+                ks = json.load(f)["kernels"]
+        except (OSError, KeyError, ValueError):
+            continue
+        v = _pmc_kernel(ks, kernel)
+        if v is not None:
+            return v, os.path.relpath(path, REPO)
+    return None, None
+
+
+def _pmc_kernel(ks, kernel):
     # the k_link class as the bench times it (fast path + looped generic kernel)
     if "link_class" in ks and kernel == "bcsim::k_link":
         return ks["link_class"]["timed_window"]["hbm_bytes_per_launch"]
@@ -312,8 +334,17 @@ def main():
     msgs = c1["delivered_total"] - c0["delivered_total"]
     commits = commit_records(sim, args.workload) - cm0
     dt, msgs, commits = aggregate(dist, f"cuda:{local}", dt, msgs, commits)
-    # breakdown pass (untimed): every kernel class timed over as many more steps
+    # breakdown pass (untimed): every kernel class timed.  One process: a fresh engine replays
+    # the warm-up and then the timed window's steps (the same simulated interval -- a run can
+    # go quiet after it, e.g. PBFT under FQCODEL); node-partitioned: as many steps after it
     os.environ["BCSIM_KSTATS"] = "15"
+    if dist is None:
+        sim.close()
+        sim = new_sim()
+        t_sim = 0
+        for _ in range(args.warmup):
+            t_sim += period
+            sim.run(t_sim)
     sim.reset_kernel_stats()
     for _ in range(args.steps):
         t_sim += period
@@ -330,8 +361,10 @@ def main():
         # roofline of the scatter (k_link): SURVEY.md §8(d) algorithmic bytes = 48 B per record
         # emitted by the timed k_link launches, over their HIP-event time on the engine stream
         ach = (lk["bytes"] / 1e9) / (lk["us"] / 1e6) if lk["us"] > 0 else 0.0
-        # PMC traffic of this workload's committed profile (none for the jittered variant)
-        traffic = None if (args.jitter or args.queue != "infinite") else pmc_traffic(args.nodes, workload=args.workload)
+        # PMC traffic of this workload's committed profile (same bench arguments)
+        traffic, traffic_src = pmc_traffic(args.nodes, workload=args.workload, replicas=args.replicas,
+                                           queue=args.queue, jitter=args.jitter)
+        avg_us = lk["us"] / max(1, lk["launches"])
         all_us = sum(v["us"] for v in ks_all.values())
         if args.workload == "pbft":
             data = "synthetic (PBFT n=%d full mesh, 3Mbps/3ms links, 50KB blocks, %s)" % (
@@ -384,8 +417,11 @@ def main():
                          # the measured HBM bytes per launch (PMC) over the same time, and their
                          # ratio to the algorithmic bytes: < 1 where the heavy waves' records travel
                          # as summaries, > 1 where bytes are re-read
-                         "traffic_GBs": (traffic / 1e9) / (lk["us"] / max(1, lk["launches"]) / 1e6)
-                         if traffic and lk["us"] > 0 else None,
+                         "traffic_GBs": (traffic / 1e9) / (avg_us / 1e6) if traffic and avg_us > 0 else None,
+                         # what the hardware moved: the PMC bytes per launch over this line's average
+                         # launch time, against the peak (frac prices the algorithmic bytes)
+                         "hw_frac": (traffic / 1e9) / (avg_us / 1e6) / HBM_PEAK_GBS if traffic and avg_us > 0 else None,
+                         "traffic_source": traffic_src,
                          "traffic_over_algorithmic": traffic / lk_launch_bytes if traffic and lk_launch_bytes else None,
                          "avg_launch_us": lk["us"] / max(1, lk["launches"]),
                          "launches": lk["launches"],

@@ -111,9 +111,10 @@ class Simulator(_abi.Handle):
 
     def loop_stats(self):
         """Cell-loop statistics (include/bcsim.h bcsim_read_loop_stats)."""
-        out = (C.c_uint64 * 4)()
-        self._call("read_loop_stats", self.h, out)
-        return dict(windows=out[0], collectives=out[1], tag_zeroes=out[2])
+        out = (C.c_uint64 * 8)()
+        self._call("read_loop_stats_ex", self.h, out)
+        return dict(windows=out[0], collectives=out[1], tag_zeroes=out[2], spec_hits=out[3], idle_parts=out[4],
+                    host_syncs=out[5], idle_checked=out[6])
 
     def reset_kernel_stats(self):
         self._call("reset_kernel_stats", self.h)

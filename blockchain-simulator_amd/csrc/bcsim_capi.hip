@@ -76,6 +76,7 @@ struct Sim {
   uint32_t next_seq = 0;      // ... of the last k_next
   uint32_t spec_seq = 0;      // ... of a speculative k_active not consumed yet (0: none)
   bool spec_on = false;       // speculative k_active behind k_next (BCSIM_SPEC=0: off)
+  bool fuse_act = true;       // ... built by k_next itself (BCSIM_FUSE_ACT=0: a k_active launch after it)
   uint64_t spec_hits = 0;
   std::vector<uint32_t> bcnt;  // bucket counts (host view)
   std::vector<uint32_t> xcnt;  // extras counts (host view)
@@ -111,6 +112,9 @@ struct Sim {
   // of k_active's list lengths (measured slower: 0.73 vs 0.53 ms per step)
   bool dev_sized = false;
   uint64_t idle_parts = 0;  // part cells cut by a run limit skipped as idle
+  uint64_t host_syncs = 0;  // times the cell loop waited on the GPU (spins, stream syncs, blocking collectives)
+  bool check_idle = false;
+  uint64_t idle_checked = 0;  // idle parts verified by check_idle_part  // debug (BCSIM_CHECK_IDLE=1): k_active verifies every skipped idle part is empty
   uint32_t gossip_l3_grid = 256;  // dense gossip: workgroups of the looped list-3 link grid (BCSIM_GL3; x8)
   uint32_t rt_min = 0;     // summary mode: k_scan_rt takes windows of at least this many scanned nodes (BCSIM_RT_MIN)
   long long next_timer = LLONG_MIN;  // earliest node timer after the last cell (k_next), unknown at start
@@ -1093,6 +1097,8 @@ static int setup_device(Sim& s) {
   if (const char* fv = std::getenv("BCSIM_DBG_DEV_ERR"); fv && *fv) s.dbg_dev_err = std::atoll(fv);
   if (const char* rs = std::getenv("BCSIM_ROW_SPLIT"); rs && *rs) s.row_split_max = static_cast<uint32_t>(std::atoi(rs));
   if (const char* ab = std::getenv("BCSIM_ACT_RB"); ab && *ab == '0') s.dev_sized = true;
+  if (const char* ci = std::getenv("BCSIM_CHECK_IDLE"); ci && *ci == '1') s.check_idle = true;
+  if (const char* fa = std::getenv("BCSIM_FUSE_ACT"); fa && *fa == '0') s.fuse_act = false;
   if (const char* g3 = std::getenv("BCSIM_GL3"); g3 && *g3) s.gossip_l3_grid = std::max<uint32_t>(8, static_cast<uint32_t>(std::atoi(g3)) / 8 * 8);
   {
     const char* sp = std::getenv("BCSIM_SPEC");
@@ -1355,6 +1361,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
         s.act_h[1] = s.act_m[1];
       } else {
         HIPCHK(hipMemcpyAsync(s.act_h, s.kp.act_n, 16, hipMemcpyDeviceToHost, s.stream));
+        if (!s.act_m) ++s.host_syncs;  // (with a mirror, mirror_wait counted it)
         HIPCHK(hipStreamSynchronize(s.stream));
       }
       grid = dim3((s.act_h[0] + 7) / 8 * 8);
@@ -1678,6 +1685,7 @@ static int group_cell(Sim& s, long long cell) {
     }
     HIPCHK(hipMemcpyAsync(s.bcnt_h, s.kp.bucket_cnt, 8ull * s.B, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipMemcpyAsync(&s.ov_min, s.kp.scal + 1, 8, hipMemcpyDeviceToHost, s.stream));
+    ++s.host_syncs;
     HIPCHK(hipStreamSynchronize(s.stream));
     for (uint32_t k = 0; k < s.B; ++k) {
       s.bcnt[k] = s.bcnt_h[k];
@@ -1723,6 +1731,7 @@ static int group_cell(Sim& s, long long cell) {
 // BCSIM_SPIN=0, a plain stream sync.
 constexpr int kSpinUs = 500;  // mirror_wait: spin at most this long, then a stream sync
 static int mirror_wait(Sim& s, const uint32_t* w, uint32_t seq) {
+  ++s.host_syncs;
   static const bool spin = [] {
     const char* e = std::getenv("BCSIM_SPIN");
     return !(e && *e == '0');
@@ -1759,6 +1768,7 @@ static int readback(Sim& s, bool after_next = false) {
     std::memcpy(s.ctl_h, s.ctl_m, nb);
   } else {
     HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, nb, hipMemcpyDeviceToHost, s.stream));
+    if (!(after_next && s.ctl_m)) ++s.host_syncs;
     HIPCHK(hipStreamSynchronize(s.stream));
   }
   return readback_apply(s);
@@ -1820,6 +1830,7 @@ static int exchange(Sim& s, long long cell, int lrc, bool tick) {
     const size_t nb = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
     HIPCHK(hipMemcpyAsync(s.ctlw_h, s.ctlw_d, 2ull * P * W * 8, hipMemcpyDeviceToHost, s.stream));
     HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, nb, hipMemcpyDeviceToHost, s.stream));
+    ++s.host_syncs;
     HIPCHK(hipStreamSynchronize(s.stream));
     const int arc = readback_apply(s);
     if (!lrc) lrc = arc;
@@ -1849,6 +1860,7 @@ static int exchange(Sim& s, long long cell, int lrc, bool tick) {
   }
   rc = s.xp->ctl_exchange(s.stream, snd.data(), rcv.data());
   ++s.ctl_collectives;
+  ++s.host_syncs;  // (host words in and out)
   if (rc) return rc;
   if (lrc) return lrc;
   }
@@ -1904,6 +1916,7 @@ static int sync_vlog(Sim& s, int lrc = 0) {
   }
   uint32_t cnt = 0;
   HIPCHK(hipMemcpyAsync(&cnt, s.kp.vlog_cnt, 4, hipMemcpyDeviceToHost, s.stream));
+  ++s.host_syncs;
   HIPCHK(hipStreamSynchronize(s.stream));
   cnt = std::min(cnt, s.kp.cap_vlog);
   const uint32_t mine = cnt - s.vsync;
@@ -1949,6 +1962,7 @@ static int sync_leaders(Sim& s) {
   int rc = launch(s, KS_AUX, k_lead, dim3(s.R), dim3(1024), 0, s.kp_dev);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(s.lead_w.data(), s.kp.lead_loc, s.NT, hipMemcpyDeviceToHost, s.stream));
+  ++s.host_syncs;
   HIPCHK(hipStreamSynchronize(s.stream));
   for (size_t k = 0; k < s.lead_w.size(); k += 4096) {  // (one call for N <= 32768 nodes)
     const uint32_t n = static_cast<uint32_t>(std::min<size_t>(4096, s.lead_w.size() - k));
@@ -2050,6 +2064,34 @@ static long long local_next_cell(const Sim& s, bool with_tick) {
   return c;
 }
 
+// Debug (BCSIM_CHECK_IDLE=1): the part [lo, hi) of cell `cell` that run() skips as
+// idle (the tick's leading part, or a part cut by the run limit) must hold no node with work:
+// k_active -- the rule every window uses -- runs for it and the run fails if either list is not
+// empty.  The speculative lists of the next window are overwritten, so that window runs k_active
+// itself.
+static int check_idle_part(Sim& s, long long cell, long long lo, long long hi) {
+  if (s.sparse) return BCSIM_OK;
+  s.spec_seq = 0;
+  HIPCHK(hipMemsetAsync(s.kp.act_n, 0, 16, s.stream));
+  const uint64_t nl = static_cast<uint64_t>(s.R) * s.nloc;
+  const uint64_t nb = std::max<uint64_t>((nl + kActChunk - 1) / kActChunk, std::min<uint64_t>(1024, (nl + 255) / 256));
+  const uint32_t chunk = static_cast<uint32_t>(((nl + nb - 1) / nb + 255) / 256 * 256);
+  int rc = launch(s, KS_AUX, k_active, dim3(static_cast<uint32_t>((nl + chunk - 1) / chunk)), dim3(256), 0, s.kp_dev, lo, hi,
+                  static_cast<uint32_t>(cell % s.B), static_cast<uint32_t>((cell + kOpRing - 1) % kOpRing), chunk, ++s.mseq, 0);
+  if (rc) return rc;
+  uint32_t n[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(n, s.kp.act_n, 16, hipMemcpyDeviceToHost, s.stream));
+  HIPCHK(hipStreamSynchronize(s.stream));
+  if (n[0] || n[1]) {
+    g_detail = "idle part [" + std::to_string(lo) + ", " + std::to_string(hi) + ") of cell " + std::to_string(cell) +
+               " was skipped but k_active lists " + std::to_string(n[0]) + " / " + std::to_string(n[1]) + " nodes";
+    return BCSIM_E_STATE;
+  }
+  HIPCHK(hipMemsetAsync(s.kp.act_n, 0, 16, s.stream));
+  ++s.idle_checked;
+  return BCSIM_OK;
+}
+
 static int run(Sim& s, int64_t t_until) {
   int rc;
   if (!s.started) {
@@ -2091,6 +2133,7 @@ static int run(Sim& s, int64_t t_until) {
         int64_t cv[2] = {c, lerr};
         if ((rc = s.xp->allreduce_i64(s.stream, cv, 2, 0))) return rc;
         ++s.ctl_collectives;
+        ++s.host_syncs;
         if (cv[1] < 0) {
           if (lerr) return lerr;
           g_detail = "another rank of the partition failed";
@@ -2164,6 +2207,10 @@ static int run(Sim& s, int64_t t_until) {
       const bool idle = !s.xp && s.bcnt[c % s.B] == 0 && s.next_local >= tk && s.next_timer >= tk &&
                         !(lo <= 0 && 0 < tk) && !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < tk);
       if (!lrc && tk > lo && !idle) lrc = do_scan(s, c, lo, tk, cs, false);
+      if (!lrc && tk > lo && idle) {
+        ++s.idle_parts;
+        if (s.check_idle) lrc = check_idle_part(s, c, lo, tk);
+      }
       if (s.xp) {
         if ((rc = sync_vlog(s, lrc)) || (rc = sync_leaders(s))) return rc;
       } else if (lrc) {
@@ -2181,6 +2228,7 @@ static int run(Sim& s, int64_t t_until) {
                         s.next_timer >= hi && !(lo <= 0 && 0 < hi) &&
                         !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi);
       if (idle) {
+        if (s.check_idle && (rc = check_idle_part(s, c, lo, hi))) return rc;
         s.t_done = hi;
         ++s.cells;
         ++s.idle_parts;
@@ -2215,8 +2263,11 @@ static int run(Sim& s, int64_t t_until) {
                     s.cfg.stop_ns, 1};
     }
     s.next_seq = ++s.mseq;
-    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b, s.next_seq, pa);
-    if (!lrc && spec) {
+    // (k_next builds the predicted window's lists itself unless BCSIM_FUSE_ACT=0: no k_active launch)
+    const uint32_t fused_seq = spec && s.fuse_act ? ++s.mseq : 0u;
+    if (!lrc) lrc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, clr_b, s.next_seq, pa, fused_seq);
+    if (!lrc && fused_seq) s.spec_seq = fused_seq;
+    if (!lrc && spec && !fused_seq) {
       const uint64_t nl = static_cast<uint64_t>(s.R) * s.nloc;
       const uint64_t nb = std::max<uint64_t>((nl + kActChunk - 1) / kActChunk, std::min<uint64_t>(1024, (nl + 255) / 256));
       const uint32_t chunk = static_cast<uint32_t>(((nl + nb - 1) / nb + 255) / 256 * 256);
@@ -2605,6 +2656,20 @@ int bcsim_read_loop_stats(bcsim_sim* h, uint64_t* out4) {
   out4[1] = s.ctl_collectives;
   out4[2] = s.tag_zeroes;
   out4[3] = 0;
+  return BCSIM_OK;
+}
+
+int bcsim_read_loop_stats_ex(bcsim_sim* h, uint64_t* out8) {
+  if (!h || !out8) return BCSIM_E_INVAL;
+  const Sim& s = *h->s;
+  out8[0] = s.cells;
+  out8[1] = s.ctl_collectives;
+  out8[2] = s.tag_zeroes;
+  out8[3] = s.spec_hits;
+  out8[4] = s.idle_parts;
+  out8[5] = s.host_syncs;
+  out8[6] = s.idle_checked;
+  out8[7] = 0;
   return BCSIM_OK;
 }
 

@@ -9338,7 +9338,72 @@ __device__ inline void predict_window(const KP& p, const PredArgs& a, long long 
   pv[3] = hi;
 }
 
-__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b, uint32_t seq, PredArgs pa) {
+// k_active's rule for k_next's predicted window, in k_next's one workgroup (N <= 4096, the
+// speculative path): the lists k_active(spec = 1) would build after k_next, without its launch.
+// n_loc <= 4 * blockDim.x; the words of a lane's four gnodes are loaded before any is used, the
+// lists are compacted in ascending gnode order (block ranks) like k_active's.
+__device__ inline void next_active(const KP& p, const long long* pv, uint32_t act_seq) {
+  const uint32_t tid = tidx();
+  const uint64_t n_loc = static_cast<uint64_t>(p.R) * p.nloc;
+  const long long c = pv[1], t_hi = pv[3];
+  const uint32_t b = static_cast<uint32_t>(c % p.n_buckets), obp = static_cast<uint32_t>((c + kOpRing - 1) % kOpRing);
+  const long long bm = p.bmin[b];
+  uint8_t* const sfa = p.eslot ? p.sflag : reinterpret_cast<uint8_t*>(p.act_n);  // (a dummy word without slots)
+  __shared__ uint32_t wcnt[kMaxWaves];
+  constexpr uint32_t kU = 4;
+  uint32_t fl[kU];
+  uint8_t f8[kU], t8[kU], sfb[kU];
+  long long tn[kU], on[kU];
+#pragma unroll
+  for (uint32_t u = 0; u < kU; ++u) {
+    const uint32_t j = tid + u * blockDim.x;
+    const uint32_t k = j < n_loc ? j : 0u;
+    const uint32_t g = (k / p.nloc) * p.N + p.nlo + k % p.nloc;
+    const uint32_t rep = g / p.N, i = g % p.N;
+    f8[u] = AT(p.iflag, static_cast<size_t>(b) * p.NT + g, static_cast<uint64_t>(p.n_buckets) * p.NT);
+    t8[u] = p.mesh ? AT(p.rtile, kRtPad * ((static_cast<size_t>(b) * p.R + rep) * p.n_tiles + (i >> 6)), kRtPad * (static_cast<uint64_t>(p.n_buckets) * p.R * p.n_tiles))
+                   : static_cast<uint8_t>(0);
+    tn[u] = AT(p.node_tnext, g, p.NT);
+    on[u] = AT(p.node_onext, g, p.NT);
+    sfb[u] = gbl(sfa)[p.eslot ? static_cast<size_t>(obp) * p.NT + g : 0u];
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < kU; ++u) {
+    const uint32_t j = tid + u * blockDim.x;
+    // (a predicted window holds neither START nor STOP)
+    const bool sc = j < n_loc && (((f8[u] | t8[u]) != 0 && bm < t_hi) || tn[u] < t_hi);  // (node_flagged_w)
+    const bool lk = j < n_loc && (sc || on[u] < t_hi || (p.eslot && (sfb[u] & (2u | kSfD1))));
+    fl[u] = (sc ? 1u : 0u) | (lk ? 2u : 0u);
+  }
+  uint32_t ps = 0, pl = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < kU; ++u) {  // (uniform: every lane runs every block rank)
+    const uint32_t j = tid + u * blockDim.x;
+    const uint32_t g = j < n_loc ? (j / p.nloc) * p.N + p.nlo + j % p.nloc : 0u;
+    uint32_t ts, tl;
+    const uint32_t rs = block_rank((fl[u] & 1u) != 0, wcnt, ts);
+    if (fl[u] & 1u) p.act[ps + rs] = g;
+    const uint32_t rl = block_rank((fl[u] & 2u) != 0, wcnt, tl);
+    if (fl[u] & 2u) p.act[p.NT + pl + rl] = g;
+    ps += ts;
+    pl += tl;
+  }
+  if (tid == 0) {
+    p.act_n[0] = ps;
+    p.act_n[1] = pl;
+    if (p.act_mirror) {
+      p.act_mirror[0] = ps;
+      p.act_mirror[1] = pl;
+      __threadfence_system();
+      __hip_atomic_store(p.act_mirror + 2, act_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // (host spins on it)
+    }
+  }
+}
+
+// act_seq != 0 (one workgroup, speculation on): the predicted window's active lists too
+// (next_active), published before the control block
+__global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b, uint32_t seq, PredArgs pa,
+                                               uint32_t act_seq) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (blockIdx.x == 0) {
@@ -9392,6 +9457,32 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     redt[wv] = mt;
   }
   __syncthreads();
+  if (nb == 1 && act_seq) {  // (uniform) every wave stays for the active lists
+    __shared__ long long s_pv[4];
+    m = lane < nwv ? red[lane] : LLONG_MAX;
+    mt = lane < nwv ? redt[lane] : LLONG_MAX;
+    for (int d = 32; d > 0; d >>= 1) {
+      m = min(m, static_cast<long long>(__shfl_xor(m, d, 64)));
+      mt = min(mt, static_cast<long long>(__shfl_xor(mt, d, 64)));
+    }
+    long long pv[4];
+    if (wv == 0) {
+      predict_window(p, pa, m, pv);
+      if (lane == 0) {
+        p.scal[0] = m;
+        p.scal[3] = mt;
+        for (int k = 0; k < 4; ++k) {
+          p.pred[k] = pv[k];
+          s_pv[k] = pv[k];
+        }
+      }
+    }
+    __syncthreads();
+    for (int k = 0; k < 4; ++k) pv[k] = s_pv[k];
+    if (pv[0]) next_active(p, pv, act_seq);  // (uniform)
+    if (wv == 0) ctl_publish(p, m, mt, seq, pv);
+    return;
+  }
   if (wv != 0) return;
   m = lane < nwv ? red[lane] : LLONG_MAX;
   mt = lane < nwv ? redt[lane] : LLONG_MAX;

@@ -318,6 +318,12 @@ int bcsim_read_engine_counters(bcsim_sim* s, uint64_t* out8);
  * collectives of a node-partitioned run (control exchanges, record exchanges, all-reduces;
  * DESIGN.md §5), [2] inbox buckets zeroed for the ring-turn tag invariant, [3] 0. */
 int bcsim_read_loop_stats(bcsim_sim* s, uint64_t* out4);
+/* Extended cell-loop statistics since bcsim_create (profiling aid): [0..2] as
+ * bcsim_read_loop_stats, [3] windows whose active lists came from the speculative k_active
+ * behind k_next, [4] part cells skipped as idle (nothing can happen before the tick / run
+ * limit), [5] host syncs of the cell loop (mirror spins, stream syncs, blocking collectives),
+ * [6] idle parts verified empty (BCSIM_CHECK_IDLE=1), [7] 0. */
+int bcsim_read_loop_stats_ex(bcsim_sim* s, uint64_t* out8);
 
 #ifdef __cplusplus
 }
