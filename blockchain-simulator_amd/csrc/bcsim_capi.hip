@@ -2,6 +2,8 @@
 // declared in include/bcsim.h.  One translation unit with the kernels.
 #include "engine.hip"
 
+#include <hip/hip_ext.h>
+
 #include <chrono>
 #include <cstdlib>
 
@@ -76,7 +78,7 @@ struct Sim {
   uint32_t next_seq = 0;      // ... of the last k_next
   uint32_t spec_seq = 0;      // ... of a speculative k_active not consumed yet (0: none)
   bool spec_on = false;       // speculative k_active behind k_next (BCSIM_SPEC=0: off)
-  bool fuse_act = true;       // ... built by k_next itself (BCSIM_FUSE_ACT=0: a k_active launch after it)
+  bool fuse_act = false;      // ... built by k_next itself (BCSIM_FUSE_ACT=1; measured slower: one workgroup)
   uint64_t spec_hits = 0;
   std::vector<uint32_t> bcnt;  // bucket counts (host view)
   std::vector<uint32_t> xcnt;  // extras counts (host view)
@@ -100,6 +102,7 @@ struct Sim {
   // linked by the generic kernels on stream2 (parameter block kp_dev2: list 2, its own staging
   // area) while stream runs everyone else's link stage; joined before the link class ends
   bool l2_overlap = false;
+  bool l2_all = false;  // ... in every window with a list 2, not only the few-node scans (BCSIM_L2_OVERLAP=1)
   uint32_t win_epoch = 0, l2_pending = 0;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -131,6 +134,12 @@ struct Sim {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   std::vector<int> ev_class;
   size_t ev_used = 0;
+  // hipExtLaunchKernel timing (BCSIM_EXT_EVENTS=0: marker packets): the pending start event of the
+  // open class (recorded by its next launch on ev_start_stream), and the last launch's stop
+  bool ext_events = true;
+  hipEvent_t ev_start_pend = nullptr;
+  hipStream_t ev_start_stream = nullptr;
+  bool ev_stop_attach = false, ev_stop_done = false;
   // trace cache
   std::vector<bcsim_trace_rec> trace;
   bool trace_valid = false;
@@ -204,11 +213,24 @@ static int ev_begin(Sim& s, int cls) {
     s.ev_class.push_back(cls);
   }
   s.ev_class[s.ev_used] = cls;
-  HIPCHK(hipEventRecord(s.ev_pool[s.ev_used].first, s.stream));
+  if (s.ext_events) {  // (recorded by the next launch's own dispatch: no marker packet)
+    s.ev_start_pend = s.ev_pool[s.ev_used].first;
+    s.ev_start_stream = s.stream;
+  } else {
+    HIPCHK(hipEventRecord(s.ev_pool[s.ev_used].first, s.stream));
+  }
   return BCSIM_OK;
 }
 static int ev_end(Sim& s) {
-  HIPCHK(hipEventRecord(s.ev_pool[s.ev_used].second, s.stream));
+  if (s.ev_start_pend) {  // (nothing was launched in between)
+    HIPCHK(hipEventRecord(s.ev_start_pend, s.ev_start_stream));
+    s.ev_start_pend = nullptr;
+  }
+  s.ev_stop_attach = false;
+  if (s.ev_stop_done)
+    s.ev_stop_done = false;  // (the last launch of the class recorded it)
+  else
+    HIPCHK(hipEventRecord(s.ev_pool[s.ev_used].second, s.stream));
   s.launches[s.ev_class[s.ev_used]]++;
   ++s.ev_used;
   return BCSIM_OK;
@@ -229,6 +251,7 @@ static int ev_collect(Sim& s) {
 
 static int mirror_wait(Sim& s, const uint32_t* w, uint32_t seq);  // (below, with readback)
 static int readback_apply(Sim& s);
+static int readback(Sim& s, bool after_next = false);
 
 static int validate(const bcsim_config& c) {
   if (c.abi_version != BCSIM_ABI_VERSION) return BCSIM_E_INVAL;
@@ -797,6 +820,10 @@ static int setup_device(Sim& s) {
       const char* lo = std::getenv("BCSIM_L2_OVERLAP");
       const bool dbg = std::getenv("BCSIM_FDBG") || std::getenv("BCSIM_WGT") || sync_each();
       s.l2_overlap = s.mesh_tile && s.scan_fast && !dbg && !(lo && *lo == '0');
+      // (the summary / k_scan_pbft windows' list 2 is the leader's few-us scan: the fork and join
+      // cost more than the overlap wins there -- 0.49 vs 0.50-0.52 ms per step -- so by default
+      // only the few-node windows (the leader's 8190-arrival scan beside the row stage) fork)
+      s.l2_all = s.l2_overlap && lo && *lo == '1';
     }
     if ((rc = dalloc(s, &p.l2mark, s.l2_overlap ? NT : 1))) return rc;
     HIPCHK(hipMemset(p.l2mark, 0, (s.l2_overlap ? NT : 1) * 4));
@@ -957,6 +984,12 @@ static int setup_device(Sim& s) {
   p.pred = (decltype(p.pred))(cd->pred);
   if ((rc = dalloc(s, &p.nxt_part, 2 * kNextBlocks)) || (rc = dalloc(s, &p.nxt_done, 1))) return rc;
   HIPCHK(hipMemset(p.nxt_done, 0, 4));
+  if ((rc = dalloc(s, &p.rb_acc, 1)) || (rc = dalloc(s, &p.rb_done, 1))) return rc;
+  {
+    const long long mx = LLONG_MAX;
+    HIPCHK(hipMemcpy((void*)p.rb_acc, &mx, 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset((void*)p.rb_done, 0, 4));
+  }
   p.bucket_cnt = (decltype(p.bucket_cnt))(reinterpret_cast<uint32_t*>(ctl + sizeof(Ctl)));
   p.x_cnt = p.bucket_cnt + s.B;
   p.send_cnt = p.x_cnt + s.B;
@@ -1098,7 +1131,8 @@ static int setup_device(Sim& s) {
   if (const char* rs = std::getenv("BCSIM_ROW_SPLIT"); rs && *rs) s.row_split_max = static_cast<uint32_t>(std::atoi(rs));
   if (const char* ab = std::getenv("BCSIM_ACT_RB"); ab && *ab == '0') s.dev_sized = true;
   if (const char* ci = std::getenv("BCSIM_CHECK_IDLE"); ci && *ci == '1') s.check_idle = true;
-  if (const char* fa = std::getenv("BCSIM_FUSE_ACT"); fa && *fa == '0') s.fuse_act = false;
+  if (const char* fa = std::getenv("BCSIM_FUSE_ACT"); fa && *fa == '1') s.fuse_act = true;
+  if (const char* xe = std::getenv("BCSIM_EXT_EVENTS"); xe && *xe == '0') s.ext_events = false;
   if (const char* g3 = std::getenv("BCSIM_GL3"); g3 && *g3) s.gossip_l3_grid = std::max<uint32_t>(8, static_cast<uint32_t>(std::atoi(g3)) / 8 * 8);
   {
     const char* sp = std::getenv("BCSIM_SPEC");
@@ -1178,7 +1212,27 @@ static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, 
   const bool timed = cls >= 0 && ((kstat_mask() >> cls) & 1u);
   int rc = timed ? ev_begin(s, cls) : BCSIM_OK;
   if (rc) return rc;
-  hipLaunchKernelGGL(kernel, grid, block, lds, s.stream, args...);
+  if (timed && s.ext_events) s.ev_stop_attach = true;
+  // timing events of a class are recorded by its first / last launch's dispatch (hipExtLaunchKernel:
+  // the kernel's own start / end timestamps) instead of separate marker packets, each of which
+  // cost a few us of dispatch gap
+  hipEvent_t st = nullptr, sp = nullptr;
+  if (s.ev_start_pend) {
+    if (s.stream == s.ev_start_stream)
+      st = s.ev_start_pend;
+    else
+      HIPCHK(hipEventRecord(s.ev_start_pend, s.ev_start_stream));  // (a launch on the other stream first)
+    s.ev_start_pend = nullptr;
+  }
+  if (s.ev_stop_attach) {
+    sp = s.ev_pool[s.ev_used].second;
+    s.ev_stop_attach = false;
+    s.ev_stop_done = true;
+  }
+  if (st || sp)
+    hipExtLaunchKernelGGL(kernel, grid, block, static_cast<uint32_t>(lds), s.stream, st, sp, 0u, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, lds, s.stream, args...);
   HIPCHK(hipGetLastError());
   if (timed) {
     rc = ev_end(s);
@@ -1303,6 +1357,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
         // (the looped grid may not exceed the workgroups the per-workgroup staging areas
         // were allocated for: xstage / xmeta hold grid_link of them)
         // (list 3 is almost always empty here; BCSIM_GL3: its grid, 8-256 measured alike)
+        ((s.ev_stop_attach = timed && s.ext_events), false) ||
         (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(s.gossip_l3_grid, s.grid_link)), dim3(s.bs_link),
                      link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
       return rc;
@@ -1400,7 +1455,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   else if (use_rt) {
     // the scan of every receiver tile; the nodes it leaves (list 2, materialised) to the generic
     // kernel as after k_scan_pbft
-    const uint32_t wep = s.l2_overlap ? (++s.win_epoch == 0 ? ++s.win_epoch : s.win_epoch) : 0u;
+    const uint32_t wep = s.l2_all ? (++s.win_epoch == 0 ? ++s.win_epoch : s.win_epoch) : 0u;
     rc = launch(s, KS_SCAN, k_scan_rt, grid_rt, dim3(1024), 0, s.kp_dev, cell, lo, hi, cs, xa, wep, 0);
     if (!rc && wep) {
       HIPCHK(hipEventRecord(s.ev_fork, s.stream));
@@ -1438,7 +1493,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
   else if (s.scan_fast && !(lo <= 0 && 0 < hi) && !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi)) {
     // PBFT heavy waves: one pass over each row in registers; the nodes it leaves (list 2) to
     // the generic kernel -- a small looped grid, with the doubled staging window if there is one
-    const uint32_t wep = s.l2_overlap ? (++s.win_epoch == 0 ? ++s.win_epoch : s.win_epoch) : 0u;
+    const uint32_t wep = s.l2_all ? (++s.win_epoch == 0 ? ++s.win_epoch : s.win_epoch) : 0u;
     rc = launch(s, KS_SCAN, k_scan_pbft, grid, dim3(kFastLanes), 0, s.kp_dev, cell, lo, hi, cs, xa, wep);
     if (!rc && wep) {  // fork: list 2 is scanned (and linked, below) on the second stream
       HIPCHK(hipEventRecord(s.ev_fork, s.stream));
@@ -1532,6 +1587,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     const bool timed = (kstat_mask() >> KS_LINK) & 1u;
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
     if ((rc = launch(s, -1, k_paxos_link, grid, dim3(kPxLinkThreads), 0, s.kp_dev, cell, lo, hi)) ||
+        ((s.ev_stop_attach = timed && s.ext_events), false) ||
         (rc = launch(s, -1, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw, 3)))
       return rc;
     if (timed) {
@@ -1587,6 +1643,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
           (s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, rgrid.x))) ||
           (!s.sum && (rc = launch(s, -1, k_mesh_tile, dim3(nt), dim3(kTileThreads), 0, s.kp_dev, cell, lo, hi, ep))) ||
           (!s.sum && s.kp.wgtt && (rc = tile_phase_report(s, cell, nt))) ||
+          ((s.ev_stop_attach = timed && s.ext_events && !wep), false) ||
           (rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
     } else {
@@ -1674,13 +1731,20 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
 // receiver.
 static int group_cell(Sim& s, long long cell) {
   const uint32_t b = static_cast<uint32_t>(cell % s.B);
-  if (s.ov_min <= cell + static_cast<long long>(s.B) - 1) {
+  if (s.ov_min <= cell + static_cast<long long>(s.B) - 1 && s.ctl_m) {
     // the overflow count as of the last read-back (nothing appends to the list between the
-    // end-of-cell read-back and here)
+    // end-of-cell read-back and here); the launch resets the bound and the list itself and
+    // publishes the control block: one spin, no copies (the path below without a mirror)
+    const uint32_t nov = s.ctl_h->ov_cnt;
+    s.next_seq = ++s.mseq;
+    int rc = launch(s, KS_GROUP, k_rebin, dim3(std::max<uint32_t>(1u, (nov + 255) / 256)), dim3(256), 0, s.kp_dev, cell, nov,
+                    s.next_seq);
+    if (rc || (rc = readback(s, true))) return rc;
+  } else if (s.ov_min <= cell + static_cast<long long>(s.B) - 1) {
     const uint32_t nov = s.ctl_h->ov_cnt;
     HIPCHK(hipMemcpyAsync(s.kp.scal + 1, s.act_h + 4, 8, hipMemcpyHostToDevice, s.stream));  // LLONG_MAX (pinned)
     if (nov) {
-      int rc = launch(s, KS_GROUP, k_rebin, dim3((nov + 255) / 256), dim3(256), 0, s.kp_dev, cell, nov);
+      int rc = launch(s, KS_GROUP, k_rebin, dim3((nov + 255) / 256), dim3(256), 0, s.kp_dev, cell, nov, 0u);
       if (rc) return rc;
     }
     HIPCHK(hipMemcpyAsync(s.bcnt_h, s.kp.bucket_cnt, 8ull * s.B, hipMemcpyDeviceToHost, s.stream));
@@ -1760,7 +1824,7 @@ static int mirror_wait(Sim& s, const uint32_t* w, uint32_t seq) {
 
 // after_next: right after k_next, which published the control block to the host-mapped
 // mirror -- the read-back is the stream sync alone
-static int readback(Sim& s, bool after_next = false) {
+static int readback(Sim& s, bool after_next) {
   const size_t nb = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
   int w = 1;
   if (after_next && s.ctl_m && (w = mirror_wait(s, reinterpret_cast<uint32_t*>(s.ctl_m) + nb / 4, s.next_seq)) < 0) return w;

@@ -50,6 +50,7 @@ namespace bcsim {
 // instructions instead of flat_* ones.
 #define GP(T) T*
 constexpr uint32_t kKstStripes = 64;
+constexpr int kMaxBuckets = 64;
 constexpr uint32_t kNextBlocks = 512;  // k_next workgroups at most (41 M gnodes: 2 per CU)  // kstat[kKstStripes][8]: per-workgroup stripes, summed on the host
 struct KP {
   uint32_t N, R, NT, E;
@@ -288,6 +289,8 @@ struct KP {
                     // [4] earliest arrival cell shipped to another rank (node-partitioned)
   GP(long long) nxt_part;  // [kNextBlocks] k_next per-workgroup minima
   GP(uint32_t) nxt_done;   // k_next workgroups finished (the last one reduces and resets it)
+  GP(long long) rb_acc;    // k_rebin (publishing): the staying records' minimum cell (LLONG_MAX between launches)
+  GP(uint32_t) rb_done;    // k_rebin workgroups finished (the last one resets it)
   // node partition (multi-GPU PDES): this rank owns nodes
   // [nlo, nlo + nloc) of every replica; records for other ranks' receivers
   // are staged in sendbuf and exchanged once per cell
@@ -1175,7 +1178,10 @@ __global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
 }
 
 // one overflow record: into its bucket if its cell entered the ring, else `stay` = its cell
-__device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long long& stay) {
+// (lbm / lb: the workgroup's per-bucket minimum arrival time and busy flags in LDS, flushed once
+// per workgroup -- a leader's block of 4095 overflow records lowered one bucket's bmin and set its
+// count word 4095 times: same-address atomics serialised in L2, ~50 us per k_rebin)
+__device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long long& stay, long long* lbm, uint32_t* lb) {
   if (o.cell < 0) return;
   if (o.cell < g_cur + static_cast<long long>(p.n_buckets)) {
     const uint32_t b = static_cast<uint32_t>(o.cell % p.n_buckets);
@@ -1198,8 +1204,8 @@ __device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long lon
       AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
     }
     AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(p.n_buckets) * p.NT) = 1;
-    bmin_lower(p, b, o.cell * p.L + static_cast<long long>(x.r.t_off));
-    mark_busy(&p.bucket_cnt[b]);
+    atomicMin(&lbm[b], o.cell * p.L + static_cast<long long>(x.r.t_off));
+    lb[b] = 1u;
     o.cell = -1;
   } else {
     stay = o.cell;
@@ -1210,13 +1216,27 @@ __device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long lon
 // The overflow horizon of the records that stay is reduced per workgroup (one atomicMin
 // each): a saturated PBFT leader keeps tens of thousands of PRE_PREPAREs in the list and a
 // same-address atomic per record took 0.3-0.5 ms per launch.
-__global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n) {
+__device__ inline void ctl_publish(const KP& p, long long s0, long long s3, uint32_t seq, const long long* pv = nullptr);
+
+// seq != 0 (host-mapped control mirror): the launch leaves the overflow bound itself -- the last
+// workgroup stores the staying records' minimum as scal[1] (no host reset before the launch),
+// empties the list when nothing stays, and publishes the control block (bucket counts, scal[1])
+// with seq, so that group_cell reads it with one spin instead of copies and a stream sync.
+__global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long long g_cur, uint32_t n, uint32_t seq) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ long long wmin[4];
+  __shared__ long long lbm[kMaxBuckets];
+  __shared__ uint32_t lb[kMaxBuckets];
+  const uint32_t B = p.n_buckets;
+  for (uint32_t q = tidx(); q < B; q += blockDim.x) {
+    lbm[q] = LLONG_MAX;
+    lb[q] = 0;
+  }
+  __syncthreads();
   const uint32_t k = blockIdx.x * blockDim.x + tidx();
   long long stay = LLONG_MAX;
-  if (k < n) rebin_one(p, g_cur, AT(p.ov, k, p.cap_ov), stay);
+  if (k < n) rebin_one(p, g_cur, AT(p.ov, k, p.cap_ov), stay, lbm, lb);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const long long y = __shfl_xor(stay, off, 64);
@@ -1224,11 +1244,40 @@ __global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long l
   }
   if ((tidx() & 63u) == 0) wmin[tidx() >> 6] = stay;
   __syncthreads();
+  for (uint32_t q = tidx(); q < B; q += blockDim.x)
+    if (lb[q]) {
+      bmin_lower(p, q, lbm[q]);
+      mark_busy(&p.bucket_cnt[q]);
+    }
+  if (!seq) {
+    if (tidx() == 0) {
+      long long m = wmin[0];
+      for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) m = wmin[w] < m ? wmin[w] : m;
+      if (m != LLONG_MAX) gmin(&p.scal[1], m);
+    }
+    return;
+  }
+  __shared__ int s_last;
   if (tidx() == 0) {
     long long m = wmin[0];
     for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) m = wmin[w] < m ? wmin[w] : m;
-    if (m != LLONG_MAX) gmin(&p.scal[1], m);
+    if (m != LLONG_MAX) gmin(p.rb_acc, m);
+    __threadfence();
+    s_last = gadd_r(p.rb_done, 1u) == gridDim.x - 1;
   }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (tidx() == 0) {
+    const long long m = __hip_atomic_load(p.rb_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.scal[1] = m;
+    if (m == LLONG_MAX) *p.ov_cnt = 0;  // (everything rebinned: the list starts again)
+    __hip_atomic_store(p.rb_acc, LLONG_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p.rb_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+  }
+  __syncthreads();
+  if (tidx() < 64) ctl_publish(p, p.scal[0], p.scal[3], seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -4258,7 +4307,6 @@ constexpr int kBcastCap = 64;  // due broadcasts per node per cell
 constexpr int kTile = 64;        // receiver tile of the full-mesh tile flags (rtile)
 static_assert(kTile == static_cast<int>(kTR), "k_mesh_tile: one receiver tile per workgroup");
 constexpr int kMaxTiles = 1024;  // 64-node tiles (N <= 65536)
-constexpr int kMaxBuckets = 64;
 
 __device__ inline bool op_key_less(const Op& a, uint32_t sa, const Op& b, uint32_t sb) {
   if (a.t != b.t) return a.t < b.t;
@@ -8795,7 +8843,7 @@ __global__ __launch_bounds__(256) void k_active(const KP* __restrict__ pk, long 
 
 // ---------------------------------------------------------------------------
 // place one received record (the rules of a local emission)
-__device__ inline void import_one(const KP& p, long long g_cur, XRec x, uint32_t* lb, long long& ovmin) {
+__device__ inline void import_one(const KP& p, long long g_cur, XRec x, uint32_t* lb, long long* lbm, long long& ovmin) {
   const uint32_t B = p.n_buckets;
   const uint32_t rep = x.g / p.N;
   if (x.cell < g_cur + static_cast<long long>(B)) {
@@ -8812,7 +8860,7 @@ __device__ inline void import_one(const KP& p, long long g_cur, XRec x, uint32_t
         set_err(p, BCSIM_E_OVERFLOW);
     }
     set_flag_once(&AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(B) * p.NT));
-    bmin_lower(p, b, x.cell * p.L + static_cast<long long>(x.r.t_off));
+    atomicMin(&lbm[b], x.cell * p.L + static_cast<long long>(x.r.t_off));  // (flushed per workgroup)
     atomicAdd(&lb[b], 1u);
   } else {
     const uint32_t pos = gadd_r(p.ov_cnt, 1u);
@@ -8864,9 +8912,13 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
   const KP& p = *pk;
   BAIL_IF_ERR();
   __shared__ uint32_t lb[kMaxBuckets];
+  __shared__ long long lbm[kMaxBuckets];
   __shared__ long long ovmin_s;
   const uint32_t B = p.n_buckets;
-  for (uint32_t k = tidx(); k < B; k += blockDim.x) lb[k] = 0;
+  for (uint32_t k = tidx(); k < B; k += blockDim.x) {
+    lb[k] = 0;
+    lbm[k] = LLONG_MAX;
+  }
   if (tidx() == 0) ovmin_s = LLONG_MAX;
   __syncthreads();
   const uint32_t k = blockIdx.x * blockDim.x + tidx();
@@ -8888,7 +8940,7 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
           y.r.sub = sub0 + j;
           y.slot = s * N1 + (i < s ? i : i - 1);
           y.g = rep * p.N + s;
-          import_one(p, g_cur, y, lb, ovmin);
+          import_one(p, g_cur, y, lb, lbm, ovmin);
         }
       }
     } else {
@@ -8897,13 +8949,16 @@ __global__ __launch_bounds__(256) void k_import(const KP* __restrict__ pk, long 
         if (po) p.fqpeer[edge_loc(p, x.g / p.N, x.slot)] = 49152u + po;
         x.cell = static_cast<long long>(cw & ((1ull << kXPortShift) - 1));
       }
-      import_one(p, g_cur, x, lb, ovmin);
+      import_one(p, g_cur, x, lb, lbm, ovmin);
     }
   }
   if (ovmin != LLONG_MAX) atomicMin(&ovmin_s, ovmin);
   __syncthreads();
   for (uint32_t q = tidx(); q < B; q += blockDim.x)
-    if (lb[q]) mark_busy(&p.bucket_cnt[q]);
+    if (lb[q]) {
+      bmin_lower(p, q, lbm[q]);
+      mark_busy(&p.bucket_cnt[q]);
+    }
   if (tidx() == 0 && ovmin_s != LLONG_MAX) gmin(&p.scal[1], ovmin_s);
 }
 
@@ -9280,7 +9335,7 @@ __global__ __launch_bounds__(256) void k_zero16(uint4* __restrict__ dst, uint64_
 // (scal[0] = words 6-7, scal[3] = words 12-13 of the control block)
 // then the window's sequence number in the word after them, which the host spins on
 // (the prediction's four words follow scal[6]: words 18-25)
-__device__ inline void ctl_publish(const KP& p, long long s0, long long s3, uint32_t seq, const long long* pv = nullptr) {
+__device__ inline void ctl_publish(const KP& p, long long s0, long long s3, uint32_t seq, const long long* pv) {
   if (!p.ctl_mirror) return;
   const uint32_t lane = tidx() & 63u;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(p.err);
@@ -9476,11 +9531,13 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
           s_pv[k] = pv[k];
         }
       }
+      // (the control block first: the host's end-of-window work overlaps the list building, as
+      // it overlapped a k_active launch after k_next)
+      ctl_publish(p, m, mt, seq, pv);
     }
     __syncthreads();
     for (int k = 0; k < 4; ++k) pv[k] = s_pv[k];
     if (pv[0]) next_active(p, pv, act_seq);  // (uniform)
-    if (wv == 0) ctl_publish(p, m, mt, seq, pv);
     return;
   }
   if (wv != 0) return;
