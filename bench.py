@@ -321,6 +321,7 @@ def main():
     c0 = sim.counters()
     cm0 = commit_records(sim, args.workload)
     link_before = sim.kernel_stats()["link"]["launches"]  # k_link launches before the timed region
+    ls0 = sim.loop_stats()
     sim.reset_kernel_stats()
     barrier()
     w0 = time.perf_counter()
@@ -331,6 +332,8 @@ def main():
     dt = time.perf_counter() - w0
     c1 = sim.counters()
     ks = sim.kernel_stats()
+    ls1 = sim.loop_stats()
+    loop = {k: ls1[k] - ls0[k] for k in ls1}
     msgs = c1["delivered_total"] - c0["delivered_total"]
     commits = commit_records(sim, args.workload) - cm0
     dt, msgs, commits = aggregate(dist, f"cuda:{local}", dt, msgs, commits)
@@ -432,6 +435,12 @@ def main():
                          "pipeline": {"kernels": "k_scan + k_link classes", "achieved": pipe_ach,
                                       "frac": pipe_ach / HBM_PEAK_GBS, "us": sl_us,
                                       "records": ks_all["link"]["bytes"] / 48.0}},
+            # the cell loop over the timed steps (rank 0): windows, host syncs (spins, stream syncs,
+            # blocking collectives), windows run as device-chained windows
+            "loop": {"windows_per_step": loop["windows"] / args.steps,
+                     "host_syncs_per_window": loop["host_syncs"] / max(1, loop["windows"]),
+                     "chain_windows": loop["chain_windows"], "spec_hits": loop["spec_hits"],
+                     "idle_parts": loop["idle_parts"], "collectives": loop["collectives"]},
             "kernel_us": {k: v["us"] for k, v in ks.items()},
             "kernel_launches": {k: v["launches"] for k, v in ks.items()},
             # untimed pass of as many steps with every kernel class timed (the timed region

@@ -114,7 +114,7 @@ class Simulator(_abi.Handle):
         out = (C.c_uint64 * 8)()
         self._call("read_loop_stats_ex", self.h, out)
         return dict(windows=out[0], collectives=out[1], tag_zeroes=out[2], spec_hits=out[3], idle_parts=out[4],
-                    host_syncs=out[5], idle_checked=out[6])
+                    host_syncs=out[5], idle_checked=out[6], chain_windows=out[7])
 
     def reset_kernel_stats(self):
         self._call("reset_kernel_stats", self.h)

@@ -37,6 +37,7 @@ struct Ctl {
   int32_t dbg;
   long long scal[6];  // next_local, ov_min_cell, n_alive_ticks, next timer, min shipped cell, (pad)
   long long pred[4];  // k_next's prediction of the next window: valid, cell, lo, hi (engine.hip k_next)
+  long long win[kWinWords];  // device-chained windows (engine.hip k_win): the chain's state after its last k_next
   // followed by bucket_cnt[B] and x_cnt[B]
 };
 
@@ -115,6 +116,11 @@ struct Sim {
   // of k_active's list lengths (measured slower: 0.73 vs 0.53 ms per step)
   bool dev_sized = false;
   uint64_t idle_parts = 0;  // part cells cut by a run limit skipped as idle
+  // device-chained windows (dense gossip, one rank; BCSIM_CHAIN=0: off): k_win decides up to
+  // chain_k windows on the device per host sync
+  bool chain_on = false;
+  uint32_t chain_k = 4;
+  uint64_t chains = 0, chain_windows = 0;
   uint64_t host_syncs = 0;  // times the cell loop waited on the GPU (spins, stream syncs, blocking collectives)
   bool check_idle = false;
   uint64_t idle_checked = 0;  // idle parts verified by check_idle_part  // debug (BCSIM_CHECK_IDLE=1): k_active verifies every skipped idle part is empty
@@ -241,6 +247,7 @@ constexpr size_t kEvBatch = 256;  // timing events read back per batch
 static int ev_collect(Sim& s) {
   if (s.ev_used) HIPCHK(hipStreamSynchronize(s.stream));
   for (size_t k = 0; k < s.ev_used; ++k) {
+    if (s.ev_class[k] < 0) continue;  // (a chained window that did not run)
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, s.ev_pool[k].first, s.ev_pool[k].second));
     s.us[s.ev_class[k]] += 1000.0 * ms;
@@ -982,6 +989,7 @@ static int setup_device(Sim& s) {
   p.ov_cnt = (decltype(p.ov_cnt))(&cd->ov_cnt);
   p.scal = (decltype(p.scal))(cd->scal);
   p.pred = (decltype(p.pred))(cd->pred);
+  p.win = (decltype(p.win))(cd->win);
   if ((rc = dalloc(s, &p.nxt_part, 2 * kNextBlocks)) || (rc = dalloc(s, &p.nxt_done, 1))) return rc;
   HIPCHK(hipMemset(p.nxt_done, 0, 4));
   if ((rc = dalloc(s, &p.rb_acc, 1)) || (rc = dalloc(s, &p.rb_done, 1))) return rc;
@@ -1140,6 +1148,12 @@ static int setup_device(Sim& s) {
                 s.ctl_m != nullptr;
   }
   if (const char* dv = std::getenv("BCSIM_DBG_EVENTS"); dv && *dv) p.dbg_tmax = std::atoll(dv);  // debug event log
+  {
+    const char* ch = std::getenv("BCSIM_CHAIN");
+    s.chain_on = !(ch && *ch == '0') && s.gossip_link && s.gossip_frontier && !s.xp && !s.pdes && !s.sparse &&
+                 s.kp.dbg_tmax == LLONG_MIN && s.dbg_fail_cell < 0 && s.dbg_dev_err < 0 &&
+                 s.dbg_fail_import < 0;
+  }
   std::vector<long long> big_ll(NT, LLONG_MAX);
   HIPCHK(hipMemcpy(p.node_tnext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p.node_onext, big_ll.data(), NT * 8, hipMemcpyHostToDevice));
@@ -2128,6 +2142,88 @@ static long long local_next_cell(const Sim& s, bool with_tick) {
   return c;
 }
 
+// Device-chained windows (dense gossip): up to K windows enqueued at once, each
+// k_win (the next window from the device's control block, or the end of the chain) -> the gossip
+// window kernels with cell = -1 -> k_next (the window's bookkeeping); then ONE host sync on the last
+// k_next's mirror.  The windows k_win did not open run no-op kernels; their timing events and
+// launch counts are dropped.  The caller has checked that the first window needs no host work.
+static int run_chain(Sim& s, long long lim) {
+  const uint32_t K = s.chain_k;
+  const bool timed = (kstat_mask() >> KS_LINK) & 1u;
+  const uint32_t per_wg = 256 / s.gossip_g;
+  const dim3 gg(static_cast<uint32_t>((static_cast<uint64_t>(s.R) * s.nloc + per_wg - 1) / per_wg));
+  const uint32_t na = static_cast<uint32_t>(static_cast<uint64_t>(s.R) * s.nloc);
+  const uint32_t nbn = s.NT <= 4096u ? 1u : static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
+  const size_t lds = scan_lds_bytes(s.kp);
+  const long long stop = s.stop_pending && s.cfg.stop_ns >= 0 ? static_cast<long long>(s.cfg.stop_ns) : -1ll;
+  std::vector<size_t> ev_at(K, SIZE_MAX), ev_nx(K, SIZE_MAX);
+  int rc;
+  for (uint32_t k = 0; k < K; ++k) {
+    if ((rc = launch(s, -1, k_win, dim3(1), dim3(64), 0, s.kp_dev, k == 0 ? 1 : 0, static_cast<long long>(s.t_done),
+                     s.last_full, lim, stop)))
+      return rc;
+    if (timed) {
+      ev_at[k] = s.ev_used;
+      if ((rc = ev_begin(s, KS_LINK))) return rc;
+    }
+    if ((rc = launch(s, -1, k_gossip_active, dim3((na + 1023) / 1024), dim3(1024), 0, s.kp_dev, -1ll, 0ll)) ||
+        (rc = launch(s, -1, k_gossip_cell, gg, dim3(256), 0, s.kp_dev, -1ll, 0ll, 0ll, 0ll, 0, s.gossip_g, 0, 0, 1)) ||
+        (rc = launch(s, -1, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), dim3(s.bs_scan), lds, s.kp_dev, -1ll, 0ll, 0ll,
+                     0ll, 0, 0)) ||
+        ((s.ev_stop_attach = timed && s.ext_events), false) ||
+        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(s.gossip_l3_grid, s.grid_link)),
+                     dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, -1ll, 0ll, 0ll, 0)))
+      return rc;
+    if (timed) {
+      if ((rc = ev_end(s))) return rc;
+    } else {
+      s.launches[KS_LINK]++;
+    }
+    s.next_seq = ++s.mseq;
+    ev_nx[k] = s.ev_used;
+    if ((rc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, kClrWin, s.next_seq, PredArgs{}, 0u))) return rc;
+    if (s.ev_used == ev_nx[k]) ev_nx[k] = SIZE_MAX;  // (k_next untimed)
+  }
+  // the one sync: the last k_next's control block (readback without applying yet: the timing
+  // events of the windows that did not run are dropped first)
+  const size_t nb = sizeof(Ctl) + 8ull * s.B + 4ull * kMaxRanks;
+  const int w = s.ctl_m ? mirror_wait(s, reinterpret_cast<uint32_t*>(s.ctl_m) + nb / 4, s.next_seq) : 1;
+  if (w < 0) return w;
+  if (w == 0) {
+    std::memcpy(s.ctl_h, s.ctl_m, nb);
+  } else {
+    HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, nb, hipMemcpyDeviceToHost, s.stream));
+    if (!s.ctl_m) ++s.host_syncs;
+    HIPCHK(hipStreamSynchronize(s.stream));
+  }
+  const long long* wv = s.ctl_h->win;
+  const uint32_t done = static_cast<uint32_t>(std::min<long long>(wv[kWinCount], K));
+  for (uint32_t k = done; k < K; ++k) {
+    if (timed && ev_at[k] < s.ev_used) s.ev_class[ev_at[k]] = -1;
+    if (ev_nx[k] < s.ev_used) s.ev_class[ev_nx[k]] = -1;
+    s.launches[KS_LINK]--;
+    s.launches[KS_AUX]--;
+  }
+  if ((rc = readback_apply(s))) return rc;
+  if (done) {
+    s.t_done = wv[kWinTDone];
+    s.last_full = wv[kWinLastFull];
+    s.grouped_cell = wv[kWinGrouped];
+    s.cells += done;
+    s.x_active = 0;
+    s.start_pending = false;
+  }
+  s.chain_windows += done;
+  ++s.chains;
+  // (the next chain: twice as long after a full one, just longer than this one otherwise)
+  s.chain_k = done == K ? std::min<uint32_t>(2 * K, 32) : std::max<uint32_t>(2, done + 1);
+  if (!done) {
+    g_detail = "device window chain made no progress (k_win end reason " + std::to_string(wv[kWinDead]) + ")";
+    return BCSIM_E_STATE;
+  }
+  return BCSIM_OK;
+}
+
 // Debug (BCSIM_CHECK_IDLE=1): the part [lo, hi) of cell `cell` that run() skips as
 // idle (the tick's leading part, or a part cut by the run limit) must hold no node with work:
 // k_active -- the rule every window uses -- runs for it and the run fails if either list is not
@@ -2253,6 +2349,18 @@ static int run(Sim& s, int64_t t_until) {
         }
       }
       break;
+    }
+    if (s.chain_on && s.cells > 0 && !s.start_pending && s.grouped_cell < 0 && s.xcnt[c % s.B] == 0 &&
+        !(s.ov_min <= c + static_cast<long long>(s.B) - 1) && !(lo <= 0 && 0 < hi) &&
+        !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi)) {
+      // no host work before this window (group_cell, START / STOP) and no ring-tag zeroing due in
+      // [last_full + 1, c]: a device chain from here
+      const long long t0 = (s.last_full + 1) / s.B;
+      const long long z = (t0 % 32 == 31) ? s.last_full + 1 : ((t0 / 32) * 32 + 31) * static_cast<long long>(s.B);
+      if (c < z) {
+        if ((rc = run_chain(s, lim))) return rc;
+        continue;
+      }
     }
     int lrc = carried;  // this rank's status of the cell
     if (!lrc && s.grouped_cell != c) {
@@ -2733,7 +2841,7 @@ int bcsim_read_loop_stats_ex(bcsim_sim* h, uint64_t* out8) {
   out8[4] = s.idle_parts;
   out8[5] = s.host_syncs;
   out8[6] = s.idle_checked;
-  out8[7] = 0;
+  out8[7] = s.chain_windows;
   return BCSIM_OK;
 }
 

@@ -285,6 +285,7 @@ struct KP {
   GP(long long) node_tnext;
   GP(long long) node_onext;
   GP(long long) pred;  // k_next's prediction of the next window {valid, cell, lo, hi} (control block)
+  GP(long long) win;   // device-chained windows (k_win): kWin* words (control block)
   GP(long long) scal;  // [0] next_local, [1] ov_min_cell, [2] n_alive_ticks, [3] next timer,
                     // [4] earliest arrival cell shipped to another rank (node-partitioned)
   GP(long long) nxt_part;  // [kNextBlocks] k_next per-workgroup minima
@@ -2917,12 +2918,32 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
 // LOOP: a small grid walks list 2, the nodes k_gossip_scan / k_paxos_scan left over
 // (Raft / Paxos / gossip: at most 256 lanes, so that lane 0's protocol state machine -- Ctx and
 // the node state, live across the event loop -- has the registers it needs instead of scratch)
+// Device-chained windows (dense gossip): k_win decides each window on the device
+// and the window's kernels, launched with cell = -1, take it from the control block's win words
+// (or do nothing when k_win found none: the chain ended, the host takes over).
+enum : int { kWinValid = 0, kWinCell, kWinLo, kWinHi, kWinFw, kWinLoop, kWinTDone, kWinLastFull, kWinGrouped,
+             kWinCount, kWinDead, kWinLim, kWinWords = 12 };
+__device__ inline bool win_take(const KP& p, long long& cell, long long& lo, long long& hi, int& fw) {
+  if (cell >= 0) return true;
+  if (!p.win[kWinValid]) return false;
+  cell = p.win[kWinCell];
+  lo = p.win[kWinLo];
+  hi = p.win[kWinHi];
+  fw = static_cast<int>(p.win[kWinFw]);
+  return true;
+}
+
 template <int PROTO, bool SP, bool LOOP = false>
 __global__ __launch_bounds__(PROTO == BCSIM_PBFT ? 1024 : 256) void k_scan(const KP* pk, long long cell, long long t_lo,
                                                long long t_hi, long long cs, int final_win, int x_active) {
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (LOOP) {
+    if (cell < 0) {  // (a chained window: only when the window needs the generic scan)
+      if (!win_take(p, cell, t_lo, t_hi, final_win) || !p.win[kWinLoop]) return;
+      cs = cell * p.L;
+      x_active = 0;
+    }
     for (ListRange lr = list_range(p.act_n[2]); lr.k < lr.end; lr.k += lr.step) {
       scan_node<PROTO, SP>(pk, p.act[2ull * p.NT + lr.k], cell, t_lo, t_hi, cs, final_win, x_active);
       __syncthreads();
@@ -5811,6 +5832,7 @@ __global__ __launch_bounds__(QM != 0 ? 256 : (LOOP ? kLinkLoopThreads : 1024)) v
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (LOOP) {
+    if (!win_take(p, cell, t_lo, t_hi, final_win)) return;  // (a chained window, or none)
     const uint32_t ll = p.loop_list;
     for (ListRange lr = list_range(p.act_n[ll]); lr.k < lr.end; lr.k += lr.step) {
       const uint32_t g = p.act[static_cast<size_t>(ll) * p.NT + lr.k];
@@ -8103,6 +8125,13 @@ __global__ __launch_bounds__(256) void k_gossip_cell(const KP* __restrict__ pk, 
                                                      int final_win, int fl) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  if (cell < 0) {  // (a chained window, or none)
+    if (!win_take(p, cell, t_lo, t_hi, final_win)) return;
+    cs = cell * p.L;
+    x_active = 0;
+    loop = static_cast<int>(p.win[kWinLoop]);
+    fl = 1;
+  }
   if (fl && blockIdx.x * (blockDim.x / G) >= p.act_n[0]) return;
   const bool left = gossip_scan_body(pk, cell, t_lo, t_hi, cs, x_active, G, loop, fl != 0);
   __syncthreads();  // (the node's new ops, n_ops and node_onext: written by one lane of its group)
@@ -8116,6 +8145,11 @@ __global__ __launch_bounds__(256) void k_gossip_cell(const KP* __restrict__ pk, 
 __global__ __launch_bounds__(1024) void k_gossip_active(const KP* __restrict__ pk, long long cell, long long t_hi) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  if (cell < 0) {  // (a chained window, or none)
+    if (!p.win[kWinValid]) return;
+    cell = p.win[kWinCell];
+    t_hi = p.win[kWinHi];
+  }
   __shared__ uint32_t wcnt[kMaxWaves], s_base;
   const uint32_t na = p.R * p.nloc, lane = tidx() & 63u, wv = tidx() >> 6;
   const uint32_t k = blockIdx.x * blockDim.x + tidx();
@@ -9359,18 +9393,27 @@ struct PredArgs {
   long long t_done, lim, tick, ch, stop_ns;
   int on;
 };
+// the earliest cell held by a busy bucket, seen from cell cdone (local_next_cell's bucket term) --
+// one bucket per lane and a wave minimum (B <= 64; the whole wave calls it): a serial loop over the
+// buckets was one dependent load round trip each
+__device__ inline long long bucket_min_cell(const KP& p, long long cdone) {
+  const uint32_t B = p.n_buckets, lane = tidx() & 63u;
+  long long cb = LLONG_MAX;
+  if (lane < B && p.bucket_cnt[lane])
+    cb = cdone + ((static_cast<long long>(lane) - cdone % B) % B + B) % B;
+  for (int d = 32; d > 0; d >>= 1) {
+    const long long y = __shfl_xor(cb, d, 64);
+    cb = y < cb ? y : cb;
+  }
+  return cb;
+}
 __device__ inline void predict_window(const KP& p, const PredArgs& a, long long next_local, long long* pv) {
   pv[0] = 0;
   pv[1] = pv[2] = pv[3] = 0;
   if (!a.on) return;
   const uint32_t B = p.n_buckets;
   const long long L = p.L, cdone = a.t_done / L;
-  long long c = a.ch;
-  for (uint32_t b = 0; b < B; ++b)
-    if (p.bucket_cnt[b]) {
-      const long long cb = cdone + ((static_cast<long long>(b) - cdone % B) % B + B) % B;
-      c = cb < c ? cb : c;
-    }
+  long long c = min(a.ch, bucket_min_cell(p, cdone));
   if (next_local != LLONG_MAX) {
     const long long x = (next_local > a.t_done ? next_local : a.t_done) / L;
     c = x < c ? x : c;
@@ -9455,12 +9498,100 @@ __device__ inline void next_active(const KP& p, const long long* pv, uint32_t ac
   }
 }
 
+// A chained window is over (k_next's publishing lane, before the control block goes out): the
+// host's end-of-window bookkeeping (run(): t_done, last_full, grouped_cell, cells) on the device.
+constexpr uint32_t kClrWin = 0xFFFFFFFEu;  // k_next's clr_b for a chained window: from the win words
+__device__ inline void win_advance(const KP& p) {
+  if (!p.win[kWinValid]) return;
+  const long long c = p.win[kWinCell];
+  p.win[kWinTDone] = p.win[kWinHi];
+  p.win[kWinCount] += 1;
+  if (p.win[kWinFw]) {
+    p.win[kWinLastFull] = c;
+    p.win[kWinGrouped] = -1;
+  } else {
+    p.win[kWinGrouped] = c;  // (a part cell, cut by the run limit)
+  }
+  p.win[kWinValid] = 0;
+  __threadfence();
+}
+
+// k_win (one lane): the next window of a device chain -- run()'s rule (local_next_cell and the cell
+// bounds) on the control block as k_next left it -- or the end of the chain when the window needs
+// the host: START / STOP, extras to group, overflow to rebin, a bucket due for the ring-tag
+// zeroing, a pending part cell, the run limit, a device error.  init: the chain's first window
+// (the host's t_done / last_full); stop_ns: the pending STOP time or -1.
+__global__ __launch_bounds__(64) void k_win(const KP* __restrict__ pk, int init, long long t_done, long long last_full,
+                                            long long lim, long long stop_ns) {
+  const KP& p = *pk;
+  long long* const w = p.win;
+  const long long bc = bucket_min_cell(p, (init ? t_done : w[kWinTDone]) / p.L);  // (all 64 lanes)
+  if (tidx() != 0) return;
+  if (init) {
+    w[kWinTDone] = t_done;
+    w[kWinLastFull] = last_full;
+    w[kWinGrouped] = -1;
+    w[kWinCount] = 0;
+    w[kWinDead] = 0;
+    w[kWinLim] = lim;
+  }
+  w[kWinValid] = 0;
+  if (w[kWinDead]) return;
+  const long long B = p.n_buckets, L = p.L, td = w[kWinTDone], lf = w[kWinLastFull];
+  int dead = 0;
+  long long c = LLONG_MAX, lo = 0, hi = 0, ce = 0;
+  const long long ov = p.scal[1];
+  if (*p.err) {
+    dead = 1;
+  } else if (w[kWinGrouped] >= 0) {
+    dead = 2;
+  } else {
+    c = bc;
+    const long long nl = p.scal[0];
+    if (nl != LLONG_MAX) c = min(c, (nl > td ? nl : td) / L);
+    if (ov != LLONG_MAX) c = min(c, ov);
+    if (stop_ns >= 0 && stop_ns >= td) c = min(c, stop_ns / L);
+    if (c == LLONG_MAX || c * L >= lim) {
+      dead = 3;
+    } else {
+      const long long cs = c * L;
+      ce = cs + L;
+      lo = cs > td ? cs : td;
+      hi = ce < lim ? ce : lim;
+      // the first cell after last_full that ends a 32-turn ring period (zero_tag_buckets)
+      const long long t0 = (lf + 1) / B;
+      const long long z = (t0 % 32 == 31) ? lf + 1 : ((t0 / 32) * 32 + 31) * B;
+      if (lo >= hi) dead = 4;
+      else if (p.x_cnt[c % B]) dead = 5;
+      else if (ov != LLONG_MAX && ov <= c + B - 1) dead = 6;
+      else if (lo <= 0 && 0 < hi) dead = 7;
+      else if (stop_ns >= 0 && lo <= stop_ns && stop_ns < hi) dead = 8;
+      else if (c >= z) dead = 9;
+    }
+  }
+  if (dead) {
+    w[kWinDead] = dead;
+    return;
+  }
+  w[kWinCell] = c;
+  w[kWinLo] = lo;
+  w[kWinHi] = hi;
+  w[kWinFw] = hi == ce ? 1 : 0;
+  w[kWinLoop] = p.scal[3] < hi ? 1 : 0;  // (a timer due: the generic scan too, as run() decides)
+  __threadfence();
+  w[kWinValid] = 1;
+}
+
 // act_seq != 0 (one workgroup, speculation on): the predicted window's active lists too
-// (next_active), published before the control block
+// (next_active), published before the control block.  clr_b == kClrWin: a chained window's
+// (its finished bucket from the win words; its bookkeeping by the publishing lane)
 __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32_t clr_b, uint32_t seq, PredArgs pa,
                                                uint32_t act_seq) {
   const KP& p = *pk;
   BAIL_IF_ERR();
+  const bool chained = clr_b == kClrWin;
+  if (chained)
+    clr_b = p.win[kWinValid] && p.win[kWinFw] ? static_cast<uint32_t>(p.win[kWinCell] % p.n_buckets) : 0xFFFFFFFFu;
   if (blockIdx.x == 0) {
     if (tidx() < 4) p.act_n[tidx()] = 0;
     if (clr_b < p.n_buckets) {
@@ -9554,6 +9685,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
       p.scal[0] = m;
       p.scal[3] = mt;
       for (int k = 0; k < 4; ++k) p.pred[k] = pv[k];
+      if (chained) win_advance(p);
     }
     ctl_publish(p, m, mt, seq, pv);
     return;
@@ -9581,6 +9713,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     p.scal[3] = mmt;
     p.pred[0] = 0;  // (no prediction with several workgroups)
     __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (chained) win_advance(p);
   }
   ctl_publish(p, mm, mmt, seq);
 }

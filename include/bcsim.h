@@ -322,7 +322,8 @@ int bcsim_read_loop_stats(bcsim_sim* s, uint64_t* out4);
  * bcsim_read_loop_stats, [3] windows whose active lists came from the speculative k_active
  * behind k_next, [4] part cells skipped as idle (nothing can happen before the tick / run
  * limit), [5] host syncs of the cell loop (mirror spins, stream syncs, blocking collectives),
- * [6] idle parts verified empty (BCSIM_CHECK_IDLE=1), [7] 0. */
+ * [6] idle parts verified empty (BCSIM_CHECK_IDLE=1), [7] windows run as device-chained windows
+ * (k_win, dense gossip). */
 int bcsim_read_loop_stats_ex(bcsim_sim* s, uint64_t* out8);
 
 #ifdef __cplusplus

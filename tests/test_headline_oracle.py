@@ -51,10 +51,19 @@ def test_c4_pbft4096_bench_steps_match_oracle(env, oracle_cache, engine_lib):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("env", [{"BCSIM_CHECK_IDLE": "1"}, {"BCSIM_SPEC": "0"}], ids=["spec_on", "spec_off"])
+@pytest.mark.parametrize("env", [{"BCSIM_CHECK_IDLE": "1"}, {"BCSIM_SPEC": "0", "BCSIM_CHAIN": "0"}],
+                         ids=["spec_chain_on", "spec_chain_off"])
 def test_small_cases_in_bench_steps_match_oracle(env, engine_lib):
-    outs = _child(["cases", "pbft16_fixed_100", "pbft512_small", "pbft100_fixed", "pbft8_rep3_ctr"], env, 560)
+    """PBFT (speculative k_active, idle parts) and gossip (device-chained windows, DESIGN.md §4.2b:
+    k_win decides the windows on the device, the run limit ends a chain mid-cell) in 50 ms steps."""
+    outs = _child(["cases", "pbft16_fixed_100", "pbft512_small", "pbft100_fixed", "pbft8_rep3_ctr",
+                   "gossip64_d4_fixed", "gossip512_d8_blocks", "gossip200_d8_jitter_ctr"], env, 560)
     assert all(o["diff"] is None for o in outs), outs
+    gossip = [o for o in outs if o["case"].startswith("gossip") and "jitter" not in o["case"]]
     if env.get("BCSIM_CHECK_IDLE") == "1":
         assert sum(o["spec_hits"] for o in outs) > 0, outs
         assert all(o["idle_checked"] == o["idle_parts"] for o in outs), outs
+        assert all(o["chain_windows"] > o["windows"] // 2 for o in gossip), gossip
+        assert all(o["host_syncs"] < o["windows"] for o in gossip), gossip
+    else:
+        assert all(o["chain_windows"] == 0 for o in outs), outs

@@ -28,8 +28,9 @@ SWITCHES = [
     {"BCSIM_SUM": "0", "BCSIM_FEW_SCAN": "0"},        # no record summaries (k_mesh_tile, k_scan_pbft)
     {"BCSIM_NO_DESC": "1"},         # no reply / echo descriptors
     {"BCSIM_SPEC": "0"},            # no speculative k_active behind k_next
-    {"BCSIM_FUSE_ACT": "0"},        # the speculative lists by a k_active launch, not by k_next
     {"BCSIM_L2_OVERLAP": "1"},      # list 2 on the second stream in every window (default: few-node scans)
+    {"BCSIM_CHAIN": "0"},           # no device-chained gossip windows (one host sync per window)
+    {"BCSIM_FUSE_ACT": "1"},        # k_next builds the speculative lists (opt-in)
 ]
 
 
