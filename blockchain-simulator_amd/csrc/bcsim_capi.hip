@@ -166,6 +166,7 @@ struct Sim {
   bool next_known = false;     // last cell's control exchange (no separate all-reduce needed)
   uint64_t ctl_collectives = 0;  // collectives + host syncs of the cell loop (engine counters)
   uint64_t last_import = 0;      // records k_import placed at the last exchange
+  int carry_err = 0;             // device control words: a failure found after k_ctl sent "fine"
   std::vector<int64_t> lead_w; // leader flags packed for the all-reduce
 };
 
@@ -1910,16 +1911,20 @@ static int exchange(Sim& s, long long cell, int lrc, bool tick) {
     HIPCHK(hipMemcpyAsync(s.ctl_h, s.ctl_d, nb, hipMemcpyDeviceToHost, s.stream));
     ++s.host_syncs;
     HIPCHK(hipStreamSynchronize(s.stream));
-    const int arc = readback_apply(s);
-    if (!lrc) lrc = arc;
-    for (uint32_t r = 0; r < P && !lrc; ++r)
+    if (lrc) return lrc;  // (k_ctl sent kPeerErr: every peer leaves at this exchange)
+    // a failure found only now, after k_ctl told the peers this rank is fine: the
+    // peers go on into the record exchange, so this rank joins it too (sizes clamped to its
+    // buffer) and the failure rides the next cell's control words (run(): lerr)
+    int arc = readback_apply(s);
+    for (uint32_t r = 0; r < P && !arc; ++r)
       if (s.scnt_h[r] > s.kp.cap_send) {
         g_detail = "multi-GPU send list overflowed";
-        lrc = BCSIM_E_OVERFLOW;
+        arc = BCSIM_E_OVERFLOW;
       }
-    for (uint32_t r = 0; r < P; ++r) sb[r] = static_cast<uint64_t>(s.ctlw_h[r * W]);
+    s.carry_err = arc;
+    const uint64_t cap_b = static_cast<uint64_t>(s.kp.cap_send) * sizeof(XRec);
+    for (uint32_t r = 0; r < P; ++r) sb[r] = std::min<uint64_t>(static_cast<uint64_t>(s.ctlw_h[r * W]), cap_b);
     std::memcpy(rcv.data(), s.ctlw_h + static_cast<size_t>(P) * W, static_cast<size_t>(P) * W * 8);
-    if (lrc) return lrc;
   } else {
   for (uint32_t r = 0; r < P && !lrc; ++r)
     if (s.scnt_h[r] > s.kp.cap_send) {
@@ -2142,11 +2147,12 @@ static long long local_next_cell(const Sim& s, bool with_tick) {
   return c;
 }
 
-// Device-chained windows (dense gossip): up to K windows enqueued at once, each
-// k_win (the next window from the device's control block, or the end of the chain) -> the gossip
-// window kernels with cell = -1 -> k_next (the window's bookkeeping); then ONE host sync on the last
-// k_next's mirror.  The windows k_win did not open run no-op kernels; their timing events and
-// launch counts are dropped.  The caller has checked that the first window needs no host work.
+// Device-chained windows (dense gossip): up to K windows enqueued at once --
+// k_win opens the first from the host's state, each window's kernels run with cell = -1 (the window
+// from the control block's win words), and its k_next closes it and decides the next (or ends the
+// chain) -- then ONE host sync on the last k_next's mirror.  The windows that were never opened run
+// no-op kernels; their timing events and launch counts are dropped.  The caller has checked that the
+// first window needs no host work.
 static int run_chain(Sim& s, long long lim) {
   const uint32_t K = s.chain_k;
   const bool timed = (kstat_mask() >> KS_LINK) & 1u;
@@ -2159,8 +2165,9 @@ static int run_chain(Sim& s, long long lim) {
   std::vector<size_t> ev_at(K, SIZE_MAX), ev_nx(K, SIZE_MAX);
   int rc;
   for (uint32_t k = 0; k < K; ++k) {
-    if ((rc = launch(s, -1, k_win, dim3(1), dim3(64), 0, s.kp_dev, k == 0 ? 1 : 0, static_cast<long long>(s.t_done),
-                     s.last_full, lim, stop)))
+    // (the first window from the host's state; each later one decided by the k_next before it)
+    if (k == 0 && (rc = launch(s, -1, k_win, dim3(1), dim3(64), 0, s.kp_dev, static_cast<long long>(s.t_done), s.last_full,
+                               lim, stop)))
       return rc;
     if (timed) {
       ev_at[k] = s.ev_used;
@@ -2476,6 +2483,10 @@ static int run(Sim& s, int64_t t_until) {
       // the bucket counts after k_import (a failure here rides the next cell's exchange); with
       // nothing imported the end-of-cell read-back before the exchange is still current
       lerr = s.last_import ? readback(s) : 0;
+      if (s.carry_err) {  // (the device-word exchange's late failure)
+        lerr = s.carry_err;
+        s.carry_err = 0;
+      }
       if (!lerr && s.dbg_fail_import >= 0 && static_cast<long long>(s.cells) > s.dbg_fail_import) {
         g_detail = "injected failure after the exchange (BCSIM_DBG_FAIL_IMPORT)";  // test hook
         lerr = BCSIM_E_OVERFLOW;

@@ -2922,7 +2922,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
 // and the window's kernels, launched with cell = -1, take it from the control block's win words
 // (or do nothing when k_win found none: the chain ended, the host takes over).
 enum : int { kWinValid = 0, kWinCell, kWinLo, kWinHi, kWinFw, kWinLoop, kWinTDone, kWinLastFull, kWinGrouped,
-             kWinCount, kWinDead, kWinLim, kWinWords = 12 };
+             kWinCount, kWinDead, kWinLim, kWinStop, kWinWords = 16 };
 __device__ inline bool win_take(const KP& p, long long& cell, long long& lo, long long& hi, int& fw) {
   if (cell >= 0) return true;
   if (!p.win[kWinValid]) return false;
@@ -9516,28 +9516,18 @@ __device__ inline void win_advance(const KP& p) {
   __threadfence();
 }
 
-// k_win (one lane): the next window of a device chain -- run()'s rule (local_next_cell and the cell
-// bounds) on the control block as k_next left it -- or the end of the chain when the window needs
-// the host: START / STOP, extras to group, overflow to rebin, a bucket due for the ring-tag
-// zeroing, a pending part cell, the run limit, a device error.  init: the chain's first window
-// (the host's t_done / last_full); stop_ns: the pending STOP time or -1.
-__global__ __launch_bounds__(64) void k_win(const KP* __restrict__ pk, int init, long long t_done, long long last_full,
-                                            long long lim, long long stop_ns) {
-  const KP& p = *pk;
+// The next window of a device chain -- run()'s rule (local_next_cell and the cell bounds) on the
+// control block as k_next left it -- or the end of the chain when the window needs the host:
+// START / STOP, extras to group, overflow to rebin, a bucket due for the ring-tag zeroing, a
+// pending part cell, the run limit, a device error.  Called by a whole wave (the bucket term is one
+// bucket per lane); lane 0 writes the win words.
+__device__ inline void win_decide(const KP& p) {
   long long* const w = p.win;
-  const long long bc = bucket_min_cell(p, (init ? t_done : w[kWinTDone]) / p.L);  // (all 64 lanes)
-  if (tidx() != 0) return;
-  if (init) {
-    w[kWinTDone] = t_done;
-    w[kWinLastFull] = last_full;
-    w[kWinGrouped] = -1;
-    w[kWinCount] = 0;
-    w[kWinDead] = 0;
-    w[kWinLim] = lim;
-  }
-  w[kWinValid] = 0;
-  if (w[kWinDead]) return;
-  const long long B = p.n_buckets, L = p.L, td = w[kWinTDone], lf = w[kWinLastFull];
+  const bool dead0 = w[kWinDead] != 0;
+  const long long td = w[kWinTDone];
+  const long long bc = bucket_min_cell(p, td / p.L);  // (uniform: every lane)
+  if ((tidx() & 63u) != 0 || dead0) return;
+  const long long B = p.n_buckets, L = p.L, lf = w[kWinLastFull], lim = w[kWinLim], stop_ns = w[kWinStop];
   int dead = 0;
   long long c = LLONG_MAX, lo = 0, hi = 0, ce = 0;
   const long long ov = p.scal[1];
@@ -9571,6 +9561,8 @@ __global__ __launch_bounds__(64) void k_win(const KP* __restrict__ pk, int init,
   }
   if (dead) {
     w[kWinDead] = dead;
+    w[kWinValid] = 0;
+    __threadfence();
     return;
   }
   w[kWinCell] = c;
@@ -9580,6 +9572,29 @@ __global__ __launch_bounds__(64) void k_win(const KP* __restrict__ pk, int init,
   w[kWinLoop] = p.scal[3] < hi ? 1 : 0;  // (a timer due: the generic scan too, as run() decides)
   __threadfence();
   w[kWinValid] = 1;
+  __threadfence();
+}
+
+// k_win (one wave): a device chain's first window from the host's state (t_done, last_full, the
+// run limit, the pending STOP time or -1); every later window is decided by the k_next that ends
+// the one before it (k_next: win_advance, then win_decide).
+__global__ __launch_bounds__(64) void k_win(const KP* __restrict__ pk, long long t_done, long long last_full, long long lim,
+                                            long long stop_ns) {
+  const KP& p = *pk;
+  long long* const w = p.win;
+  if (tidx() == 0) {
+    w[kWinTDone] = t_done;
+    w[kWinLastFull] = last_full;
+    w[kWinGrouped] = -1;
+    w[kWinCount] = 0;
+    w[kWinDead] = 0;
+    w[kWinLim] = lim;
+    w[kWinStop] = stop_ns;
+    w[kWinValid] = 0;
+    __threadfence();
+  }
+  __builtin_amdgcn_wave_barrier();
+  win_decide(p);
 }
 
 // act_seq != 0 (one workgroup, speculation on): the predicted window's active lists too
@@ -9687,6 +9702,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
       for (int k = 0; k < 4; ++k) p.pred[k] = pv[k];
       if (chained) win_advance(p);
     }
+    if (chained) win_decide(p);  // (the whole wave: the chain's next window)
     ctl_publish(p, m, mt, seq, pv);
     return;
   }
@@ -9715,6 +9731,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (chained) win_advance(p);
   }
+  if (chained) win_decide(p);  // (the whole wave: the chain's next window)
   ctl_publish(p, mm, mmt, seq);
 }
 
