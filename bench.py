@@ -322,6 +322,7 @@ def main():
     cm0 = commit_records(sim, args.workload)
     link_before = sim.kernel_stats()["link"]["launches"]  # k_link launches before the timed region
     ls0 = sim.loop_stats()
+    hs0 = sim.host_stats()
     sim.reset_kernel_stats()
     barrier()
     w0 = time.perf_counter()
@@ -334,6 +335,8 @@ def main():
     ks = sim.kernel_stats()
     ls1 = sim.loop_stats()
     loop = {k: ls1[k] - ls0[k] for k in ls1}
+    hs1 = sim.host_stats()
+    host = {k: hs1[k] - hs0[k] for k in hs1}
     msgs = c1["delivered_total"] - c0["delivered_total"]
     commits = commit_records(sim, args.workload) - cm0
     dt, msgs, commits = aggregate(dist, f"cuda:{local}", dt, msgs, commits)
@@ -440,7 +443,11 @@ def main():
             "loop": {"windows_per_step": loop["windows"] / args.steps,
                      "host_syncs_per_window": loop["host_syncs"] / max(1, loop["windows"]),
                      "chain_windows": loop["chain_windows"], "spec_hits": loop["spec_hits"],
-                     "idle_parts": loop["idle_parts"], "collectives": loop["collectives"]},
+                     "idle_parts": loop["idle_parts"], "collectives": loop["collectives"],
+                     # host time per step inside kernel launches / waiting on the mirror words
+                     "host_launch_us_per_step": host["launch_us"] / args.steps,
+                     "host_wait_us_per_step": host["wait_us"] / args.steps,
+                     "launches_per_step": host["launches"] / args.steps},
             "kernel_us": {k: v["us"] for k, v in ks.items()},
             "kernel_launches": {k: v["launches"] for k, v in ks.items()},
             # untimed pass of as many steps with every kernel class timed (the timed region

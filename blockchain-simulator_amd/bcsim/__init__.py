@@ -116,6 +116,12 @@ class Simulator(_abi.Handle):
         return dict(windows=out[0], collectives=out[1], tag_zeroes=out[2], spec_hits=out[3], idle_parts=out[4],
                     host_syncs=out[5], idle_checked=out[6], chain_windows=out[7])
 
+    def host_stats(self):
+        """Host time of the cell loop (include/bcsim.h bcsim_read_host_stats)."""
+        out = (C.c_double * 4)()
+        self._call("read_host_stats", self.h, out)
+        return dict(launch_us=out[0], wait_us=out[1], launches=int(out[2]))
+
     def reset_kernel_stats(self):
         self._call("reset_kernel_stats", self.h)
 

@@ -122,6 +122,8 @@ struct Sim {
   uint32_t chain_k = 4;
   uint64_t chains = 0, chain_windows = 0;
   uint64_t host_syncs = 0;  // times the cell loop waited on the GPU (spins, stream syncs, blocking collectives)
+  double host_launch_us = 0, host_wait_us = 0;  // host time inside kernel launches / mirror waits
+  uint64_t host_launches = 0;
   bool check_idle = false;
   uint64_t idle_checked = 0;  // idle parts verified by check_idle_part  // debug (BCSIM_CHECK_IDLE=1): k_active verifies every skipped idle part is empty
   uint32_t gossip_l3_grid = 256;  // dense gossip: workgroups of the looped list-3 link grid (BCSIM_GL3; x8)
@@ -1224,6 +1226,15 @@ static uint32_t kstat_mask() {
 template <typename K, typename... Args>
 static int launch_named(Sim& s, const char* name, int cls, K kernel, dim3 grid, dim3 block, size_t lds,
                         Args... args) {
+  const auto h0 = std::chrono::steady_clock::now();
+  struct HostClock {  // (host time spent launching: bcsim_read_host_stats)
+    Sim& s;
+    std::chrono::steady_clock::time_point t0;
+    ~HostClock() {
+      s.host_launch_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      ++s.host_launches;
+    }
+  } hclock{s, h0};
   const bool timed = cls >= 0 && ((kstat_mask() >> cls) & 1u);
   int rc = timed ? ev_begin(s, cls) : BCSIM_OK;
   if (rc) return rc;
@@ -1811,6 +1822,11 @@ static int group_cell(Sim& s, long long cell) {
 constexpr int kSpinUs = 500;  // mirror_wait: spin at most this long, then a stream sync
 static int mirror_wait(Sim& s, const uint32_t* w, uint32_t seq) {
   ++s.host_syncs;
+  struct HostClock {  // (host time spent waiting: bcsim_read_host_stats)
+    Sim& s;
+    std::chrono::steady_clock::time_point t0;
+    ~HostClock() { s.host_wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); }
+  } hclock{s, std::chrono::steady_clock::now()};
   static const bool spin = [] {
     const char* e = std::getenv("BCSIM_SPIN");
     return !(e && *e == '0');
@@ -2153,21 +2169,44 @@ static long long local_next_cell(const Sim& s, bool with_tick) {
 // chain) -- then ONE host sync on the last k_next's mirror.  The windows that were never opened run
 // no-op kernels; their timing events and launch counts are dropped.  The caller has checked that the
 // first window needs no host work.
-static int run_chain(Sim& s, long long lim) {
-  const uint32_t K = s.chain_k;
+static int run_chain(Sim& s, long long c, long long lim) {
+  // at most one window per cell up to the first cell the host knows the chain must stop before: the
+  // run limit, the next timer (its window is the host's), an overflow rebin, extras to group, the
+  // ring-tag zeroing -- a window that is never opened still costs its dispatches
+  const long long L = s.L, B = s.B;
+  long long cend = (lim - 1) / L;
+  // the window of the next timer (the origin's block tick) gets the generic scan at its chain
+  // position -- one window per cell from c; a second timer ends the chain (k_win / k_next)
+  unsigned long long loop_mask = 0;
+  if (s.next_timer != LLONG_MAX && s.next_timer >= 0) {
+    const long long j = s.next_timer / L - c;
+    if (j >= 0 && j < 32) loop_mask = 1ull << j;
+    else cend = std::min(cend, s.next_timer / L - 1);
+  }
+  if (s.ov_min != LLONG_MAX) cend = std::min(cend, s.ov_min - B);
+  {
+    const long long t0 = (s.last_full + 1) / B;
+    const long long z = (t0 % 32 == 31) ? s.last_full + 1 : ((t0 / 32) * 32 + 31) * B;
+    cend = std::min(cend, z - 1);
+  }
+  for (long long x = c + 1; x <= cend && x < c + B; ++x)
+    if (s.xcnt[x % B]) {
+      cend = x - 1;
+      break;
+    }
+  const uint32_t K = static_cast<uint32_t>(std::max<long long>(1, std::min<long long>(s.chain_k, cend - c + 1)));
   const bool timed = (kstat_mask() >> KS_LINK) & 1u;
   const uint32_t per_wg = 256 / s.gossip_g;
   const dim3 gg(static_cast<uint32_t>((static_cast<uint64_t>(s.R) * s.nloc + per_wg - 1) / per_wg));
   const uint32_t na = static_cast<uint32_t>(static_cast<uint64_t>(s.R) * s.nloc);
   const uint32_t nbn = s.NT <= 4096u ? 1u : static_cast<uint32_t>(std::min<uint64_t>(kNextBlocks, (s.NT + 2047) / 2048));
-  const size_t lds = scan_lds_bytes(s.kp);
   const long long stop = s.stop_pending && s.cfg.stop_ns >= 0 ? static_cast<long long>(s.cfg.stop_ns) : -1ll;
   std::vector<size_t> ev_at(K, SIZE_MAX), ev_nx(K, SIZE_MAX);
   int rc;
   for (uint32_t k = 0; k < K; ++k) {
     // (the first window from the host's state; each later one decided by the k_next before it)
     if (k == 0 && (rc = launch(s, -1, k_win, dim3(1), dim3(64), 0, s.kp_dev, static_cast<long long>(s.t_done), s.last_full,
-                               lim, stop)))
+                               lim, stop, loop_mask)))
       return rc;
     if (timed) {
       ev_at[k] = s.ev_used;
@@ -2175,8 +2214,11 @@ static int run_chain(Sim& s, long long lim) {
     }
     if ((rc = launch(s, -1, k_gossip_active, dim3((na + 1023) / 1024), dim3(1024), 0, s.kp_dev, -1ll, 0ll)) ||
         (rc = launch(s, -1, k_gossip_cell, gg, dim3(256), 0, s.kp_dev, -1ll, 0ll, 0ll, 0ll, 0, s.gossip_g, 0, 0, 1)) ||
-        (rc = launch(s, -1, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), dim3(s.bs_scan), lds, s.kp_dev, -1ll, 0ll, 0ll,
-                     0ll, 0, 0)) ||
+        // (the generic scan where the host expects the origin's block tick; it exits at once when
+        // the window at this position has no timer due)
+        (((loop_mask >> k) & 1ull) &&
+         (rc = launch(s, -1, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), dim3(s.bs_scan), scan_lds_bytes(s.kp), s.kp_dev,
+                      -1ll, 0ll, 0ll, 0ll, 0, 0))) ||
         ((s.ev_stop_attach = timed && s.ext_events), false) ||
         (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(s.gossip_l3_grid, s.grid_link)),
                      dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, -1ll, 0ll, 0ll, 0)))
@@ -2186,9 +2228,11 @@ static int run_chain(Sim& s, long long lim) {
     } else {
       s.launches[KS_LINK]++;
     }
-    s.next_seq = ++s.mseq;
+    // (only the chain's last k_next publishes the control block to the host: the others skip the
+    // host-memory writes and their system-scope fence)
+    const uint32_t seq = k + 1 == K ? (s.next_seq = ++s.mseq) : 0u;
     ev_nx[k] = s.ev_used;
-    if ((rc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, kClrWin, s.next_seq, PredArgs{}, 0u))) return rc;
+    if ((rc = launch(s, KS_AUX, k_next, dim3(nbn), dim3(1024), 0, s.kp_dev, kClrWin, seq, PredArgs{}, 0u))) return rc;
     if (s.ev_used == ev_nx[k]) ev_nx[k] = SIZE_MAX;  // (k_next untimed)
   }
   // the one sync: the last k_next's control block (readback without applying yet: the timing
@@ -2222,8 +2266,9 @@ static int run_chain(Sim& s, long long lim) {
   }
   s.chain_windows += done;
   ++s.chains;
-  // (the next chain: twice as long after a full one, just longer than this one otherwise)
-  s.chain_k = done == K ? std::min<uint32_t>(2 * K, 32) : std::max<uint32_t>(2, done + 1);
+  // (the next chain: twice as long after a full one, as long as this one otherwise -- a window that
+  // was never opened still costs its dispatches, one chain more costs a host sync)
+  s.chain_k = done == K ? std::min<uint32_t>(2 * s.chain_k, 32) : std::max<uint32_t>(2, done);
   if (!done) {
     g_detail = "device window chain made no progress (k_win end reason " + std::to_string(wv[kWinDead]) + ")";
     return BCSIM_E_STATE;
@@ -2357,7 +2402,7 @@ static int run(Sim& s, int64_t t_until) {
       }
       break;
     }
-    if (s.chain_on && s.cells > 0 && !s.start_pending && s.grouped_cell < 0 && s.xcnt[c % s.B] == 0 &&
+    if (s.chain_on && s.cells > 0 && !s.start_pending && s.grouped_cell < 0 && s.xcnt[c % s.B] == 0 && s.next_timer >= lo &&
         !(s.ov_min <= c + static_cast<long long>(s.B) - 1) && !(lo <= 0 && 0 < hi) &&
         !(s.cfg.stop_ns >= 0 && lo <= s.cfg.stop_ns && s.cfg.stop_ns < hi)) {
       // no host work before this window (group_cell, START / STOP) and no ring-tag zeroing due in
@@ -2365,7 +2410,7 @@ static int run(Sim& s, int64_t t_until) {
       const long long t0 = (s.last_full + 1) / s.B;
       const long long z = (t0 % 32 == 31) ? s.last_full + 1 : ((t0 / 32) * 32 + 31) * static_cast<long long>(s.B);
       if (c < z) {
-        if ((rc = run_chain(s, lim))) return rc;
+        if ((rc = run_chain(s, c, lim))) return rc;
         continue;
       }
     }
@@ -2853,6 +2898,16 @@ int bcsim_read_loop_stats_ex(bcsim_sim* h, uint64_t* out8) {
   out8[5] = s.host_syncs;
   out8[6] = s.idle_checked;
   out8[7] = s.chain_windows;
+  return BCSIM_OK;
+}
+
+int bcsim_read_host_stats(bcsim_sim* h, double* out4) {
+  if (!h || !out4) return BCSIM_E_INVAL;
+  const Sim& s = *h->s;
+  out4[0] = s.host_launch_us;
+  out4[1] = s.host_wait_us;
+  out4[2] = static_cast<double>(s.host_launches);
+  out4[3] = 0;
   return BCSIM_OK;
 }
 

@@ -2922,7 +2922,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
 // and the window's kernels, launched with cell = -1, take it from the control block's win words
 // (or do nothing when k_win found none: the chain ended, the host takes over).
 enum : int { kWinValid = 0, kWinCell, kWinLo, kWinHi, kWinFw, kWinLoop, kWinTDone, kWinLastFull, kWinGrouped,
-             kWinCount, kWinDead, kWinLim, kWinStop, kWinWords = 16 };
+             kWinCount, kWinDead, kWinLim, kWinStop, kWinLoopMask, kWinWords = 16 };
 __device__ inline bool win_take(const KP& p, long long& cell, long long& lo, long long& hi, int& fw) {
   if (cell >= 0) return true;
   if (!p.win[kWinValid]) return false;
@@ -9370,7 +9370,7 @@ __global__ __launch_bounds__(256) void k_zero16(uint4* __restrict__ dst, uint64_
 // then the window's sequence number in the word after them, which the host spins on
 // (the prediction's four words follow scal[6]: words 18-25)
 __device__ inline void ctl_publish(const KP& p, long long s0, long long s3, uint32_t seq, const long long* pv) {
-  if (!p.ctl_mirror) return;
+  if (!p.ctl_mirror || !seq) return;  // (seq 0: a chained window's k_next before the chain's last)
   const uint32_t lane = tidx() & 63u;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(p.err);
   for (uint32_t k = lane; k < p.ctl_words; k += 64) {
@@ -9557,6 +9557,10 @@ __device__ inline void win_decide(const KP& p) {
       else if (lo <= 0 && 0 < hi) dead = 7;
       else if (stop_ns >= 0 && lo <= stop_ns && stop_ns < hi) dead = 8;
       else if (c >= z) dead = 9;
+      // (a timer due: the generic scan too, launched by the host only at the chain positions where
+      // it expects one -- anywhere else the window is the host's)
+      else if (p.scal[3] < hi && !((static_cast<unsigned long long>(w[kWinLoopMask]) >> min(w[kWinCount], 63ll)) & 1ull))
+        dead = 10;
     }
   }
   if (dead) {
@@ -9569,7 +9573,7 @@ __device__ inline void win_decide(const KP& p) {
   w[kWinLo] = lo;
   w[kWinHi] = hi;
   w[kWinFw] = hi == ce ? 1 : 0;
-  w[kWinLoop] = p.scal[3] < hi ? 1 : 0;  // (a timer due: the generic scan too, as run() decides)
+  w[kWinLoop] = p.scal[3] < hi ? 1 : 0;
   __threadfence();
   w[kWinValid] = 1;
   __threadfence();
@@ -9579,10 +9583,11 @@ __device__ inline void win_decide(const KP& p) {
 // run limit, the pending STOP time or -1); every later window is decided by the k_next that ends
 // the one before it (k_next: win_advance, then win_decide).
 __global__ __launch_bounds__(64) void k_win(const KP* __restrict__ pk, long long t_done, long long last_full, long long lim,
-                                            long long stop_ns) {
+                                            long long stop_ns, unsigned long long loop_mask) {
   const KP& p = *pk;
   long long* const w = p.win;
   if (tidx() == 0) {
+    w[kWinLoopMask] = static_cast<long long>(loop_mask);
     w[kWinTDone] = t_done;
     w[kWinLastFull] = last_full;
     w[kWinGrouped] = -1;

@@ -20,11 +20,12 @@ trap "kill $hb 2>/dev/null" EXIT
 [ -n "$SKIP_PYTEST" ] || step pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread
 [ -n "$ONLY_PYTEST" ] && exit 0
 step bench_pbft 240 python bench.py --steps 20 --warmup 5
-step bench_gossip 240 python bench.py --workload gossip
-step bench_gossip_pdes1 240 python bench.py --workload gossip --pdes1 --no-cpu-baseline
+step bench_gossip 240 python bench.py --workload gossip --steps 20 --warmup 5
+step bench_gossip_pdes1 240 python bench.py --workload gossip --pdes1 --no-cpu-baseline --steps 20 --warmup 5
+step bench_pbft_pdes1 240 python bench.py --pdes1 --no-cpu-baseline --steps 20 --warmup 5
 step bench_paxos 300 python bench.py --workload paxos
 step bench_pbft_jitter 240 python bench.py --jitter
 step bench_pbft_fq 400 python bench.py --queue fqcodel --steps 20 --warmup 5 --cpu-budget 10
 [ "$2" = "noprof" ] && exit 0
-bash tests/gpu_prof.sh $tag/prof --steps 20 --warmup 5 --no-cpu-baseline > $out/prof.log 2>&1 || { tail -5 $out/prof.log; exit 1; }
+bash tests/gpu_prof_all.sh $tag/prof > $out/prof.log 2>&1 || { tail -5 $out/prof.log; exit 1; }
 tail -3 $out/prof.log
