@@ -447,7 +447,8 @@ def main():
                      # host time per step inside kernel launches / waiting on the mirror words
                      "host_launch_us_per_step": host["launch_us"] / args.steps,
                      "host_wait_us_per_step": host["wait_us"] / args.steps,
-                     "launches_per_step": host["launches"] / args.steps},
+                     "launches_per_step": host["launches"] / args.steps,
+                     "chained_frontier_hits": host["frontier_hits"]},
             "kernel_us": {k: v["us"] for k, v in ks.items()},
             "kernel_launches": {k: v["launches"] for k, v in ks.items()},
             # untimed pass of as many steps with every kernel class timed (the timed region

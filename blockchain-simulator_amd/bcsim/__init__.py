@@ -120,7 +120,7 @@ class Simulator(_abi.Handle):
         """Host time of the cell loop (include/bcsim.h bcsim_read_host_stats)."""
         out = (C.c_double * 4)()
         self._call("read_host_stats", self.h, out)
-        return dict(launch_us=out[0], wait_us=out[1], launches=int(out[2]))
+        return dict(launch_us=out[0], wait_us=out[1], launches=int(out[2]), frontier_hits=int(out[3]))
 
     def reset_kernel_stats(self):
         self._call("reset_kernel_stats", self.h)

@@ -120,7 +120,7 @@ struct Sim {
   // chain_k windows on the device per host sync
   bool chain_on = false;
   uint32_t chain_k = 4;
-  uint64_t chains = 0, chain_windows = 0;
+  uint64_t chains = 0, chain_windows = 0, chain_fr_hits = 0;
   uint64_t host_syncs = 0;  // times the cell loop waited on the GPU (spins, stream syncs, blocking collectives)
   double host_launch_us = 0, host_wait_us = 0;  // host time inside kernel launches / mirror waits
   uint64_t host_launches = 0;
@@ -2265,6 +2265,7 @@ static int run_chain(Sim& s, long long c, long long lim) {
     s.start_pending = false;
   }
   s.chain_windows += done;
+  s.chain_fr_hits += static_cast<uint64_t>(wv[kWinFrHits]);
   ++s.chains;
   // (the next chain: twice as long after a full one, as long as this one otherwise -- a window that
   // was never opened still costs its dispatches, one chain more costs a host sync)
@@ -2907,7 +2908,7 @@ int bcsim_read_host_stats(bcsim_sim* h, double* out4) {
   out4[0] = s.host_launch_us;
   out4[1] = s.host_wait_us;
   out4[2] = static_cast<double>(s.host_launches);
-  out4[3] = 0;
+  out4[3] = static_cast<double>(s.chain_fr_hits);
   return BCSIM_OK;
 }
 

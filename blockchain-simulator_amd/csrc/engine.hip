@@ -2922,7 +2922,7 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
 // and the window's kernels, launched with cell = -1, take it from the control block's win words
 // (or do nothing when k_win found none: the chain ended, the host takes over).
 enum : int { kWinValid = 0, kWinCell, kWinLo, kWinHi, kWinFw, kWinLoop, kWinTDone, kWinLastFull, kWinGrouped,
-             kWinCount, kWinDead, kWinLim, kWinStop, kWinLoopMask, kWinWords = 16 };
+             kWinCount, kWinDead, kWinLim, kWinStop, kWinLoopMask, kWinFrCell, kWinFrHi, kWinFrHits, kWinWords = 20 };
 __device__ inline bool win_take(const KP& p, long long& cell, long long& lo, long long& hi, int& fw) {
   if (cell >= 0) return true;
   if (!p.win[kWinValid]) return false;
@@ -5832,6 +5832,8 @@ __global__ __launch_bounds__(QM != 0 ? 256 : (LOOP ? kLinkLoopThreads : 1024)) v
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (LOOP) {
+    if (cell < 0 && p.win[kWinValid] && blockIdx.x == 0 && tidx() == 0)
+      p.act_n[0] = 0;  // (a chained window: list 0 is free again -- the closing k_next builds the next frontier)
     if (!win_take(p, cell, t_lo, t_hi, final_win)) return;  // (a chained window, or none)
     const uint32_t ll = p.loop_list;
     for (ListRange lr = list_range(p.act_n[ll]); lr.k < lr.end; lr.k += lr.step) {
@@ -8146,7 +8148,7 @@ __global__ __launch_bounds__(1024) void k_gossip_active(const KP* __restrict__ p
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (cell < 0) {  // (a chained window, or none)
-    if (!p.win[kWinValid]) return;
+    if (!p.win[kWinValid] || p.win[kWinFrCell] >= 0) return;  // (none, or its frontier built by k_next)
     cell = p.win[kWinCell];
     t_hi = p.win[kWinHi];
   }
@@ -9515,6 +9517,9 @@ __device__ inline void win_advance(const KP& p) {
   p.win[kWinValid] = 0;
   __threadfence();
 }
+// (kWinFrCell / kWinFrHi: the window whose frontier the closing k_next built into list 0 -- the
+// guess cell + 1 -- or -1; k_gossip_active skips a window whose frontier is ready, and a guess
+// that missed empties the list for it)
 
 // The next window of a device chain -- run()'s rule (local_next_cell and the cell bounds) on the
 // control block as k_next left it -- or the end of the chain when the window needs the host:
@@ -9563,6 +9568,12 @@ __device__ inline void win_decide(const KP& p) {
         dead = 10;
     }
   }
+  const bool fr_hit = !dead && w[kWinFrCell] == c && w[kWinFrHi] == hi;
+  if (fr_hit) w[kWinFrHits] += 1;
+  if (!fr_hit && w[kWinFrCell] >= 0) {
+    p.act_n[0] = 0;  // (the speculative frontier was for another window: k_gossip_active builds it)
+    w[kWinFrCell] = -1;
+  }
   if (dead) {
     w[kWinDead] = dead;
     w[kWinValid] = 0;
@@ -9588,6 +9599,8 @@ __global__ __launch_bounds__(64) void k_win(const KP* __restrict__ pk, long long
   long long* const w = p.win;
   if (tidx() == 0) {
     w[kWinLoopMask] = static_cast<long long>(loop_mask);
+    w[kWinFrCell] = -1;
+    w[kWinFrHits] = 0;
     w[kWinTDone] = t_done;
     w[kWinLastFull] = last_full;
     w[kWinGrouped] = -1;
@@ -9610,10 +9623,48 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
   const KP& p = *pk;
   BAIL_IF_ERR();
   const bool chained = clr_b == kClrWin;
-  if (chained)
-    clr_b = p.win[kWinValid] && p.win[kWinFw] ? static_cast<uint32_t>(p.win[kWinCell] % p.n_buckets) : 0xFFFFFFFFu;
+  // a chained window being closed: the frontier of the guessed next window (cell + 1, up to the
+  // run limit) into list 0 -- k_gossip_active's rule on the node state this window left; list 0's
+  // count was reset by the window's k_link (after k_gossip_cell read it)
+  const bool frs = chained && p.win[kWinValid] != 0;  // (chains run dense gossip only)
+  long long fr_c = -1, fr_hi = 0;
+  if (chained) {
+    const long long c0 = p.win[kWinCell];
+    clr_b = p.win[kWinValid] && p.win[kWinFw] ? static_cast<uint32_t>(c0 % p.n_buckets) : 0xFFFFFFFFu;
+    fr_c = c0 + 1;
+    fr_hi = min((c0 + 2) * p.L, p.win[kWinLim]);
+  }
+  if (frs) {
+    __shared__ uint32_t fwc[kMaxWaves], fbase;
+    const uint32_t fb = static_cast<uint32_t>(fr_c % p.n_buckets), lane = tidx() & 63u, wv = tidx() >> 6;
+    for (uint32_t k0 = blockIdx.x * blockDim.x; k0 < p.NT; k0 += gridDim.x * blockDim.x) {  // (uniform)
+      const uint32_t g = k0 + tidx();
+      bool a = false;
+      if (g < p.NT) {  // (one rank: gnode = list index)
+        const bool f = node_flagged_w(p, fb, g, g / p.N, g % p.N, fr_hi);
+        const long long tn = AT(p.node_tnext, g, p.NT), on = AT(p.node_onext, g, p.NT);
+        const uint32_t no = AT(p.n_ops, g, p.NT);
+        a = f | (tn < fr_hi) | ((no != 0) & (on < fr_hi));
+      }
+      const unsigned long long mk = __ballot(a);
+      if (lane == 0) fwc[wv] = static_cast<uint32_t>(__popcll(mk));
+      __syncthreads();
+      if (tidx() == 0) {
+        uint32_t t = 0;
+        for (uint32_t q = 0; q < (blockDim.x >> 6); ++q) {
+          const uint32_t c = fwc[q];
+          fwc[q] = t;
+          t += c;
+        }
+        fbase = t ? gadd_r(&p.act_n[0], t) : 0u;
+      }
+      __syncthreads();
+      if (a) AT(p.act, fbase + fwc[wv] + static_cast<uint32_t>(__popcll(mk & ((1ull << lane) - 1ull))), 4ull * p.NT) = g;
+      __syncthreads();
+    }
+  }
   if (blockIdx.x == 0) {
-    if (tidx() < 4) p.act_n[tidx()] = 0;
+    if (tidx() < 4 && !(frs && tidx() == 0)) p.act_n[tidx()] = 0;
     if (clr_b < p.n_buckets) {
       if (tidx() == 0) {
         p.bucket_cnt[clr_b] = 0;
@@ -9705,7 +9756,11 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
       p.scal[0] = m;
       p.scal[3] = mt;
       for (int k = 0; k < 4; ++k) p.pred[k] = pv[k];
-      if (chained) win_advance(p);
+      if (chained) {
+        win_advance(p);
+        p.win[kWinFrCell] = frs ? fr_c : -1;
+        p.win[kWinFrHi] = fr_hi;
+      }
     }
     if (chained) win_decide(p);  // (the whole wave: the chain's next window)
     ctl_publish(p, m, mt, seq, pv);
@@ -9734,7 +9789,11 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     p.scal[3] = mmt;
     p.pred[0] = 0;  // (no prediction with several workgroups)
     __hip_atomic_store(p.nxt_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (chained) win_advance(p);
+    if (chained) {
+      win_advance(p);
+      p.win[kWinFrCell] = frs ? fr_c : -1;
+      p.win[kWinFrHi] = fr_hi;
+    }
   }
   if (chained) win_decide(p);  // (the whole wave: the chain's next window)
   ctl_publish(p, mm, mmt, seq);

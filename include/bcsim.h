@@ -327,7 +327,7 @@ int bcsim_read_loop_stats(bcsim_sim* s, uint64_t* out4);
 int bcsim_read_loop_stats_ex(bcsim_sim* s, uint64_t* out8);
 /* Host-side costs of the cell loop since bcsim_create (profiling aid): [0] microseconds spent
  * inside kernel launches, [1] microseconds spent waiting on the host-mapped mirror words,
- * [2] kernel launches, [3] 0. */
+ * [2] kernel launches, [3] device-chained windows whose frontier the closing k_next had built. */
 int bcsim_read_host_stats(bcsim_sim* s, double* out4);
 
 #ifdef __cplusplus

@@ -63,6 +63,7 @@ def stepped_cases(names):
             sim.run()
             got = (sim.trace(), sim.counters(), sim.status())
             ls = sim.loop_stats()
+            ls["frontier_hits"] = sim.host_stats()["frontier_hits"]
         d = compare(oracle.run(c, topology=topo), got) if got[2]["error"] == 0 else f"status {got[2]}"
         print(json.dumps({"case": name, "steps": k, "diff": d, **ls}), flush=True)
         bad += d is not None

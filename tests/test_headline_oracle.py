@@ -64,6 +64,7 @@ def test_small_cases_in_bench_steps_match_oracle(env, engine_lib):
         assert sum(o["spec_hits"] for o in outs) > 0, outs
         assert all(o["idle_checked"] == o["idle_parts"] for o in outs), outs
         assert all(o["chain_windows"] > 0 for o in gossip), gossip           # chains ran (and ended) ...
+        assert sum(o["frontier_hits"] for o in gossip) > 0, gossip           # k_next built frontiers
         assert sum(o["host_syncs"] for o in gossip) < sum(o["windows"] for o in gossip), gossip  # fewer syncs
     else:
         assert all(o["chain_windows"] == 0 for o in outs), outs
