@@ -9626,7 +9626,9 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
   // a chained window being closed: the frontier of the guessed next window (cell + 1, up to the
   // run limit) into list 0 -- k_gossip_active's rule on the node state this window left; list 0's
   // count was reset by the window's k_link (after k_gossip_cell read it)
-  const bool frs = chained && p.win[kWinValid] != 0;  // (chains run dense gossip only)
+  // (not by the chain's last k_next -- seq != 0, it publishes to the host: the host's own window
+  // that may follow builds list 0 from an empty count)
+  const bool frs = chained && p.win[kWinValid] != 0 && seq == 0;  // (chains run dense gossip only)
   long long fr_c = -1, fr_hi = 0;
   if (chained) {
     const long long c0 = p.win[kWinCell];
