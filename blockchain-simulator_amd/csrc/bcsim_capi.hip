@@ -2212,7 +2212,9 @@ static int run_chain(Sim& s, long long c, long long lim) {
       ev_at[k] = s.ev_used;
       if ((rc = ev_begin(s, KS_LINK))) return rc;
     }
-    if ((rc = launch(s, -1, k_gossip_active, dim3((na + 1023) / 1024), dim3(1024), 0, s.kp_dev, -1ll, 0ll)) ||
+    // (the frontier: k_gossip_active for the chain's first window; later ones get it from the k_next
+    // before them, or k_gossip_cell walks every gnode after a missed guess)
+    if ((k == 0 && (rc = launch(s, -1, k_gossip_active, dim3((na + 1023) / 1024), dim3(1024), 0, s.kp_dev, -1ll, 0ll))) ||
         (rc = launch(s, -1, k_gossip_cell, gg, dim3(256), 0, s.kp_dev, -1ll, 0ll, 0ll, 0ll, 0, s.gossip_g, 0, 0, 1)) ||
         // (the generic scan where the host expects the origin's block tick; it exits at once when
         // the window at this position has no timer due)

@@ -8132,7 +8132,9 @@ __global__ __launch_bounds__(256) void k_gossip_cell(const KP* __restrict__ pk, 
     cs = cell * p.L;
     x_active = 0;
     loop = static_cast<int>(p.win[kWinLoop]);
-    fl = 1;
+    // the frontier list when one was built (by k_gossip_active, -2, or by the closing k_next);
+    // after a missed guess (-1, no k_gossip_active in the chain's later windows) every gnode
+    fl = p.win[kWinFrCell] != -1 ? 1 : 0;
   }
   if (fl && blockIdx.x * (blockDim.x / G) >= p.act_n[0]) return;
   const bool left = gossip_scan_body(pk, cell, t_lo, t_hi, cs, x_active, G, loop, fl != 0);
@@ -8151,6 +8153,7 @@ __global__ __launch_bounds__(1024) void k_gossip_active(const KP* __restrict__ p
     if (!p.win[kWinValid] || p.win[kWinFrCell] >= 0) return;  // (none, or its frontier built by k_next)
     cell = p.win[kWinCell];
     t_hi = p.win[kWinHi];
+    if (blockIdx.x == 0 && tidx() == 0) p.win[kWinFrCell] = -2;  // (list 0 built here)
   }
   __shared__ uint32_t wcnt[kMaxWaves], s_base;
   const uint32_t na = p.R * p.nloc, lane = tidx() & 63u, wv = tidx() >> 6;
