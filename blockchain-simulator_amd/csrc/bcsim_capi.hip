@@ -108,6 +108,11 @@ struct Sim {
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   KP* kp_dev2 = nullptr;
+  // summary mode: a link stage of at most link_few senders and no scan in the window (the
+  // leader's block windows) runs the looped generic kernel over list 1 alone -- one dispatch
+  // instead of k_mesh_prep + k_mesh_row + the looped kernel (BCSIM_LINK_FEW=0: off)
+  KP* kp_dev_l1 = nullptr;
+  uint32_t link_few = 1;
   bool gossip_frontier = true;  // dense gossip: k_gossip_cell over the window's frontier (BCSIM_GOSSIP_FRONTIER=0: all)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   bool sum = false;  // heavy-wave record summaries (BCSIM_SUM=0: off)
@@ -122,6 +127,7 @@ struct Sim {
   uint32_t chain_k = 4;
   uint64_t chains = 0, chain_windows = 0, chain_fr_hits = 0;
   uint64_t host_syncs = 0;  // times the cell loop waited on the GPU (spins, stream syncs, blocking collectives)
+  uint64_t link_few_windows = 0;  // windows linked by the generic kernel alone (link_few)
   double host_launch_us = 0, host_wait_us = 0;  // host time inside kernel launches / mirror waits
   uint64_t host_launches = 0;
   bool check_idle = false;
@@ -1183,6 +1189,13 @@ static int setup_device(Sim& s) {
     HIPCHK(hipEventCreateWithFlags(&s.ev_fork, hipEventDisableTiming | hipEventDisableSystemFence));
     HIPCHK(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming | hipEventDisableSystemFence));
   }
+  if (s.sum) {  // (summary mode) the looped generic link stage over list 1: windows of few senders
+    KP k1 = s.kp;
+    k1.loop_list = 1;
+    if ((rc = dalloc(s, &s.kp_dev_l1, 1))) return rc;
+    HIPCHK(hipMemcpy(s.kp_dev_l1, &k1, sizeof(KP), hipMemcpyHostToDevice));
+    if (const char* lf = std::getenv("BCSIM_LINK_FEW"); lf && *lf) s.link_few = static_cast<uint32_t>(std::atoi(lf));
+  }
   if (!s.sparse && !s.pdes && c.protocol == BCSIM_PBFT) {
     KP kb = s.kp;
     kb.cap_arr = 2 * s.kp.cap_arr;
@@ -1392,6 +1405,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     return BCSIM_OK;
   }
   uint32_t n_link = 1;
+  uint32_t scan_n = UINT32_MAX;  // (nodes scanned in the window, when read back)
   bool scan_dsz = false;  // (summary mode: the scan grids are sized on the device)
   {  // compact lists of the window's active gnodes
     // contiguous chunks of >= 256 gnodes (<= kActChunk), at most ~1024 workgroups (N=4096:
@@ -1447,6 +1461,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       }
       grid = dim3((s.act_h[0] + 7) / 8 * 8);
       n_link = s.act_h[1];
+      scan_n = s.act_h[0];
       if (dsz && (dmask & 1u)) {
         grid = dim3((s.NT + 7) / 8 * 8);
         scan_dsz = true;
@@ -1650,6 +1665,13 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
       if ((rc = launch(s, -1, k_link_mesh<true, 1, false>, grid, dim3(256), 0, s.kp_dev, cell, lo, hi, fw, z, z)) ||
           (rc = launch(s, -1, (k_link<false, true, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
         return rc;
+    } else if (s.kp_dev_l1 && !wep && n_link != kDevSized && n_link <= s.link_few && scan_n == 0) {
+      // (few senders, nothing scanned: the generic stage flushes their uniform row words and
+      // descriptors and links them -- what k_mesh_prep hands it anyway for the leader's block)
+      s.ev_stop_attach = timed && s.ext_events;
+      if ((rc = launch(s, -1, (k_link<false, false, true>), gl, bl, link_lds_bytes(s.kp), s.kp_dev_l1, cell, lo, hi, fw)))
+        return rc;
+      ++s.link_few_windows;
     } else if (s.mesh_tile && (n_link >= s.tile_min || s.sum)) {  // (summary mode: k_mesh_row keeps row-uniform link state)
       // the simple nodes' edges by 32 x 64 (sender x receiver) tiles; a launch
       // epoch tells this launch's jobs from stale ones

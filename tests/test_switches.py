@@ -31,6 +31,7 @@ SWITCHES = [
     {"BCSIM_L2_OVERLAP": "1"},      # list 2 on the second stream in every window (default: few-node scans)
     {"BCSIM_CHAIN": "0"},           # no device-chained gossip windows (one host sync per window)
     {"BCSIM_FUSE_ACT": "1"},        # k_next builds the speculative lists (opt-in)
+    {"BCSIM_LINK_FEW": "0"},        # few-sender windows through k_mesh_prep + k_mesh_row too
 ]
 
 
