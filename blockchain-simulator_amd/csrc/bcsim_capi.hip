@@ -967,6 +967,11 @@ static int setup_device(Sim& s) {
       (rc = dalloc(s, &p.xmeta, (static_cast<size_t>(s.grid_link) + (s.l2_overlap ? kLoopGrid : 0)) * p.cap_stage)) ||
       (rc = dalloc(s, &p.ov, p.cap_ov)))
     return rc;
+  // (dense layout: the overflow list is compacted at every rebin -- k_rebin / k_ov_back)
+  if (!s.sparse) {
+    if ((rc = dalloc(s, &p.ov_tmp, p.cap_ov)) || (rc = dalloc(s, &p.rb_n, 2))) return rc;
+    HIPCHK(hipMemset((void*)p.rb_n, 0, 8));
+  }
   // active lists of k_scan / k_link (k_active; emptied by k_next / k_pbft_tick)
   if ((rc = dalloc(s, &p.act, 4 * NT)) || (rc = dalloc(s, &p.act_n, 4))) return rc;
   HIPCHK(hipMemset(p.act_n, 0, 16));
@@ -1788,6 +1793,11 @@ static int group_cell(Sim& s, long long cell) {
     int rc = launch(s, KS_GROUP, k_rebin, dim3(std::max<uint32_t>(1u, (nov + 255) / 256)), dim3(256), 0, s.kp_dev, cell, nov,
                     s.next_seq);
     if (rc || (rc = readback(s, true))) return rc;
+    // (compacted: the records that stay go back to the list's front before anything appends)
+    const uint32_t ns = s.ctl_h->ov_cnt;
+    if (s.kp.ov_tmp && ns &&
+        (rc = launch(s, KS_GROUP, k_ov_back, dim3(std::min<uint32_t>(1024, (ns + 255) / 256)), dim3(256), 0, s.kp_dev)))
+      return rc;
   } else if (s.ov_min <= cell + static_cast<long long>(s.B) - 1) {
     const uint32_t nov = s.ctl_h->ov_cnt;
     HIPCHK(hipMemcpyAsync(s.kp.scal + 1, s.act_h + 4, 8, hipMemcpyHostToDevice, s.stream));  // LLONG_MAX (pinned)

@@ -292,6 +292,11 @@ struct KP {
   GP(uint32_t) nxt_done;   // k_next workgroups finished (the last one reduces and resets it)
   GP(long long) rb_acc;    // k_rebin (publishing): the staying records' minimum cell (LLONG_MAX between launches)
   GP(uint32_t) rb_done;    // k_rebin workgroups finished (the last one resets it)
+  // k_rebin (publishing, dense): the records that stay beyond the ring, compacted (cap_ov) and
+  // counted (rb_n[0] during the launch, rb_n[1] the total for k_ov_back) -- the overflow list
+  // keeps only live records instead of growing by every block's far-future records
+  GP(XRec) ov_tmp;
+  GP(uint32_t) rb_n;
   // node partition (multi-GPU PDES): this rank owns nodes
   // [nlo, nlo + nloc) of every replica; records for other ranks' receivers
   // are staged in sendbuf and exchanged once per cell
@@ -1238,6 +1243,31 @@ __global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long l
   const uint32_t k = blockIdx.x * blockDim.x + tidx();
   long long stay = LLONG_MAX;
   if (k < n) rebin_one(p, g_cur, AT(p.ov, k, p.cap_ov), stay, lbm, lb);
+  if (seq && p.ov_tmp) {  // (compaction: the staying records to ov_tmp, one atomic per workgroup)
+    __shared__ uint32_t cw[4], cbase;
+    const bool st = stay != LLONG_MAX;
+    const unsigned long long m = __ballot(st);
+    const uint32_t lane = tidx() & 63u, wv = tidx() >> 6;
+    if (lane == 0) cw[wv] = static_cast<uint32_t>(__popcll(m));
+    __syncthreads();
+    if (tidx() == 0) {
+      uint32_t t = 0;
+      for (uint32_t q = 0; q < (blockDim.x >> 6); ++q) {
+        const uint32_t c = cw[q];
+        cw[q] = t;
+        t += c;
+      }
+      cbase = t ? gadd_r(&p.rb_n[0], t) : 0u;
+    }
+    __syncthreads();
+    if (st) {
+      const uint32_t pos = cbase + cw[wv] + static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
+      if (pos < p.cap_ov)
+        AT(p.ov_tmp, pos, p.cap_ov) = AT(p.ov, k, p.cap_ov);
+      else
+        set_err(p, BCSIM_E_OVERFLOW);
+    }
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const long long y = __shfl_xor(stay, off, 64);
@@ -1272,13 +1302,28 @@ __global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long l
   if (tidx() == 0) {
     const long long m = __hip_atomic_load(p.rb_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     p.scal[1] = m;
-    if (m == LLONG_MAX) *p.ov_cnt = 0;  // (everything rebinned: the list starts again)
+    if (p.ov_tmp) {  // (the list is the staying records now: k_ov_back copies them to its front)
+      const uint32_t ns = __hip_atomic_load(&p.rb_n[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *p.ov_cnt = ns;
+      p.rb_n[1] = ns;
+      __hip_atomic_store(&p.rb_n[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (m == LLONG_MAX) {
+      *p.ov_cnt = 0;  // (everything rebinned: the list starts again)
+    }
     __hip_atomic_store(p.rb_acc, LLONG_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(p.rb_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __threadfence();
   }
   __syncthreads();
   if (tidx() < 64) ctl_publish(p, p.scal[0], p.scal[3], seq);
+}
+
+// the compacted overflow list back to the front of the list (after a publishing k_rebin)
+__global__ __launch_bounds__(256) void k_ov_back(const KP* __restrict__ pk) {
+  const KP& p = *pk;
+  const uint32_t n = p.rb_n[1];
+  for (uint32_t k = blockIdx.x * blockDim.x + tidx(); k < n; k += gridDim.x * blockDim.x)
+    AT(p.ov, k, p.cap_ov) = AT(p.ov_tmp, k, p.cap_ov);
 }
 
 // ---------------------------------------------------------------------------
@@ -3896,7 +3941,7 @@ __global__ __launch_bounds__(1024) void k_scan_rt(const KP* __restrict__ pk, lon
         const uint32_t lo32 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(mm)), k));
         const uint32_t hi32 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(mm >> 32)), k));
         const unsigned long long mk = (static_cast<unsigned long long>(hi32) << 32) | lo32;
-        if (!((mk >> lane) & 1ull)) continue;
+        if (!((mk >> lane) & 1ull) || !dv) continue;
         const uint32_t s = ch * 64u + static_cast<uint32_t>(k);
         const uint32_t tofk = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ea.z), k));
         const uint32_t basek = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ea.w), k));
