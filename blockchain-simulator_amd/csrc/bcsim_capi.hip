@@ -113,6 +113,7 @@ struct Sim {
   // instead of k_mesh_prep + k_mesh_row + the looped kernel (BCSIM_LINK_FEW=0: off)
   KP* kp_dev_l1 = nullptr;
   uint32_t link_few = 1;
+  bool px_cap4 = false;  // sparse Paxos: k_paxos_link<4> (BCSIM_PX_CAP=4) instead of <kPxCap>
   bool gossip_frontier = true;  // dense gossip: k_gossip_cell over the window's frontier (BCSIM_GOSSIP_FRONTIER=0: all)
   uint32_t few_scan = 64;  // k_scan launches of at most this many nodes use kp_dev_big (BCSIM_FEW_SCAN)
   bool sum = false;  // heavy-wave record summaries (BCSIM_SUM=0: off)
@@ -1155,6 +1156,7 @@ static int setup_device(Sim& s) {
   if (const char* ci = std::getenv("BCSIM_CHECK_IDLE"); ci && *ci == '1') s.check_idle = true;
   if (const char* fa = std::getenv("BCSIM_FUSE_ACT"); fa && *fa == '1') s.fuse_act = true;
   if (const char* xe = std::getenv("BCSIM_EXT_EVENTS"); xe && *xe == '0') s.ext_events = false;
+  if (const char* pc = std::getenv("BCSIM_PX_CAP"); pc && *pc == '4') s.px_cap4 = true;
   if (const char* g3 = std::getenv("BCSIM_GL3"); g3 && *g3) s.gossip_l3_grid = std::max<uint32_t>(8, static_cast<uint32_t>(std::atoi(g3)) / 8 * 8);
   {
     const char* sp = std::getenv("BCSIM_SPEC");
@@ -1632,7 +1634,8 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
     // sparse Paxos: one lane per acceptor first, the generic kernel over the rest (list 3)
     const bool timed = (kstat_mask() >> KS_LINK) & 1u;
     if (timed && (rc = ev_begin(s, KS_LINK))) return rc;
-    if ((rc = launch(s, -1, k_paxos_link, grid, dim3(kPxLinkThreads), 0, s.kp_dev, cell, lo, hi)) ||
+    if ((rc = s.px_cap4 ? launch(s, -1, k_paxos_link<4>, grid, dim3(kPxLinkThreads), 0, s.kp_dev, cell, lo, hi)
+                        : launch(s, -1, k_paxos_link<kPxCap>, grid, dim3(kPxLinkThreads), 0, s.kp_dev, cell, lo, hi)) ||
         ((s.ev_stop_attach = timed && s.ext_events), false) ||
         (rc = launch(s, -1, k_link_sparse, grid, dim3(s.bs_link), 0, s.kp_dev, cell, lo, hi, fw, 3)))
       return rc;

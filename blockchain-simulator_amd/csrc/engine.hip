@@ -8619,8 +8619,12 @@ struct PxLinkShared {
   uint32_t lbase[kMaxBuckets + 1];
   long long ovmin;
   uint32_t c[5];  // records, due ops, edges, echoes, kept
+  uint32_t rp[256 * kPxCap];  // (list << 24 | rank) of each lane's records, in walk order (CAP <= kPxCap)
 };
 constexpr uint32_t kPxLinkThreads = 256;
+// CAP: the most pending ops a lane holds in registers (nodes with more go to list 3); 8 by
+// default, 4 with BCSIM_PX_CAP=4 (fewer registers: more waves in flight on the latency-bound walk)
+template <int CAP>
 __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restrict__ pk, long long cell, long long t_lo,
                                                                long long t_hi) {
   const KP& p = *pk;
@@ -8645,15 +8649,15 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
     const uint32_t kl = base + tid;
     const uint32_t g = kl < na ? p.act[p.NT + kl] : 0u;
     const uint32_t n = kl < na ? AT(p.n_ops, g, p.NT) : 0u;
-    bool fast = kl < na && n <= static_cast<uint32_t>(kPxCap);
+    bool fast = kl < na && n <= static_cast<uint32_t>(CAP);
     Op* ops = p.ops + (kl < na ? op_base(p, g) : 0);
     // the ops, all loads in flight at once; bit c of due: op c is due
-    RawOp o[kPxCap];
+    RawOp o[CAP];
 #pragma unroll
-    for (int c = 0; c < kPxCap; ++c) o[c] = (fast && static_cast<uint32_t>(c) < n) ? ld_raw(ops + c) : raw_zero();
+    for (int c = 0; c < CAP; ++c) o[c] = (fast && static_cast<uint32_t>(c) < n) ? ld_raw(ops + c) : raw_zero();
     uint32_t due = 0;
 #pragma unroll
-    for (int c = 0; c < kPxCap; ++c) {
+    for (int c = 0; c < CAP; ++c) {
       if (static_cast<uint32_t>(c) >= n) continue;
       const uint32_t kind = raw_kind(o[c]);
       if ((kind != OP_SEND && kind != OP_ECHO) || o[c].b.y == kInvalid) fast = false;
@@ -8665,10 +8669,15 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
     }
     uint32_t c_rec = 0, c_ops = 0, c_edges = 0, c_echo = 0, c_sends = 0;
     long long ovmin = LLONG_MAX;
-    if (fast && due) {
+    // The due ops in (edge, key) order through each edge's FIFO, twice: pass 0 counts each record
+    // into its list (an LDS rank, kept in L.rp) and reads the link words only; after one global
+    // atomic per list, pass 1 repeats the identical walk and writes every record straight to its
+    // list position and the link words back -- no per-workgroup staging copy of the records.
+    auto walk = [&](const int pass) {
+      if (!(fast && due)) return;
       const uint32_t rep = g / p.N, i = g % p.N;
       const uint32_t e0 = AT(p.row, i, p.N + 1);
-      uint32_t left = due;
+      uint32_t left = due, ri = 0;
       uint32_t cur_e = kInvalid;
       uint64_t* lwp = nullptr;
       int64_t bu = 0;
@@ -8679,7 +8688,7 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
         RawOp ob = raw_zero();
         uint32_t best = kInvalid;
 #pragma unroll
-        for (int c = 0; c < kPxCap; ++c) {
+        for (int c = 0; c < CAP; ++c) {
           const bool cand = (left >> c) & 1u;
           const bool take = cand && (best == kInvalid || o[c].b.y < ob.b.y ||
                                      (o[c].b.y == ob.b.y && raw_key_less(o[c], raw_sub(o[c]), ob, raw_sub(ob))));
@@ -8688,8 +8697,8 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
         }
         left &= ~(1u << best);
         const uint32_t e = ob.b.y;
-        if (e != cur_e) {  // a new edge: store the previous one's link word, load this one's
-          if (lwp) {
+        if (e != cur_e) {  // a new edge: store the previous one's link word (pass 1), load this one's
+          if (lwp && pass) {
             if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
             *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
           }
@@ -8703,28 +8712,42 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
           slot = p.mesh ? sn * (p.N - 1) + (i < sn ? i : i - 1) : AT(p.rev, e, p.E);
           dg = rep * p.N + sn;
           pr = p.prop_const >= 0 ? p.prop_const : AT(p.prop, e, p.E);
-          ++c_edges;
+          if (!pass) ++c_edges;
         }
-        ++c_ops;
         const uint32_t kind = raw_kind(ob);
-        if (kind == OP_SEND) ++c_sends;
+        if (!pass) {
+          ++c_ops;
+          if (kind == OP_SEND) ++c_sends;
+        }
         const int big = (raw_flags(ob) & OPF_BIG) ? 1 : 0;
         const int64_t ot = raw_t(ob);
         const int64_t start = bu > ot ? bu : ot;
         bu = start + sel2(p.tx_tot, big);
         if (kind == OP_ECHO) {
-          ++c_echo;
+          if (!pass) ++c_echo;
           continue;
         }
         const int64_t ta = bu + pr;
         const long long ca = ta / p.L;
         const long long rel = ca - cell;
         if (rel < 1) {
-          set_err(p, BCSIM_E_TIE);
+          if (!pass) set_err(p, BCSIM_E_TIE);
           continue;
         }
-        ++c_rec;
         lc = static_cast<uint32_t>(ca) & 0xFFFFu;
+        const uint32_t list = rel < static_cast<long long>(B) ? static_cast<uint32_t>(ca % B) : B;
+        const uint32_t rs = tid * CAP + ri++;
+        if (!pass) {
+          ++c_rec;
+          L.rp[rs] = (list << 24) | atomicAdd(&L.lst[list], 1u);
+          if (list < B) {
+            atomicAdd(&L.lcnt[list], 1u);
+            atomicMin(&L.lmin[list], static_cast<uint32_t>(ta - ca * p.L));
+          } else if (ca < ovmin) {
+            ovmin = ca;
+          }
+          continue;
+        }
         XRec x;
         {
           const uint32_t w3 = (ob.b.w & 0x00FFFFFFu) | (static_cast<uint32_t>(RF_VALID | (big ? RF_BIG : 0)) << 24);
@@ -8734,27 +8757,25 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
         x.cell = ca;
         x.slot = slot;
         x.g = dg;
-        if (rel < static_cast<long long>(B)) {
-          const uint32_t bk = static_cast<uint32_t>(ca % B);
-          link_stage(p, L, g, bk, x);
-          set_flag_once(&AT(p.iflag, static_cast<size_t>(bk) * p.NT + dg, static_cast<uint64_t>(B) * p.NT));
-          atomicAdd(&L.lcnt[bk], 1u);
-          atomicMin(&L.lmin[bk], static_cast<uint32_t>(ta - ca * p.L));
+        const uint32_t pos = L.lbase[list] + (L.rp[rs] & 0xFFFFFFu);
+        if (list == B) {
+          if (pos < p.cap_ov) p.ov[pos] = x;
         } else {
-          link_stage(p, L, g, B, x);
-          if (ca < ovmin) ovmin = ca;
+          if (pos < p.cap_x) p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = x;
+          set_flag_once(&AT(p.iflag, static_cast<size_t>(list) * p.NT + dg, static_cast<uint64_t>(B) * p.NT));
         }
       }
-      if (lwp) {
+      if (lwp && pass) {
         if (bu >= (1ll << 47)) set_err(p, BCSIM_E_OVERFLOW);
         *lwp = (static_cast<uint64_t>(bu) << 16) | lc;
       }
-    }
+    };
+    walk(0);
     if (fast && (due || n)) {  // ordered compaction of the ops not yet due
       uint32_t kept = 0;
       long long omin = LLONG_MAX;
 #pragma unroll
-      for (int c = 0; c < kPxCap; ++c) {
+      for (int c = 0; c < CAP; ++c) {
         if (static_cast<uint32_t>(c) >= n || ((due >> c) & 1u)) continue;
         if (raw_t(o[c]) < omin) omin = raw_t(o[c]);
         uint4* w = reinterpret_cast<uint4*>(ops + kept);
@@ -8784,17 +8805,7 @@ __global__ __launch_bounds__(kPxLinkThreads) void k_paxos_link(const KP* __restr
       L.lbase[k] = b0;
     }
     __syncthreads();
-    const uint32_t nst = min(L.nst, p.cap_stage);
-    for (uint32_t k = tid; k < nst; k += bs) {
-      const size_t sidx = static_cast<size_t>(blockIdx.x) * p.cap_stage + k;
-      const uint32_t meta = p.xmeta[sidx], list = meta >> 24;
-      const uint32_t pos = L.lbase[list] + (meta & 0xFFFFFFu);
-      if (list == B) {
-        if (pos < p.cap_ov) p.ov[pos] = p.xstage[sidx];
-      } else if (pos < p.cap_x) {
-        p.xbuf[static_cast<size_t>(list) * p.cap_x + pos] = p.xstage[sidx];
-      }
-    }
+    walk(1);
     for (uint32_t k = tid; k < B; k += bs)
       if (L.lcnt[k]) {
         mark_busy(&p.bucket_cnt[k]);
