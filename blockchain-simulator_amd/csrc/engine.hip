@@ -2968,13 +2968,21 @@ __device__ __attribute__((always_inline)) inline void scan_node(const KP* pk, ui
 // (or do nothing when k_win found none: the chain ended, the host takes over).
 enum : int { kWinValid = 0, kWinCell, kWinLo, kWinHi, kWinFw, kWinLoop, kWinTDone, kWinLastFull, kWinGrouped,
              kWinCount, kWinDead, kWinLim, kWinStop, kWinLoopMask, kWinFrCell, kWinFrHi, kWinFrHits, kWinWords = 20 };
+// (the words are workgroup-uniform: read into scalar registers, so the kernels that take them keep
+// their window bounds where the kernel arguments were)
+__device__ inline long long win_word(const KP& p, int k) {
+  const long long v = p.win[k];
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<unsigned long long>(v) >> 32));
+  return static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo);
+}
 __device__ inline bool win_take(const KP& p, long long& cell, long long& lo, long long& hi, int& fw) {
   if (cell >= 0) return true;
-  if (!p.win[kWinValid]) return false;
-  cell = p.win[kWinCell];
-  lo = p.win[kWinLo];
-  hi = p.win[kWinHi];
-  fw = static_cast<int>(p.win[kWinFw]);
+  if (!win_word(p, kWinValid)) return false;
+  cell = win_word(p, kWinCell);
+  lo = win_word(p, kWinLo);
+  hi = win_word(p, kWinHi);
+  fw = static_cast<int>(win_word(p, kWinFw));
   return true;
 }
 
@@ -2984,10 +2992,12 @@ __global__ __launch_bounds__(PROTO == BCSIM_PBFT ? 1024 : 256) void k_scan(const
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (LOOP) {
-    if (cell < 0) {  // (a chained window: only when the window needs the generic scan)
-      if (!win_take(p, cell, t_lo, t_hi, final_win) || !p.win[kWinLoop]) return;
-      cs = cell * p.L;
-      x_active = 0;
+    if constexpr (PROTO == BCSIM_GOSSIP && !SP) {
+      if (cell < 0) {  // (a chained window: only when the window needs the generic scan)
+        if (!win_take(p, cell, t_lo, t_hi, final_win) || !win_word(p, kWinLoop)) return;
+        cs = cell * p.L;
+        x_active = 0;
+      }
     }
     for (ListRange lr = list_range(p.act_n[2]); lr.k < lr.end; lr.k += lr.step) {
       scan_node<PROTO, SP>(pk, p.act[2ull * p.NT + lr.k], cell, t_lo, t_hi, cs, final_win, x_active);
@@ -5877,9 +5887,13 @@ __global__ __launch_bounds__(QM != 0 ? 256 : (LOOP ? kLinkLoopThreads : 1024)) v
   const KP& p = *pk;
   BAIL_IF_ERR();
   if (LOOP) {
-    if (cell < 0 && p.win[kWinValid] && blockIdx.x == 0 && tidx() == 0)
-      p.act_n[0] = 0;  // (a chained window: list 0 is free again -- the closing k_next builds the next frontier)
-    if (!win_take(p, cell, t_lo, t_hi, final_win)) return;  // (a chained window, or none)
+    if constexpr (!QM && !XR) {
+      if (cell < 0) {  // (a chained window, or none)
+        if (!win_take(p, cell, t_lo, t_hi, final_win)) return;
+        if (blockIdx.x == 0 && tidx() == 0)
+          p.act_n[0] = 0;  // (list 0 is free again -- the closing k_next builds the next frontier)
+      }
+    }
     const uint32_t ll = p.loop_list;
     for (ListRange lr = list_range(p.act_n[ll]); lr.k < lr.end; lr.k += lr.step) {
       const uint32_t g = p.act[static_cast<size_t>(ll) * p.NT + lr.k];
