@@ -126,6 +126,7 @@ struct Sim {
   // chain_k windows on the device per host sync
   bool chain_on = false;
   uint32_t chain_k = 4;
+  uint32_t chain_l3_grid = 16;  // chained windows: the looped generic link grid (list 3 is almost always empty; BCSIM_CHAIN_L3)
   uint64_t chains = 0, chain_windows = 0, chain_fr_hits = 0;
   uint64_t host_syncs = 0;  // times the cell loop waited on the GPU (spins, stream syncs, blocking collectives)
   uint64_t link_few_windows = 0;  // windows linked by the generic kernel alone (link_few)
@@ -1157,6 +1158,7 @@ static int setup_device(Sim& s) {
   if (const char* fa = std::getenv("BCSIM_FUSE_ACT"); fa && *fa == '1') s.fuse_act = true;
   if (const char* xe = std::getenv("BCSIM_EXT_EVENTS"); xe && *xe == '0') s.ext_events = false;
   if (const char* pc = std::getenv("BCSIM_PX_CAP"); pc && *pc == '4') s.px_cap4 = true;
+  if (const char* cl = std::getenv("BCSIM_CHAIN_L3"); cl && *cl) s.chain_l3_grid = std::max<uint32_t>(8, static_cast<uint32_t>(std::atoi(cl)) / 8 * 8);
   if (const char* g3 = std::getenv("BCSIM_GL3"); g3 && *g3) s.gossip_l3_grid = std::max<uint32_t>(8, static_cast<uint32_t>(std::atoi(g3)) / 8 * 8);
   {
     const char* sp = std::getenv("BCSIM_SPEC");
@@ -1404,7 +1406,7 @@ static int do_scan(Sim& s, long long cell, long long lo, long long hi, long long
         // were allocated for: xstage / xmeta hold grid_link of them)
         // (list 3 is almost always empty here; BCSIM_GL3: its grid, 8-256 measured alike)
         ((s.ev_stop_attach = timed && s.ext_events), false) ||
-        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(s.gossip_l3_grid, s.grid_link)), dim3(s.bs_link),
+        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(s.chain_l3_grid, s.grid_link)), dim3(s.bs_link),
                      link_lds_bytes(s.kp), s.kp_dev, cell, lo, hi, fw)))
       return rc;
     if (timed) return ev_end(s);
@@ -2257,7 +2259,7 @@ static int run_chain(Sim& s, long long c, long long lim) {
          (rc = launch(s, -1, (k_scan<BCSIM_GOSSIP, false, true>), dim3(256), dim3(s.bs_scan), scan_lds_bytes(s.kp), s.kp_dev,
                       -1ll, 0ll, 0ll, 0ll, 0, 0))) ||
         ((s.ev_stop_attach = timed && s.ext_events), false) ||
-        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(s.gossip_l3_grid, s.grid_link)),
+        (rc = launch(s, -1, (k_link<false, false, true>), dim3(std::min<uint32_t>(s.chain_l3_grid, s.grid_link)),
                      dim3(s.bs_link), link_lds_bytes(s.kp), s.kp_dev, -1ll, 0ll, 0ll, 0)))
       return rc;
     if (timed) {
