@@ -9709,6 +9709,7 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
     fr_c = c0 + 1;
     fr_hi = min((c0 + 2) * p.L, p.win[kWinLim]);
   }
+  long long fm = LLONG_MAX, fmt = LLONG_MAX;  // (with the frontier pass: its next-event minima too)
   if (frs) {
     __shared__ uint32_t fwc[kMaxWaves], fbase;
     const uint32_t fb = static_cast<uint32_t>(fr_c % p.n_buckets), lane = tidx() & 63u, wv = tidx() >> 6;
@@ -9720,6 +9721,8 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
         const long long tn = AT(p.node_tnext, g, p.NT), on = AT(p.node_onext, g, p.NT);
         const uint32_t no = AT(p.n_ops, g, p.NT);
         a = f | (tn < fr_hi) | ((no != 0) & (on < fr_hi));
+        fm = min(fm, min(tn, on));
+        fmt = min(fmt, tn);
       }
       const unsigned long long mk = __ballot(a);
       if (lane == 0) fwc[wv] = static_cast<uint32_t>(__popcll(mk));
@@ -9756,9 +9759,10 @@ __global__ __launch_bounds__(1024) void k_next(const KP* __restrict__ pk, uint32
   // scal[0] = the next event time (timers and pending ops), scal[3] = the next timer alone;
   // wave minima by shuffles, one LDS slot per wave, one barrier
   __shared__ long long red[kMaxWaves], redt[kMaxWaves];
-  long long m = LLONG_MAX, mt = LLONG_MAX;
+  long long m = fm, mt = fmt;
   const uint32_t nb = gridDim.x, stride = nb * blockDim.x;
-  uint32_t k = blockIdx.x * blockDim.x + tidx();
+  // (the frontier pass covered every gnode of this workgroup's share: no second pass)
+  uint32_t k = frs ? p.NT : blockIdx.x * blockDim.x + tidx();
   // four gnodes per lane per step, their eight loads issued before any is used (PBFT n=4096:
   // one workgroup, no cross-workgroup combine)
   for (; k + 3u * stride < p.NT; k += 4u * stride) {
