@@ -1187,7 +1187,11 @@ __global__ void k_xplace(const KP* __restrict__ pk, uint32_t b, uint32_t n) {
 // (lbm / lb: the workgroup's per-bucket minimum arrival time and busy flags in LDS, flushed once
 // per workgroup -- a leader's block of 4095 overflow records lowered one bucket's bmin and set its
 // count word 4095 times: same-address atomics serialised in L2, ~50 us per k_rebin)
-__device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long long& stay, long long* lbm, uint32_t* lb) {
+// (xb / xrk / xo: a second record of its edge -- the extras list of bucket xb at workgroup rank
+// xrk, written by k_rebin once the workgroup's ranks have one base per bucket: a block's 4095
+// records appended to one bucket's list one atomic each serialised in L2)
+__device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long long& stay, long long* lbm, uint32_t* lb,
+                                 uint32_t* lx, int& xb, uint32_t& xrk, XRec& xo) {
   if (o.cell < 0) return;
   if (o.cell < g_cur + static_cast<long long>(p.n_buckets)) {
     const uint32_t b = static_cast<uint32_t>(o.cell % p.n_buckets);
@@ -1202,12 +1206,9 @@ __device__ inline void rebin_one(const KP& p, long long g_cur, XRec& o, long lon
         xs_mark(p, b, rep, k < d ? k : k + 1, d, static_cast<uint32_t>(x.r.flags) << 24);
       }
     } else {
-      const uint32_t pos = list_append(&p.x_cnt[b]);
-      if (pos >= p.cap_x) {
-        set_err(p, BCSIM_E_OVERFLOW);
-        return;
-      }
-      AT(p.xbuf, static_cast<size_t>(b) * p.cap_x + pos, p.cap_xbuf) = x;
+      xb = static_cast<int>(b);
+      xrk = atomicAdd(&lx[b], 1u);
+      xo = x;
     }
     AT(p.iflag, static_cast<size_t>(b) * p.NT + x.g, static_cast<uint64_t>(p.n_buckets) * p.NT) = 1;
     atomicMin(&lbm[b], o.cell * p.L + static_cast<long long>(x.r.t_off));
@@ -1233,16 +1234,20 @@ __global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long l
   BAIL_IF_ERR();
   __shared__ long long wmin[4];
   __shared__ long long lbm[kMaxBuckets];
-  __shared__ uint32_t lb[kMaxBuckets];
+  __shared__ uint32_t lb[kMaxBuckets], lx[kMaxBuckets], lxb[kMaxBuckets];
   const uint32_t B = p.n_buckets;
   for (uint32_t q = tidx(); q < B; q += blockDim.x) {
     lbm[q] = LLONG_MAX;
     lb[q] = 0;
+    lx[q] = 0;
   }
   __syncthreads();
   const uint32_t k = blockIdx.x * blockDim.x + tidx();
   long long stay = LLONG_MAX;
-  if (k < n) rebin_one(p, g_cur, AT(p.ov, k, p.cap_ov), stay, lbm, lb);
+  int xb = -1;
+  uint32_t xrk = 0;
+  XRec xo{};
+  if (k < n) rebin_one(p, g_cur, AT(p.ov, k, p.cap_ov), stay, lbm, lb, lx, xb, xrk, xo);
   if (seq && p.ov_tmp) {  // (compaction: the staying records to ov_tmp, one atomic per workgroup)
     __shared__ uint32_t cw[4], cbase;
     const bool st = stay != LLONG_MAX;
@@ -1275,11 +1280,21 @@ __global__ __launch_bounds__(256) void k_rebin(const KP* __restrict__ pk, long l
   }
   if ((tidx() & 63u) == 0) wmin[tidx() >> 6] = stay;
   __syncthreads();
-  for (uint32_t q = tidx(); q < B; q += blockDim.x)
+  for (uint32_t q = tidx(); q < B; q += blockDim.x) {
     if (lb[q]) {
       bmin_lower(p, q, lbm[q]);
       mark_busy(&p.bucket_cnt[q]);
     }
+    if (lx[q]) lxb[q] = atomicAdd(&p.x_cnt[q], lx[q]);
+  }
+  __syncthreads();
+  if (xb >= 0) {  // (the workgroup's extras: one list atomic per bucket above)
+    const uint32_t pos = lxb[xb] + xrk;
+    if (pos >= p.cap_x)
+      set_err(p, BCSIM_E_OVERFLOW);
+    else
+      AT(p.xbuf, static_cast<size_t>(xb) * p.cap_x + pos, p.cap_xbuf) = xo;
+  }
   if (!seq) {
     if (tidx() == 0) {
       long long m = wmin[0];
